@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Benchmark of the ERP hot path on MI355X: ERP image-pairs/sec (4k x 4k kpts, 10k RANSAC iters).
+
+Workload (BASELINE.json configs[1] shape): synthetic ERP pairs of 4096 x 4096 64-D SURF-like
+descriptors + keypoints (W x H = 5376 x 2688), exact k=2 + ratio-0.3 match -> gather ->
+eight_point::find with 10 000 initial_guess iterations (glibc-replay sampler, reference
+defaults otherwise).  A step = one erp_pair_batch_run over a batch of B such pairs resident
+in HBM; every step recomputes everything (no cached outputs).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs B] [--iters I] [--kpts N]
+
+N > 1: launched by torch.distributed.run, one rank per GPU; each rank runs its own B pairs
+(weak scaling, independent pairs = the reference's per-pair process) and the per-pair result
+records are all-gathered over RCCL every step (the "best-model gather" of configs[2]).
+Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_VALU_UNFUSED = 157.3 / 2  # TFLOP/s: 157.3 counts an FMA as 2; sub/mul/add are 1 each
+PEAK_FP64_VALU = 78.6               # TFLOP/s (MI355X spec, FMA = 2)
+PEAK_HBM = 8000.0                   # GB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=8, help="pairs per step per GPU")
+    ap.add_argument("--iters", type=int, default=10000)
+    ap.add_argument("--kpts", type=int, default=4096)
+    ap.add_argument("--seed", type=int, default=20200423)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--profile-tag", default="r01")
+    return ap.parse_args()
+
+
+def make_batch(rank: int, B: int, kpts: int, seed: int):
+    from erp_match_eightpoint_test_amd import synth
+    pairs = [synth.make_pair(seed + 1000 * rank + i, n_kpts=kpts) for i in range(B)]
+    return pairs
+
+
+def to_device(pairs, dev):
+    import torch
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    ol = np.concatenate([[0], np.cumsum([len(p["desc_l"]) for p in pairs])]).astype(np.int64)
+    orr = np.concatenate([[0], np.cumsum([len(p["desc_r"]) for p in pairs])]).astype(np.int64)
+    return dict(desc_l=t(np.concatenate([p["desc_l"] for p in pairs])),
+                desc_r=t(np.concatenate([p["desc_r"] for p in pairs])),
+                kp_l=t(np.concatenate([p["kp_l"] for p in pairs])),
+                kp_r=t(np.concatenate([p["kp_r"] for p in pairs])),
+                off_l=t(ol), off_r=t(orr),
+                width=t(np.array([p["W"] for p in pairs], np.int32)),
+                height=t(np.array([p["H"] for p in pairs], np.int32)),
+                max_nq=int(np.diff(ol).max()), max_nt=int(np.diff(orr).max()))
+
+
+def stage_work(stage, B, kpts, iters, res):
+    """algorithmic work of ONE launch of `stage` over the batch:
+    returns (amount, unit, peak, bound, note)."""
+    M = res["M"].astype(np.float64)
+    s = np.floor(M * 0.25)
+    K = res["K"].astype(np.float64)
+    if stage == "knn2_partial":
+        flops = 3.0 * kpts * kpts * 64 * B  # sub, mul, add per element (flann::L2 order, no FMA)
+        return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", "3*N*T*64 fp32 ops per pair"
+    if stage == "sampler_gram":
+        flops = float(np.sum(s * iters * (12 + 72)))  # 12 mul + 36 FMA per sampled row, fp64
+        return flops, "TFLOP/s", PEAK_FP64_VALU, "valu", "84 fp64 flops per sampled row"
+    if stage == "consensus_rows":
+        flops = float(np.sum(K * K * 9.0))  # 3 sub, 3 mul, 2 add, 1 sqrt per distance
+        return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", "9 fp32 ops per distance, K^2"
+    if stage == "eigen":
+        flops = float(iters * B * 40000.0)
+        return flops, "TFLOP/s", PEAK_FP64_VALU, "valu", "~4e4 fp64 flops per 9x9 Jacobi"
+    return None
+
+
+def cpu_baseline(pairs, iters, budget_s):
+    """the oracle (CPU restatement, exact brute force + OpenCV-style SVD) on host cores: whole
+    pairs of the same workload, as many as fit in ~budget_s (at least one)."""
+    import oracle as O
+    O.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    os.environ["OMP_NUM_THREADS"] = str(threads)
+    t0 = time.perf_counter()
+    n = 0
+    for p in pairs:
+        mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=threads)
+        kl = p["kp_l"][mt["queryIdx"]]
+        kr = p["kp_r"][mt["trainIdx"]]
+        O.find(p["W"], p["H"], kl, kr, O.make_cfg(iters=iters))
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{n} whole pair(s) of the bench workload ({len(pairs[0]['desc_l'])}x"
+                      f"{len(pairs[0]['desc_r'])} kpts, {iters} iters) through oracle/ "
+                      f"(exact-BF CPU restatement, OpenMP {threads} threads), {dt:.1f} s"}
+
+
+def load_pmc(tag, stage):
+    path = os.path.join(ROOT, "profiles", f"{tag}_pmc_{stage}.json")
+    if os.path.exists(path):
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
+    pairs = make_batch(rank, args.pairs, args.kpts, args.seed)
+    b = to_device(pairs, dev)
+    ctx = Context(local)
+    runner = PairBatchRunner(ctx=ctx, iters=args.iters)
+    runner.reserve(args.pairs, b["max_nq"], b["max_nt"])
+    call = lambda: runner.run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"],  # noqa
+                              b["off_r"], b["width"], b["height"], b["max_nq"], b["max_nt"])
+    gathered = None
+    if dist is not None:
+        gathered = torch.empty((world, args.pairs, 56), dtype=torch.uint8, device=dev)
+    for _ in range(args.warmup):
+        out = call()
+        if dist is not None:
+            dist.all_gather_into_tensor(gathered, out["results"])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    ctx.set_profiling(True)
+    ctx.stage_times()  # clear
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = call()
+        if dist is not None:
+            dist.all_gather_into_tensor(gathered, out["results"])
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    stages = ctx.stage_times()
+    ctx.set_profiling(False)
+    elapsed = t1 - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    res = results_to_numpy(out["results"])
+    ok = bool(np.all(res["status"] == 0))
+    err_deg = [float(np.degrees(np.abs(r["R"] - p["euler_gt"])).mean()) for r, p in zip(res, pairs)]
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    total_pairs = world * args.pairs * args.steps
+    value = total_pairs / elapsed
+    # dominant kernel roofline from the live HIP-event stage times
+    dom = max((k for k in stages if stages[k][1] > 0), key=lambda k: stages[k][0])
+    roof = None
+    w = stage_work(dom, args.pairs, args.kpts, args.iters, res)
+    if w is not None:
+        amount, unit, peak, bound, note = w
+        avg_s = stages[dom][0] / stages[dom][1] / 1e3
+        achieved = amount / avg_s / 1e12
+        roof = {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
+                "frac": achieved / peak, "traffic": load_pmc(args.profile_tag, dom),
+                "avg_launch_ms": avg_s * 1e3, "work_per_launch": amount, "work_note": note}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(pairs, args.iters, args.cpu_seconds)
+    line = {
+        "metric": "ERP image-pairs/sec (4k x 4k kpts, 10k RANSAC iters); match-set bit-exact",
+        "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32+f64",
+        "data": "synthetic (seeded SURF-like descriptors + ERP keypoints, synth.make_pair)",
+        "config": {"workload": "configs[1] shape: 4096x4096 kpts/pair, 10k initial_guess iters, "
+                               f"batch of {args.pairs} independent pairs per step per GPU",
+                   "kpts": args.kpts, "iters": args.iters, "pairs_per_step_per_gpu": args.pairs,
+                   "parallelism": f"pair-sharded x{world}", "sampler": "glibc replay (seed 1)"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "stages_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in stages.items()},
+        "check": {"all_status_ok": ok, "mean_abs_euler_err_deg_max": max(err_deg),
+                  "M_mean": float(res["M"].mean()), "K_mean": float(res["K"].mean())},
+    }
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,70 @@
+"""Build the in-tree gfx950 library (hipcc, no cmake): lib/liberp_match.so.
+
+The library holds the HIP kernels, the C ABI (include/erp_match.h) and the C++ class API
+(include/erp/*.hpp).  It is built in-tree so it travels to the GPU box with the repository
+snapshot; nothing is installed into site-packages.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB_DIR = os.path.join(PKG, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "liberp_match.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("ERP_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["kernels.hip", "capi.hip", "host_api.cpp"]
+HEADERS = ["erp_device.hpp", "erp_kernels.hpp"]
+PUBLIC_HEADERS = ["erp_match.h", os.path.join("erp", "feature_matcher.hpp"),
+                  os.path.join("erp", "eight_point.hpp")]
+
+# -ffp-contract=off: the matcher's flann::L2 order, the ratio test and the consensus
+# distances must round exactly like the reference's x86-64 code (no FMA contraction).
+# Never add -ffast-math / -fno-hip-fp32-correctly-rounded-divide-sqrt: sqrtf must be
+# correctly rounded for bit-exact DMatch.distance.
+CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
+            "-Wno-unused-function", f"--offload-arch={ARCH}"]
+
+
+def _inputs():
+    files = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    files += [os.path.join(ROOT, "include", h) for h in PUBLIC_HEADERS]
+    files.append(os.path.abspath(__file__))
+    return files
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return False
+    t = os.path.getmtime(LIB_PATH)
+    return all(os.path.getmtime(f) <= t for f in _inputs() if os.path.exists(f))
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB_PATH
+    os.makedirs(LIB_DIR, exist_ok=True)
+    objs = []
+    for src in SOURCES:
+        obj = os.path.join(LIB_DIR, os.path.splitext(src)[0] + ".o")
+        cmd = [HIPCC, *CXXFLAGS, "-I", os.path.join(ROOT, "include"), "-c",
+               os.path.join(CSRC, src), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    tmp = LIB_PATH + ".tmp"
+    subprocess.run([HIPCC, *CXXFLAGS, "-shared", "-o", tmp, *objs], check=True)
+    os.replace(tmp, LIB_PATH)
+    for o in objs:
+        os.remove(o)
+    return LIB_PATH
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,184 @@
+"""ctypes binding of include/erp_match.h (the C ABI of lib/liberp_match.so).
+
+This is exactly the binding a Python user of the reference path would add (see
+INTEGRATION.md).  There is no CPU fallback: if the HIP library is missing or no device is
+visible, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _build
+
+P = C.c_void_p
+
+ERP_OK = 0
+ERP_INVALID_ARG = 1
+ERP_TOO_FEW_POINTS = 2
+ERP_NO_VALID_HYPOTHESIS = 3
+ERP_HIP_ERROR = 4
+ERP_NO_DEVICE = 5
+ERP_OUT_OF_MEMORY = 6
+ERP_INTERNAL = 7
+STATUS_NAMES = {0: "ok", 1: "invalid argument", 2: "too few points",
+                3: "no valid rotation hypothesis", 4: "HIP error", 5: "no HIP device",
+                6: "out of device memory", 7: "internal consistency check failed"}
+
+
+class DMatch(C.Structure):
+    _fields_ = [("queryIdx", C.c_int32), ("trainIdx", C.c_int32), ("imgIdx", C.c_int32),
+                ("distance", C.c_float)]
+
+
+class Point2f(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float)]
+
+
+class RansacCfg(C.Structure):
+    _fields_ = [("iters", C.c_int32), ("sampler", C.c_int32), ("sample_frac", C.c_double),
+                ("trim_lo", C.c_double), ("trim_hi", C.c_double), ("valid_abs", C.c_double),
+                ("seed", C.c_uint32), ("reserved", C.c_uint32), ("offset", C.c_uint64)]
+
+
+class Hypothesis(C.Structure):
+    _fields_ = [("R1", C.c_float * 3), ("R2", C.c_float * 3), ("T", C.c_float * 3),
+                ("R1_valid", C.c_int32), ("R2_valid", C.c_int32), ("E", C.c_double * 9)]
+
+
+class PairResult(C.Structure):
+    _fields_ = [("R", C.c_float * 3), ("T", C.c_float * 3), ("status", C.c_int32),
+                ("M", C.c_int32), ("K", C.c_int32), ("min_idx", C.c_int32),
+                ("sample_n", C.c_int32), ("near_ties", C.c_int32), ("min_dist", C.c_double)]
+
+
+class PairBatch(C.Structure):
+    _fields_ = [("n_pairs", C.c_int32), ("dim", C.c_int32), ("max_nq", C.c_int32),
+                ("max_nt", C.c_int32), ("desc_l", P), ("desc_r", P), ("kp_l", P), ("kp_r", P),
+                ("off_l", P), ("off_r", P), ("width", P), ("height", P)]
+
+
+class BatchOutputs(C.Structure):
+    _fields_ = [("results", P), ("matches", P), ("key_left", P), ("key_right", P), ("hyps", P),
+                ("samples", P), ("rvec", P), ("tvec", P), ("dist", P)]
+
+
+DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"),
+                         ("distance", "<f4")])
+HYP_DTYPE = np.dtype([("R1", "<f4", 3), ("R2", "<f4", 3), ("T", "<f4", 3), ("R1_valid", "<i4"),
+                      ("R2_valid", "<i4"), ("E", "<f8", 9)], align=True)
+RESULT_DTYPE = np.dtype([("R", "<f4", 3), ("T", "<f4", 3), ("status", "<i4"), ("M", "<i4"),
+                         ("K", "<i4"), ("min_idx", "<i4"), ("sample_n", "<i4"),
+                         ("near_ties", "<i4"), ("min_dist", "<f8")], align=True)
+assert DMATCH_DTYPE.itemsize == C.sizeof(DMatch) == 16
+assert HYP_DTYPE.itemsize == C.sizeof(Hypothesis) == 120
+assert RESULT_DTYPE.itemsize == C.sizeof(PairResult) == 56
+assert C.sizeof(RansacCfg) == 56
+
+# every symbol include/erp_match.h declares (checked by tests/test_capi_symbols.py)
+EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransac_cfg_default",
+            "erp_abi_version", "erp_ctx_reserve", "erp_match_knn2_ratio", "erp_match_two_image",
+            "erp_eight_point_find_dev", "erp_eight_point_find", "erp_initial_guess",
+            "erp_eight_point_estimation", "erp_pair_batch_run", "erp_ctx_set_profiling",
+            "erp_stage_name", "erp_ctx_stage_times"]
+STAGES = ["knn2_partial", "knn2_merge", "bearings", "jump_prep", "sampler_gram", "eigen",
+          "valid_compact", "consensus_rows", "consensus_final"]
+
+
+class ErpError(RuntimeError):
+    def __init__(self, status: int, where: str):
+        super().__init__(f"{where}: {STATUS_NAMES.get(status, status)} (erp_status {status})")
+        self.status = status
+
+
+_lib = None
+
+
+def lib_path() -> str:
+    return _build.LIB_PATH
+
+
+def load(build_if_missing: bool = False):
+    """Load lib/liberp_match.so.  Raises if it is missing: there is no fallback path."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        if build_if_missing:
+            _build.build()
+        else:
+            raise RuntimeError(f"HIP library {path} is not built; run __graft_entry__.build() or "
+                               "python -m erp_match_eightpoint_test_amd._build")
+    L = C.CDLL(path)
+    L.erp_ctx_create.argtypes = [C.c_int32, C.POINTER(P)]
+    L.erp_ctx_destroy.argtypes = [P]
+    L.erp_status_string.argtypes = [C.c_int]
+    L.erp_status_string.restype = C.c_char_p
+    L.erp_ransac_cfg_default.argtypes = [C.POINTER(RansacCfg)]
+    L.erp_ransac_cfg_default.restype = None
+    L.erp_abi_version.restype = C.c_int32
+    L.erp_ctx_reserve.argtypes = [P, C.c_int32, C.c_int32, C.c_int32, C.c_int32]
+    L.erp_match_knn2_ratio.argtypes = [P, P, C.c_int32, P, C.c_int32, C.c_int32, C.c_float, P, P, P]
+    L.erp_match_two_image.argtypes = [P, P, C.c_int32, P, C.c_int32, C.c_int32, P, P]
+    L.erp_eight_point_find_dev.argtypes = [P, C.c_int32, C.c_int32, P, P, C.c_int32,
+                                           C.POINTER(RansacCfg), P, P, P]
+    L.erp_eight_point_find.argtypes = [P, C.c_int32, C.c_int32, P, P, C.c_int32,
+                                       C.POINTER(RansacCfg), P, P, P]
+    L.erp_initial_guess.argtypes = [P, P, P, C.c_int32, C.POINTER(RansacCfg), P, P, P]
+    L.erp_eight_point_estimation.argtypes = [P, P, P, C.c_int32, P]
+    L.erp_pair_batch_run.argtypes = [P, C.POINTER(PairBatch), C.c_float, C.POINTER(RansacCfg),
+                                     C.POINTER(BatchOutputs), P]
+    L.erp_ctx_set_profiling.argtypes = [P, C.c_int32]
+    L.erp_stage_name.argtypes = [C.c_int32]
+    L.erp_stage_name.restype = C.c_char_p
+    L.erp_ctx_stage_times.argtypes = [P, P, P]
+    _lib = L
+    return L
+
+
+def default_cfg(**kw) -> RansacCfg:
+    cfg = RansacCfg()
+    load().erp_ransac_cfg_default(C.byref(cfg))
+    for k, v in kw.items():
+        setattr(cfg, k, v)
+    return cfg
+
+
+def check(status: int, where: str):
+    if status != ERP_OK:
+        raise ErpError(status, where)
+
+
+class Context:
+    """erp_ctx: one per device/thread; owns the grow-only device scratch."""
+
+    def __init__(self, device: int = 0):
+        self.L = load()
+        self.h = P()
+        check(self.L.erp_ctx_create(device, C.byref(self.h)), "erp_ctx_create")
+        self.device = device
+
+    def set_profiling(self, enable: bool = True):
+        check(self.L.erp_ctx_set_profiling(self.h, 1 if enable else 0), "set_profiling")
+
+    def stage_times(self) -> dict:
+        """{stage: (total_ms, launches)} since the last call (syncs on the recorded events)."""
+        ms = np.zeros(len(STAGES), np.float64)
+        n = np.zeros(len(STAGES), np.int64)
+        check(self.L.erp_ctx_stage_times(self.h, ms.ctypes.data_as(P), n.ctypes.data_as(P)),
+              "stage_times")
+        return {s: (float(ms[i]), int(n[i])) for i, s in enumerate(STAGES)}
+
+    def close(self):
+        if self.h:
+            self.L.erp_ctx_destroy(self.h)
+            self.h = P()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,553 @@
+// capi.hip -- the C ABI declared in include/erp_match.h: context, device scratch and the
+// orchestration of the hot-path kernels on one HIP stream.  No host round trip inside a
+// pipeline run (match counts, sample sizes and hypothesis counts stay on the device).
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/erp_match.h"
+#include "erp_kernels.hpp"
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+};
+
+// grow-only device buffer; returns false on allocation failure
+bool ensure(DevBuf& b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (b.n >= bytes) return true;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+    if (hipMalloc(&b.p, bytes) != hipSuccess) return false;
+    b.n = bytes;
+    return true;
+}
+
+// glibc rand() window before draw `offset` of a stream seeded with `seed` (host, sequential;
+// same recurrence the kernels jump along).  31 words r[n-31..n-1].
+void host_glibc_window(uint32_t seed, uint64_t offset, uint32_t out[31]) {
+    int32_t r0[34];
+    if (seed == 0) seed = 1;
+    r0[0] = (int32_t)seed;
+    for (int i = 1; i < 31; i++) {
+        const long hi = r0[i - 1] / 127773, lo = r0[i - 1] % 127773;
+        long word = 16807 * lo - 2836 * hi;
+        if (word < 0) word += 2147483647;
+        r0[i] = (int32_t)word;
+    }
+    for (int i = 31; i < 34; i++) r0[i] = r0[i - 31];
+    uint32_t ring[34];
+    for (int i = 0; i < 34; i++) ring[i] = (uint32_t)r0[i];
+    uint64_t pos = 34;                    // absolute index of the next word
+    const uint64_t end = 344 + offset;    // draw k uses word k + 344
+    for (; pos < end; pos++) {
+        const uint32_t s = (uint32_t)(pos % 34);
+        ring[s] = ring[(pos - 3) % 34] + ring[(pos - 31) % 34];
+    }
+    for (int j = 0; j < 31; j++) out[j] = ring[(end - 31 + j) % 34];
+}
+
+}  // namespace
+
+struct erp_ctx {
+    int device = 0;
+    std::mutex mu;
+    // stage timing
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
+    DevBuf part, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
+        sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d;
+    bool w0_valid = false;
+    uint32_t w0_seed = 0;
+    uint64_t w0_offset = 0;
+};
+
+#define ERP_CK(x)                                         \
+    do {                                                  \
+        if ((x) != hipSuccess) return ERP_HIP_ERROR;      \
+    } while (0)
+
+namespace {
+
+// records an event pair around one launch when profiling is on
+struct StageTimer {
+    erp_ctx* c;
+    int stage;
+    hipStream_t st;
+    size_t idx = (size_t)-1;
+    StageTimer(erp_ctx* c_, int stage_, hipStream_t st_) : c(c_), stage(stage_), st(st_) {
+        if (!c->profiling) return;
+        while (c->ev_pool.size() < c->ev_used + 2) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return;
+            c->ev_pool.push_back(e);
+        }
+        idx = c->ev_used;
+        c->ev_used += 2;
+        (void)hipEventRecord(c->ev_pool[idx], st);
+    }
+    ~StageTimer() {
+        if (idx == (size_t)-1) return;
+        (void)hipEventRecord(c->ev_pool[idx + 1], st);
+        c->ev_rec.emplace_back(stage, idx);
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int32_t erp_abi_version(void) { return ERP_MATCH_ABI_VERSION; }
+
+const char* erp_status_string(erp_status s) {
+    switch (s) {
+        case ERP_OK: return "ok";
+        case ERP_INVALID_ARG: return "invalid argument";
+        case ERP_TOO_FEW_POINTS: return "too few points";
+        case ERP_NO_VALID_HYPOTHESIS: return "no valid rotation hypothesis";
+        case ERP_HIP_ERROR: return "HIP error";
+        case ERP_NO_DEVICE: return "no HIP device";
+        case ERP_OUT_OF_MEMORY: return "out of device memory";
+        case ERP_INTERNAL: return "internal consistency check failed";
+    }
+    return "unknown";
+}
+
+void erp_ransac_cfg_default(erp_ransac_cfg* cfg) {
+    if (!cfg) return;
+    memset(cfg, 0, sizeof(*cfg));
+    cfg->iters = 80;
+    cfg->sampler = ERP_SAMPLER_GLIBC;
+    cfg->sample_frac = 0.25;
+    cfg->trim_lo = 0.2;
+    cfg->trim_hi = 0.8;
+    cfg->valid_abs = 1.57;
+    cfg->seed = 1;
+    cfg->offset = 0;
+}
+
+erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
+    if (!out) return ERP_INVALID_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ERP_NO_DEVICE;
+    if (device < 0 || device >= n) return ERP_INVALID_ARG;
+    ERP_CK(hipSetDevice(device));
+    erp_ctx* c = new (std::nothrow) erp_ctx();
+    if (!c) return ERP_OUT_OF_MEMORY;
+    c->device = device;
+    erp::init_constants();
+    *out = c;
+    return ERP_OK;
+}
+
+erp_status erp_ctx_destroy(erp_ctx* ctx) {
+    if (!ctx) return ERP_INVALID_ARG;
+    (void)hipSetDevice(ctx->device);
+    DevBuf* all[] = {&ctx->part, &ctx->matches, &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
+                     &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
+                     &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
+                     &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d};
+    for (DevBuf* b : all)
+        if (b->p) (void)hipFree(b->p);
+    for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    delete ctx;
+    return ERP_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+erp::BatchShape make_shape(int n_pairs, int max_nq, int max_nt, int iters, double frac) {
+    erp::BatchShape sh{};
+    sh.n_pairs = n_pairs;
+    sh.max_nq = std::max(max_nq, 1);
+    sh.max_nt = std::max(max_nt, 1);
+    const int qblocks = (sh.max_nq + 255) / 256;
+    const int tmax = (sh.max_nt + 63) / 64;
+    int chunks = (2048 + qblocks * n_pairs - 1) / (qblocks * n_pairs);
+    chunks = std::max(1, std::min(chunks, tmax));
+    int chunk_len = (sh.max_nt + chunks - 1) / chunks;
+    chunk_len = (chunk_len + 63) / 64 * 64;
+    sh.chunk_len = chunk_len;
+    sh.chunks = (sh.max_nt + chunk_len - 1) / chunk_len;
+    sh.iters = std::max(iters, 1);
+    sh.max_s = std::max((int)(sh.max_nq * frac), 1);
+    sh.idx_stride = sh.max_s;
+    return sh;
+}
+
+erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_batch_outputs* out) {
+    const size_t P = (size_t)sh.n_pairs;
+    const size_t nwaves = (size_t)(sh.iters + 63) / 64;
+    bool ok = ensure(c->counts, P * 4) && ensure(c->flags, P * 4) &&
+              ensure(c->pts, P * sh.max_nq * 48) && ensure(c->polyR, P * 65 * 31 * 4) &&
+              ensure(c->polyQ, P * erp::kMaxQ * 31 * 4) &&
+              ensure(c->idx, P * nwaves * (size_t)sh.idx_stride * 64 * 2) &&
+              ensure(c->gram, P * sh.iters * 36 * 8) && ensure(c->rv, P * 6 * sh.iters * 4) &&
+              ensure(c->kcount, P * 4) && ensure(c->sortbuf, P * (size_t)erp::sortbuf_len(sh.iters) * 4) &&
+              ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result));
+    if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
+    if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
+    if (ok && !(out && out->dist)) ok = ensure(c->tmean, P * 2 * sh.iters * 8);
+    return ok ? ERP_OK : ERP_OUT_OF_MEMORY;
+}
+
+erp_status upload_w0(erp_ctx* c, const erp_ransac_cfg* cfg, hipStream_t st) {
+    if (!c->w0_valid || c->w0_seed != cfg->seed || c->w0_offset != cfg->offset) {
+        uint32_t w[31];
+        host_glibc_window(cfg->seed, cfg->offset, w);
+        ERP_CK(hipMemcpyAsync(c->w0.p, w, sizeof(w), hipMemcpyHostToDevice, st));
+        ERP_CK(hipStreamSynchronize(st));
+        c->w0_valid = true;
+        c->w0_seed = cfg->seed;
+        c->w0_offset = cfg->offset;
+    }
+    return ERP_OK;
+}
+
+bool cfg_ok(const erp_ransac_cfg* cfg) {
+    return cfg && cfg->iters >= 1 && cfg->sampler == ERP_SAMPLER_GLIBC && cfg->sample_frac > 0 &&
+           cfg->sample_frac <= 1.0 && cfg->trim_lo >= 0 && cfg->trim_hi <= 1.0 &&
+           cfg->trim_lo <= cfg->trim_hi;
+}
+
+// estimator stages after counts/pts are in place
+erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
+                         const erp_batch_outputs* out, erp_pair_result* results, hipStream_t st) {
+    erp_ctx* ctx = c;
+    auto* counts = (int32_t*)c->counts.p;
+    auto* flags = (int32_t*)c->flags.p;
+    auto* hyps = (out && out->hyps) ? out->hyps : (erp_hypothesis*)c->hyps.p;
+    auto* tv = (out && out->tvec) ? out->tvec : (float*)c->tv.p;
+    auto* tmean = (out && out->dist) ? out->dist : (double*)c->tmean.p;
+    {
+        StageTimer _t(ctx, ERP_STAGE_JUMP_PREP, st);
+        ERP_CK(erp::launch_jump_prep(counts, sh, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_SAMPLER_GRAM, st);
+        ERP_CK(erp::launch_sampler_gram(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
+                                        (uint32_t*)c->w0.p, (double*)c->pts.p, sh, cfg->sample_frac,
+                                        (uint16_t*)c->idx.p, (double*)c->gram.p,
+                                        out ? out->samples : nullptr, flags, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
+        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac, cfg->valid_abs, hyps,
+                                 st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_VALID_COMPACT, st);
+        ERP_CK(erp::launch_valid_compact(counts, hyps, sh, cfg->sample_frac, (float*)c->rv.p, tv,
+                                         (int32_t*)c->kcount.p, out ? out->rvec : nullptr, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_CONSENSUS_ROWS, st);
+        ERP_CK(erp::launch_consensus_rows((int32_t*)c->kcount.p, (float*)c->rv.p, sh, cfg->trim_lo,
+                                          cfg->trim_hi, tmean, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_CONSENSUS_FINAL, st);
+        ERP_CK(erp::launch_consensus_final(counts, (int32_t*)c->kcount.p, (float*)c->rv.p, tv, tmean,
+                                           flags, sh, cfg->sample_frac, cfg->trim_lo, cfg->trim_hi,
+                                           (float*)c->sortbuf.p, results, st));
+    }
+    return ERP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable) {
+    if (!ctx) return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->profiling = enable != 0;
+    return ERP_OK;
+}
+
+const char* erp_stage_name(int32_t stage) {
+    static const char* names[ERP_STAGE_COUNT] = {
+        "knn2_partial", "knn2_merge", "bearings", "jump_prep", "sampler_gram",
+        "eigen", "valid_compact", "consensus_rows", "consensus_final"};
+    return (stage >= 0 && stage < ERP_STAGE_COUNT) ? names[stage] : "unknown";
+}
+
+erp_status erp_ctx_stage_times(erp_ctx* ctx, double* total_ms, int64_t* launches) {
+    if (!ctx || !total_ms || !launches) return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    for (int k = 0; k < ERP_STAGE_COUNT; k++) {
+        total_ms[k] = 0;
+        launches[k] = 0;
+    }
+    for (const auto& r : ctx->ev_rec) {
+        ERP_CK(hipEventSynchronize(ctx->ev_pool[r.second + 1]));
+        float ms = 0;
+        ERP_CK(hipEventElapsedTime(&ms, ctx->ev_pool[r.second], ctx->ev_pool[r.second + 1]));
+        total_ms[r.first] += ms;
+        launches[r.first] += 1;
+    }
+    ctx->ev_rec.clear();
+    ctx->ev_used = 0;
+    return ERP_OK;
+}
+
+erp_status erp_ctx_reserve(erp_ctx* ctx, int32_t n_pairs, int32_t max_nq, int32_t max_nt,
+                           int32_t iters) {
+    if (!ctx || n_pairs < 1 || max_nq < 0 || max_nt < 0 || iters < 1) return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    const erp::BatchShape sh = make_shape(n_pairs, max_nq, max_nt, iters, 0.25);
+    if (!ensure(ctx->part, (size_t)n_pairs * sh.chunks * sh.max_nq * sizeof(erp::Top2)) ||
+        !ensure(ctx->matches, (size_t)n_pairs * sh.max_nq * sizeof(erp_dmatch)))
+        return ERP_OUT_OF_MEMORY;
+    return ensure_estimator(ctx, sh, nullptr);
+}
+
+erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* b, float ratio,
+                              const erp_ransac_cfg* cfg, const erp_batch_outputs* out,
+                              void* stream) {
+    if (!ctx || !b || !out || !out->results || !cfg_ok(cfg)) return ERP_INVALID_ARG;
+    if (b->n_pairs < 1 || b->dim != erp::kDim || b->max_nq < 0 || b->max_nt < 0 ||
+        b->max_nq > 65535 || !b->desc_l || !b->desc_r || !b->kp_l || !b->kp_r || !b->off_l ||
+        !b->off_r || !b->width || !b->height)
+        return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    const erp::BatchShape sh = make_shape(b->n_pairs, b->max_nq, b->max_nt, cfg->iters,
+                                          cfg->sample_frac);
+    if (!ensure(ctx->part, (size_t)sh.n_pairs * sh.chunks * sh.max_nq * sizeof(erp::Top2)))
+        return ERP_OUT_OF_MEMORY;
+    erp_dmatch* matches = out->matches;
+    if (!matches) {
+        if (!ensure(ctx->matches, (size_t)sh.n_pairs * sh.max_nq * sizeof(erp_dmatch)))
+            return ERP_OUT_OF_MEMORY;
+        matches = (erp_dmatch*)ctx->matches.p;
+    }
+    erp_status es = ensure_estimator(ctx, sh, out);
+    if (es != ERP_OK) return es;
+    es = upload_w0(ctx, cfg, st);
+    if (es != ERP_OK) return es;
+    ERP_CK(hipMemsetAsync(ctx->flags.p, 0, (size_t)sh.n_pairs * 4, st));
+    {
+        StageTimer _t(ctx, ERP_STAGE_KNN2_PARTIAL, st);
+        ERP_CK(erp::launch_knn2_partial(b->desc_l, b->desc_r, b->off_l, b->off_r, sh,
+                                        (erp::Top2*)ctx->part.p, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_KNN2_MERGE, st);
+        ERP_CK(erp::launch_knn2_merge((erp::Top2*)ctx->part.p, b->off_l, b->off_r, sh, ratio, matches,
+                                      (int32_t*)ctx->counts.p, (int32_t*)ctx->flags.p, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_BEARINGS, st);
+        ERP_CK(erp::launch_bearings_from_matches(matches, (int32_t*)ctx->counts.p, b->kp_l, b->kp_r,
+                                                 b->off_l, b->off_r, b->width, b->height, sh,
+                                                 (double*)ctx->pts.p, out->key_left, out->key_right,
+                                                 st));
+    }
+    return run_estimator(ctx, sh, cfg, out, out->results, st);
+}
+
+erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,
+                                const float* d_train, int32_t nt, int32_t dim, float ratio,
+                                erp_dmatch* d_out, int32_t* d_count, void* stream) {
+    if (!ctx || nq < 0 || nt < 0 || dim != erp::kDim || !d_out || !d_count) return ERP_INVALID_ARG;
+    if (nq > 0 && (!d_query || !d_train)) return ERP_INVALID_ARG;
+    if (nq > 0 && nt < 2) return ERP_TOO_FEW_POINTS;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (nq == 0) {
+        ERP_CK(hipMemsetAsync(d_count, 0, 4, st));
+        return ERP_OK;
+    }
+    const erp::BatchShape sh = make_shape(1, nq, nt, 1, 0.25);
+    if (!ensure(ctx->part, (size_t)sh.chunks * sh.max_nq * sizeof(erp::Top2)) ||
+        !ensure(ctx->off, 4 * sizeof(int64_t)) || !ensure(ctx->flags, 16))
+        return ERP_OUT_OF_MEMORY;
+    const int64_t offs[4] = {0, nq, 0, nt};
+    ERP_CK(hipMemcpyAsync(ctx->off.p, offs, sizeof(offs), hipMemcpyHostToDevice, st));
+    const int64_t* oq = (const int64_t*)ctx->off.p;
+    {
+        StageTimer _t(ctx, ERP_STAGE_KNN2_PARTIAL, st);
+        ERP_CK(erp::launch_knn2_partial(d_query, d_train, oq, oq + 2, sh, (erp::Top2*)ctx->part.p, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_KNN2_MERGE, st);
+        ERP_CK(erp::launch_knn2_merge((erp::Top2*)ctx->part.p, oq, oq + 2, sh, ratio, d_out, d_count,
+                                      (int32_t*)ctx->flags.p, st));
+    }
+    // offs must outlive the async copy
+    ERP_CK(hipStreamSynchronize(st));
+    return ERP_OK;
+}
+
+erp_status erp_match_two_image(erp_ctx* ctx, const float* h_desc1, int32_t n1, const float* h_desc2,
+                               int32_t n2, int32_t dim, erp_dmatch* h_out, int32_t* h_count) {
+    if (!ctx || n1 < 0 || n2 < 0 || dim != erp::kDim || !h_out || !h_count) return ERP_INVALID_ARG;
+    if (n1 > 0 && (!h_desc1 || !h_desc2)) return ERP_INVALID_ARG;
+    if (n1 > 0 && n2 < 2) return ERP_TOO_FEW_POINTS;
+    *h_count = 0;
+    if (n1 == 0) return ERP_OK;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ERP_CK(hipSetDevice(ctx->device));
+        if (!ensure(ctx->in_a, (size_t)n1 * dim * 4) || !ensure(ctx->in_b, (size_t)n2 * dim * 4) ||
+            !ensure(ctx->in_c, (size_t)n1 * sizeof(erp_dmatch) + 16))
+            return ERP_OUT_OF_MEMORY;
+        ERP_CK(hipMemcpy(ctx->in_a.p, h_desc1, (size_t)n1 * dim * 4, hipMemcpyHostToDevice));
+        ERP_CK(hipMemcpy(ctx->in_b.p, h_desc2, (size_t)n2 * dim * 4, hipMemcpyHostToDevice));
+    }
+    int32_t* d_count = (int32_t*)((char*)ctx->in_c.p + (size_t)n1 * sizeof(erp_dmatch));
+    erp_status s = erp_match_knn2_ratio(ctx, (const float*)ctx->in_a.p, n1, (const float*)ctx->in_b.p,
+                                        n2, dim, 0.3f, (erp_dmatch*)ctx->in_c.p, d_count, nullptr);
+    if (s != ERP_OK) return s;
+    ERP_CK(hipDeviceSynchronize());
+    int32_t m = 0;
+    ERP_CK(hipMemcpy(&m, d_count, 4, hipMemcpyDeviceToHost));
+    if (m > 0) ERP_CK(hipMemcpy(h_out, ctx->in_c.p, (size_t)m * sizeof(erp_dmatch), hipMemcpyDeviceToHost));
+    *h_count = m;
+    return ERP_OK;
+}
+
+erp_status erp_eight_point_find_dev(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* d_kl,
+                                    const erp_point2f* d_kr, int32_t m, const erp_ransac_cfg* cfg,
+                                    erp_pair_result* d_result, erp_hypothesis* d_hyps,
+                                    void* stream) {
+    if (!ctx || W <= 0 || H <= 0 || m < 0 || m > 65535 || !d_result || !cfg_ok(cfg))
+        return ERP_INVALID_ARG;
+    if (m > 0 && (!d_kl || !d_kr)) return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    const erp::BatchShape sh = make_shape(1, m, m, cfg->iters, cfg->sample_frac);
+    erp_batch_outputs out{};
+    out.results = d_result;
+    out.hyps = d_hyps;
+    erp_status es = ensure_estimator(ctx, sh, &out);
+    if (es != ERP_OK) return es;
+    es = upload_w0(ctx, cfg, st);
+    if (es != ERP_OK) return es;
+    ERP_CK(hipMemsetAsync(ctx->flags.p, 0, 4, st));
+    ERP_CK(hipMemcpyAsync(ctx->counts.p, &m, 4, hipMemcpyHostToDevice, st));
+    {
+        StageTimer _t(ctx, ERP_STAGE_BEARINGS, st);
+        ERP_CK(erp::launch_bearings_direct(d_kl, d_kr, m, W, H, (double*)ctx->pts.p, st));
+    }
+    es = run_estimator(ctx, sh, cfg, &out, d_result, st);
+    if (es != ERP_OK) return es;
+    ERP_CK(hipStreamSynchronize(st));  // m lives on the caller's stack
+    return ERP_OK;
+}
+
+erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* h_kl,
+                                const erp_point2f* h_kr, int32_t m, const erp_ransac_cfg* cfg,
+                                float R_out[3], float T_out[3], erp_pair_result* h_result) {
+    if (!ctx || m < 0 || (m > 0 && (!h_kl || !h_kr))) return ERP_INVALID_ARG;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ERP_CK(hipSetDevice(ctx->device));
+        if (!ensure(ctx->in_a, (size_t)m * 8 + 8) || !ensure(ctx->in_b, (size_t)m * 8 + 8) ||
+            !ensure(ctx->in_c, sizeof(erp_pair_result)))
+            return ERP_OUT_OF_MEMORY;
+        if (m > 0) {
+            ERP_CK(hipMemcpy(ctx->in_a.p, h_kl, (size_t)m * 8, hipMemcpyHostToDevice));
+            ERP_CK(hipMemcpy(ctx->in_b.p, h_kr, (size_t)m * 8, hipMemcpyHostToDevice));
+        }
+    }
+    erp_status s = erp_eight_point_find_dev(ctx, W, H, (const erp_point2f*)ctx->in_a.p,
+                                            (const erp_point2f*)ctx->in_b.p, m, cfg,
+                                            (erp_pair_result*)ctx->in_c.p, nullptr, nullptr);
+    if (s != ERP_OK) return s;
+    erp_pair_result r;
+    ERP_CK(hipMemcpy(&r, ctx->in_c.p, sizeof(r), hipMemcpyDeviceToHost));
+    if (h_result) *h_result = r;
+    if (R_out)
+        for (int k = 0; k < 3; k++) R_out[k] = r.R[k];
+    if (T_out)
+        for (int k = 0; k < 3; k++) T_out[k] = r.T[k];
+    return (erp_status)r.status;
+}
+
+erp_status erp_initial_guess(erp_ctx* ctx, const double* h_bl, const double* h_br, int32_t m,
+                             const erp_ransac_cfg* cfg, float R_out[3], float T_out[3],
+                             erp_pair_result* h_result) {
+    if (!ctx || m < 0 || m > 65535 || (m > 0 && (!h_bl || !h_br)) || !cfg_ok(cfg))
+        return ERP_INVALID_ARG;
+    erp_pair_result r;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        ERP_CK(hipSetDevice(ctx->device));
+        const erp::BatchShape sh = make_shape(1, m, m, cfg->iters, cfg->sample_frac);
+        erp_status es = ensure_estimator(ctx, sh, nullptr);
+        if (es != ERP_OK) return es;
+        if (!ensure(ctx->in_c, sizeof(erp_pair_result))) return ERP_OUT_OF_MEMORY;
+        es = upload_w0(ctx, cfg, nullptr);
+        if (es != ERP_OK) return es;
+        std::vector<double> pts((size_t)std::max(m, 1) * 6);
+        for (int32_t i = 0; i < m; i++)
+            for (int k = 0; k < 3; k++) {
+                pts[(size_t)i * 6 + k] = h_bl[(size_t)i * 3 + k];
+                pts[(size_t)i * 6 + 3 + k] = h_br[(size_t)i * 3 + k];
+            }
+        ERP_CK(hipMemcpy(ctx->pts.p, pts.data(), (size_t)m * 48, hipMemcpyHostToDevice));
+        ERP_CK(hipMemcpy(ctx->counts.p, &m, 4, hipMemcpyHostToDevice));
+        ERP_CK(hipMemset(ctx->flags.p, 0, 4));
+        es = run_estimator(ctx, sh, cfg, nullptr, (erp_pair_result*)ctx->in_c.p, nullptr);
+        if (es != ERP_OK) return es;
+        ERP_CK(hipMemcpy(&r, ctx->in_c.p, sizeof(r), hipMemcpyDeviceToHost));
+    }
+    if (h_result) *h_result = r;
+    if (R_out)
+        for (int k = 0; k < 3; k++) R_out[k] = r.R[k];
+    if (T_out)
+        for (int k = 0; k < 3; k++) T_out[k] = r.T[k];
+    return (erp_status)r.status;
+}
+
+erp_status erp_eight_point_estimation(erp_ctx* ctx, const double* h_bl, const double* h_br,
+                                      int32_t m, erp_hypothesis* h_out) {
+    if (!ctx || m < 0 || !h_out || (m > 0 && (!h_bl || !h_br))) return ERP_INVALID_ARG;
+    if (m < 1) return ERP_TOO_FEW_POINTS;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    if (!ensure(ctx->in_d, (size_t)m * 48 + 36 * 8 + sizeof(erp_hypothesis) + 64)) return ERP_OUT_OF_MEMORY;
+    std::vector<double> pts((size_t)m * 6);
+    for (int32_t i = 0; i < m; i++)
+        for (int k = 0; k < 3; k++) {
+            pts[(size_t)i * 6 + k] = h_bl[(size_t)i * 3 + k];
+            pts[(size_t)i * 6 + 3 + k] = h_br[(size_t)i * 3 + k];
+        }
+    char* base = (char*)ctx->in_d.p;
+    double* d_pts = (double*)base;
+    double* d_gram = (double*)(base + (size_t)m * 48);
+    int32_t* d_cnt = (int32_t*)(base + (size_t)m * 48 + 36 * 8);
+    erp_hypothesis* d_h = (erp_hypothesis*)(base + (size_t)m * 48 + 36 * 8 + 16);
+    ERP_CK(hipMemcpy(d_pts, pts.data(), pts.size() * 8, hipMemcpyHostToDevice));
+    ERP_CK(hipMemcpy(d_cnt, &m, 4, hipMemcpyHostToDevice));
+    ERP_CK(erp::launch_gram_all(d_pts, m, d_gram, nullptr));
+    erp::BatchShape sh = make_shape(1, m, m, 1, 1.0);
+    ERP_CK(erp::launch_eigen(d_cnt, d_gram, sh, 1.0, 1.57, d_h, nullptr));
+    ERP_CK(hipMemcpy(h_out, d_h, sizeof(erp_hypothesis), hipMemcpyDeviceToHost));
+    return ERP_OK;
+}
+
+}  // extern "C"

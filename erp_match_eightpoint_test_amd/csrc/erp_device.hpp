@@ -1,0 +1,414 @@
+// erp_device.hpp -- per-hypothesis math of the eight-point estimator, written once and compiled
+// for gfx950 (inside the HIP kernels) and for the host (tests/host_math harness only, so the
+// numerics can be checked against the oracle without a GPU).  No OpenCV.
+//
+// What each function follows in the reference:
+//   gram_jacobi9      SVDecomp(A_mat, w, u, vt); e = vt.row(vt.rows-1)  src/eight_point.cpp:39-44
+//                     -- evaluated in Gram space (G = A^T A, 9x9, fp64) with the SAME cyclic
+//                        one-sided Jacobi rotation formulas/order OpenCV's JacobiSVDImpl_ applies
+//                        to the columns of A, so the right singular vectors agree up to sign.
+//   svd3_opencv       SVDecomp on 3x3 (src/eight_point.cpp:46, and inside decomposeEssentialMat)
+//                     -- OpenCV JacobiSVDImpl_ restated operation-for-operation, so the sign
+//                        conventions that decide T's sign and the R1/R2 order match.
+//   decompose_e       cv::decomposeEssentialMat (src/eight_point.cpp:54)
+//   rot2eular         src/erp_rotation.cpp:43-63
+//   pixel_to_bearing  src/eight_point.cpp:163-186
+//   estimate_from_e   src/eight_point.cpp:42-84 (rank-2 fix, decompose, Euler, validity)
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define ERP_HD __host__ __device__
+#define ERP_INLINE __forceinline__
+#else
+#include <math.h>
+#define ERP_HD
+#define ERP_INLINE inline
+#endif
+
+namespace erp {
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kDblEps = 2.2204460492503131e-16;
+constexpr double kDblMin = 2.2250738585072014e-308;
+
+struct Hyp {            // per-iteration record (parity/debug output and consensus input)
+    float R1[3], R2[3], T[3];
+    int32_t R1_valid, R2_valid;
+    double E[9];        // e = eigen/singular vector reshaped row-major (sign arbitrary)
+};
+
+// ---------------------------------------------------------------- small 3x3 helpers ----
+// cv::gemm small-matrix path: d[i][j] = a[i][0]*b[0][j] + a[i][1]*b[1][j] + a[i][2]*b[2][j]
+ERP_HD ERP_INLINE void gemm33(const double* a, const double* b, double* d) {
+    double t[9];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+            t[i * 3 + j] = a[i * 3 + 0] * b[0 * 3 + j] + a[i * 3 + 1] * b[1 * 3 + j] + a[i * 3 + 2] * b[2 * 3 + j];
+#pragma unroll
+    for (int k = 0; k < 9; k++) d[k] = t[k];
+}
+
+ERP_HD ERP_INLINE double det33(const double* m) {
+    return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
+           m[2] * (m[3] * m[7] - m[4] * m[6]);
+}
+
+ERP_HD ERP_INLINE uint32_t cv_rng_next(uint64_t& state) {
+    state = (uint64_t)(uint32_t)state * 4164903690U + (uint32_t)(state >> 32);
+    return (uint32_t)state;
+}
+
+// OpenCV 3.4 SVDecomp(src 3x3, flags=0): at == false, so At = src^T (rows = columns of src),
+// JacobiSVDImpl_<double>(At, W, Vt, m=3, n=3, n1=3, DBL_MIN, 10*DBL_EPSILON);
+// u = At^T (normalised), vt = Vt.  Operation order follows the scalar template.
+ERP_HD inline void svd3_opencv(const double* src, double* w_out, double* u, double* vt) {
+    double At[9], V[9], W[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) At[i * 3 + k] = src[k * 3 + i];
+    const double eps = kDblEps * 10;
+    const double minval = kDblMin;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const double t = At[i * 3 + k];
+            sd += t * t;
+        }
+        W[i] = sd;
+#pragma unroll
+        for (int k = 0; k < 3; k++) V[i * 3 + k] = 0;
+        V[i * 3 + i] = 1;
+    }
+    for (int iter = 0; iter < 30; iter++) {  // max_iter = max(m, 30)
+        bool changed = false;
+#pragma unroll
+        for (int pr = 0; pr < 3; pr++) {
+            const int i = pr < 2 ? 0 : 1;
+            const int j = pr == 0 ? 1 : 2;
+            double a = W[i], p = 0, b = W[j];
+#pragma unroll
+            for (int k = 0; k < 3; k++) p += At[i * 3 + k] * At[j * 3 + k];
+            if (fabs(p) <= eps * sqrt(a * b)) continue;
+            p *= 2;
+            const double beta = a - b, gamma = hypot(p, beta);
+            double c, s;
+            if (beta < 0) {
+                const double delta = (gamma - beta) * 0.5;
+                s = sqrt(delta / gamma);
+                c = p / (gamma * s * 2);
+            } else {
+                c = sqrt((gamma + beta) / (gamma * 2));
+                s = p / (gamma * c * 2);
+            }
+            a = b = 0;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const double t0 = c * At[i * 3 + k] + s * At[j * 3 + k];
+                const double t1 = -s * At[i * 3 + k] + c * At[j * 3 + k];
+                At[i * 3 + k] = t0;
+                At[j * 3 + k] = t1;
+                a += t0 * t0;
+                b += t1 * t1;
+            }
+            W[i] = a;
+            W[j] = b;
+            changed = true;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const double t0 = c * V[i * 3 + k] + s * V[j * 3 + k];
+                const double t1 = -s * V[i * 3 + k] + c * V[j * 3 + k];
+                V[i * 3 + k] = t0;
+                V[j * 3 + k] = t1;
+            }
+        }
+        if (!changed) break;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        double sd = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const double t = At[i * 3 + k];
+            sd += t * t;
+        }
+        W[i] = sqrt(sd);
+    }
+    // selection sort descending, swapping rows of At and Vt
+    for (int i = 0; i < 2; i++) {
+        int j = i;
+        for (int k = i + 1; k < 3; k++)
+            if (W[j] < W[k]) j = k;
+        if (i != j) {
+            double t = W[i];
+            W[i] = W[j];
+            W[j] = t;
+            for (int k = 0; k < 3; k++) {
+                t = At[i * 3 + k];
+                At[i * 3 + k] = At[j * 3 + k];
+                At[j * 3 + k] = t;
+                t = V[i * 3 + k];
+                V[i * 3 + k] = V[j * 3 + k];
+                V[j * 3 + k] = t;
+            }
+        }
+    }
+    uint64_t rng = 0x12345678;
+    for (int i = 0; i < 3; i++) {
+        double sd = W[i];
+        for (int ii = 0; ii < 100 && sd <= minval; ii++) {
+            const double val0 = 1. / 3;
+            for (int k = 0; k < 3; k++) At[i * 3 + k] = (cv_rng_next(rng) & 256) != 0 ? val0 : -val0;
+            for (int it2 = 0; it2 < 2; it2++) {
+                for (int j = 0; j < i; j++) {
+                    sd = 0;
+                    for (int k = 0; k < 3; k++) sd += At[i * 3 + k] * At[j * 3 + k];
+                    double asum = 0;
+                    for (int k = 0; k < 3; k++) {
+                        const double t = At[i * 3 + k] - sd * At[j * 3 + k];
+                        At[i * 3 + k] = t;
+                        asum += fabs(t);
+                    }
+                    asum = asum > eps * 100 ? 1 / asum : 0;
+                    for (int k = 0; k < 3; k++) At[i * 3 + k] *= asum;
+                }
+            }
+            sd = 0;
+            for (int k = 0; k < 3; k++) {
+                const double t = At[i * 3 + k];
+                sd += t * t;
+            }
+            sd = sqrt(sd);
+        }
+        const double s = sd > minval ? 1 / sd : 0.;
+#pragma unroll
+        for (int k = 0; k < 3; k++) At[i * 3 + k] *= s;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; i++) w_out[i] = W[i];
+    // u = transpose(temp_u): u[r][c] = At[c][r]
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) u[r * 3 + c] = At[c * 3 + r];
+#pragma unroll
+    for (int k = 0; k < 9; k++) vt[k] = V[k];
+}
+
+// cv::decomposeEssentialMat restated
+ERP_HD inline void decompose_e(const double* E, double* R1, double* R2, double* t) {
+    double D[3], U[9], Vt[9];
+    svd3_opencv(E, D, U, Vt);
+    if (det33(U) < 0)
+#pragma unroll
+        for (int k = 0; k < 9; k++) U[k] *= -1.;
+    if (det33(Vt) < 0)
+#pragma unroll
+        for (int k = 0; k < 9; k++) Vt[k] *= -1.;
+    const double Wm[9] = {0, 1, 0, -1, 0, 0, 0, 0, 1};
+    const double Wt[9] = {0, -1, 0, 1, 0, 0, 0, 0, 1};
+    double tmp[9];
+    gemm33(U, Wm, tmp);
+    gemm33(tmp, Vt, R1);
+    gemm33(U, Wt, tmp);
+    gemm33(tmp, Vt, R2);
+    t[0] = U[2] * 1.0;
+    t[1] = U[5] * 1.0;
+    t[2] = U[8] * 1.0;
+}
+
+ERP_HD ERP_INLINE void rot2eular(const double* R, double* e) {
+    const double sy = sqrt(R[8] * R[8] + R[5] * R[5]);
+    const bool singular = sy < 1e-6;
+    if (!singular) {
+        e[0] = atan2(-R[5], R[8]);
+        e[1] = atan2(R[2], sy);
+        e[2] = atan2(-R[1], R[0]);
+    } else {
+        e[0] = 0;
+        e[1] = atan2(R[2], sy);
+        e[2] = atan2(-R[1], R[0]);
+    }
+}
+
+// eight_point::find pixel -> bearing: lon = 2*M_PI*(pt.x / im_width) with the division in
+// float, lat likewise; OMAF axes.
+ERP_HD ERP_INLINE void pixel_to_bearing(int32_t W, int32_t H, float px, float py, double* b) {
+    const float fx = px / (float)W;
+    const float fy = py / (float)H;
+    const double lon = 2 * kPi * (double)fx;
+    const double lat = kPi * (double)fy;
+    const double sl = sin(lat);
+    b[0] = -sl * cos(lon);
+    b[1] = sl * sin(lon);
+    b[2] = cos(lat);
+}
+
+ERP_HD ERP_INLINE double max_vec(const float* v) {
+    if ((v[0] > v[1]) && (v[0] > v[2])) return v[0];
+    else if (v[1] > v[2])
+        return v[1];
+    else
+        return v[2];
+}
+
+// Rank-2 correction, decomposition, Euler conversion and validity
+// (src/eight_point.cpp:42-84).  e: 9-vector (E row-major, sign irrelevant: every step below is
+// odd in E and decomposeEssentialMat's det fixes cancel the sign exactly).
+ERP_HD inline void estimate_from_e(const double* e, double valid_abs, Hyp& h) {
+    double wf[3], uf[9], vtf[9];
+    svd3_opencv(e, wf, uf, vtf);
+    wf[2] = 0.0;
+    const double wd[9] = {wf[0], 0, 0, 0, wf[1], 0, 0, 0, wf[2]};
+    double tmp[9], Ec[9];
+    gemm33(uf, wd, tmp);
+    gemm33(tmp, vtf, Ec);
+    double R1[9], R2[9], t[3];
+    decompose_e(Ec, R1, R2, t);
+    double e1[3], e2[3];
+    rot2eular(R1, e1);
+    rot2eular(R2, e2);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        h.R1[k] = (float)e1[k];
+        h.R2[k] = (float)e2[k];
+        h.T[k] = (float)t[k];
+    }
+    const float a1[3] = {fabsf(h.R1[0]), fabsf(h.R1[1]), fabsf(h.R1[2])};
+    const float a2[3] = {fabsf(h.R2[0]), fabsf(h.R2[1]), fabsf(h.R2[2])};
+    h.R1_valid = max_vec(a1) < valid_abs;
+    h.R2_valid = max_vec(a2) < valid_abs;
+#pragma unroll
+    for (int k = 0; k < 9; k++) h.E[k] = e[k];
+}
+
+// ------------------------------------------------------------ Gram-space Jacobi (9x9) ----
+// G index of the 36 distinct Gram values: A column a = 3*i + j holds l_i * r_j, so
+//   G[a][b] = sum_p (l_i l_k)(r_j r_l)  with a = (i,j), b = (k,l)
+// = LL[u(i,k)] * RR[u(j,l)] summed, u(.,.) the index of the unordered pair in
+// {00,01,02,11,12,22}.  gram36[6*u1 + u2] = sum_p LL_p[u1] * RR_p[u2].
+ERP_HD ERP_INLINE int sym3(int i, int k) {
+    // 00->0 01->1 02->2 11->3 12->4 22->5
+    const int a = i < k ? i : k, b = i < k ? k : i;
+    return a == 0 ? b : (a == 1 ? 2 + b : 5);
+}
+
+ERP_HD ERP_INLINE void gram36_to_full(const double* g36, double* G) {
+#pragma unroll
+    for (int a = 0; a < 9; a++)
+#pragma unroll
+        for (int b = 0; b < 9; b++) {
+            const int i = a / 3, j = a % 3, k = b / 3, l = b % 3;
+            G[a * 9 + b] = g36[6 * sym3(i, k) + sym3(j, l)];
+        }
+}
+
+// Cyclic Jacobi on the symmetric Gram matrix, mirroring OpenCV's one-sided Jacobi on A's
+// columns: pair order (i<j row by row), angle from (a=G_ii, b=G_jj, p=G_ij) with the same
+// formulas, Vt rows rotated the same way, then rows sorted by sqrt(G_ii) descending.
+// Returns in `e` the Vt row index min(s,9)-1 (thin SVD rule of _SVDcompute for s < 9).
+// Convergence: OpenCV's |p| <= 10*eps*sqrt(a*b), plus an absolute floor of
+// 4*eps*trace(G) that the Gram formulation needs (rounding noise of size eps*||G|| would
+// otherwise keep re-rotating exact null directions).
+ERP_HD inline void gram_jacobi9(const double* G_in, int32_t s, double* e) {
+    double G[81], V[81];
+#pragma unroll
+    for (int k = 0; k < 81; k++) {
+        G[k] = G_in[k];
+        V[k] = (k % 10) == 0 ? 1.0 : 0.0;
+    }
+    double tr = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) tr += G[i * 10];
+    const double eps = kDblEps * 10;
+    const double floor_abs = 4 * kDblEps * tr;
+    for (int sweep = 0; sweep < 40; sweep++) {
+        bool changed = false;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+#pragma unroll
+            for (int j = i + 1; j < 9; j++) {
+                const double a = G[i * 9 + i], b = G[j * 9 + j], p = G[i * 9 + j];
+                const double ap = fabs(p);
+                if (ap <= eps * sqrt(fabs(a * b)) || ap <= floor_abs) continue;
+                const double p2 = 2 * p;
+                const double beta = a - b, gamma = hypot(p2, beta);
+                double c, s;
+                if (beta < 0) {
+                    const double delta = (gamma - beta) * 0.5;
+                    s = sqrt(delta / gamma);
+                    c = p2 / (gamma * s * 2);
+                } else {
+                    c = sqrt((gamma + beta) / (gamma * 2));
+                    s = p2 / (gamma * c * 2);
+                }
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    if (k == i || k == j) continue;
+                    const double gik = G[i * 9 + k], gjk = G[j * 9 + k];
+                    const double ni = c * gik + s * gjk;
+                    const double nj = -s * gik + c * gjk;
+                    G[i * 9 + k] = ni;
+                    G[k * 9 + i] = ni;
+                    G[j * 9 + k] = nj;
+                    G[k * 9 + j] = nj;
+                }
+                const double cs2p = 2 * c * s * p;
+                G[i * 9 + i] = c * c * a + cs2p + s * s * b;
+                G[j * 9 + j] = s * s * a - cs2p + c * c * b;
+                G[i * 9 + j] = 0;
+                G[j * 9 + i] = 0;
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    const double vi = V[i * 9 + k], vj = V[j * 9 + k];
+                    V[i * 9 + k] = c * vi + s * vj;
+                    V[j * 9 + k] = -s * vi + c * vj;
+                }
+                changed = true;
+            }
+        }
+        if (!changed) break;
+    }
+    // W = sqrt(diag), selection order of JacobiSVDImpl_ (first maximum), keep only the
+    // permutation (rows of V are not moved: we track the index instead).
+    double W[9];
+    int order[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        const double d = G[i * 10];
+        W[i] = sqrt(d > 0 ? d : 0);
+        order[i] = i;
+    }
+    for (int i = 0; i < 8; i++) {
+        int j = i;
+        for (int k = i + 1; k < 9; k++)
+            if (W[j] < W[k]) j = k;
+        if (i != j) {
+            const double t = W[i];
+            W[i] = W[j];
+            W[j] = t;
+            const int o = order[i];
+            order[i] = order[j];
+            order[j] = o;
+        }
+    }
+    const int rows = s < 9 ? s : 9;
+    const int sel = order[rows - 1];
+    // dynamic row select without dynamic register indexing
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        double v = 0;
+#pragma unroll
+        for (int r = 0; r < 9; r++) v = (r == sel) ? V[r * 9 + k] : v;
+        e[k] = v;
+    }
+}
+
+}  // namespace erp

@@ -1,0 +1,87 @@
+// erp_kernels.hpp -- launchers of the gfx950 kernels (implemented in kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/erp_match.h"
+
+namespace erp {
+
+constexpr int kDim = 64;          // SURF descriptor length (extended=false)
+constexpr int kMaxQ = 24;         // jump polynomials x^(64(M-1)2^k): waves per pair < 2^24
+constexpr int kPolyWords = 31;    // glibc TYPE_3 degree
+
+struct Top2 {                     // partial k=2 result of one train chunk for one query
+    float d0;                     // best squared distance
+    int32_t j0;                   // its train index (lowest index among ties)
+    float d1;                     // second squared distance
+};
+
+// scratch the pipeline needs for one batch (all device pointers, sized by the context)
+struct Workspace {
+    Top2* part;                   // [pairs][chunks][max_nq]
+    erp_dmatch* matches;          // [pairs][max_nq]
+    int32_t* counts;              // [pairs] M
+    double* pts;                  // [pairs][max_nq][6] bearings (l, r)
+    uint32_t* polyR;              // [pairs][65][31]  x^(l(M-1)) mod P
+    uint32_t* polyQ;              // [pairs][kMaxQ][31]
+    uint16_t* idx;                // [pairs][iters_pad][max_s] sample lists (wave-interleaved)
+    double* gram;                 // [pairs][iters][36]
+    erp_hypothesis* hyps;         // [pairs][iters]
+    float* rv;                    // [pairs][3][2*iters] valid R (SoA)
+    float* tv;                    // [pairs][2*iters][3] their T
+    int32_t* kcount;              // [pairs]
+    double* tmean;                // [pairs][2*iters]
+    float* sortbuf;               // [pairs][2*iters] exact tie resolution scratch
+    int32_t* flags;               // [pairs] internal error flags
+};
+
+struct BatchShape {
+    int n_pairs;
+    int max_nq, max_nt;
+    int chunks, chunk_len;
+    int iters;
+    int max_s;                    // (int)(max_nq * sample_frac)
+    int idx_stride;               // words of one hypothesis list in idx (>= max_s)
+};
+
+void init_constants();            // reduction table for the jump polynomials (once per device)
+
+hipError_t launch_knn2_partial(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                               const int64_t* off_t, const BatchShape& sh, Top2* part,
+                               hipStream_t st);
+hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
+                             const BatchShape& sh, float ratio, erp_dmatch* matches,
+                             int32_t* counts, int32_t* flags, hipStream_t st);
+hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t* counts,
+                                        const erp_point2f* kp_l, const erp_point2f* kp_r,
+                                        const int64_t* off_l, const int64_t* off_r,
+                                        const int32_t* width, const int32_t* height,
+                                        const BatchShape& sh, double* pts, erp_point2f* key_l,
+                                        erp_point2f* key_r, hipStream_t st);
+hipError_t launch_bearings_direct(const erp_point2f* kl, const erp_point2f* kr, int32_t m,
+                                  int32_t W, int32_t H, double* pts, hipStream_t st);
+hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_t* polyR,
+                            uint32_t* polyQ, hipStream_t st);
+hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
+                               const uint32_t* w0, const double* pts, const BatchShape& sh,
+                               double sample_frac, uint16_t* idx, double* gram, int32_t* samples,
+                               int32_t* flags, hipStream_t st);
+hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
+                        double sample_frac, double valid_abs, erp_hypothesis* hyps,
+                        hipStream_t st);
+hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyps,
+                                const BatchShape& sh, double sample_frac, float* rv, float* tv,
+                                int32_t* kcount, float* rv_aos, hipStream_t st);
+hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream_t st);
+hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const BatchShape& sh,
+                                 double trim_lo, double trim_hi, double* tmean, hipStream_t st);
+hipError_t launch_consensus_final(const int32_t* counts, const int32_t* kcount, const float* rv,
+                                  const float* tv, const double* tmean, const int32_t* flags,
+                                  const BatchShape& sh, double sample_frac, double trim_lo,
+                                  double trim_hi, float* sortbuf, erp_pair_result* results,
+                                  hipStream_t st);
+int sortbuf_len(int iters);        // power of two >= 2*iters (exact tie re-scoring scratch)
+
+}  // namespace erp

@@ -1,0 +1,1038 @@
+// kernels.hip -- gfx950 kernels of the ERP matcher + spherical eight-point hot path.
+//
+// Compiled with -ffp-contract=off: every f32 expression that must round like the reference
+// (flann::L2 accumulation, ratio test, consensus distances) is written in the reference's
+// order and must not be fused; FMA is used only where written explicitly (__builtin_fma in
+// the fp64 Gram accumulation, which is parity-checked by tolerance).
+//
+// Stage                    reference                                   kernel
+// exact k=2 + ratio        src/feature_matcher.cpp:42-59               knn2_partial / knn2_merge
+// gather + pixel->bearing  src/spherical_surf.cpp:155-162,
+//                          src/eight_point.cpp:163-186                 bearings_*
+// random_array sampler     src/eight_point.hpp:30-59 (glibc replay)    jump_prep / sampler_gram
+// A^T A of the sample      src/eight_point.cpp:22-39                   sampler_gram
+// SVD, rank 2, decompose   src/eight_point.cpp:39-84                   eigen
+// push valid R1/R2         src/eight_point.cpp:113-126                 valid_compact
+// trimmed-mean consensus   src/eight_point.cpp:129-149                 consensus_rows / _final
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include "erp_device.hpp"
+#include "erp_kernels.hpp"
+
+namespace erp {
+
+namespace {
+
+constexpr float kInf = __builtin_huge_valf();
+
+// x^(31+d) mod (x^31 - x^28 - 1), d = 0..29: reduction of a 61-coefficient product
+__constant__ uint32_t c_red[30][31];
+
+__device__ __forceinline__ int wave_lane() { return threadIdx.x & 63; }
+
+// exclusive scan over a block of BLOCK threads (BLOCK multiple of 64, <= 1024)
+template <int BLOCK>
+__device__ int block_exclusive_scan(int v, int* ws, int* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        int t = lane < BLOCK / 64 ? ws[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < BLOCK / 64; o <<= 1) {
+            const int y = __shfl_up(t, o, 64);
+            if (lane >= o) t += y;
+        }
+        if (lane < BLOCK / 64) ws[lane] = t;
+    }
+    __syncthreads();
+    const int base = wid ? ws[wid - 1] : 0;
+    *total = ws[BLOCK / 64 - 1];
+    __syncthreads();
+    return base + x - v;
+}
+
+// ===================================================================== matcher =========
+// One thread = one query descriptor held in VGPRs (64 f32); a 64-row tile of train
+// descriptors is staged in LDS and read as wave-uniform (broadcast) float4s.  Distance in the
+// flann::L2<float> order: per group of 4, acc += d0*d0 + d1*d1 + d2*d2 + d3*d3 (no FMA).
+// Each block covers 256 queries x one train chunk; knn2_merge folds the chunks in order.
+__global__ __launch_bounds__(256) void knn2_partial_kernel(const float* __restrict__ dq,
+                                                           const float* __restrict__ dt,
+                                                           const int64_t* __restrict__ off_q,
+                                                           const int64_t* __restrict__ off_t,
+                                                           int chunk_len, int chunks, int max_nq,
+                                                           Top2* __restrict__ part) {
+    __shared__ float4 tile[64 * 16];
+    const int p = blockIdx.z;
+    const int64_t qbase = off_q[p];
+    const int nq = (int)(off_q[p + 1] - qbase);
+    const int64_t tbase = off_t[p];
+    const int nt = (int)(off_t[p + 1] - tbase);
+    const int q0 = blockIdx.x * 256;
+    const int t0 = blockIdx.y * chunk_len;
+    if (q0 >= nq || t0 >= nt) return;
+    const int t1 = min(t0 + chunk_len, nt);
+    const int q = q0 + threadIdx.x;
+    const bool qv = q < nq;
+    float4 qr[16];
+    const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + (qv ? q : 0)) * kDim);
+#pragma unroll
+    for (int c = 0; c < 16; c++) qr[c] = qp[c];
+    float b0 = kInf, b1 = kInf;
+    int j0 = -1;
+    for (int tt = t0; tt < t1; tt += 64) {
+        const int n = min(64, t1 - tt);
+        __syncthreads();
+        const float4* tp = reinterpret_cast<const float4*>(dt + (tbase + tt) * kDim);
+        for (int k = threadIdx.x; k < n * 16; k += 256) tile[k] = tp[k];
+        __syncthreads();
+        for (int v = 0; v < n; v++) {
+            float acc = 0.f;
+#pragma unroll
+            for (int c = 0; c < 16; c++) {
+                const float4 tv = tile[v * 16 + c];
+                const float d0 = qr[c].x - tv.x;
+                const float d1 = qr[c].y - tv.y;
+                const float d2 = qr[c].z - tv.z;
+                const float d3 = qr[c].w - tv.w;
+                acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+            }
+            if (acc < b0) {
+                b1 = b0;
+                b0 = acc;
+                j0 = tt + v;
+            } else if (acc < b1) {
+                b1 = acc;
+            }
+        }
+    }
+    if (qv) part[((size_t)p * chunks + blockIdx.y) * max_nq + q] = Top2{b0, j0, b1};
+}
+
+// Fold chunk partials in train order (lowest index wins ties), apply the ratio test
+// d0 < ratio * d1 on the sqrt'd distances (convertToDMatches + feature_matcher.cpp:52), and
+// compact the survivors in ascending queryIdx order.  One block (1024 threads) per pair.
+__device__ __forceinline__ void merge_query(const Top2* part, size_t stride, int nch, int q,
+                                            float& B0, int& J, float& B1) {
+    B0 = kInf;
+    B1 = kInf;
+    J = -1;
+    for (int c = 0; c < nch; c++) {
+        const Top2 t = part[(size_t)c * stride + q];
+        if (t.d0 < B0) {
+            B1 = fminf(B0, t.d1);
+            B0 = t.d0;
+            J = t.j0;
+        } else {
+            B1 = fminf(B1, t.d0);
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void knn2_merge_kernel(const Top2* __restrict__ part,
+                                                          const int64_t* __restrict__ off_q,
+                                                          const int64_t* __restrict__ off_t,
+                                                          int chunk_len, int chunks, int max_nq,
+                                                          float ratio, erp_dmatch* __restrict__ out,
+                                                          int32_t* __restrict__ counts,
+                                                          int32_t* __restrict__ flags) {
+    __shared__ int ws[16];
+    const int p = blockIdx.x;
+    const int nq = (int)(off_q[p + 1] - off_q[p]);
+    const int nt = (int)(off_t[p + 1] - off_t[p]);
+    if (nt < 2 || nq <= 0) {
+        if (threadIdx.x == 0) {
+            counts[p] = 0;
+            if (nq > 0) flags[p] |= 1;  // knn_matches[i][1] would not exist (UB in the reference)
+        }
+        return;
+    }
+    const int nch = (nt + chunk_len - 1) / chunk_len;
+    const Top2* pp = part + (size_t)p * chunks * max_nq;
+    const int per = (nq + 1023) / 1024;
+    const int qa = min(nq, (int)threadIdx.x * per), qb = min(nq, qa + per);
+    int cnt = 0;
+    for (int q = qa; q < qb; q++) {
+        float B0, B1;
+        int J;
+        merge_query(pp, (size_t)max_nq, nch, q, B0, J, B1);
+        const float d0 = __builtin_sqrtf(B0), d1 = __builtin_sqrtf(B1);
+        cnt += (d0 < ratio * d1) ? 1 : 0;
+    }
+    int total;
+    int pos = block_exclusive_scan<1024>(cnt, ws, &total);
+    erp_dmatch* o = out + (size_t)p * max_nq;
+    for (int q = qa; q < qb; q++) {
+        float B0, B1;
+        int J;
+        merge_query(pp, (size_t)max_nq, nch, q, B0, J, B1);
+        const float d0 = __builtin_sqrtf(B0), d1 = __builtin_sqrtf(B1);
+        if (d0 < ratio * d1) o[pos++] = erp_dmatch{q, J, 0, d0};
+    }
+    if (threadIdx.x == 0) counts[p] = total;
+}
+
+// ============================================================== gather + bearings =======
+__global__ void bearings_from_matches_kernel(const erp_dmatch* __restrict__ matches,
+                                             const int32_t* __restrict__ counts,
+                                             const erp_point2f* __restrict__ kp_l,
+                                             const erp_point2f* __restrict__ kp_r,
+                                             const int64_t* __restrict__ off_l,
+                                             const int64_t* __restrict__ off_r,
+                                             const int32_t* __restrict__ width,
+                                             const int32_t* __restrict__ height, int max_nq,
+                                             double* __restrict__ pts, erp_point2f* key_l,
+                                             erp_point2f* key_r) {
+    const int p = blockIdx.y;
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= counts[p]) return;
+    const erp_dmatch dm = matches[(size_t)p * max_nq + m];
+    const erp_point2f kl = kp_l[off_l[p] + dm.queryIdx];
+    const erp_point2f kr = kp_r[off_r[p] + dm.trainIdx];
+    double* o = pts + ((size_t)p * max_nq + m) * 6;
+    pixel_to_bearing(width[p], height[p], kl.x, kl.y, o);
+    pixel_to_bearing(width[p], height[p], kr.x, kr.y, o + 3);
+    if (key_l) key_l[(size_t)p * max_nq + m] = kl;
+    if (key_r) key_r[(size_t)p * max_nq + m] = kr;
+}
+
+__global__ void bearings_direct_kernel(const erp_point2f* __restrict__ kl,
+                                       const erp_point2f* __restrict__ kr, int m, int W, int H,
+                                       double* __restrict__ pts) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    pixel_to_bearing(W, H, kl[i].x, kl[i].y, pts + (size_t)i * 6);
+    pixel_to_bearing(W, H, kr[i].x, kr[i].y, pts + (size_t)i * 6 + 3);
+}
+
+// ============================================================ glibc jump-ahead ==========
+// glibc TYPE_3: r[n+31] = r[n+28] + r[n] (mod 2^32), so x^d mod P(x) = x^31 - x^28 - 1 maps a
+// 31-word window r[n..n+30] to r[n+d..n+d+30].  One wave per pair computes
+//   R_l = x^(l(M-1)) (l = 0..64) and Q_k = x^(64(M-1) 2^k),
+// the hops from a wave's first hypothesis to each lane's hypothesis and between waves.
+__device__ void pmul(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t* tmp) {
+    const int lane = wave_lane();
+    if (lane < 61) {
+        const int lo = lane > 30 ? lane - 30 : 0, hi = lane < 30 ? lane : 30;
+        uint32_t c = 0;
+        for (int i = lo; i <= hi; i++) c += a[i] * b[lane - i];
+        tmp[lane] = c;
+    }
+    __syncthreads();
+    if (lane < 31) {
+        uint32_t acc = tmp[lane];
+#pragma unroll
+        for (int d = 0; d < 30; d++) acc += tmp[31 + d] * c_red[d][lane];
+        out[lane] = acc;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(64) void jump_prep_kernel(const int32_t* __restrict__ counts,
+                                                       double sample_frac, int nq_needed,
+                                                       uint32_t* __restrict__ polyR,
+                                                       uint32_t* __restrict__ polyQ) {
+    __shared__ uint32_t res[32], base[32], r1[32], t2[32], tmp[64];
+    const int p = blockIdx.x, lane = wave_lane();
+    const int M = counts[p];
+    if ((int)(M * sample_frac) < 1 || M < 2) return;
+    if (lane < 31) {
+        res[lane] = lane == 0 ? 1u : 0u;
+        base[lane] = lane == 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    uint32_t e = (uint32_t)(M - 1);
+    while (e) {
+        if (e & 1u) {
+            pmul(res, base, t2, tmp);
+            if (lane < 31) res[lane] = t2[lane];
+            __syncthreads();
+        }
+        e >>= 1;
+        if (e) {
+            pmul(base, base, t2, tmp);
+            if (lane < 31) base[lane] = t2[lane];
+            __syncthreads();
+        }
+    }
+    uint32_t* R = polyR + (size_t)p * 65 * 31;
+    if (lane < 31) {
+        R[lane] = lane == 0 ? 1u : 0u;
+        R[31 + lane] = res[lane];
+        r1[lane] = res[lane];
+    }
+    __syncthreads();
+    for (int l = 2; l <= 64; l++) {
+        pmul(res, r1, t2, tmp);
+        if (lane < 31) {
+            res[lane] = t2[lane];
+            R[l * 31 + lane] = t2[lane];
+        }
+        __syncthreads();
+    }
+    uint32_t* Q = polyQ + (size_t)p * kMaxQ * 31;
+    for (int k = 0; k < nq_needed; k++) {
+        if (k > 0) {
+            pmul(res, res, t2, tmp);
+            if (lane < 31) res[lane] = t2[lane];
+            __syncthreads();
+        }
+        if (lane < 31) Q[k * 31 + lane] = res[lane];
+    }
+}
+
+// window (31 words in win[]) -> apply polynomial c: win <- x^d window.  ext: 61 words scratch.
+__device__ void apply_coop(const uint32_t* __restrict__ c, uint32_t* win, uint32_t* ext) {
+    const int lane = wave_lane();
+    if (lane < 31) ext[lane] = win[lane];
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t t[61];
+#pragma unroll
+        for (int k = 0; k < 31; k++) t[k] = ext[k];
+#pragma unroll
+        for (int d = 31; d < 61; d++) {
+            t[d] = t[d - 3] + t[d - 31];
+            ext[d] = t[d];
+        }
+    }
+    __syncthreads();
+    uint32_t acc = 0;
+    if (lane < 31) {
+#pragma unroll
+        for (int j = 0; j < 31; j++) acc += c[j] * ext[lane + j];
+    }
+    __syncthreads();
+    if (lane < 31) win[lane] = acc;
+    __syncthreads();
+}
+
+// ====================================================== sampler + Gram accumulation =====
+// One lane = one initial_guess iteration h (src/eight_point.cpp:99-112).  The reference
+// shuffles iota(M) with M-1 rand() calls (libstdc++ random_shuffle) and keeps the first
+// sample_n entries.  Here the same draws are replayed BACKWARDS from the hypothesis's end
+// window (glibc's recurrence runs backwards just as cheaply: r[n-31] = r[n] - r[n-3]), which
+// lets the final prefix SET be decided with an s-bit bitmap per lane instead of an M-entry
+// array:
+//   steps i >= s: i stays in the prefix iff it is the LAST hit on position j_i < s;
+//   steps i <  s: track the set T of prefix positions whose value is still unresolved
+//                 (initially the positions never hit by a step >= s); reverse step i emits i
+//                 iff j_i is in T, and then T[j_i] := T[i].
+// The emitted indices (exactly s of them) are written to a per-lane list, then the lane
+// accumulates the 36 distinct Gram values sum (l l^T)_(ik) (r r^T)_(jl) of its rows in fp64.
+__global__ __launch_bounds__(64) void sampler_gram_kernel(
+    const int32_t* __restrict__ counts, const uint32_t* __restrict__ polyR,
+    const uint32_t* __restrict__ polyQ, const uint32_t* __restrict__ w0,
+    const double* __restrict__ pts, int max_nq, int iters, int nwaves, int idx_stride,
+    double sample_frac, uint16_t* __restrict__ idx, double* __restrict__ gram,
+    int32_t* __restrict__ samples, int32_t* __restrict__ flags) {
+    extern __shared__ uint32_t shm[];
+    uint32_t* win = shm;        // 32
+    uint32_t* ext = shm + 32;   // 64
+    uint32_t* bm = shm + 96;    // [nwords][64]
+    const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || M < 2) return;
+    const int h = w * 64 + lane;
+    const int nwords = (s + 31) >> 5;
+    for (int k = 0; k < nwords; k++) bm[k * 64 + lane] = 0u;
+    if (lane < 31) win[lane] = w0[lane];
+    __syncthreads();
+    const uint32_t* Q = polyQ + (size_t)p * kMaxQ * 31;
+    for (int k = 0; k < kMaxQ && (w >> k); k++)
+        if ((w >> k) & 1) apply_coop(Q + k * 31, win, ext);
+    // extend the wave's base window to 61 words
+    if (lane < 31) ext[lane] = win[lane];
+    __syncthreads();
+    if (lane == 0) {
+        uint32_t t[61];
+#pragma unroll
+        for (int k = 0; k < 31; k++) t[k] = ext[k];
+#pragma unroll
+        for (int d = 31; d < 61; d++) {
+            t[d] = t[d - 3] + t[d - 31];
+            ext[d] = t[d];
+        }
+    }
+    __syncthreads();
+    // this lane's END window: x^((lane+1)(M-1)) applied to the wave base
+    uint32_t ring[31];
+    {
+        const uint32_t* R = polyR + ((size_t)p * 65 + (lane + 1)) * 31;
+        uint32_t c[31];
+#pragma unroll
+        for (int j = 0; j < 31; j++) c[j] = R[j];
+#pragma unroll
+        for (int t = 0; t < 31; t++) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < 31; j++) acc += c[j] * ext[t + j];
+            ring[t] = acc;
+        }
+    }
+    uint16_t* my = idx + ((size_t)p * nwaves + w) * (size_t)idx_stride * 64 + lane;
+    int emitted = 0;
+    int i = M - 1;
+    uint32_t cur = 0;
+    int curw = -1;
+    while (i >= 1) {
+#pragma unroll
+        for (int u = 0; u < 31; u++) {
+            if (i >= 1) {
+                const int slot = 30 - u;
+                const uint32_t rv = ring[slot];
+                ring[slot] = rv - ring[(slot + 28) % 31];
+                const uint32_t x = rv >> 1;
+                const uint32_t j = x % (uint32_t)(i + 1);
+                bool em = false;
+                if (i >= s) {
+                    if (j < (uint32_t)s) {
+                        const uint32_t bit = 1u << (j & 31);
+                        const uint32_t old = atomicOr(&bm[(j >> 5) * 64 + lane], bit);
+                        em = !(old & bit);
+                    }
+                } else {
+                    const int wi = i >> 5;
+                    if (wi != curw) {
+                        cur = bm[wi * 64 + lane];
+                        curw = wi;
+                    }
+                    const bool bT = !((cur >> (i & 31)) & 1u);
+                    if ((int)j == i) {
+                        em = bT;
+                    } else {
+                        const uint32_t bit = 1u << (j & 31);
+                        uint32_t* wp = &bm[(j >> 5) * 64 + lane];
+                        const uint32_t old = bT ? atomicAnd(wp, ~bit) : atomicOr(wp, bit);
+                        if ((int)(j >> 5) == wi) cur = bT ? (cur & ~bit) : (cur | bit);
+                        em = !(old & bit);
+                    }
+                }
+                if (em) {
+                    if (emitted < idx_stride) my[(size_t)emitted * 64] = (uint16_t)i;
+                    emitted++;
+                }
+                i--;
+            }
+        }
+    }
+    {
+        const uint32_t word0 = (curw == 0) ? cur : bm[lane];
+        if (!(word0 & 1u)) {
+            if (emitted < idx_stride) my[(size_t)emitted * 64] = 0;
+            emitted++;
+        }
+    }
+    if (emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
+    // Gram of the s sampled rows
+    double g[36];
+#pragma unroll
+    for (int k = 0; k < 36; k++) g[k] = 0.0;
+    const double* P = pts + (size_t)p * max_nq * 6;
+    const int n = min(s, idx_stride);
+    for (int k = 0; k < n; k++) {
+        const int v = my[(size_t)k * 64];
+        const double* pt = P + (size_t)v * 6;
+        const double l0 = pt[0], l1 = pt[1], l2 = pt[2], r0 = pt[3], r1 = pt[4], r2 = pt[5];
+        const double LL[6] = {l0 * l0, l0 * l1, l0 * l2, l1 * l1, l1 * l2, l2 * l2};
+        const double RR[6] = {r0 * r0, r0 * r1, r0 * r2, r1 * r1, r1 * r2, r2 * r2};
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+            for (int b = 0; b < 6; b++) g[6 * a + b] = __builtin_fma(LL[a], RR[b], g[6 * a + b]);
+        if (samples && h < iters) samples[((size_t)p * iters + h) * idx_stride + k] = v;
+    }
+    if (h < iters) {
+        double* go = gram + ((size_t)p * iters + h) * 36;
+#pragma unroll
+        for (int k = 0; k < 36; k++) go[k] = g[k];
+    }
+}
+
+// Gram of ALL m rows (eight_point_estimation called directly, src/manual.cpp:152)
+__global__ __launch_bounds__(256) void gram_all_kernel(const double* __restrict__ pts, int m,
+                                                       double* __restrict__ gram) {
+    __shared__ double red[36][256];
+    const int tid = threadIdx.x;
+    double g[36];
+#pragma unroll
+    for (int k = 0; k < 36; k++) g[k] = 0.0;
+    for (int v = tid; v < m; v += 256) {
+        const double* pt = pts + (size_t)v * 6;
+        const double l0 = pt[0], l1 = pt[1], l2 = pt[2], r0 = pt[3], r1 = pt[4], r2 = pt[5];
+        const double LL[6] = {l0 * l0, l0 * l1, l0 * l2, l1 * l1, l1 * l2, l2 * l2};
+        const double RR[6] = {r0 * r0, r0 * r1, r0 * r2, r1 * r1, r1 * r2, r2 * r2};
+#pragma unroll
+        for (int a = 0; a < 6; a++)
+#pragma unroll
+            for (int b = 0; b < 6; b++) g[6 * a + b] = __builtin_fma(LL[a], RR[b], g[6 * a + b]);
+    }
+#pragma unroll
+    for (int k = 0; k < 36; k++) red[k][tid] = g[k];
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o)
+#pragma unroll
+            for (int k = 0; k < 36; k++) red[k][tid] += red[k][tid + o];
+        __syncthreads();
+    }
+    if (tid < 36) gram[tid] = red[tid][0];
+}
+
+// ========================================================= per-hypothesis solve ==========
+__global__ __launch_bounds__(64) void eigen_kernel(const int32_t* __restrict__ counts,
+                                                   const double* __restrict__ gram, int iters,
+                                                   double sample_frac, double valid_abs,
+                                                   erp_hypothesis* __restrict__ hyps) {
+    const int p = blockIdx.y;
+    const int h = blockIdx.x * 64 + threadIdx.x;
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || h >= iters) return;
+    const double* gi = gram + ((size_t)p * iters + h) * 36;
+    double g36[36], G[81], e[9];
+#pragma unroll
+    for (int k = 0; k < 36; k++) g36[k] = gi[k];
+    gram36_to_full(g36, G);
+    gram_jacobi9(G, s, e);
+    Hyp hy;
+    estimate_from_e(e, valid_abs, hy);
+    erp_hypothesis* o = hyps + (size_t)p * iters + h;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        o->R1[k] = hy.R1[k];
+        o->R2[k] = hy.R2[k];
+        o->T[k] = hy.T[k];
+    }
+    o->R1_valid = hy.R1_valid;
+    o->R2_valid = hy.R2_valid;
+#pragma unroll
+    for (int k = 0; k < 9; k++) o->E[k] = hy.E[k];
+}
+
+// push R1 (if valid) then R2 (if valid) per iteration, in iteration order
+__global__ __launch_bounds__(1024) void valid_compact_kernel(const int32_t* __restrict__ counts,
+                                                             const erp_hypothesis* __restrict__ hyps,
+                                                             int iters, double sample_frac,
+                                                             float* __restrict__ rv,
+                                                             float* __restrict__ tv,
+                                                             int32_t* __restrict__ kcount,
+                                                             float* __restrict__ rv_aos) {
+    __shared__ int ws[16];
+    const int p = blockIdx.x;
+    const int M = counts[p];
+    if ((int)(M * sample_frac) < 1) {
+        if (threadIdx.x == 0) kcount[p] = 0;
+        return;
+    }
+    const erp_hypothesis* H = hyps + (size_t)p * iters;
+    const int per = (iters + 1023) / 1024;
+    const int ha = min(iters, (int)threadIdx.x * per), hb = min(iters, ha + per);
+    int cnt = 0;
+    for (int h = ha; h < hb; h++) cnt += (H[h].R1_valid != 0) + (H[h].R2_valid != 0);
+    int total;
+    int pos = block_exclusive_scan<1024>(cnt, ws, &total);
+    const int stride = 2 * iters;
+    float* X = rv + (size_t)p * 3 * stride;
+    float* T = tv + (size_t)p * 3 * stride;
+    float* A = rv_aos ? rv_aos + (size_t)p * 3 * stride : nullptr;
+    for (int h = ha; h < hb; h++) {
+        const erp_hypothesis hy = H[h];
+        if (hy.R1_valid) {
+            X[pos] = hy.R1[0];
+            X[stride + pos] = hy.R1[1];
+            X[2 * stride + pos] = hy.R1[2];
+            if (A) {
+                A[3 * pos] = hy.R1[0];
+                A[3 * pos + 1] = hy.R1[1];
+                A[3 * pos + 2] = hy.R1[2];
+            }
+            T[3 * pos] = hy.T[0];
+            T[3 * pos + 1] = hy.T[1];
+            T[3 * pos + 2] = hy.T[2];
+            pos++;
+        }
+        if (hy.R2_valid) {
+            X[pos] = hy.R2[0];
+            X[stride + pos] = hy.R2[1];
+            X[2 * stride + pos] = hy.R2[2];
+            if (A) {
+                A[3 * pos] = hy.R2[0];
+                A[3 * pos + 1] = hy.R2[1];
+                A[3 * pos + 2] = hy.R2[2];
+            }
+            T[3 * pos] = hy.T[0];
+            T[3 * pos + 1] = hy.T[1];
+            T[3 * pos + 2] = hy.T[2];
+            pos++;
+        }
+    }
+    if (threadIdx.x == 0) kcount[p] = total;
+}
+
+// ================================================================= consensus ============
+// dist_ij = (double) sqrtf(dx*dx + dy*dy + dz*dz) on Vec3f differences (src/eight_point.cpp:138-139)
+__device__ __forceinline__ float rdist(float xi, float yi, float zi, float xj, float yj, float zj) {
+    const float dx = xi - xj;
+    const float dy = yi - yj;
+    const float dz = zi - zj;
+    return __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
+}
+
+// find the bin holding `rank` in hist[0..2047] (block of 256); returns bin, writes #before
+__device__ int find_bin_2048(const uint32_t* hist, long rank, long* before, int* ws, int* res) {
+    const int tid = threadIdx.x;
+    uint32_t loc = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) loc += hist[tid * 8 + k];
+    int total;
+    const int ex = block_exclusive_scan<256>((int)loc, ws, &total);
+    if ((long)ex <= rank && rank < (long)ex + (long)loc) {
+        long c = ex;
+        for (int k = 0; k < 8; k++) {
+            const long nc = c + hist[tid * 8 + k];
+            if (rank < nc) {
+                res[0] = tid * 8 + k;
+                res[1] = (int)c;
+                break;
+            }
+            c = nc;
+        }
+    }
+    __syncthreads();
+    const int bin = res[0];
+    *before = res[1];
+    __syncthreads();
+    return bin;
+}
+
+// Trimmed mean of row i: value at ranks [lo, hi) of the K distances, lo = (long)(K*0.2),
+// hi = (long)(K*0.8).  Exact order statistics by a 3-level radix select on the f32 bit
+// patterns (11+11+10 bits), then the window sum in fp64 (fixed order; the reference's sorted
+// sequential sum may differ in the last bits -- the final kernel re-scores near ties exactly).
+__global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __restrict__ kcount,
+                                                             const float* __restrict__ rv,
+                                                             int stride, double trim_lo,
+                                                             double trim_hi,
+                                                             double* __restrict__ tmean) {
+    __shared__ uint32_t histA[2048], histB[2048];
+    __shared__ int ws[8];
+    __shared__ int res[2];
+    __shared__ double red[256];
+    const int p = blockIdx.y, i = blockIdx.x, tid = threadIdx.x;
+    const int K = kcount[p];
+    if (i >= K) return;
+    const float* X = rv + (size_t)p * 3 * stride;
+    const float* Y = X + stride;
+    const float* Z = Y + stride;
+    const float xi = X[i], yi = Y[i], zi = Z[i];
+    const long lo = (long)(K * trim_lo);
+    const long hi = (long)(K * trim_hi);
+    if (hi <= lo) {
+        if (tid == 0) tmean[(size_t)p * stride + i] = __builtin_nan("");
+        return;
+    }
+    const long ra = lo, rb = hi - 1;
+    // level 0
+    for (int k = tid; k < 2048; k += 256) histA[k] = 0;
+    __syncthreads();
+    for (int j = tid; j < K; j += 256) {
+        const uint32_t key = __float_as_uint(rdist(xi, yi, zi, X[j], Y[j], Z[j]));
+        atomicAdd(&histA[key >> 21], 1u);
+    }
+    __syncthreads();
+    long ca, cb;
+    const int ba = find_bin_2048(histA, ra, &ca, ws, res);
+    const int bb = find_bin_2048(histA, rb, &cb, ws, res);
+    // level 1
+    for (int k = tid; k < 2048; k += 256) {
+        histA[k] = 0;
+        histB[k] = 0;
+    }
+    __syncthreads();
+    for (int j = tid; j < K; j += 256) {
+        const uint32_t key = __float_as_uint(rdist(xi, yi, zi, X[j], Y[j], Z[j]));
+        const uint32_t top = key >> 21;
+        if (top == (uint32_t)ba) atomicAdd(&histA[(key >> 10) & 2047], 1u);
+        if (top == (uint32_t)bb) atomicAdd(&histB[(key >> 10) & 2047], 1u);
+    }
+    __syncthreads();
+    long ca1, cb1;
+    const int ba1 = find_bin_2048(histA, ra - ca, &ca1, ws, res);
+    const int bb1 = find_bin_2048(histB, rb - cb, &cb1, ws, res);
+    const uint32_t pa = ((uint32_t)ba << 11) | (uint32_t)ba1;  // key >> 10
+    const uint32_t pb = ((uint32_t)bb << 11) | (uint32_t)bb1;
+    // level 2 (10 bits)
+    for (int k = tid; k < 2048; k += 256) {
+        histA[k] = 0;
+        histB[k] = 0;
+    }
+    __syncthreads();
+    for (int j = tid; j < K; j += 256) {
+        const uint32_t key = __float_as_uint(rdist(xi, yi, zi, X[j], Y[j], Z[j]));
+        const uint32_t top = key >> 10;
+        if (top == pa) atomicAdd(&histA[key & 1023], 1u);
+        if (top == pb) atomicAdd(&histB[key & 1023], 1u);
+    }
+    __syncthreads();
+    long ca2, cb2;
+    const int ba2 = find_bin_2048(histA, ra - ca - ca1, &ca2, ws, res);
+    const int bb2 = find_bin_2048(histB, rb - cb - cb1, &cb2, ws, res);
+    const uint32_t va = (pa << 10) | (uint32_t)ba2;  // key at rank lo
+    const uint32_t vb = (pb << 10) | (uint32_t)bb2;  // key at rank hi-1
+    const long lt_a = ca + ca1 + ca2;                // #keys < va
+    const long le_a = lt_a + histA[ba2];             // #keys <= va
+    const long lt_b = cb + cb1 + cb2;                // #keys < vb
+    // level 3: sum of the keys strictly between va and vb
+    double acc = 0.0;
+    for (int j = tid; j < K; j += 256) {
+        const float d = rdist(xi, yi, zi, X[j], Y[j], Z[j]);
+        const uint32_t key = __float_as_uint(d);
+        if (key > va && key < vb) acc += (double)d;
+    }
+    red[tid] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (tid < o) red[tid] += red[tid + o];
+        __syncthreads();
+    }
+    if (tid == 0) {
+        double sum;
+        if (va == vb) {
+            sum = (double)(hi - lo) * (double)__uint_as_float(va);
+        } else {
+            const long na = le_a - lo;   // ranks lo .. le_a-1 hold va
+            const long nb = hi - lt_b;   // ranks lt_b .. hi-1 hold vb
+            sum = red[0] + (double)na * (double)__uint_as_float(va) +
+                  (double)nb * (double)__uint_as_float(vb);
+        }
+        tmean[(size_t)p * stride + i] = sum / ((double)(hi - lo) * 1.0);
+    }
+}
+
+// exact sorted-sequential trimmed mean of one row (std::sort + std::accumulate semantics)
+__device__ double exact_row_mean(const float* X, const float* Y, const float* Z, int K, int i,
+                                 long lo, long hi, float* buf, int npow2, double* sres) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const float xi = X[i], yi = Y[i], zi = Z[i];
+    for (int j = tid; j < npow2; j += nt) buf[j] = j < K ? rdist(xi, yi, zi, X[j], Y[j], Z[j]) : kInf;
+    __syncthreads();
+    for (int k = 2; k <= npow2; k <<= 1) {
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int t = tid; t < npow2; t += nt) {
+                const int ixj = t ^ jj;
+                if (ixj > t) {
+                    const float a = buf[t], b = buf[ixj];
+                    const bool up = (t & k) == 0;
+                    if ((a > b) == up) {
+                        buf[t] = b;
+                        buf[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (tid == 0) {
+        double acc = 0.0;
+        for (long k = lo; k < hi; k++) acc += (double)buf[k];
+        sres[0] = acc / ((double)(hi - lo) * 1.0);
+    }
+    __syncthreads();
+    const double r = sres[0];
+    __syncthreads();
+    return r;
+}
+
+// argmin (std::min_element: first minimum, NaN never wins unless at index 0), exact re-score
+// of rows within a relative 1e-9 band of the minimum, and the per-pair result record.
+__global__ __launch_bounds__(1024) void consensus_final_kernel(
+    const int32_t* __restrict__ counts, const int32_t* __restrict__ kcount,
+    const float* __restrict__ rv, const float* __restrict__ tv, const double* __restrict__ tmean,
+    const int32_t* __restrict__ flags, int stride, int npow2, double sample_frac, double trim_lo,
+    double trim_hi, float* __restrict__ sortbuf, erp_pair_result* __restrict__ results) {
+    __shared__ double sv[1024];
+    __shared__ int si[1024];
+    __shared__ int cand[64];
+    __shared__ int ncand;
+    __shared__ double sres[1];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int M = counts[p];
+    const int K = kcount[p];
+    const int s = (int)(M * sample_frac);
+    erp_pair_result r;
+    for (int k = 0; k < 3; k++) {
+        r.R[k] = 0.f;
+        r.T[k] = 0.f;
+    }
+    r.M = M;
+    r.K = K;
+    r.sample_n = s;
+    r.min_idx = -1;
+    r.near_ties = 0;
+    r.min_dist = 0.0;
+    const int fl = flags[p];
+    if (fl & 1) r.status = ERP_TOO_FEW_POINTS;
+    else if (fl & 2)
+        r.status = ERP_INTERNAL;
+    else if (s < 1)
+        r.status = ERP_TOO_FEW_POINTS;
+    else if (K == 0)
+        r.status = ERP_NO_VALID_HYPOTHESIS;
+    else
+        r.status = ERP_OK;
+    if (r.status != ERP_OK) {
+        if (tid == 0) results[p] = r;
+        return;
+    }
+    const double* Tm = tmean + (size_t)p * stride;
+    const float* X = rv + (size_t)p * 3 * stride;
+    const float* Y = X + stride;
+    const float* Z = Y + stride;
+    int best;
+    double bv;
+    if (__builtin_isnan(Tm[0])) {
+        best = 0;
+        bv = Tm[0];
+    } else {
+        double v = __builtin_huge_val();
+        int bi = 0x7fffffff;
+        for (int k = tid; k < K; k += 1024) {
+            const double t = Tm[k];
+            if (t < v) {  // NaN never compares less; strided order keeps the first index
+                v = t;
+                bi = k;
+            }
+        }
+        sv[tid] = v;
+        si[tid] = bi;
+        __syncthreads();
+        for (int o = 512; o > 0; o >>= 1) {
+            if (tid < o) {
+                const double a = sv[tid], b = sv[tid + o];
+                const int ia = si[tid], ib = si[tid + o];
+                if (b < a || (b == a && ib < ia)) {
+                    sv[tid] = b;
+                    si[tid] = ib;
+                }
+            }
+            __syncthreads();
+        }
+        best = si[0];
+        bv = sv[0];
+        __syncthreads();
+        // near ties: rows within 1e-9 (relative) of the approximate minimum
+        if (tid == 0) ncand = 0;
+        __syncthreads();
+        const double tol = 1e-9 * fabs(bv) + 1e-300;
+        for (int k = tid; k < K; k += 1024) {
+            if (Tm[k] <= bv + tol) {
+                const int slot = atomicAdd(&ncand, 1);
+                if (slot < 64) cand[slot] = k;
+            }
+        }
+        __syncthreads();
+        const int nc = ncand;
+        if (nc > 1) {
+            // sort candidate indices (few) ascending
+            if (tid == 0) {
+                const int n = nc < 64 ? nc : 64;
+                for (int a = 1; a < n; a++) {
+                    const int key = cand[a];
+                    int b = a - 1;
+                    while (b >= 0 && cand[b] > key) {
+                        cand[b + 1] = cand[b];
+                        b--;
+                    }
+                    cand[b + 1] = key;
+                }
+            }
+            __syncthreads();
+            const int n = nc < 64 ? nc : 64;
+            const long lo = (long)(K * trim_lo), hi = (long)(K * trim_hi);
+            float* buf = sortbuf + (size_t)p * npow2;
+            double ev = __builtin_huge_val();
+            int eb = -1;
+            for (int c = 0; c < n; c++) {
+                const int row = cand[c];
+                bool dup = false;  // identical R vector as an earlier candidate => identical T
+                for (int d = 0; d < c; d++) {
+                    const int o = cand[d];
+                    if (X[o] == X[row] && Y[o] == Y[row] && Z[o] == Z[row]) dup = true;
+                }
+                if (dup) continue;
+                const double t = exact_row_mean(X, Y, Z, K, row, lo, hi, buf, npow2, sres);
+                if (eb < 0 || t < ev) {
+                    ev = t;
+                    eb = row;
+                }
+            }
+            if (nc > 64) r.near_ties = -nc;  // more candidates than re-scored: flagged
+            else
+                r.near_ties = n;
+            if (eb >= 0) {
+                best = eb;
+                bv = ev;
+            }
+        }
+    }
+    if (tid == 0) {
+        r.min_idx = best;
+        r.min_dist = bv;
+        r.R[0] = X[best];
+        r.R[1] = Y[best];
+        r.R[2] = Z[best];
+        const float* T = tv + (size_t)p * 3 * stride + 3 * (size_t)best;
+        r.T[0] = T[0];
+        r.T[1] = T[1];
+        r.T[2] = T[2];
+        results[p] = r;
+    }
+}
+
+}  // namespace
+
+// ====================================================================== launchers =======
+void init_constants() {
+    uint32_t red[30][31] = {};
+    uint32_t v[31] = {};
+    v[28] = 1;
+    v[0] = 1;
+    for (int d = 0; d < 30; d++) {
+        for (int k = 0; k < 31; k++) red[d][k] = v[k];
+        uint32_t nv[31];
+        const uint32_t top = v[30];
+        nv[0] = 0;
+        for (int k = 1; k < 31; k++) nv[k] = v[k - 1];
+        nv[28] += top;
+        nv[0] += top;
+        for (int k = 0; k < 31; k++) v[k] = nv[k];
+    }
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_red), red, sizeof(red));
+}
+
+hipError_t launch_knn2_partial(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                               const int64_t* off_t, const BatchShape& sh, Top2* part,
+                               hipStream_t st) {
+    dim3 grid((sh.max_nq + 255) / 256, sh.chunks, sh.n_pairs);
+    hipLaunchKernelGGL(knn2_partial_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
+                       sh.chunk_len, sh.chunks, sh.max_nq, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
+                             const BatchShape& sh, float ratio, erp_dmatch* matches,
+                             int32_t* counts, int32_t* flags, hipStream_t st) {
+    hipLaunchKernelGGL(knn2_merge_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, part, off_q, off_t,
+                       sh.chunk_len, sh.chunks, sh.max_nq, ratio, matches, counts, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t* counts,
+                                        const erp_point2f* kp_l, const erp_point2f* kp_r,
+                                        const int64_t* off_l, const int64_t* off_r,
+                                        const int32_t* width, const int32_t* height,
+                                        const BatchShape& sh, double* pts, erp_point2f* key_l,
+                                        erp_point2f* key_r, hipStream_t st) {
+    dim3 grid((sh.max_nq + 255) / 256, sh.n_pairs);
+    hipLaunchKernelGGL(bearings_from_matches_kernel, grid, dim3(256), 0, st, matches, counts, kp_l,
+                       kp_r, off_l, off_r, width, height, sh.max_nq, pts, key_l, key_r);
+    return hipGetLastError();
+}
+
+hipError_t launch_bearings_direct(const erp_point2f* kl, const erp_point2f* kr, int32_t m,
+                                  int32_t W, int32_t H, double* pts, hipStream_t st) {
+    if (m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(bearings_direct_kernel, dim3((m + 255) / 256), dim3(256), 0, st, kl, kr, m,
+                       W, H, pts);
+    return hipGetLastError();
+}
+
+static int q_needed(int iters) {
+    const int nwaves = (iters + 63) / 64;
+    int kq = 0;
+    while ((1 << kq) < nwaves) kq++;
+    return kq;
+}
+
+hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_t* polyR,
+                            uint32_t* polyQ, hipStream_t st) {
+    // sample_frac is only used to skip pairs with sample_n < 1; pass a tiny positive value so
+    // every pair with M >= 2 gets polynomials (the sampler decides on its own)
+    hipLaunchKernelGGL(jump_prep_kernel, dim3(sh.n_pairs), dim3(64), 0, st, counts, 1.0,
+                       q_needed(sh.iters), polyR, polyQ);
+    return hipGetLastError();
+}
+
+hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
+                               const uint32_t* w0, const double* pts, const BatchShape& sh,
+                               double sample_frac, uint16_t* idx, double* gram, int32_t* samples,
+                               int32_t* flags, hipStream_t st) {
+    const int nwaves = (sh.iters + 63) / 64;
+    const int nwords = (sh.max_s + 31) / 32;
+    const size_t shmem = (96 + (size_t)nwords * 64) * sizeof(uint32_t);
+    hipLaunchKernelGGL(sampler_gram_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
+                       polyR, polyQ, w0, pts, sh.max_nq, sh.iters, nwaves, sh.idx_stride,
+                       sample_frac, idx, gram, samples, flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream_t st) {
+    hipLaunchKernelGGL(gram_all_kernel, dim3(1), dim3(256), 0, st, pts, m, gram);
+    return hipGetLastError();
+}
+
+hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
+                        double sample_frac, double valid_abs, erp_hypothesis* hyps,
+                        hipStream_t st) {
+    dim3 grid((sh.iters + 63) / 64, sh.n_pairs);
+    hipLaunchKernelGGL(eigen_kernel, grid, dim3(64), 0, st, counts, gram, sh.iters, sample_frac,
+                       valid_abs, hyps);
+    return hipGetLastError();
+}
+
+hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyps,
+                                const BatchShape& sh, double sample_frac, float* rv, float* tv,
+                                int32_t* kcount, float* rv_aos, hipStream_t st) {
+    hipLaunchKernelGGL(valid_compact_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, hyps,
+                       sh.iters, sample_frac, rv, tv, kcount, rv_aos);
+    return hipGetLastError();
+}
+
+hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const BatchShape& sh,
+                                 double trim_lo, double trim_hi, double* tmean, hipStream_t st) {
+    dim3 grid(2 * sh.iters, sh.n_pairs);
+    hipLaunchKernelGGL(consensus_rows_kernel, grid, dim3(256), 0, st, kcount, rv, 2 * sh.iters,
+                       trim_lo, trim_hi, tmean);
+    return hipGetLastError();
+}
+
+int sortbuf_len(int iters) {
+    int p = 1;
+    while (p < 2 * iters) p <<= 1;
+    return p;
+}
+
+hipError_t launch_consensus_final(const int32_t* counts, const int32_t* kcount, const float* rv,
+                                  const float* tv, const double* tmean, const int32_t* flags,
+                                  const BatchShape& sh, double sample_frac, double trim_lo,
+                                  double trim_hi, float* sortbuf, erp_pair_result* results,
+                                  hipStream_t st) {
+    hipLaunchKernelGGL(consensus_final_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, kcount,
+                       rv, tv, tmean, flags, 2 * sh.iters, sortbuf_len(sh.iters), sample_frac,
+                       trim_lo, trim_hi, sortbuf, results);
+    return hipGetLastError();
+}
+
+}  // namespace erp

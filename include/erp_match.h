@@ -1,0 +1,212 @@
+/*
+ * erp_match.h -- C ABI of the MI355X-native ERP matcher + spherical eight-point estimator.
+ *
+ * This is the drop-in boundary for the reference's hot path (Kitsunetic/ERP_match_eightpoint_test):
+ *
+ *   erp_match_two_image / erp_match_knn2_ratio
+ *       replaces  std::vector<cv::DMatch> feature_matcher::match_two_image(
+ *                     const cv::Mat& descriptor1, const cv::Mat& descriptor2)
+ *                 /root/reference/src/feature_matcher.hpp:36, body src/feature_matcher.cpp:42-59
+ *                 (FLANN knnMatch k=2 + ratio 0.3f; here: EXACT k=2 in flann::L2 order).
+ *   erp_eight_point_find
+ *       replaces  void eight_point::find(int im_width, int im_height,
+ *                     std::vector<cv::KeyPoint>& key_left, std::vector<cv::KeyPoint>& key_right,
+ *                     cv::Vec3f& R_vec_out, cv::Vec3f& T_vec_out, int match_size)
+ *                 /root/reference/src/eight_point.hpp:11-14, body src/eight_point.cpp:152-192
+ *                 (initial_guess :87-150 and the random_array sampler eight_point.hpp:30-59 run
+ *                  inside; the iteration count, sample fraction, trim window and validity bound
+ *                  are the hard-coded constants of :99,:102,:143,:76 exposed in erp_ransac_cfg).
+ *   erp_eight_point_estimation
+ *       replaces  void eight_point::eight_point_estimation(int, int, std::vector<cv::Point3d>&,
+ *                     std::vector<cv::Point3d>&, cv::Vec3f& R1, cv::Vec3f& R2, cv::Vec3f& T,
+ *                     bool& R1_valid, bool& R2_valid, int match_size)
+ *                 /root/reference/src/eight_point.hpp:15-19, body src/eight_point.cpp:16-85
+ *   erp_pair_batch_run
+ *       the fused hot path for many ERP pairs at once: spherical_surf::do_all's
+ *       match -> gather (src/spherical_surf.cpp:153-162, 177) -> eight_point::find
+ *       (src/automatic.cpp:117-126 calls exactly this sequence per pair).
+ *
+ * Conventions: plain C types only; `void* stream` is a hipStream_t (NULL = default stream);
+ * device-pointer entry points are asynchronous on that stream, host-pointer ones synchronous.
+ * No C++ exception crosses this boundary; every call returns an erp_status.  The reference's
+ * undefined behaviour cases are given explicit statuses (see erp_status).
+ */
+#ifndef ERP_MATCH_H
+#define ERP_MATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ERP_MATCH_ABI_VERSION 1
+
+typedef enum erp_status {
+    ERP_OK = 0,
+    ERP_INVALID_ARG = 1,
+    ERP_TOO_FEW_POINTS = 2,       /* train set < 2 (knn_matches[i][1] UB, feature_matcher.cpp:52),
+                                     or (int)(M*sample_frac) < 1 (A_mat with 0 rows, :18) */
+    ERP_NO_VALID_HYPOTHESIS = 3,  /* K == 0: R_vec_arr[min_idx] on an empty vector (:148) */
+    ERP_HIP_ERROR = 4,
+    ERP_NO_DEVICE = 5,
+    ERP_OUT_OF_MEMORY = 6,
+    ERP_INTERNAL = 7
+} erp_status;
+
+/* cv::DMatch layout */
+typedef struct erp_dmatch {
+    int32_t queryIdx;
+    int32_t trainIdx;
+    int32_t imgIdx;
+    float distance;
+} erp_dmatch;
+
+/* cv::KeyPoint::pt (the only KeyPoint field the hot path reads) */
+typedef struct erp_point2f {
+    float x;
+    float y;
+} erp_point2f;
+
+typedef enum erp_sampler {
+    ERP_SAMPLER_GLIBC = 0 /* replay of glibc rand() + libstdc++ random_shuffle (the reference) */
+} erp_sampler;
+
+/* initial_guess parameters; erp_ransac_cfg_default() gives the reference constants. */
+typedef struct erp_ransac_cfg {
+    int32_t iters;       /* 80   src/eight_point.cpp:99 */
+    int32_t sampler;     /* ERP_SAMPLER_GLIBC */
+    double sample_frac;  /* 0.25 :102 */
+    double trim_lo;      /* 0.2  :143 */
+    double trim_hi;      /* 0.8  :143 */
+    double valid_abs;    /* 1.57 :76,81 */
+    uint32_t seed;       /* 1: the reference never calls srand() */
+    uint32_t reserved;
+    uint64_t offset;     /* rand() calls consumed before initial_guess (e.g. by FLANN) */
+} erp_ransac_cfg;
+
+/* one initial_guess iteration (R1, R2, T as Vec3f; E = the solved 9-vector, sign arbitrary) */
+typedef struct erp_hypothesis {
+    float R1[3];
+    float R2[3];
+    float T[3];
+    int32_t R1_valid;
+    int32_t R2_valid;
+    double E[9];
+} erp_hypothesis;
+
+/* per-pair result of find / the batch pipeline */
+typedef struct erp_pair_result {
+    float R[3];          /* R_vec_out (XYZ Euler, rad) */
+    float T[3];          /* T_vec_out (unit) */
+    int32_t status;      /* erp_status of this pair */
+    int32_t M;           /* matches after the ratio test (match_size) */
+    int32_t K;           /* valid rotation hypotheses */
+    int32_t min_idx;     /* consensus winner in R_vec_arr order */
+    int32_t sample_n;    /* (int)(M * sample_frac) */
+    int32_t near_ties;   /* rows re-scored exactly by the near-tie resolver */
+    double min_dist;     /* trimmed-mean distance of the winner */
+} erp_pair_result;
+
+/* device pointers describing a batch of ERP pairs (rows concatenated pair after pair) */
+typedef struct erp_pair_batch {
+    int32_t n_pairs;
+    int32_t dim;                /* descriptor length (64 for SURF; the fast path needs 64) */
+    int32_t max_nq;             /* host-known upper bound of rows per pair (queries / left) */
+    int32_t max_nt;             /* ... (train / right) */
+    const float* desc_l;        /* [sum nq][dim] queries  (descriptor1) */
+    const float* desc_r;        /* [sum nt][dim] train    (descriptor2) */
+    const erp_point2f* kp_l;    /* [sum nq] keypoints of desc_l rows */
+    const erp_point2f* kp_r;    /* [sum nt] */
+    const int64_t* off_l;       /* [n_pairs+1] row offsets into desc_l / kp_l */
+    const int64_t* off_r;       /* [n_pairs+1] */
+    const int32_t* width;       /* [n_pairs] ERP width  (im_width) */
+    const int32_t* height;      /* [n_pairs] ERP height (im_height) */
+} erp_pair_batch;
+
+/* optional device outputs of the batch pipeline (NULL = not needed) */
+typedef struct erp_batch_outputs {
+    erp_pair_result* results;   /* [n_pairs] (required) */
+    erp_dmatch* matches;        /* [n_pairs][max_nq], queryIdx/trainIdx local to the pair */
+    erp_point2f* key_left;      /* [n_pairs][max_nq] gathered matched keypoints (valid_key_left) */
+    erp_point2f* key_right;     /* [n_pairs][max_nq] */
+    erp_hypothesis* hyps;       /* [n_pairs][iters] */
+    int32_t* samples;           /* [n_pairs][iters][max sample_n] sampled match indices (as a set,
+                                   order unspecified) */
+    float* rvec;                /* [n_pairs][2*iters][3] R_vec_arr */
+    float* tvec;                /* [n_pairs][2*iters][3] T_vec_arr */
+    double* dist;               /* [n_pairs][2*iters] trimmed means (approximate; the winner and
+                                   near ties are exact) */
+} erp_batch_outputs;
+
+typedef struct erp_ctx erp_ctx;
+
+/* ---- context ---- */
+erp_status erp_ctx_create(int32_t device, erp_ctx** out);
+erp_status erp_ctx_destroy(erp_ctx* ctx);
+const char* erp_status_string(erp_status s);
+void erp_ransac_cfg_default(erp_ransac_cfg* cfg);
+int32_t erp_abi_version(void);
+/* Pre-size device scratch so later calls allocate nothing (graph-capture friendly). */
+erp_status erp_ctx_reserve(erp_ctx* ctx, int32_t n_pairs, int32_t max_nq, int32_t max_nt,
+                           int32_t iters);
+
+/* ---- stage timing (the reference's START_TIME/STOP_TIME, src/debug_print.h:9-13, applied to
+   the hot path): HIP events recorded around every kernel on the pipeline's stream. ---- */
+typedef enum erp_stage {
+    ERP_STAGE_KNN2_PARTIAL = 0, /* exact k=2 distance sweep (dominant matcher kernel) */
+    ERP_STAGE_KNN2_MERGE = 1,   /* chunk fold + ratio test + compaction */
+    ERP_STAGE_BEARINGS = 2,     /* gather + pixel -> bearing */
+    ERP_STAGE_JUMP_PREP = 3,    /* glibc jump-ahead polynomials */
+    ERP_STAGE_SAMPLER_GRAM = 4, /* random_array replay + A^T A */
+    ERP_STAGE_EIGEN = 5,        /* 9x9 Jacobi, rank-2 fix, decomposeEssentialMat, Euler */
+    ERP_STAGE_VALID_COMPACT = 6,
+    ERP_STAGE_CONSENSUS_ROWS = 7,
+    ERP_STAGE_CONSENSUS_FINAL = 8,
+    ERP_STAGE_COUNT = 9
+} erp_stage;
+erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable);
+const char* erp_stage_name(int32_t stage);
+/* Waits for the recorded events, writes per-stage total milliseconds and launch counts
+   (arrays of ERP_STAGE_COUNT), then clears the record. */
+erp_status erp_ctx_stage_times(erp_ctx* ctx, double* total_ms, int64_t* launches);
+
+/* ---- matcher (feature_matcher::match_two_image) ---- */
+/* device pointers; writes up to nq matches in ascending queryIdx order and *d_count. */
+erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,
+                                const float* d_train, int32_t nt, int32_t dim, float ratio,
+                                erp_dmatch* d_out, int32_t* d_count, void* stream);
+/* host pointers, synchronous: the drop-in for match_two_image (ratio 0.3f). */
+erp_status erp_match_two_image(erp_ctx* ctx, const float* h_desc1, int32_t n1,
+                               const float* h_desc2, int32_t n2, int32_t dim,
+                               erp_dmatch* h_out, int32_t* h_count);
+
+/* ---- estimator (eight_point::find / eight_point_estimation) ---- */
+/* device pointers: m matched keypoint pairs -> result (R, T, diagnostics). */
+erp_status erp_eight_point_find_dev(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* d_kl,
+                                    const erp_point2f* d_kr, int32_t m, const erp_ransac_cfg* cfg,
+                                    erp_pair_result* d_result, erp_hypothesis* d_hyps,
+                                    void* stream);
+/* host pointers, synchronous: the drop-in for eight_point::find. */
+erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* h_kl,
+                                const erp_point2f* h_kr, int32_t m, const erp_ransac_cfg* cfg,
+                                float R_out[3], float T_out[3], erp_pair_result* h_result);
+/* host pointers, synchronous: initial_guess on m bearing pairs (m x 3 doubles each), i.e. find
+   after the pixel->bearing step (src/eight_point.cpp:87-150). */
+erp_status erp_initial_guess(erp_ctx* ctx, const double* h_bl, const double* h_br, int32_t m,
+                             const erp_ransac_cfg* cfg, float R_out[3], float T_out[3],
+                             erp_pair_result* h_result);
+/* host pointers, synchronous: one eight_point_estimation on m bearing pairs (m x 3 doubles). */
+erp_status erp_eight_point_estimation(erp_ctx* ctx, const double* h_bl, const double* h_br,
+                                      int32_t m, erp_hypothesis* h_out);
+
+/* ---- fused batch: match -> gather -> find for every pair ---- */
+erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* batch, float ratio,
+                              const erp_ransac_cfg* cfg, const erp_batch_outputs* out,
+                              void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ERP_MATCH_H */

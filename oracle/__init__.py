@@ -1,0 +1,250 @@
+"""ctypes wrapper of the CPU oracle (oracle/erp_oracle.c).  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module; it
+is the parity checker, never the thing measured or shipped.  Every function cites the
+reference file:line it restates in oracle/erp_oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liberp_oracle.so")
+
+
+class DMatch(C.Structure):
+    _fields_ = [("queryIdx", C.c_int32), ("trainIdx", C.c_int32), ("imgIdx", C.c_int32),
+                ("distance", C.c_float)]
+
+
+DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"),
+                         ("distance", "<f4")])
+
+
+class Glibc(C.Structure):
+    _fields_ = [("r", C.c_uint32 * 34), ("pos", C.c_uint32)]
+
+
+class Hyp(C.Structure):
+    _fields_ = [("R1", C.c_float * 3), ("R2", C.c_float * 3), ("T", C.c_float * 3),
+                ("R1_valid", C.c_int32), ("R2_valid", C.c_int32), ("E", C.c_double * 9),
+                ("E_corr", C.c_double * 9)]
+
+
+HYP_DTYPE = np.dtype([("R1", "<f4", 3), ("R2", "<f4", 3), ("T", "<f4", 3), ("R1_valid", "<i4"),
+                      ("R2_valid", "<i4"), ("E", "<f8", 9), ("E_corr", "<f8", 9)], align=True)
+assert HYP_DTYPE.itemsize == C.sizeof(Hyp)
+
+
+class Cfg(C.Structure):
+    _fields_ = [("iters", C.c_int32), ("sample_frac", C.c_double), ("trim_lo", C.c_double),
+                ("trim_hi", C.c_double), ("valid_abs", C.c_double), ("seed", C.c_uint32),
+                ("offset", C.c_uint64)]
+
+
+class Diag(C.Structure):
+    _fields_ = [("K", C.c_int32), ("min_idx", C.c_int32), ("sample_n", C.c_int32),
+                ("status", C.c_int32), ("min_dist", C.c_double)]
+
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile the oracle with its Makefile (gcc only; no reference sources involved)."""
+    if force or not os.path.exists(LIB_PATH) or (
+            os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "erp_oracle.c"))):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.erpo_glibc_seed.argtypes = [C.POINTER(Glibc), C.c_uint32]
+        L.erpo_glibc_rand.argtypes = [C.POINTER(Glibc)]
+        L.erpo_glibc_rand.restype = C.c_int32
+        L.erpo_glibc_discard.argtypes = [C.POINTER(Glibc), C.c_uint64]
+        L.erpo_glibc_window.argtypes = [C.POINTER(Glibc), P]
+        L.erpo_random_array.argtypes = [P, C.c_int32, C.POINTER(Glibc)]
+        L.erpo_l2sq.argtypes = [P, P, C.c_int32]
+        L.erpo_l2sq.restype = C.c_float
+        L.erpo_match_two_image.argtypes = [P, C.c_int32, P, C.c_int32, C.c_int32, C.c_float, P, P,
+                                           P, P, C.c_int32]
+        L.erpo_match_two_image.restype = C.c_int32
+        L.erpo_eular2rot.argtypes = [P, P]
+        L.erpo_rot2eular.argtypes = [P, P]
+        L.erpo_pixel_to_bearing.argtypes = [C.c_int32, C.c_int32, C.c_float, C.c_float, P]
+        L.erpo_svdecomp.argtypes = [P, C.c_int32, C.c_int32, P, P, P]
+        L.erpo_svdecomp.restype = C.c_int
+        L.erpo_eight_point_estimation.argtypes = [P, P, C.c_int32, C.POINTER(Hyp)]
+        L.erpo_eight_point_estimation.restype = C.c_int
+        L.erpo_consensus.argtypes = [P, C.c_int32, C.c_double, C.c_double, C.POINTER(C.c_int32), P]
+        L.erpo_consensus.restype = C.c_int
+        L.erpo_initial_guess.argtypes = [P, P, C.c_int32, C.POINTER(Cfg), P, P, C.POINTER(Diag), P,
+                                         P, P, P, P]
+        L.erpo_initial_guess.restype = C.c_int
+        L.erpo_find.argtypes = [C.c_int32, C.c_int32, P, P, C.c_int32, C.POINTER(Cfg), P, P,
+                                C.POINTER(Diag), P, P, P, P, P]
+        L.erpo_find.restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def make_cfg(iters=80, sample_frac=0.25, trim_lo=0.2, trim_hi=0.8, valid_abs=1.57, seed=1,
+             offset=0) -> Cfg:
+    """Reference defaults: src/eight_point.cpp:99 (80), :102 (0.25), :143 (0.2/0.8), :76 (1.57)."""
+    return Cfg(iters, sample_frac, trim_lo, trim_hi, valid_abs, seed, offset)
+
+
+class GlibcRand:
+    """glibc rand() restatement (seed 1 = never seeded, as in the reference)."""
+
+    def __init__(self, seed: int = 1, offset: int = 0):
+        self.g = Glibc()
+        lib().erpo_glibc_seed(C.byref(self.g), seed)
+        if offset:
+            lib().erpo_glibc_discard(C.byref(self.g), offset)
+
+    def rand(self) -> int:
+        return lib().erpo_glibc_rand(C.byref(self.g))
+
+    def window(self) -> np.ndarray:
+        w = np.zeros(31, np.uint32)
+        lib().erpo_glibc_window(C.byref(self.g), _p(w))
+        return w
+
+    def random_array(self, n: int) -> np.ndarray:
+        a = np.zeros(max(n, 1), np.int32)
+        lib().erpo_random_array(_p(a), n, C.byref(self.g))
+        return a[:n]
+
+
+def match_two_image(q: np.ndarray, t: np.ndarray, ratio: float = 0.3, nthreads: int = 0):
+    """Exact k=2 + Lowe ratio (src/feature_matcher.cpp:42-59).
+
+    Returns (matches structured array, best (nq,), d0sq (nq,), d1sq (nq,))."""
+    q = np.ascontiguousarray(q, np.float32)
+    t = np.ascontiguousarray(t, np.float32)
+    nq, dim = q.shape
+    nt = t.shape[0]
+    out = np.zeros(max(nq, 1), DMATCH_DTYPE)
+    best = np.zeros(max(nq, 1), np.int32)
+    d0 = np.zeros(max(nq, 1), np.float32)
+    d1 = np.zeros(max(nq, 1), np.float32)
+    m = lib().erpo_match_two_image(_p(q), nq, _p(t), nt, dim, ratio, _p(out), _p(best), _p(d0),
+                                   _p(d1), nthreads)
+    if m < 0:
+        raise ValueError(f"erpo_match_two_image failed ({m})")
+    return out[:m].copy(), best[:nq], d0[:nq], d1[:nq]
+
+
+def l2sq(a: np.ndarray, b: np.ndarray) -> float:
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return lib().erpo_l2sq(_p(a), _p(b), a.shape[0])
+
+
+def eular2rot(e) -> np.ndarray:
+    e = np.ascontiguousarray(e, np.float64)
+    R = np.zeros(9, np.float64)
+    lib().erpo_eular2rot(_p(e), _p(R))
+    return R.reshape(3, 3)
+
+
+def rot2eular(R) -> np.ndarray:
+    R = np.ascontiguousarray(R, np.float64).reshape(9)
+    e = np.zeros(3, np.float64)
+    lib().erpo_rot2eular(_p(R), _p(e))
+    return e
+
+
+def pixel_to_bearing(W: int, H: int, kp: np.ndarray) -> np.ndarray:
+    kp = np.asarray(kp, np.float32).reshape(-1, 2)
+    out = np.zeros((kp.shape[0], 3), np.float64)
+    b = np.zeros(3, np.float64)
+    for i in range(kp.shape[0]):
+        lib().erpo_pixel_to_bearing(W, H, float(kp[i, 0]), float(kp[i, 1]), _p(b))
+        out[i] = b
+    return out
+
+
+def svdecomp(a: np.ndarray):
+    a = np.ascontiguousarray(a, np.float64)
+    m, n = a.shape
+    k = min(m, n)
+    w = np.zeros(k, np.float64)
+    u = np.zeros((m, k), np.float64)
+    vt = np.zeros((k, n), np.float64)
+    if lib().erpo_svdecomp(_p(a), m, n, _p(w), _p(u), _p(vt)) != 0:
+        raise ValueError("svdecomp failed")
+    return w, u, vt
+
+
+def eight_point_estimation(bl: np.ndarray, br: np.ndarray) -> np.ndarray:
+    bl = np.ascontiguousarray(bl, np.float64)
+    br = np.ascontiguousarray(br, np.float64)
+    h = Hyp()
+    rc = lib().erpo_eight_point_estimation(_p(bl), _p(br), bl.shape[0], C.byref(h))
+    if rc != 0:
+        raise ValueError(f"eight_point_estimation failed ({rc})")
+    return np.frombuffer(bytes(h), HYP_DTYPE)[0]
+
+
+def consensus(rvec: np.ndarray, trim_lo=0.2, trim_hi=0.8):
+    rvec = np.ascontiguousarray(rvec, np.float32).reshape(-1, 3)
+    K = rvec.shape[0]
+    mi = C.c_int32(0)
+    dist = np.zeros(max(K, 1), np.float64)
+    rc = lib().erpo_consensus(_p(rvec), K, trim_lo, trim_hi, C.byref(mi), _p(dist))
+    return rc, mi.value, dist[:K]
+
+
+def _run_guess(fn, args, m, cfg: Cfg, want_detail: bool):
+    iters = cfg.iters
+    sample_n = int(m * cfg.sample_frac) if m > 0 else 0
+    R = np.zeros(3, np.float32)
+    T = np.zeros(3, np.float32)
+    diag = Diag()
+    hyp = np.zeros(max(iters, 1), HYP_DTYPE) if want_detail else None
+    samples = np.zeros(max(iters * sample_n, 1), np.int32) if want_detail else None
+    rvec = np.zeros((max(2 * iters, 1), 3), np.float32) if want_detail else None
+    tvec = np.zeros((max(2 * iters, 1), 3), np.float32) if want_detail else None
+    dist = np.zeros(max(2 * iters, 1), np.float64) if want_detail else None
+    rc = fn(*args, C.byref(cfg), _p(R), _p(T), C.byref(diag), _p(hyp), _p(samples), _p(rvec),
+            _p(tvec), _p(dist))
+    res = {"rc": rc, "R": R, "T": T, "K": diag.K, "min_idx": diag.min_idx,
+           "sample_n": diag.sample_n, "status": diag.status, "min_dist": diag.min_dist}
+    if want_detail:
+        K = max(diag.K, 0)
+        res.update(hyp=hyp[:iters], samples=samples[:iters * sample_n].reshape(iters, sample_n),
+                   rvec=rvec[:K], tvec=tvec[:K], dist=dist[:K])
+    return res
+
+
+def initial_guess(bl, br, cfg: Cfg | None = None, detail: bool = False):
+    cfg = cfg or make_cfg()
+    bl = np.ascontiguousarray(bl, np.float64)
+    br = np.ascontiguousarray(br, np.float64)
+    m = bl.shape[0]
+    return _run_guess(lib().erpo_initial_guess, (_p(bl), _p(br), m), m, cfg, detail)
+
+
+def find(W: int, H: int, kl, kr, cfg: Cfg | None = None, detail: bool = False):
+    """eight_point::find (src/eight_point.cpp:152-192) on pixel keypoints (m x 2 float)."""
+    cfg = cfg or make_cfg()
+    kl = np.ascontiguousarray(kl, np.float32).reshape(-1, 2)
+    kr = np.ascontiguousarray(kr, np.float32).reshape(-1, 2)
+    m = kl.shape[0]
+    return _run_guess(lib().erpo_find, (W, H, _p(kl), _p(kr), m), m, cfg, detail)

@@ -1,0 +1,259 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the golden fixtures.
+
+Bars (DESIGN.md "Parity"):
+* matches: (queryIdx, trainIdx, distance bits) bit-exact;
+* sampler: every iteration's sampled index set identical (glibc replay is integer work);
+* per-iteration E within 1e-8 (after sign alignment; north_star allows 1e-4), {R1,R2} equal as a
+  set within 2e-6 rad, T within 2e-6;
+* final R, T: equal to the oracle's within 2e-6 (same consensus winner up to identical values).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+from erp_match_eightpoint_test_amd import synth
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def ctx(gpu_lib):
+    from erp_match_eightpoint_test_amd import Context
+    return Context(0)
+
+
+def _npz(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+# ------------------------------------------------------------------------------ matcher
+def test_match_golden_fixture(ctx):
+    from erp_match_eightpoint_test_amd import feature_matcher
+    g = _npz("match_384.npz")
+    fm = feature_matcher(ctx=ctx)
+    mt = fm.match_two_image(g["desc_l"], g["desc_r"])
+    assert np.array_equal(mt["queryIdx"], g["query"])
+    assert np.array_equal(mt["trainIdx"], g["train"])
+    assert np.array_equal(mt["distance"].view(np.uint32), g["dist_bits"])
+    assert np.all(mt["imgIdx"] == 0)
+
+
+@pytest.mark.parametrize("nq,nt", [(1, 2), (2, 2), (63, 65), (300, 4097), (2048, 2048),
+                                   (4096, 4096), (5000, 1000)])
+def test_match_vs_oracle_sizes(ctx, oracle, nq, nt):
+    from erp_match_eightpoint_test_amd import feature_matcher
+    p = synth.make_pair(nq * 7 + nt, n_kpts=nq, n_train=nt)
+    ref, _, _, _ = oracle.match_two_image(p["desc_l"], p["desc_r"])
+    mt = feature_matcher(ctx=ctx).match_two_image(p["desc_l"], p["desc_r"])
+    assert len(mt) == len(ref)
+    assert np.array_equal(mt.view(np.uint32), ref.view(np.uint32))
+
+
+def test_match_ties_and_ratio_boundary(ctx, oracle):
+    from erp_match_eightpoint_test_amd import feature_matcher
+    rng = np.random.default_rng(5)
+    t = synth.random_descriptors(rng, 700)
+    t[500:520] = t[10:30]                        # duplicates across chunks
+    q = np.concatenate([t[5:40], synth.random_descriptors(rng, 60)])
+    q[40] = q[41]
+    ref, _, _, _ = oracle.match_two_image(q, t)
+    mt = feature_matcher(ctx=ctx).match_two_image(q, t)
+    assert np.array_equal(mt.view(np.uint32), ref.view(np.uint32))
+
+
+def test_match_edge_counts(ctx):
+    from erp_match_eightpoint_test_amd import ErpError, feature_matcher
+    fm = feature_matcher(ctx=ctx)
+    assert len(fm.match_two_image(np.zeros((0, 64), np.float32), np.zeros((5, 64), np.float32))) == 0
+    with pytest.raises(ErpError):
+        fm.match_two_image(np.ones((3, 64), np.float32), np.ones((1, 64), np.float32))
+
+
+def test_match_device_path(ctx, oracle):
+    import torch
+    from erp_match_eightpoint_test_amd import feature_matcher
+    p = synth.make_pair(99, n_kpts=1500)
+    ref, _, _, _ = oracle.match_two_image(p["desc_l"], p["desc_r"])
+    q = torch.from_numpy(p["desc_l"]).cuda()
+    t = torch.from_numpy(p["desc_r"]).cuda()
+    out = feature_matcher(ctx=ctx).match_two_image(q, t).cpu().numpy()
+    assert np.array_equal(out.view(np.uint32).reshape(-1), ref.view(np.uint32).reshape(-1))
+
+
+# --------------------------------------------------------------------------- estimator
+def _check_hyps(gh, oh, tol=2e-6):
+    for a, b in zip(gh, oh):
+        assert a["R1_valid"] + a["R2_valid"] == b["R1_valid"] + b["R2_valid"]
+        same = max(np.abs(a["R1"] - b["R1"]).max(), np.abs(a["R2"] - b["R2"]).max())
+        swap = max(np.abs(a["R1"] - b["R2"]).max(), np.abs(a["R2"] - b["R1"]).max())
+        assert min(same, swap) <= tol
+        assert np.abs(a["T"] - b["T"]).max() <= tol
+        e = min(np.abs(a["E"] - b["E"]).max(), np.abs(a["E"] + b["E"]).max())
+        assert e <= 1e-8
+
+
+def _run_find_dev(ctx, kl, kr, W, H, iters):
+    import ctypes as C
+    import torch
+    from erp_match_eightpoint_test_amd import capi, hyps_to_numpy
+    cfg = capi.default_cfg(iters=iters)
+    m = kl.shape[0]
+    dkl = torch.from_numpy(np.ascontiguousarray(kl, np.float32)).cuda()
+    dkr = torch.from_numpy(np.ascontiguousarray(kr, np.float32)).cuda()
+    res = torch.zeros(capi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    hyp = torch.zeros((iters, capi.HYP_DTYPE.itemsize), dtype=torch.uint8, device="cuda")
+    st = ctx.L.erp_eight_point_find_dev(ctx.h, W, H, dkl.data_ptr(), dkr.data_ptr(), m,
+                                        C.byref(cfg), res.data_ptr(), hyp.data_ptr(),
+                                        torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    r = res.cpu().numpy().view(capi.RESULT_DTYPE)[0]
+    return st, r, hyps_to_numpy(hyp.unsqueeze(0))[0]
+
+
+def test_find_golden_fixture(ctx):
+    g = _npz("find_400_it80.npz")
+    st, r, hyps = _run_find_dev(ctx, g["kl"], g["kr"], int(g["W"]), int(g["H"]), 80)
+    assert st == 0 and r["status"] == 0
+    _check_hyps(hyps, g["hyp"])
+    assert r["K"] == int(g["K"])
+    assert np.abs(r["R"] - g["R"]).max() <= 2e-6
+    assert np.abs(r["T"] - g["T"]).max() <= 2e-6
+    # KAT: the recovered rotation is the synthetic ground truth (two_synthesis_image_test)
+    assert np.degrees(np.abs(r["R"] - g["euler_gt"])).mean() < 1.0
+
+
+def test_find_host_api_matches_dev(ctx):
+    from erp_match_eightpoint_test_amd import eight_point
+    g = _npz("find_400_it80.npz")
+    ep = eight_point(ctx=ctx)
+    R, T = ep.find(int(g["W"]), int(g["H"]), g["kl"], g["kr"], 400)
+    assert np.abs(R - g["R"]).max() <= 2e-6 and np.abs(T - g["T"]).max() <= 2e-6
+
+
+def test_find_manual_regime_fixture(ctx):
+    g = _npz("find_manual_100_it500.npz")
+    st, r, hyps = _run_find_dev(ctx, g["kl"], g["kr"], int(g["W"]), int(g["H"]), 500)
+    assert st == 0 and r["status"] == 0
+    _check_hyps(hyps, g["hyp"])
+    assert r["K"] == int(g["K"])
+    assert np.abs(r["R"] - g["R"]).max() <= 2e-6
+    assert np.abs(r["T"] - g["T"]).max() <= 2e-6
+
+
+@pytest.mark.parametrize("m", [4, 8, 20, 35, 36])
+def test_find_thin_svd_edges(ctx, m):
+    g = _npz("find_edges.npz")
+    st, r, hyps = _run_find_dev(ctx, g[f"m{m}_kl"], g[f"m{m}_kr"], 5376, 2688, 80)
+    assert st == int(g[f"m{m}_status"]) == 0
+    if m >= 8:  # sample_n = 1 (m = 4) is rank-1: the rank-2 fix / decomposition is
+        # ill-posed there (documented), so only the sampled sets and E are compared
+        _check_hyps(hyps, g[f"m{m}_hyp"])
+        assert np.abs(r["R"] - g[f"m{m}_R"]).max() <= 2e-6
+    else:
+        for a, b in zip(hyps, g[f"m{m}_hyp"]):
+            assert min(np.abs(a["E"] - b["E"]).max(), np.abs(a["E"] + b["E"]).max()) <= 1e-8
+
+
+def test_find_too_few_points(ctx):
+    from erp_match_eightpoint_test_amd import ErpError, eight_point
+    ep = eight_point(ctx=ctx)
+    with pytest.raises(ErpError) as ei:
+        ep.find(5376, 2688, np.zeros((3, 2), np.float32), np.zeros((3, 2), np.float32), 3)
+    assert ei.value.status == 2
+
+
+def test_eight_point_estimation_api(ctx, oracle):
+    from erp_match_eightpoint_test_amd import eight_point
+    c = synth.make_correspondences(7, m=40, outlier_frac=0.0, W=2048, H=1024)
+    bl = oracle.pixel_to_bearing(2048, 1024, c["kp_l"])
+    br = oracle.pixel_to_bearing(2048, 1024, c["kp_r"])
+    ho = oracle.eight_point_estimation(bl, br)
+    R1, R2, T, v1, v2, E = eight_point(ctx=ctx).eight_point_estimation(2048, 1024, bl, br)
+    same = max(np.abs(R1 - ho["R1"]).max(), np.abs(R2 - ho["R2"]).max())
+    swap = max(np.abs(R1 - ho["R2"]).max(), np.abs(R2 - ho["R1"]).max())
+    assert min(same, swap) <= 2e-6
+    assert np.abs(T - ho["T"]).max() <= 2e-6
+    assert min(np.abs(E - ho["E"]).max(), np.abs(E + ho["E"]).max()) <= 1e-8
+
+
+# ---------------------------------------------------------------------- batch pipeline
+def _batch(pairs, device="cuda"):
+    import torch
+    dl = np.concatenate([p["desc_l"] for p in pairs])
+    dr = np.concatenate([p["desc_r"] for p in pairs])
+    kl = np.concatenate([p["kp_l"] for p in pairs])
+    kr = np.concatenate([p["kp_r"] for p in pairs])
+    ol = np.concatenate([[0], np.cumsum([len(p["desc_l"]) for p in pairs])]).astype(np.int64)
+    orr = np.concatenate([[0], np.cumsum([len(p["desc_r"]) for p in pairs])]).astype(np.int64)
+    W = np.array([p["W"] for p in pairs], np.int32)
+    H = np.array([p["H"] for p in pairs], np.int32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+    return (t(dl), t(dr), t(kl), t(kr), t(ol), t(orr), t(W), t(H),
+            int(np.diff(ol).max()), int(np.diff(orr).max()))
+
+
+def test_batch_pipeline_vs_oracle(ctx, oracle):
+    from erp_match_eightpoint_test_amd import PairBatchRunner, hyps_to_numpy, results_to_numpy
+    import torch
+    pairs = [synth.make_pair(1000 + i, n_kpts=n) for i, n in enumerate([512, 700, 300, 1024])]
+    args = _batch(pairs)
+    run = PairBatchRunner(ctx=ctx, iters=200)
+    outs = run.run(*args, want=("matches", "hyps", "samples", "rvec", "dist"))
+    torch.cuda.synchronize()
+    res = results_to_numpy(outs["results"])
+    hyps = hyps_to_numpy(outs["hyps"])
+    for i, p in enumerate(pairs):
+        ref, _, _, _ = oracle.match_two_image(p["desc_l"], p["desc_r"])
+        M = len(ref)
+        assert res[i]["M"] == M
+        got = outs["matches"][i, :M].cpu().numpy()
+        assert np.array_equal(got.view(np.uint32).reshape(-1), ref.view(np.uint32).reshape(-1))
+        kl = p["kp_l"][ref["queryIdx"]]
+        kr = p["kp_r"][ref["trainIdx"]]
+        o = oracle.find(p["W"], p["H"], kl, kr, oracle.make_cfg(iters=200), detail=True)
+        s = o["sample_n"]
+        got_s = np.sort(outs["samples"][i, :, :s].cpu().numpy(), axis=1)
+        assert np.array_equal(got_s, np.sort(o["samples"], axis=1))
+        _check_hyps(hyps[i], o["hyp"])
+        assert res[i]["K"] == o["K"]
+        assert np.abs(res[i]["R"] - o["R"]).max() <= 2e-6
+        assert np.abs(res[i]["T"] - o["T"]).max() <= 2e-6
+        # consensus: the oracle's trimmed means on the GPU's own R list pick the same winner
+        K = o["K"]
+        rv = outs["rvec"][i, :K].cpu().numpy()
+        _, mi, dref = oracle.consensus(rv)
+        assert mi == res[i]["min_idx"] or np.array_equal(rv[mi], rv[res[i]["min_idx"]])
+        d = outs["dist"][i, :K].cpu().numpy()
+        assert np.allclose(d, dref, rtol=1e-12, atol=0)
+
+
+def test_batch_full_size_properties(ctx, oracle):
+    """configs[1] shape: 4096 x 4096 keypoints, 10k iterations.  Size-independent checks:
+    matches bit-exact vs the oracle, sampled sets of a spread of iterations vs the oracle's
+    glibc replay (jump-ahead across 10k * (M-1) draws), KAT on the recovered rotation."""
+    import torch
+    from erp_match_eightpoint_test_amd import PairBatchRunner, results_to_numpy
+    p = synth.make_pair(20200423, n_kpts=4096)
+    args = _batch([p])
+    run = PairBatchRunner(ctx=ctx, iters=10000)
+    outs = run.run(*args, want=("matches", "samples"))
+    torch.cuda.synchronize()
+    r = results_to_numpy(outs["results"])[0]
+    ref, _, _, _ = oracle.match_two_image(p["desc_l"], p["desc_r"], nthreads=8)
+    M = len(ref)
+    assert r["status"] == 0 and r["M"] == M
+    got = outs["matches"][0, :M].cpu().numpy()
+    assert np.array_equal(got.view(np.uint32).reshape(-1), ref.view(np.uint32).reshape(-1))
+    s = int(M * 0.25)
+    g = oracle.GlibcRand(1)
+    samples = outs["samples"][0].cpu().numpy()
+    check = {0, 1, 63, 64, 65, 127, 4095, 9999}
+    for it in range(10000):
+        a = g.random_array(M)
+        if it in check:
+            assert np.array_equal(np.sort(samples[it, :s]), np.sort(a[:s])), it
+    assert np.degrees(np.abs(r["R"] - p["euler_gt"])).mean() < 1.0
