@@ -77,7 +77,7 @@ def stage_work(stage, B, kpts, iters, res):
     if stage == "knn2_partial":
         flops = 3.0 * kpts * kpts * 64 * B  # sub, mul, add per element (flann::L2 order, no FMA)
         return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", "3*N*T*64 fp32 ops per pair"
-    if stage == "sampler_gram":
+    if stage == "gram":
         flops = float(np.sum(s * iters * (12 + 72)))  # 12 mul + 36 FMA per sampled row, fp64
         return flops, "TFLOP/s", PEAK_FP64_VALU, "valu", "84 fp64 flops per sampled row"
     if stage == "consensus_rows":
@@ -145,7 +145,7 @@ def main():
                               b["off_r"], b["width"], b["height"], b["max_nq"], b["max_nt"])
     gathered = None
     if dist is not None:
-        gathered = torch.empty((world, args.pairs, 56), dtype=torch.uint8, device=dev)
+        gathered = torch.empty((world, args.pairs, 64), dtype=torch.uint8, device=dev)
     for _ in range(args.warmup):
         out = call()
         if dist is not None:
@@ -209,7 +209,9 @@ def main():
         "cpu_baseline": cpu,
         "stages_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in stages.items()},
         "check": {"all_status_ok": ok, "mean_abs_euler_err_deg_max": max(err_deg),
-                  "M_mean": float(res["M"].mean()), "K_mean": float(res["K"].mean())},
+                  "M_mean": float(res["M"].mean()), "K_mean": float(res["K"].mean()),
+                  "consensus_survivors": res["survivors"].tolist(),
+                  "near_ties": res["near_ties"].tolist()},
     }
     print(json.dumps(line))
     if dist is not None:

@@ -51,7 +51,8 @@ class Hypothesis(C.Structure):
 class PairResult(C.Structure):
     _fields_ = [("R", C.c_float * 3), ("T", C.c_float * 3), ("status", C.c_int32),
                 ("M", C.c_int32), ("K", C.c_int32), ("min_idx", C.c_int32),
-                ("sample_n", C.c_int32), ("near_ties", C.c_int32), ("min_dist", C.c_double)]
+                ("sample_n", C.c_int32), ("near_ties", C.c_int32), ("survivors", C.c_int32),
+                ("reserved", C.c_int32), ("min_dist", C.c_double)]
 
 
 class PairBatch(C.Structure):
@@ -71,10 +72,11 @@ HYP_DTYPE = np.dtype([("R1", "<f4", 3), ("R2", "<f4", 3), ("T", "<f4", 3), ("R1_
                       ("R2_valid", "<i4"), ("E", "<f8", 9)], align=True)
 RESULT_DTYPE = np.dtype([("R", "<f4", 3), ("T", "<f4", 3), ("status", "<i4"), ("M", "<i4"),
                          ("K", "<i4"), ("min_idx", "<i4"), ("sample_n", "<i4"),
-                         ("near_ties", "<i4"), ("min_dist", "<f8")], align=True)
+                         ("near_ties", "<i4"), ("survivors", "<i4"), ("reserved", "<i4"),
+                         ("min_dist", "<f8")], align=True)
 assert DMATCH_DTYPE.itemsize == C.sizeof(DMatch) == 16
 assert HYP_DTYPE.itemsize == C.sizeof(Hypothesis) == 120
-assert RESULT_DTYPE.itemsize == C.sizeof(PairResult) == 56
+assert RESULT_DTYPE.itemsize == C.sizeof(PairResult) == 64
 assert C.sizeof(RansacCfg) == 56
 
 # every symbol include/erp_match.h declares (checked by tests/test_capi_symbols.py)
@@ -83,8 +85,9 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_eight_point_find_dev", "erp_eight_point_find", "erp_initial_guess",
             "erp_eight_point_estimation", "erp_pair_batch_run", "erp_ctx_set_profiling",
             "erp_stage_name", "erp_ctx_stage_times"]
-STAGES = ["knn2_partial", "knn2_merge", "bearings", "jump_prep", "sampler_gram", "eigen",
-          "valid_compact", "consensus_rows", "consensus_final"]
+STAGES = ["knn2_partial", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
+          "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
+          "consensus_select", "windows", "gram"]
 
 
 class ErpError(RuntimeError):

@@ -69,7 +69,8 @@ struct erp_ctx {
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
     DevBuf part, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
-        sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d;
+        sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins;
+    double2* rtab = nullptr;
     bool w0_valid = false;
     uint32_t w0_seed = 0;
     uint64_t w0_offset = 0;
@@ -150,6 +151,11 @@ erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
     if (!c) return ERP_OUT_OF_MEMORY;
     c->device = device;
     erp::init_constants();
+    c->rtab = erp::make_recip_table();
+    if (!c->rtab) {
+        delete c;
+        return ERP_OUT_OF_MEMORY;
+    }
     *out = c;
     return ERP_OK;
 }
@@ -160,10 +166,12 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
     DevBuf* all[] = {&ctx->part, &ctx->matches, &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
                      &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
-                     &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d};
+                     &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
+                     &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->rtab) (void)hipFree(ctx->rtab);
     delete ctx;
     return ERP_OK;
 }
@@ -195,12 +203,16 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
     const size_t P = (size_t)sh.n_pairs;
     const size_t nwaves = (size_t)(sh.iters + 63) / 64;
     bool ok = ensure(c->counts, P * 4) && ensure(c->flags, P * 4) &&
-              ensure(c->pts, P * sh.max_nq * 48) && ensure(c->polyR, P * 65 * 31 * 4) &&
+              ensure(c->pts, P * (sh.max_nq + 1) * 48) &&
+              ensure(c->wins, P * nwaves * 31 * 64 * 4) && ensure(c->polyR, P * 65 * 31 * 4) &&
               ensure(c->polyQ, P * erp::kMaxQ * 31 * 4) &&
               ensure(c->idx, P * nwaves * (size_t)sh.idx_stride * 64 * 2) &&
               ensure(c->gram, P * sh.iters * 36 * 8) && ensure(c->rv, P * 6 * sh.iters * 4) &&
               ensure(c->kcount, P * 4) && ensure(c->sortbuf, P * (size_t)erp::sortbuf_len(sh.iters) * 4) &&
-              ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result));
+              ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result)) &&
+              ensure(c->dscale, P * 4) && ensure(c->lb, P * 2 * sh.iters * 8) &&
+              ensure(c->ub, P * 2 * sh.iters * 8) && ensure(c->surv, P * 2 * sh.iters * 4) &&
+              ensure(c->nsurv, P * 4);
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
     if (ok && !(out && out->dist)) ok = ensure(c->tmean, P * 2 * sh.iters * 8);
@@ -240,11 +252,22 @@ erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         ERP_CK(erp::launch_jump_prep(counts, sh, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p, st));
     }
     {
-        StageTimer _t(ctx, ERP_STAGE_SAMPLER_GRAM, st);
-        ERP_CK(erp::launch_sampler_gram(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
-                                        (uint32_t*)c->w0.p, (double*)c->pts.p, sh, cfg->sample_frac,
-                                        (uint16_t*)c->idx.p, (double*)c->gram.p,
-                                        out ? out->samples : nullptr, flags, st));
+        StageTimer _t(ctx, ERP_STAGE_WINDOWS, st);
+        ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
+                                   (uint32_t*)c->w0.p, c->rtab, sh, cfg->sample_frac,
+                                   (uint32_t*)c->wins.p, (uint16_t*)c->idx.p, flags, st, 0));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
+        ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
+                                   (uint32_t*)c->w0.p, c->rtab, sh, cfg->sample_frac,
+                                   (uint32_t*)c->wins.p, (uint16_t*)c->idx.p, flags, st, 1));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_GRAM, st);
+        ERP_CK(erp::launch_gram(counts, (double*)c->pts.p, (uint16_t*)c->idx.p, sh,
+                                cfg->sample_frac, (double*)c->gram.p, out ? out->samples : nullptr,
+                                st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
@@ -254,17 +277,31 @@ erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     {
         StageTimer _t(ctx, ERP_STAGE_VALID_COMPACT, st);
         ERP_CK(erp::launch_valid_compact(counts, hyps, sh, cfg->sample_frac, (float*)c->rv.p, tv,
-                                         (int32_t*)c->kcount.p, out ? out->rvec : nullptr, st));
+                                         (int32_t*)c->kcount.p, out ? out->rvec : nullptr,
+                                         (float*)c->dscale.p, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
+        ERP_CK(erp::launch_consensus_bounds((int32_t*)c->kcount.p, (float*)c->rv.p,
+                                            (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
+                                            (double*)c->lb.p, (double*)c->ub.p, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
+        ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, (double*)c->lb.p,
+                                            (double*)c->ub.p, sh, cfg->trim_lo, cfg->trim_hi,
+                                            (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_ROWS, st);
         ERP_CK(erp::launch_consensus_rows((int32_t*)c->kcount.p, (float*)c->rv.p, sh, cfg->trim_lo,
-                                          cfg->trim_hi, tmean, st));
+                                          cfg->trim_hi, (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
+                                          tmean, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_FINAL, st);
         ERP_CK(erp::launch_consensus_final(counts, (int32_t*)c->kcount.p, (float*)c->rv.p, tv, tmean,
-                                           flags, sh, cfg->sample_frac, cfg->trim_lo, cfg->trim_hi,
+                                           flags, (int32_t*)c->nsurv.p, sh, cfg->sample_frac, cfg->trim_lo, cfg->trim_hi,
                                            (float*)c->sortbuf.p, results, st));
     }
     return ERP_OK;
@@ -283,8 +320,9 @@ erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable) {
 
 const char* erp_stage_name(int32_t stage) {
     static const char* names[ERP_STAGE_COUNT] = {
-        "knn2_partial", "knn2_merge", "bearings", "jump_prep", "sampler_gram",
-        "eigen", "valid_compact", "consensus_rows", "consensus_final"};
+        "knn2_partial", "knn2_merge", "bearings", "jump_prep", "sampler",
+        "eigen", "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
+        "consensus_select", "windows", "gram"};
     return (stage >= 0 && stage < ERP_STAGE_COUNT) ? names[stage] : "unknown";
 }
 
@@ -502,13 +540,13 @@ erp_status erp_initial_guess(erp_ctx* ctx, const double* h_bl, const double* h_b
         if (!ensure(ctx->in_c, sizeof(erp_pair_result))) return ERP_OUT_OF_MEMORY;
         es = upload_w0(ctx, cfg, nullptr);
         if (es != ERP_OK) return es;
-        std::vector<double> pts((size_t)std::max(m, 1) * 6);
+        std::vector<double> pts((size_t)(m + 1) * 6, 0.0);
         for (int32_t i = 0; i < m; i++)
             for (int k = 0; k < 3; k++) {
                 pts[(size_t)i * 6 + k] = h_bl[(size_t)i * 3 + k];
                 pts[(size_t)i * 6 + 3 + k] = h_br[(size_t)i * 3 + k];
             }
-        ERP_CK(hipMemcpy(ctx->pts.p, pts.data(), (size_t)m * 48, hipMemcpyHostToDevice));
+        ERP_CK(hipMemcpy(ctx->pts.p, pts.data(), (size_t)(m + 1) * 48, hipMemcpyHostToDevice));
         ERP_CK(hipMemcpy(ctx->counts.p, &m, 4, hipMemcpyHostToDevice));
         ERP_CK(hipMemset(ctx->flags.p, 0, 4));
         es = run_estimator(ctx, sh, cfg, nullptr, (erp_pair_result*)ctx->in_c.p, nullptr);

@@ -23,7 +23,7 @@ struct Workspace {
     Top2* part;                   // [pairs][chunks][max_nq]
     erp_dmatch* matches;          // [pairs][max_nq]
     int32_t* counts;              // [pairs] M
-    double* pts;                  // [pairs][max_nq][6] bearings (l, r)
+    double* pts;                  // [pairs][max_nq + 1][6] bearings (l, r); last row = 0
     uint32_t* polyR;              // [pairs][65][31]  x^(l(M-1)) mod P
     uint32_t* polyQ;              // [pairs][kMaxQ][31]
     uint16_t* idx;                // [pairs][iters_pad][max_s] sample lists (wave-interleaved)
@@ -47,6 +47,7 @@ struct BatchShape {
 };
 
 void init_constants();            // reduction table for the jump polynomials (once per device)
+double2* make_recip_table();      // (1/d, d), d <= 65536, device memory (once per context)
 
 hipError_t launch_knn2_partial(const float* desc_q, const float* desc_t, const int64_t* off_q,
                                const int64_t* off_t, const BatchShape& sh, Top2* part,
@@ -64,24 +65,35 @@ hipError_t launch_bearings_direct(const erp_point2f* kl, const erp_point2f* kr, 
                                   int32_t W, int32_t H, double* pts, hipStream_t st);
 hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_t* polyR,
                             uint32_t* polyQ, hipStream_t st);
-hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
-                               const uint32_t* w0, const double* pts, const BatchShape& sh,
-                               double sample_frac, uint16_t* idx, double* gram, int32_t* samples,
-                               int32_t* flags, hipStream_t st);
+// part 0: lane end windows (jump-ahead); part 1: the backwards replay -> sample index lists
+hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
+                          const uint32_t* w0, const double2* rtab, const BatchShape& sh,
+                          double sample_frac, uint32_t* wins, uint16_t* idx, int32_t* flags,
+                          hipStream_t st, int part);
+hipError_t launch_gram(const int32_t* counts, const double* pts, const uint16_t* idx,
+                       const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
+                       hipStream_t st);
 hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
                         double sample_frac, double valid_abs, erp_hypothesis* hyps,
                         hipStream_t st);
 hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyps,
                                 const BatchShape& sh, double sample_frac, float* rv, float* tv,
-                                int32_t* kcount, float* rv_aos, hipStream_t st);
+                                int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st);
 hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream_t st);
+hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
+                                   const BatchShape& sh, double trim_lo, double trim_hi, double* lb,
+                                   double* ub, hipStream_t st);
+hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
+                                   const BatchShape& sh, double trim_lo, double trim_hi,
+                                   int32_t* surv, int32_t* nsurv, double* tmean, hipStream_t st);
 hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const BatchShape& sh,
-                                 double trim_lo, double trim_hi, double* tmean, hipStream_t st);
+                                 double trim_lo, double trim_hi, const int32_t* surv,
+                                 const int32_t* nsurv, double* tmean, hipStream_t st);
 hipError_t launch_consensus_final(const int32_t* counts, const int32_t* kcount, const float* rv,
                                   const float* tv, const double* tmean, const int32_t* flags,
-                                  const BatchShape& sh, double sample_frac, double trim_lo,
-                                  double trim_hi, float* sortbuf, erp_pair_result* results,
-                                  hipStream_t st);
+                                  const int32_t* nsurv, const BatchShape& sh, double sample_frac,
+                                  double trim_lo, double trim_hi, float* sortbuf,
+                                  erp_pair_result* results, hipStream_t st);
 int sortbuf_len(int iters);        // power of two >= 2*iters (exact tie re-scoring scratch)
 
 }  // namespace erp

@@ -18,6 +18,7 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "erp_device.hpp"
 #include "erp_kernels.hpp"
@@ -195,11 +196,15 @@ __global__ void bearings_from_matches_kernel(const erp_dmatch* __restrict__ matc
                                              erp_point2f* key_r) {
     const int p = blockIdx.y;
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m == 0) {  // zero sentinel row used to pad Gram batches
+        double* z = pts + ((size_t)p * (max_nq + 1) + max_nq) * 6;
+        for (int k = 0; k < 6; k++) z[k] = 0.0;
+    }
     if (m >= counts[p]) return;
     const erp_dmatch dm = matches[(size_t)p * max_nq + m];
     const erp_point2f kl = kp_l[off_l[p] + dm.queryIdx];
     const erp_point2f kr = kp_r[off_r[p] + dm.trainIdx];
-    double* o = pts + ((size_t)p * max_nq + m) * 6;
+    double* o = pts + ((size_t)p * (max_nq + 1) + m) * 6;
     pixel_to_bearing(width[p], height[p], kl.x, kl.y, o);
     pixel_to_bearing(width[p], height[p], kr.x, kr.y, o + 3);
     if (key_l) key_l[(size_t)p * max_nq + m] = kl;
@@ -210,6 +215,8 @@ __global__ void bearings_direct_kernel(const erp_point2f* __restrict__ kl,
                                        const erp_point2f* __restrict__ kr, int m, int W, int H,
                                        double* __restrict__ pts) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0)
+        for (int k = 0; k < 6; k++) pts[(size_t)m * 6 + k] = 0.0;  // zero sentinel row
     if (i >= m) return;
     pixel_to_bearing(W, H, kl[i].x, kl[i].y, pts + (size_t)i * 6);
     pixel_to_bearing(W, H, kr[i].x, kr[i].y, pts + (size_t)i * 6 + 3);
@@ -328,31 +335,23 @@ __device__ void apply_coop(const uint32_t* __restrict__ c, uint32_t* win, uint32
 //   steps i <  s: track the set T of prefix positions whose value is still unresolved
 //                 (initially the positions never hit by a step >= s); reverse step i emits i
 //                 iff j_i is in T, and then T[j_i] := T[i].
-// The emitted indices (exactly s of them) are written to a per-lane list, then the lane
-// accumulates the 36 distinct Gram values sum (l l^T)_(ik) (r r^T)_(jl) of its rows in fp64.
-__global__ __launch_bounds__(64) void sampler_gram_kernel(
+// Three kernels: windows (jump-ahead to each lane's end window), sampler (the replay, writing
+// exactly s indices per lane), gram (36 distinct Gram values of the sampled rows, fp64).
+
+// lane end windows: win[p][w][t][lane] = r[base + (64w + lane + 1)(M-1) + t]
+__global__ __launch_bounds__(64) void sampler_window_kernel(
     const int32_t* __restrict__ counts, const uint32_t* __restrict__ polyR,
-    const uint32_t* __restrict__ polyQ, const uint32_t* __restrict__ w0,
-    const double* __restrict__ pts, int max_nq, int iters, int nwaves, int idx_stride,
-    double sample_frac, uint16_t* __restrict__ idx, double* __restrict__ gram,
-    int32_t* __restrict__ samples, int32_t* __restrict__ flags) {
-    extern __shared__ uint32_t shm[];
-    uint32_t* win = shm;        // 32
-    uint32_t* ext = shm + 32;   // 64
-    uint32_t* bm = shm + 96;    // [nwords][64]
+    const uint32_t* __restrict__ polyQ, const uint32_t* __restrict__ w0, int nwaves,
+    double sample_frac, uint32_t* __restrict__ wins) {
+    __shared__ uint32_t win[32], ext[64];
     const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
     const int M = counts[p];
-    const int s = (int)(M * sample_frac);
-    if (s < 1 || M < 2) return;
-    const int h = w * 64 + lane;
-    const int nwords = (s + 31) >> 5;
-    for (int k = 0; k < nwords; k++) bm[k * 64 + lane] = 0u;
+    if ((int)(M * sample_frac) < 1 || M < 2) return;
     if (lane < 31) win[lane] = w0[lane];
     __syncthreads();
     const uint32_t* Q = polyQ + (size_t)p * kMaxQ * 31;
     for (int k = 0; k < kMaxQ && (w >> k); k++)
         if ((w >> k) & 1) apply_coop(Q + k * 31, win, ext);
-    // extend the wave's base window to 61 words
     if (lane < 31) ext[lane] = win[lane];
     __syncthreads();
     if (lane == 0) {
@@ -366,92 +365,176 @@ __global__ __launch_bounds__(64) void sampler_gram_kernel(
         }
     }
     __syncthreads();
-    // this lane's END window: x^((lane+1)(M-1)) applied to the wave base
+    uint32_t e[61];
+#pragma unroll
+    for (int k = 0; k < 61; k++) e[k] = ext[k];
+    const uint32_t* R = polyR + ((size_t)p * 65 + (lane + 1)) * 31;
+    uint32_t c[31];
+#pragma unroll
+    for (int j = 0; j < 31; j++) c[j] = R[j];
+    uint32_t* o = wins + ((size_t)p * nwaves + w) * 31 * 64 + lane;
+#pragma unroll
+    for (int t = 0; t < 31; t++) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < 31; j++) acc += c[j] * e[t + j];
+        o[t * 64] = acc;
+    }
+}
+
+// exact j = x mod d for x < 2^31, 1 <= d <= 65536.  1/d from v_rcp_f64 + one Newton step
+// (relative error << 2^-40), q0 = trunc(x/d) is then off by at most one, and the remainder
+// x - q0*d is exact in fp64 (fma), so a two-sided correction gives the exact result.
+// Everything stays in VALU: a table in memory would need SMEM/LDS loads whose lgkmcnt waits
+// also drain the replay's in-flight LDS atomics.
+__device__ __forceinline__ double recip_nr(double dd) {
+    const double r0 = __builtin_amdgcn_rcp(dd);
+    return __builtin_fma(r0, __builtin_fma(-dd, r0, 1.0), r0);
+}
+
+__device__ __forceinline__ uint32_t mod_by_recip(uint32_t x, double rinv, double dd, uint32_t d) {
+    const double xd = (double)x;
+    const double q0 = __builtin_trunc(xd * rinv);
+    int32_t j = (int32_t)__builtin_fma(-q0, dd, xd);
+    j = j < 0 ? j + (int32_t)d : j;
+    return (uint32_t)j >= d ? (uint32_t)j - d : (uint32_t)j;
+}
+
+__global__ __launch_bounds__(64) void sampler_kernel(
+    const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins,
+    const double2* __restrict__ rtab, int nwaves, int idx_stride, double sample_frac,
+    uint16_t* __restrict__ idx, int32_t* __restrict__ flags, int dbg) {
+    extern __shared__ uint32_t bm[];  // [nwords][64]
+    const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || M < 2) return;
+    const int nwords = (s + 31) >> 5;
+    for (int k = 0; k < nwords; k++) bm[k * 64 + lane] = 0u;
     uint32_t ring[31];
     {
-        const uint32_t* R = polyR + ((size_t)p * 65 + (lane + 1)) * 31;
-        uint32_t c[31];
+        const uint32_t* wi = wins + ((size_t)p * nwaves + w) * 31 * 64 + lane;
 #pragma unroll
-        for (int j = 0; j < 31; j++) c[j] = R[j];
-#pragma unroll
-        for (int t = 0; t < 31; t++) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int j = 0; j < 31; j++) acc += c[j] * ext[t + j];
-            ring[t] = acc;
-        }
+        for (int t = 0; t < 31; t++) ring[t] = wi[t * 64];
     }
     uint16_t* my = idx + ((size_t)p * nwaves + w) * (size_t)idx_stride * 64 + lane;
     int emitted = 0;
     int i = M - 1;
-    uint32_t cur = 0;
-    int curw = -1;
+    // Every step runs the same branch-free sequence (phase A = i >= s, phase B = i < s):
+    //   A: valid = j < s;   seen[j] |= bit;                emit = valid && !old
+    //   B: valid = j != i;  seen[j] := !T[i] (and + or);   emit = valid ? !old : T[i]
+    // The old words of a block's 31 steps are consumed only after the block, so the LDS
+    // atomics stream without waits.  Phase B needs the bitmap words holding positions
+    // i0..i0-30 (at most two): they are read once at the block start and mirrored in
+    // registers (curA/curB) -- a read inside the block would wait for every in-flight atomic.
+    uint32_t last0 = 0;
     while (i >= 1) {
+        const int i0 = i;
+        const int wA = i0 >> 5;
+        const int wB = (i0 - 30) > 0 ? (i0 - 30) >> 5 : 0;
+        uint32_t curA = 0, curB = 0;
+        if (i0 - 30 < s) {
+            curA = bm[wA * 64 + lane];
+            curB = bm[wB * 64 + lane];
+        }
+        uint32_t olds[31], bitsel[31];
+        uint32_t emask = 0, vmask = 0;
 #pragma unroll
         for (int u = 0; u < 31; u++) {
-            if (i >= 1) {
-                const int slot = 30 - u;
-                const uint32_t rv = ring[slot];
-                ring[slot] = rv - ring[(slot + 28) % 31];
-                const uint32_t x = rv >> 1;
-                const uint32_t j = x % (uint32_t)(i + 1);
-                bool em = false;
-                if (i >= s) {
-                    if (j < (uint32_t)s) {
-                        const uint32_t bit = 1u << (j & 31);
-                        const uint32_t old = atomicOr(&bm[(j >> 5) * 64 + lane], bit);
-                        em = !(old & bit);
-                    }
-                } else {
-                    const int wi = i >> 5;
-                    if (wi != curw) {
-                        cur = bm[wi * 64 + lane];
-                        curw = wi;
-                    }
-                    const bool bT = !((cur >> (i & 31)) & 1u);
-                    if ((int)j == i) {
-                        em = bT;
-                    } else {
-                        const uint32_t bit = 1u << (j & 31);
-                        uint32_t* wp = &bm[(j >> 5) * 64 + lane];
-                        const uint32_t old = bT ? atomicAnd(wp, ~bit) : atomicOr(wp, bit);
-                        if ((int)(j >> 5) == wi) cur = bT ? (cur & ~bit) : (cur | bit);
-                        em = !(old & bit);
-                    }
-                }
-                if (em) {
-                    if (emitted < idx_stride) my[(size_t)emitted * 64] = (uint16_t)i;
-                    emitted++;
-                }
-                i--;
+            const int ii = i0 - u;              // uniform
+            const bool live = ii >= 1;
+            const bool isB = ii < s;
+            const int slot = 30 - u;
+            const uint32_t rv = ring[slot];
+            ring[slot] = rv - ring[(slot + 28) % 31];
+            const int dv = live ? ii + 1 : 2;
+            const double dd = (double)dv;
+            const uint32_t j = mod_by_recip(rv >> 1, recip_nr(dd), dd, (uint32_t)dv);
+            const uint32_t cw = ((ii >> 5) == wA) ? curA : curB;
+            const bool bT = isB && live && !((cw >> (ii & 31)) & 1u);
+            const uint32_t bit = 1u << (j & 31);
+            const bool valid = live && (isB ? (j != (uint32_t)ii) : (j < (uint32_t)s));
+            const uint32_t andm = (valid && isB) ? ~bit : 0xffffffffu;
+            const uint32_t orm = valid ? (bT ? 0u : bit) : 0u;
+            const uint32_t w = valid ? (j >> 5) : 0u;
+            uint32_t* wp = &bm[w * 64 + lane];
+            olds[u] = atomicAnd(wp, andm);
+            atomicOr(wp, orm);
+            curA = (w == (uint32_t)wA) ? ((curA & andm) | orm) : curA;
+            curB = (w == (uint32_t)wB) ? ((curB & andm) | orm) : curB;
+            bitsel[u] = valid ? bit : 0u;
+            vmask |= valid ? (1u << u) : 0u;
+            emask |= (live && isB && j == (uint32_t)ii && bT) ? (1u << u) : 0u;
+        }
+        i = i0 - 31;
+        if (i < 1) last0 = (wB == 0) ? curB : curA;  // word 0 after the final block
+#pragma unroll
+        for (int u = 0; u < 31; u++) {
+            const bool em = (((vmask >> u) & 1u) && !(olds[u] & bitsel[u])) || ((emask >> u) & 1u);
+            if (em) {
+                if (emitted < idx_stride && !(dbg & 1)) my[(size_t)emitted * 64] = (uint16_t)(i0 - u);
+                emitted++;
             }
         }
     }
+    if (dbg & 1) my[0] = (uint16_t)emitted;
     {
-        const uint32_t word0 = (curw == 0) ? cur : bm[lane];
+        (void)last0;
+        const uint32_t word0 = bm[lane];  // position 0 (after every atomic of the replay)
         if (!(word0 & 1u)) {
             if (emitted < idx_stride) my[(size_t)emitted * 64] = 0;
             emitted++;
         }
     }
     if (emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
-    // Gram of the s sampled rows
+}
+
+// Gram of each lane's s sampled rows; rows gathered 8 at a time so the index loads and the
+// 48-byte row gathers of a batch are all in flight together.  Row max_nq of pts is a zero
+// sentinel used to pad the last batch.
+__global__ __launch_bounds__(64) void gram_kernel(const int32_t* __restrict__ counts,
+                                                  const double* __restrict__ pts, int max_nq,
+                                                  int iters, int nwaves, int idx_stride,
+                                                  double sample_frac,
+                                                  const uint16_t* __restrict__ idx,
+                                                  double* __restrict__ gram,
+                                                  int32_t* __restrict__ samples) {
+    const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || M < 2) return;
+    const int h = w * 64 + lane;
+    const uint16_t* my = idx + ((size_t)p * nwaves + w) * (size_t)idx_stride * 64 + lane;
+    const double2* P = reinterpret_cast<const double2*>(pts + (size_t)p * (max_nq + 1) * 6);
     double g[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) g[k] = 0.0;
-    const double* P = pts + (size_t)p * max_nq * 6;
     const int n = min(s, idx_stride);
-    for (int k = 0; k < n; k++) {
-        const int v = my[(size_t)k * 64];
-        const double* pt = P + (size_t)v * 6;
-        const double l0 = pt[0], l1 = pt[1], l2 = pt[2], r0 = pt[3], r1 = pt[4], r2 = pt[5];
-        const double LL[6] = {l0 * l0, l0 * l1, l0 * l2, l1 * l1, l1 * l2, l2 * l2};
-        const double RR[6] = {r0 * r0, r0 * r1, r0 * r2, r1 * r1, r1 * r2, r2 * r2};
+    constexpr int B = 8;
+    for (int k0 = 0; k0 < n; k0 += B) {
+        int v[B];
 #pragma unroll
-        for (int a = 0; a < 6; a++)
+        for (int u = 0; u < B; u++) v[u] = (k0 + u < n) ? (int)my[(size_t)(k0 + u) * 64] : max_nq;
+        double2 a[B][3];
 #pragma unroll
-            for (int b = 0; b < 6; b++) g[6 * a + b] = __builtin_fma(LL[a], RR[b], g[6 * a + b]);
-        if (samples && h < iters) samples[((size_t)p * iters + h) * idx_stride + k] = v;
+        for (int u = 0; u < B; u++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) a[u][c] = P[(size_t)v[u] * 3 + c];
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            const double l0 = a[u][0].x, l1 = a[u][0].y, l2 = a[u][1].x;
+            const double r0 = a[u][1].y, r1 = a[u][2].x, r2 = a[u][2].y;
+            const double LL[6] = {l0 * l0, l0 * l1, l0 * l2, l1 * l1, l1 * l2, l2 * l2};
+            const double RR[6] = {r0 * r0, r0 * r1, r0 * r2, r1 * r1, r1 * r2, r2 * r2};
+#pragma unroll
+            for (int a6 = 0; a6 < 6; a6++)
+#pragma unroll
+                for (int b6 = 0; b6 < 6; b6++)
+                    g[6 * a6 + b6] = __builtin_fma(LL[a6], RR[b6], g[6 * a6 + b6]);
+        }
+        if (samples && h < iters)
+            for (int u = 0; u < B && k0 + u < n; u++)
+                samples[((size_t)p * iters + h) * idx_stride + k0 + u] = v[u];
     }
     if (h < iters) {
         double* go = gram + ((size_t)p * iters + h) * 36;
@@ -528,7 +611,8 @@ __global__ __launch_bounds__(1024) void valid_compact_kernel(const int32_t* __re
                                                              float* __restrict__ rv,
                                                              float* __restrict__ tv,
                                                              int32_t* __restrict__ kcount,
-                                                             float* __restrict__ rv_aos) {
+                                                             float* __restrict__ rv_aos,
+                                                             float* __restrict__ dscale) {
     __shared__ int ws[16];
     const int p = blockIdx.x;
     const int M = counts[p];
@@ -579,6 +663,46 @@ __global__ __launch_bounds__(1024) void valid_compact_kernel(const int32_t* __re
         }
     }
     if (threadIdx.x == 0) kcount[p] = total;
+    // bounding-box diagonal of the valid R set (>= every pairwise distance): the scale of
+    // the consensus bounds histogram
+    __syncthreads();
+    float mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+    for (int k = threadIdx.x; k < total; k += 1024) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const float v = X[c * stride + k];
+            mn[c] = fminf(mn[c], v);
+            mx[c] = fmaxf(mx[c], v);
+        }
+    }
+    __shared__ float red6[6][16];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        float a = mn[c], b = mx[c];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            a = fminf(a, __shfl_xor(a, o, 64));
+            b = fmaxf(b, __shfl_xor(b, o, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            red6[c][threadIdx.x >> 6] = a;
+            red6[3 + c][threadIdx.x >> 6] = b;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double d2 = 0;
+        for (int c = 0; c < 3; c++) {
+            float a = kInf, b = -kInf;
+            for (int w = 0; w < 16; w++) {
+                a = fminf(a, red6[c][w]);
+                b = fmaxf(b, red6[3 + c][w]);
+            }
+            const double e = total > 0 ? (double)b - (double)a : 0.0;
+            d2 += e * e;
+        }
+        dscale[p] = (float)(sqrt(d2) * (1.0 + 1e-6));
+    }
 }
 
 // ================================================================= consensus ============
@@ -625,14 +749,17 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
                                                              const float* __restrict__ rv,
                                                              int stride, double trim_lo,
                                                              double trim_hi,
+                                                             const int32_t* __restrict__ surv,
+                                                             const int32_t* __restrict__ nsurv,
                                                              double* __restrict__ tmean) {
     __shared__ uint32_t histA[2048], histB[2048];
     __shared__ int ws[8];
     __shared__ int res[2];
     __shared__ double red[256];
-    const int p = blockIdx.y, i = blockIdx.x, tid = threadIdx.x;
+    const int p = blockIdx.y, tid = threadIdx.x;
     const int K = kcount[p];
-    if (i >= K) return;
+    if ((int)blockIdx.x >= nsurv[p]) return;
+    const int i = surv[(size_t)p * stride + blockIdx.x];
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
@@ -721,6 +848,156 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     }
 }
 
+// ---- pruning by rigorous bounds -------------------------------------------------------
+// Every row's K distances (the reference's exact f32 values) are binned into NB geometric
+// bins (64 per binade over 20 binades below the set's diameter, underflow in bin 0).  From the
+// exact bin counts, the trimmed sum over ranks [lo, hi) is bracketed by
+//   LB = sum_b n_b(window) * lower_edge(b),  UB = sum_b n_b(window) * upper_edge(b)
+// (relative width <= 2^-6).  A row whose LB exceeds the smallest UB cannot be the argmin; only
+// the survivors get the exact order statistics.  8 rows share each column load.
+constexpr int kBoundRows = 8;
+constexpr int kBinsPerBinade = 64;
+constexpr int kBinades = 20;
+constexpr int kNB = kBinsPerBinade * kBinades;  // 1280
+
+__device__ __forceinline__ int bounds_elo(float D) {
+    int t = (int)(__float_as_uint(D) >> 23) + 1;
+    int e = t - kBinades;
+    return e < 1 ? 1 : e;
+}
+
+__device__ __forceinline__ float bin_lower(int elo, int b) {
+    return b == 0 ? 0.f : __uint_as_float((uint32_t)((elo << 6) + b) << 17);
+}
+__device__ __forceinline__ float bin_upper(int elo, int b) {
+    return b == kNB - 1 ? kInf : __uint_as_float((uint32_t)((elo << 6) + b + 1) << 17);
+}
+
+__global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __restrict__ kcount,
+                                                               const float* __restrict__ rv,
+                                                               const float* __restrict__ dscale,
+                                                               int stride, double trim_lo,
+                                                               double trim_hi,
+                                                               double* __restrict__ lb,
+                                                               double* __restrict__ ub) {
+    __shared__ uint32_t hist[kBoundRows][kNB];
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const int K = kcount[p];
+    const int r0 = blockIdx.x * kBoundRows;
+    if (r0 >= K) return;
+    const float* X = rv + (size_t)p * 3 * stride;
+    const float* Y = X + stride;
+    const float* Z = Y + stride;
+    const int elo = bounds_elo(dscale[p]);
+    const int base = elo << 6;
+    float xi[kBoundRows], yi[kBoundRows], zi[kBoundRows];
+#pragma unroll
+    for (int r = 0; r < kBoundRows; r++) {
+        const int row = min(r0 + r, K - 1);
+        xi[r] = X[row];
+        yi[r] = Y[row];
+        zi[r] = Z[row];
+    }
+    for (int k = tid; k < kBoundRows * kNB; k += 256) (&hist[0][0])[k] = 0u;
+    __syncthreads();
+    for (int j = tid; j < K; j += 256) {
+        const float xj = X[j], yj = Y[j], zj = Z[j];
+#pragma unroll
+        for (int r = 0; r < kBoundRows; r++) {
+            const uint32_t key = __float_as_uint(rdist(xi[r], yi[r], zi[r], xj, yj, zj));
+            int b = (int)(key >> 17) - base;
+            b = b < 0 ? 0 : (b > kNB - 1 ? kNB - 1 : b);
+            atomicAdd(&hist[r][b], 1u);
+        }
+    }
+    __syncthreads();
+    // per row: 32 threads x 40 bins
+    const long lo = (long)(K * trim_lo), hi = (long)(K * trim_hi);
+    const int r = tid >> 5, sl = tid & 31;
+    constexpr int per = kNB / 32;
+    uint32_t c = 0;
+    for (int b = sl * per; b < (sl + 1) * per; b++) c += hist[r][b];
+    // exclusive scan over the 32 lanes of this row (within one wave half)
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 32);
+        if (sl >= o) x += y;
+    }
+    long cum = (long)(x - c);
+    double L = 0.0, U = 0.0;
+    for (int b = sl * per; b < (sl + 1) * per; b++) {
+        const long n = hist[r][b];
+        const long a0 = cum > lo ? cum : lo;
+        const long a1 = (cum + n) < hi ? (cum + n) : hi;
+        if (a1 > a0) {
+            L += (double)(a1 - a0) * (double)bin_lower(elo, b);
+            U += (double)(a1 - a0) * (double)bin_upper(elo, b);
+        }
+        cum += n;
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        L += __shfl_xor(L, o, 32);
+        U += __shfl_xor(U, o, 32);
+    }
+    const int row = r0 + r;
+    if (sl == 0 && row < K) {
+        const double w = (double)(hi - lo);
+        // margins cover the reference's own rounding of its sorted sequential sum
+        lb[(size_t)p * stride + row] = hi > lo ? (L / w) * (1.0 - 1e-9) : 0.0;
+        ub[(size_t)p * stride + row] = hi > lo ? (U / w) * (1.0 + 1e-9) : 0.0;
+    }
+}
+
+// survivors: rows with LB <= min UB, in row order; pruned rows get tmean = +inf
+__global__ __launch_bounds__(1024) void consensus_select_kernel(const int32_t* __restrict__ kcount,
+                                                                const double* __restrict__ lb,
+                                                                const double* __restrict__ ub,
+                                                                int stride, double trim_lo,
+                                                                double trim_hi,
+                                                                int32_t* __restrict__ surv,
+                                                                int32_t* __restrict__ nsurv,
+                                                                double* __restrict__ tmean) {
+    __shared__ double sm[16];
+    __shared__ int ws[16];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int K = kcount[p];
+    const double* L = lb + (size_t)p * stride;
+    const double* U = ub + (size_t)p * stride;
+    double* Tm = tmean + (size_t)p * stride;
+    int32_t* S = surv + (size_t)p * stride;
+    const long lo = (long)(K * trim_lo), hi = (long)(K * trim_hi);
+    if (K <= 0) {
+        if (tid == 0) nsurv[p] = 0;
+        return;
+    }
+    if (hi <= lo) {  // empty window: every mean is 0/0 = NaN, std::min_element -> index 0
+        for (int k = tid; k < K; k += 1024) Tm[k] = __builtin_nan("");
+        if (tid == 0) nsurv[p] = 0;
+        return;
+    }
+    double m = __builtin_huge_val();
+    for (int k = tid; k < K; k += 1024) m = fmin(m, U[k]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o, 64));
+    if ((tid & 63) == 0) sm[tid >> 6] = m;
+    __syncthreads();
+    double minub = sm[0];
+    for (int w = 1; w < 16; w++) minub = fmin(minub, sm[w]);
+    const int per = (K + 1023) / 1024;
+    const int ka = min(K, tid * per), kb = min(K, ka + per);
+    int cnt = 0;
+    for (int k = ka; k < kb; k++) cnt += L[k] <= minub;
+    int total;
+    int pos = block_exclusive_scan<1024>(cnt, ws, &total);
+    for (int k = ka; k < kb; k++) {
+        if (L[k] <= minub) S[pos++] = k;
+        else Tm[k] = __builtin_huge_val();
+    }
+    if (tid == 0) nsurv[p] = total;
+}
+
 // exact sorted-sequential trimmed mean of one row (std::sort + std::accumulate semantics)
 __device__ double exact_row_mean(const float* X, const float* Y, const float* Z, int K, int i,
                                  long lo, long hi, float* buf, int npow2, double* sres) {
@@ -760,8 +1037,9 @@ __device__ double exact_row_mean(const float* X, const float* Y, const float* Z,
 __global__ __launch_bounds__(1024) void consensus_final_kernel(
     const int32_t* __restrict__ counts, const int32_t* __restrict__ kcount,
     const float* __restrict__ rv, const float* __restrict__ tv, const double* __restrict__ tmean,
-    const int32_t* __restrict__ flags, int stride, int npow2, double sample_frac, double trim_lo,
-    double trim_hi, float* __restrict__ sortbuf, erp_pair_result* __restrict__ results) {
+    const int32_t* __restrict__ flags, const int32_t* __restrict__ nsurv, int stride, int npow2,
+    double sample_frac, double trim_lo, double trim_hi, float* __restrict__ sortbuf,
+    erp_pair_result* __restrict__ results) {
     __shared__ double sv[1024];
     __shared__ int si[1024];
     __shared__ int cand[64];
@@ -781,6 +1059,8 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     r.sample_n = s;
     r.min_idx = -1;
     r.near_ties = 0;
+    r.survivors = nsurv[p];
+    r.reserved = 0;
     r.min_dist = 0.0;
     const int fl = flags[p];
     if (fl & 1) r.status = ERP_TOO_FEW_POINTS;
@@ -904,6 +1184,32 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
 }  // namespace
 
 // ====================================================================== launchers =======
+// ERP_DEBUG_MODE (timing ablations only, results are wrong when set): bit0 = sampler skips
+// its index stores
+static int debug_mode() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("ERP_DEBUG_MODE");
+        v = e ? atoi(e) : 0;
+    }
+    return v;
+}
+
+// (1/d, d) for d = 0..65536 (the modulo divisors of random_shuffle), in device memory
+double2* make_recip_table() {
+    const int n = 65537;
+    double2* h = (double2*)malloc(sizeof(double2) * n);
+    for (int d = 0; d < n; d++) {
+        h[d].x = d ? 1.0 / (double)d : 0.0;
+        h[d].y = (double)d;
+    }
+    double2* dptr = nullptr;
+    if (hipMalloc(&dptr, sizeof(double2) * n) == hipSuccess)
+        (void)hipMemcpy(dptr, h, sizeof(double2) * n, hipMemcpyHostToDevice);
+    free(h);
+    return dptr;
+}
+
 void init_constants() {
     uint32_t red[30][31] = {};
     uint32_t v[31] = {};
@@ -953,9 +1259,8 @@ hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t
 
 hipError_t launch_bearings_direct(const erp_point2f* kl, const erp_point2f* kr, int32_t m,
                                   int32_t W, int32_t H, double* pts, hipStream_t st) {
-    if (m <= 0) return hipSuccess;
-    hipLaunchKernelGGL(bearings_direct_kernel, dim3((m + 255) / 256), dim3(256), 0, st, kl, kr, m,
-                       W, H, pts);
+    hipLaunchKernelGGL(bearings_direct_kernel, dim3((m + 255) / 256 + (m == 0)), dim3(256), 0, st, kl,
+                       kr, m, W, H, pts);
     return hipGetLastError();
 }
 
@@ -975,16 +1280,30 @@ hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_
     return hipGetLastError();
 }
 
-hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
-                               const uint32_t* w0, const double* pts, const BatchShape& sh,
-                               double sample_frac, uint16_t* idx, double* gram, int32_t* samples,
-                               int32_t* flags, hipStream_t st) {
+hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
+                          const uint32_t* w0, const double2* rtab, const BatchShape& sh,
+                          double sample_frac, uint32_t* wins, uint16_t* idx, int32_t* flags,
+                          hipStream_t st, int part) {
     const int nwaves = (sh.iters + 63) / 64;
-    const int nwords = (sh.max_s + 31) / 32;
-    const size_t shmem = (96 + (size_t)nwords * 64) * sizeof(uint32_t);
-    hipLaunchKernelGGL(sampler_gram_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
-                       polyR, polyQ, w0, pts, sh.max_nq, sh.iters, nwaves, sh.idx_stride,
-                       sample_frac, idx, gram, samples, flags);
+    if (part == 0) {
+        hipLaunchKernelGGL(sampler_window_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts,
+                           polyR, polyQ, w0, nwaves, sample_frac, wins);
+    } else {
+        const int nwords = (sh.max_s + 31) / 32;
+        const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
+        hipLaunchKernelGGL(sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
+                           wins, rtab, nwaves, sh.idx_stride, sample_frac, idx, flags,
+                           debug_mode());
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_gram(const int32_t* counts, const double* pts, const uint16_t* idx,
+                       const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
+                       hipStream_t st) {
+    const int nwaves = (sh.iters + 63) / 64;
+    hipLaunchKernelGGL(gram_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, pts,
+                       sh.max_nq, sh.iters, nwaves, sh.idx_stride, sample_frac, idx, gram, samples);
     return hipGetLastError();
 }
 
@@ -1004,17 +1323,35 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
 
 hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyps,
                                 const BatchShape& sh, double sample_frac, float* rv, float* tv,
-                                int32_t* kcount, float* rv_aos, hipStream_t st) {
+                                int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st) {
     hipLaunchKernelGGL(valid_compact_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, hyps,
-                       sh.iters, sample_frac, rv, tv, kcount, rv_aos);
+                       sh.iters, sample_frac, rv, tv, kcount, rv_aos, dscale);
+    return hipGetLastError();
+}
+
+hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
+                                   const BatchShape& sh, double trim_lo, double trim_hi, double* lb,
+                                   double* ub, hipStream_t st) {
+    dim3 grid((2 * sh.iters + kBoundRows - 1) / kBoundRows, sh.n_pairs);
+    hipLaunchKernelGGL(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
+                       2 * sh.iters, trim_lo, trim_hi, lb, ub);
+    return hipGetLastError();
+}
+
+hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
+                                   const BatchShape& sh, double trim_lo, double trim_hi,
+                                   int32_t* surv, int32_t* nsurv, double* tmean, hipStream_t st) {
+    hipLaunchKernelGGL(consensus_select_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, kcount, lb, ub,
+                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, tmean);
     return hipGetLastError();
 }
 
 hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const BatchShape& sh,
-                                 double trim_lo, double trim_hi, double* tmean, hipStream_t st) {
+                                 double trim_lo, double trim_hi, const int32_t* surv,
+                                 const int32_t* nsurv, double* tmean, hipStream_t st) {
     dim3 grid(2 * sh.iters, sh.n_pairs);
     hipLaunchKernelGGL(consensus_rows_kernel, grid, dim3(256), 0, st, kcount, rv, 2 * sh.iters,
-                       trim_lo, trim_hi, tmean);
+                       trim_lo, trim_hi, surv, nsurv, tmean);
     return hipGetLastError();
 }
 
@@ -1026,11 +1363,11 @@ int sortbuf_len(int iters) {
 
 hipError_t launch_consensus_final(const int32_t* counts, const int32_t* kcount, const float* rv,
                                   const float* tv, const double* tmean, const int32_t* flags,
-                                  const BatchShape& sh, double sample_frac, double trim_lo,
-                                  double trim_hi, float* sortbuf, erp_pair_result* results,
-                                  hipStream_t st) {
+                                  const int32_t* nsurv, const BatchShape& sh, double sample_frac,
+                                  double trim_lo, double trim_hi, float* sortbuf,
+                                  erp_pair_result* results, hipStream_t st) {
     hipLaunchKernelGGL(consensus_final_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, kcount,
-                       rv, tv, tmean, flags, 2 * sh.iters, sortbuf_len(sh.iters), sample_frac,
+                       rv, tv, tmean, flags, nsurv, 2 * sh.iters, sortbuf_len(sh.iters), sample_frac,
                        trim_lo, trim_hi, sortbuf, results);
     return hipGetLastError();
 }

@@ -106,6 +106,8 @@ typedef struct erp_pair_result {
     int32_t min_idx;     /* consensus winner in R_vec_arr order */
     int32_t sample_n;    /* (int)(M * sample_frac) */
     int32_t near_ties;   /* rows re-scored exactly by the near-tie resolver */
+    int32_t survivors;   /* rows whose trimmed-mean bounds did not exclude them */
+    int32_t reserved;
     double min_dist;     /* trimmed-mean distance of the winner */
 } erp_pair_result;
 
@@ -136,8 +138,10 @@ typedef struct erp_batch_outputs {
                                    order unspecified) */
     float* rvec;                /* [n_pairs][2*iters][3] R_vec_arr */
     float* tvec;                /* [n_pairs][2*iters][3] T_vec_arr */
-    double* dist;               /* [n_pairs][2*iters] trimmed means (approximate; the winner and
-                                   near ties are exact) */
+    double* dist;               /* [n_pairs][2*iters] trimmed means of the rows that survive the
+                                   bounds test (exact order statistics, fp64 sum; near ties are
+                                   re-scored with the reference's sorted sequential sum); +inf for
+                                   rows proven not to be the minimum */
 } erp_batch_outputs;
 
 typedef struct erp_ctx erp_ctx;
@@ -159,12 +163,16 @@ typedef enum erp_stage {
     ERP_STAGE_KNN2_MERGE = 1,   /* chunk fold + ratio test + compaction */
     ERP_STAGE_BEARINGS = 2,     /* gather + pixel -> bearing */
     ERP_STAGE_JUMP_PREP = 3,    /* glibc jump-ahead polynomials */
-    ERP_STAGE_SAMPLER_GRAM = 4, /* random_array replay + A^T A */
+    ERP_STAGE_SAMPLER = 4,      /* random_array replay (glibc, backwards, bitmap) */
     ERP_STAGE_EIGEN = 5,        /* 9x9 Jacobi, rank-2 fix, decomposeEssentialMat, Euler */
     ERP_STAGE_VALID_COMPACT = 6,
-    ERP_STAGE_CONSENSUS_ROWS = 7,
+    ERP_STAGE_CONSENSUS_ROWS = 7,   /* exact order statistics of the surviving rows */
     ERP_STAGE_CONSENSUS_FINAL = 8,
-    ERP_STAGE_COUNT = 9
+    ERP_STAGE_CONSENSUS_BOUNDS = 9, /* per-row trimmed-mean bounds (one pass over K^2) */
+    ERP_STAGE_CONSENSUS_SELECT = 10,
+    ERP_STAGE_WINDOWS = 11,         /* per-iteration glibc end windows (jump-ahead) */
+    ERP_STAGE_GRAM = 12,            /* A^T A of every sample (fp64) */
+    ERP_STAGE_COUNT = 13
 } erp_stage;
 erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable);
 const char* erp_stage_name(int32_t stage);
