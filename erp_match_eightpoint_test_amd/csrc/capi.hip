@@ -239,14 +239,12 @@ bool cfg_ok(const erp_ransac_cfg* cfg) {
 }
 
 // estimator stages after counts/pts are in place
-erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
-                         const erp_batch_outputs* out, erp_pair_result* results, hipStream_t st) {
+erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
+                          const erp_batch_outputs* out, hipStream_t st) {
     erp_ctx* ctx = c;
     auto* counts = (int32_t*)c->counts.p;
     auto* flags = (int32_t*)c->flags.p;
     auto* hyps = (out && out->hyps) ? out->hyps : (erp_hypothesis*)c->hyps.p;
-    auto* tv = (out && out->tvec) ? out->tvec : (float*)c->tv.p;
-    auto* tmean = (out && out->dist) ? out->dist : (double*)c->tmean.p;
     {
         StageTimer _t(ctx, ERP_STAGE_JUMP_PREP, st);
         ERP_CK(erp::launch_jump_prep(counts, sh, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p, st));
@@ -274,7 +272,21 @@ erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac, cfg->valid_abs, hyps,
                                  st));
     }
-    {
+    return ERP_OK;
+}
+
+// consensus stages after the hypothesis records are in place (counts may be null when the
+// valid list is given directly: erp_consensus_dev)
+erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
+                         const erp_batch_outputs* out, erp_pair_result* results, hipStream_t st,
+                         bool from_hyps) {
+    erp_ctx* ctx = c;
+    auto* counts = from_hyps ? (int32_t*)c->counts.p : nullptr;
+    auto* flags = from_hyps ? (int32_t*)c->flags.p : nullptr;
+    auto* hyps = (out && out->hyps) ? out->hyps : (erp_hypothesis*)c->hyps.p;
+    auto* tv = (out && out->tvec) ? out->tvec : (float*)c->tv.p;
+    auto* tmean = (out && out->dist) ? out->dist : (double*)c->tmean.p;
+    if (from_hyps) {
         StageTimer _t(ctx, ERP_STAGE_VALID_COMPACT, st);
         ERP_CK(erp::launch_valid_compact(counts, hyps, sh, cfg->sample_frac, (float*)c->rv.p, tv,
                                          (int32_t*)c->kcount.p, out ? out->rvec : nullptr,
@@ -305,6 +317,14 @@ erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                            (float*)c->sortbuf.p, results, st));
     }
     return ERP_OK;
+}
+
+
+erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
+                         const erp_batch_outputs* out, erp_pair_result* results, hipStream_t st) {
+    erp_status es = run_hypotheses(c, sh, cfg, out, st);
+    if (es != ERP_OK) return es;
+    return run_consensus(c, sh, cfg, out, results, st, true);
 }
 
 }  // namespace
@@ -421,8 +441,7 @@ erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,
     if (!ensure(ctx->part, (size_t)sh.chunks * sh.max_nq * sizeof(erp::Top2)) ||
         !ensure(ctx->off, 4 * sizeof(int64_t)) || !ensure(ctx->flags, 16))
         return ERP_OUT_OF_MEMORY;
-    const int64_t offs[4] = {0, nq, 0, nt};
-    ERP_CK(hipMemcpyAsync(ctx->off.p, offs, sizeof(offs), hipMemcpyHostToDevice, st));
+    ERP_CK(erp::launch_set_i64x4((int64_t*)ctx->off.p, 0, nq, 0, nt, st));
     const int64_t* oq = (const int64_t*)ctx->off.p;
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_PARTIAL, st);
@@ -433,8 +452,6 @@ erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,
         ERP_CK(erp::launch_knn2_merge((erp::Top2*)ctx->part.p, oq, oq + 2, sh, ratio, d_out, d_count,
                                       (int32_t*)ctx->flags.p, st));
     }
-    // offs must outlive the async copy
-    ERP_CK(hipStreamSynchronize(st));
     return ERP_OK;
 }
 
@@ -485,15 +502,62 @@ erp_status erp_eight_point_find_dev(erp_ctx* ctx, int32_t W, int32_t H, const er
     es = upload_w0(ctx, cfg, st);
     if (es != ERP_OK) return es;
     ERP_CK(hipMemsetAsync(ctx->flags.p, 0, 4, st));
-    ERP_CK(hipMemcpyAsync(ctx->counts.p, &m, 4, hipMemcpyHostToDevice, st));
+    ERP_CK(erp::launch_set_i32((int32_t*)ctx->counts.p, m, st));
     {
         StageTimer _t(ctx, ERP_STAGE_BEARINGS, st);
         ERP_CK(erp::launch_bearings_direct(d_kl, d_kr, m, W, H, (double*)ctx->pts.p, st));
     }
-    es = run_estimator(ctx, sh, cfg, &out, d_result, st);
+    return run_estimator(ctx, sh, cfg, &out, d_result, st);
+}
+
+erp_status erp_eight_point_hypotheses_dev(erp_ctx* ctx, int32_t W, int32_t H,
+                                          const erp_point2f* d_kl, const erp_point2f* d_kr,
+                                          int32_t m, const erp_ransac_cfg* cfg,
+                                          erp_hypothesis* d_hyps, void* stream) {
+    if (!ctx || W <= 0 || H <= 0 || m < 0 || m > 65535 || !d_hyps || !cfg_ok(cfg))
+        return ERP_INVALID_ARG;
+    if (m > 0 && (!d_kl || !d_kr)) return ERP_INVALID_ARG;
+    if ((int32_t)(m * cfg->sample_frac) < 1) return ERP_TOO_FEW_POINTS;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    const erp::BatchShape sh = make_shape(1, m, m, cfg->iters, cfg->sample_frac);
+    erp_batch_outputs out{};
+    out.hyps = d_hyps;
+    erp_status es = ensure_estimator(ctx, sh, &out);
     if (es != ERP_OK) return es;
-    ERP_CK(hipStreamSynchronize(st));  // m lives on the caller's stack
-    return ERP_OK;
+    es = upload_w0(ctx, cfg, st);
+    if (es != ERP_OK) return es;
+    ERP_CK(hipMemsetAsync(ctx->flags.p, 0, 4, st));
+    ERP_CK(erp::launch_set_i32((int32_t*)ctx->counts.p, m, st));
+    {
+        StageTimer _t(ctx, ERP_STAGE_BEARINGS, st);
+        ERP_CK(erp::launch_bearings_direct(d_kl, d_kr, m, W, H, (double*)ctx->pts.p, st));
+    }
+    return run_hypotheses(ctx, sh, cfg, &out, st);
+}
+
+erp_status erp_consensus_dev(erp_ctx* ctx, const float* d_rvec, const float* d_tvec, int32_t K,
+                             double trim_lo, double trim_hi, erp_pair_result* d_result,
+                             void* stream) {
+    if (!ctx || K < 0 || !d_result || (K > 0 && (!d_rvec || !d_tvec)) || trim_lo < 0 ||
+        trim_hi > 1 || trim_lo > trim_hi)
+        return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    erp_ransac_cfg cfg;
+    erp_ransac_cfg_default(&cfg);
+    cfg.trim_lo = trim_lo;
+    cfg.trim_hi = trim_hi;
+    cfg.iters = std::max((K + 1) / 2, 1);
+    const erp::BatchShape sh = make_shape(1, 1, 1, cfg.iters, cfg.sample_frac);
+    erp_status es = ensure_estimator(ctx, sh, nullptr);
+    if (es != ERP_OK) return es;
+    ERP_CK(erp::launch_consensus_input(d_rvec, d_tvec, K, 2 * sh.iters, (float*)ctx->rv.p,
+                                       (float*)ctx->tv.p, (int32_t*)ctx->kcount.p,
+                                       (float*)ctx->dscale.p, st));
+    return run_consensus(ctx, sh, &cfg, nullptr, d_result, st, false);
 }
 
 erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* h_kl,

@@ -46,6 +46,9 @@ struct BatchShape {
     int idx_stride;               // words of one hypothesis list in idx (>= max_s)
 };
 
+hipError_t launch_set_i32(int32_t* p, int32_t v, hipStream_t st);  // (values via kernel args:
+hipError_t launch_set_i64x4(int64_t* p, int64_t a, int64_t b, int64_t c, int64_t d,  // no host
+                            hipStream_t st);                                       // lifetime)
 void init_constants();            // reduction table for the jump polynomials (once per device)
 double2* make_recip_table();      // (1/d, d), d <= 65536, device memory (once per context)
 
@@ -80,6 +83,8 @@ hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyp
                                 const BatchShape& sh, double sample_frac, float* rv, float* tv,
                                 int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st);
 hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream_t st);
+hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, int stride, float* rv,
+                                  float* tv, int32_t* kcount, float* dscale, hipStream_t st);
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    const BatchShape& sh, double trim_lo, double trim_hi, double* lb,
                                    double* ub, hipStream_t st);

@@ -848,6 +848,56 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     }
 }
 
+// consensus-only entry: AoS R/T lists -> SoA rv, tv, kcount, dscale (one block)
+__global__ __launch_bounds__(1024) void consensus_input_kernel(const float* __restrict__ rvec,
+                                                               const float* __restrict__ tvec,
+                                                               int K, int stride,
+                                                               float* __restrict__ rv,
+                                                               float* __restrict__ tv,
+                                                               int32_t* __restrict__ kcount,
+                                                               float* __restrict__ dscale) {
+    __shared__ float red6[6][16];
+    float mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+    for (int k = threadIdx.x; k < K; k += 1024) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const float v = rvec[3 * (size_t)k + c];
+            rv[c * (size_t)stride + k] = v;
+            tv[3 * (size_t)k + c] = tvec[3 * (size_t)k + c];
+            mn[c] = fminf(mn[c], v);
+            mx[c] = fmaxf(mx[c], v);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        float a = mn[c], b = mx[c];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            a = fminf(a, __shfl_xor(a, o, 64));
+            b = fmaxf(b, __shfl_xor(b, o, 64));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            red6[c][threadIdx.x >> 6] = a;
+            red6[3 + c][threadIdx.x >> 6] = b;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double d2 = 0;
+        for (int c = 0; c < 3; c++) {
+            float a = kInf, b = -kInf;
+            for (int w = 0; w < 16; w++) {
+                a = fminf(a, red6[c][w]);
+                b = fmaxf(b, red6[3 + c][w]);
+            }
+            const double e = K > 0 ? (double)b - (double)a : 0.0;
+            d2 += e * e;
+        }
+        dscale[0] = (float)(sqrt(d2) * (1.0 + 1e-6));
+        kcount[0] = K;
+    }
+}
+
 // ---- pruning by rigorous bounds -------------------------------------------------------
 // Every row's K distances (the reference's exact f32 values) are binned into NB geometric
 // bins (64 per binade over 20 binades below the set's diameter, underflow in bin 0).  From the
@@ -1046,9 +1096,9 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     __shared__ int ncand;
     __shared__ double sres[1];
     const int p = blockIdx.x, tid = threadIdx.x;
-    const int M = counts[p];
     const int K = kcount[p];
-    const int s = (int)(M * sample_frac);
+    const int M = counts ? counts[p] : K;
+    const int s = counts ? (int)(M * sample_frac) : 1;
     erp_pair_result r;
     for (int k = 0; k < 3; k++) {
         r.R[k] = 0.f;
@@ -1062,7 +1112,7 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     r.survivors = nsurv[p];
     r.reserved = 0;
     r.min_dist = 0.0;
-    const int fl = flags[p];
+    const int fl = flags ? flags[p] : 0;
     if (fl & 1) r.status = ERP_TOO_FEW_POINTS;
     else if (fl & 2)
         r.status = ERP_INTERNAL;
@@ -1181,9 +1231,27 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     }
 }
 
+__global__ void set_i32_kernel(int32_t* p, int32_t v) { *p = v; }
+__global__ void set_i64x4_kernel(int64_t* p, int64_t a, int64_t b, int64_t c, int64_t d) {
+    p[0] = a;
+    p[1] = b;
+    p[2] = c;
+    p[3] = d;
+}
+
 }  // namespace
 
 // ====================================================================== launchers =======
+hipError_t launch_set_i32(int32_t* p, int32_t v, hipStream_t st) {
+    hipLaunchKernelGGL(set_i32_kernel, dim3(1), dim3(1), 0, st, p, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_i64x4(int64_t* p, int64_t a, int64_t b, int64_t c, int64_t d,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(set_i64x4_kernel, dim3(1), dim3(1), 0, st, p, a, b, c, d);
+    return hipGetLastError();
+}
 // ERP_DEBUG_MODE (timing ablations only, results are wrong when set): bit0 = sampler skips
 // its index stores
 static int debug_mode() {
@@ -1326,6 +1394,13 @@ hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyp
                                 int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st) {
     hipLaunchKernelGGL(valid_compact_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, hyps,
                        sh.iters, sample_frac, rv, tv, kcount, rv_aos, dscale);
+    return hipGetLastError();
+}
+
+hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, int stride, float* rv,
+                                  float* tv, int32_t* kcount, float* dscale, hipStream_t st) {
+    hipLaunchKernelGGL(consensus_input_kernel, dim3(1), dim3(1024), 0, st, rvec, tvec, K, stride, rv,
+                       tv, kcount, dscale);
     return hipGetLastError();
 }
 

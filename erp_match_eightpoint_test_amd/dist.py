@@ -1,0 +1,116 @@
+"""Multi-GPU partitioning of the hot path: one process per GPU, torch.distributed (RCCL on
+the GPUs, gloo in the CPU tests).
+
+Two partitions, each with a single collective at the end (no data-path exchange):
+
+* pairs (configs[2]): independent ERP pairs are split into contiguous blocks per rank; each
+  rank runs erp_pair_batch_run on its block; the 64-byte result records are all-gathered.
+* hypothesis blocks (configs[4]): the `iters` initial_guess iterations of ONE find() are split
+  into contiguous blocks [a, b) per rank.  Because the reference draws every iteration from one
+  process-global glibc rand() stream (src/eight_point.hpp:57, M-1 draws per iteration), block
+  [a, b) is exactly the single-process computation started at stream offset base + a*(M-1);
+  the per-iteration records are all-gathered in rank order (= iteration order, so the
+  R_vec_arr push order of src/eight_point.cpp:113-126 is preserved) and every rank runs the
+  same consensus on the merged list.
+
+The compute callables are pluggable: on GPUs they are the C ABI (`gpu_hypotheses`,
+`gpu_consensus`); the CPU tests plug in the oracle to check the partition semantics.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def block_range(n: int, world: int, rank: int) -> tuple[int, int]:
+    """contiguous block [a, b) of n items for `rank` out of `world` (sizes differ by <= 1)."""
+    return n * rank // world, n * (rank + 1) // world
+
+
+def all_gather_rows(t, group=None):
+    """all_gather of a tensor whose first dimension may differ per rank -> list per rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n, group=group)
+    ns = [int(x.item()) for x in ns]
+    mx = max(ns) if ns else 0
+    pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[: t.shape[0]] = t
+    bufs = [torch.zeros_like(pad) for _ in range(world)]
+    dist.all_gather(bufs, pad, group=group)
+    return [b[:k] for b, k in zip(bufs, ns)]
+
+
+def valid_list(hyps: np.ndarray):
+    """R_vec_arr / T_vec_arr of initial_guess: per iteration push R1 (if valid) then R2 (if
+    valid), each with that iteration's T (src/eight_point.cpp:113-126)."""
+    r = np.stack([hyps["R1"], hyps["R2"]], 1).reshape(-1, 3)
+    t = np.stack([hyps["T"], hyps["T"]], 1).reshape(-1, 3)
+    v = np.stack([hyps["R1_valid"] != 0, hyps["R2_valid"] != 0], 1).reshape(-1)
+    return np.ascontiguousarray(r[v], np.float32), np.ascontiguousarray(t[v], np.float32)
+
+
+def find_hypothesis_sharded(hyp_fn, consensus_fn, m: int, iters: int, offset: int, group=None):
+    """One find() with its iterations split over the ranks of `group`.
+
+    hyp_fn(iters_local, offset_local) -> numpy structured array of per-iteration records (fields
+    R1, R2, T, R1_valid, R2_valid, ...); consensus_fn(rvec, tvec) -> result.  Returns the
+    result (identical on every rank) and the merged record array."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    a, b = block_range(iters, world, rank)
+    local = hyp_fn(b - a, offset + a * (m - 1))
+    raw = torch.from_numpy(np.ascontiguousarray(local).view(np.uint8).reshape(len(local), -1).copy())
+    parts = all_gather_rows(raw, group)
+    merged = np.concatenate([p.numpy().reshape(-1).view(local.dtype) for p in parts])
+    rvec, tvec = valid_list(merged)
+    return consensus_fn(rvec, tvec), merged
+
+
+def shard_pairs(n_pairs: int, group=None) -> range:
+    import torch.distributed as dist
+    a, b = block_range(n_pairs, dist.get_world_size(group), dist.get_rank(group))
+    return range(a, b)
+
+
+# ----------------------------------------------------------------------- GPU callables
+def gpu_hypotheses(ctx, W: int, H: int, d_kl, d_kr, m: int, cfg_kwargs: dict):
+    """hyp_fn for find_hypothesis_sharded on a GPU (erp_eight_point_hypotheses_dev)."""
+    import ctypes as C
+
+    import torch
+
+    from .capi import HYP_DTYPE, check, default_cfg
+
+    def fn(iters_local: int, offset_local: int):
+        cfg = default_cfg(**dict(cfg_kwargs, iters=max(iters_local, 1), offset=offset_local))
+        out = torch.zeros((max(iters_local, 1), HYP_DTYPE.itemsize), dtype=torch.uint8,
+                          device=d_kl.device)
+        check(ctx.L.erp_eight_point_hypotheses_dev(ctx.h, W, H, d_kl.data_ptr(), d_kr.data_ptr(),
+                                                   m, C.byref(cfg), out.data_ptr(),
+                                                   torch.cuda.current_stream().cuda_stream),
+              "erp_eight_point_hypotheses_dev")
+        return out.cpu().numpy().reshape(-1).view(HYP_DTYPE)[:iters_local]
+    return fn
+
+
+def gpu_consensus(ctx, device, trim_lo: float = 0.2, trim_hi: float = 0.8):
+    """consensus_fn for find_hypothesis_sharded on a GPU (erp_consensus_dev)."""
+    import torch
+
+    from .capi import RESULT_DTYPE, check
+
+    def fn(rvec: np.ndarray, tvec: np.ndarray):
+        K = rvec.shape[0]
+        dr = torch.from_numpy(np.ascontiguousarray(rvec) if K else np.zeros((1, 3), np.float32)).to(device)
+        dt = torch.from_numpy(np.ascontiguousarray(tvec) if K else np.zeros((1, 3), np.float32)).to(device)
+        res = torch.zeros(RESULT_DTYPE.itemsize, dtype=torch.uint8, device=device)
+        check(ctx.L.erp_consensus_dev(ctx.h, dr.data_ptr(), dt.data_ptr(), K, trim_lo, trim_hi,
+                                      res.data_ptr(), torch.cuda.current_stream().cuda_stream),
+              "erp_consensus_dev")
+        return res.cpu().numpy().view(RESULT_DTYPE)[0]
+    return fn

@@ -196,6 +196,19 @@ erp_status erp_eight_point_find_dev(erp_ctx* ctx, int32_t W, int32_t H, const er
                                     const erp_point2f* d_kr, int32_t m, const erp_ransac_cfg* cfg,
                                     erp_pair_result* d_result, erp_hypothesis* d_hyps,
                                     void* stream);
+/* device pointers: the initial_guess ITERATIONS only (no consensus) -> cfg->iters records.
+   cfg->offset positions the glibc stream, so iteration block [a, b) of a larger find() is
+   reproduced exactly with iters = b - a and offset = base + a*(m-1): the hypothesis-block
+   sharding of configs[4] (src/eight_point.cpp:99-127). */
+erp_status erp_eight_point_hypotheses_dev(erp_ctx* ctx, int32_t W, int32_t H,
+                                          const erp_point2f* d_kl, const erp_point2f* d_kr,
+                                          int32_t m, const erp_ransac_cfg* cfg,
+                                          erp_hypothesis* d_hyps, void* stream);
+/* device pointers: the trimmed-mean consensus (src/eight_point.cpp:129-149) on K Euler vectors
+   d_rvec [K][3] with their translations d_tvec [K][3] (R_vec_arr / T_vec_arr order). */
+erp_status erp_consensus_dev(erp_ctx* ctx, const float* d_rvec, const float* d_tvec, int32_t K,
+                             double trim_lo, double trim_hi, erp_pair_result* d_result,
+                             void* stream);
 /* host pointers, synchronous: the drop-in for eight_point::find. */
 erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* h_kl,
                                 const erp_point2f* h_kr, int32_t m, const erp_ransac_cfg* cfg,
