@@ -70,7 +70,6 @@ struct erp_ctx {
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
     DevBuf part, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins;
-    double2* rtab = nullptr;
     bool w0_valid = false;
     uint32_t w0_seed = 0;
     uint64_t w0_offset = 0;
@@ -151,11 +150,6 @@ erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
     if (!c) return ERP_OUT_OF_MEMORY;
     c->device = device;
     erp::init_constants();
-    c->rtab = erp::make_recip_table();
-    if (!c->rtab) {
-        delete c;
-        return ERP_OUT_OF_MEMORY;
-    }
     *out = c;
     return ERP_OK;
 }
@@ -171,7 +165,6 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
-    if (ctx->rtab) (void)hipFree(ctx->rtab);
     delete ctx;
     return ERP_OK;
 }
@@ -196,6 +189,7 @@ erp::BatchShape make_shape(int n_pairs, int max_nq, int max_nt, int iters, doubl
     sh.iters = std::max(iters, 1);
     sh.max_s = std::max((int)(sh.max_nq * frac), 1);
     sh.idx_stride = sh.max_s;
+    sh.sel_words = (sh.max_nq + 30) / 31 + 1;
     return sh;
 }
 
@@ -206,7 +200,7 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->pts, P * (sh.max_nq + 1) * 48) &&
               ensure(c->wins, P * nwaves * 31 * 64 * 4) && ensure(c->polyR, P * 65 * 31 * 4) &&
               ensure(c->polyQ, P * erp::kMaxQ * 31 * 4) &&
-              ensure(c->idx, P * nwaves * (size_t)sh.idx_stride * 64 * 2) &&
+              ensure(c->idx, P * nwaves * (size_t)sh.sel_words * 64 * 4) &&
               ensure(c->gram, P * sh.iters * 36 * 8) && ensure(c->rv, P * 6 * sh.iters * 4) &&
               ensure(c->kcount, P * 4) && ensure(c->sortbuf, P * (size_t)erp::sortbuf_len(sh.iters) * 4) &&
               ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result)) &&
@@ -252,18 +246,18 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
     {
         StageTimer _t(ctx, ERP_STAGE_WINDOWS, st);
         ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
-                                   (uint32_t*)c->w0.p, c->rtab, sh, cfg->sample_frac,
-                                   (uint32_t*)c->wins.p, (uint16_t*)c->idx.p, flags, st, 0));
+                                   (uint32_t*)c->w0.p, sh, cfg->sample_frac, (uint32_t*)c->wins.p,
+                                   (uint32_t*)c->idx.p, flags, st, 0));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
         ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
-                                   (uint32_t*)c->w0.p, c->rtab, sh, cfg->sample_frac,
-                                   (uint32_t*)c->wins.p, (uint16_t*)c->idx.p, flags, st, 1));
+                                   (uint32_t*)c->w0.p, sh, cfg->sample_frac, (uint32_t*)c->wins.p,
+                                   (uint32_t*)c->idx.p, flags, st, 1));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_GRAM, st);
-        ERP_CK(erp::launch_gram(counts, (double*)c->pts.p, (uint16_t*)c->idx.p, sh,
+        ERP_CK(erp::launch_gram(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
                                 cfg->sample_frac, (double*)c->gram.p, out ? out->samples : nullptr,
                                 st));
     }

@@ -26,7 +26,7 @@ struct Workspace {
     double* pts;                  // [pairs][max_nq + 1][6] bearings (l, r); last row = 0
     uint32_t* polyR;              // [pairs][65][31]  x^(l(M-1)) mod P
     uint32_t* polyQ;              // [pairs][kMaxQ][31]
-    uint16_t* idx;                // [pairs][iters_pad][max_s] sample lists (wave-interleaved)
+    uint32_t* sel;                // [pairs][waves][sel_words][64] sample selection bitmaps
     double* gram;                 // [pairs][iters][36]
     erp_hypothesis* hyps;         // [pairs][iters]
     float* rv;                    // [pairs][3][2*iters] valid R (SoA)
@@ -43,14 +43,14 @@ struct BatchShape {
     int chunks, chunk_len;
     int iters;
     int max_s;                    // (int)(max_nq * sample_frac)
-    int idx_stride;               // words of one hypothesis list in idx (>= max_s)
+    int idx_stride;               // entries of one hypothesis in the debug samples output
+    int sel_words;                // 31-step selection words per hypothesis (>= (M-1)/31 + 1)
 };
 
 hipError_t launch_set_i32(int32_t* p, int32_t v, hipStream_t st);  // (values via kernel args:
 hipError_t launch_set_i64x4(int64_t* p, int64_t a, int64_t b, int64_t c, int64_t d,  // no host
                             hipStream_t st);                                       // lifetime)
 void init_constants();            // reduction table for the jump polynomials (once per device)
-double2* make_recip_table();      // (1/d, d), d <= 65536, device memory (once per context)
 
 hipError_t launch_knn2_partial(const float* desc_q, const float* desc_t, const int64_t* off_q,
                                const int64_t* off_t, const BatchShape& sh, Top2* part,
@@ -68,12 +68,12 @@ hipError_t launch_bearings_direct(const erp_point2f* kl, const erp_point2f* kr, 
                                   int32_t W, int32_t H, double* pts, hipStream_t st);
 hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_t* polyR,
                             uint32_t* polyQ, hipStream_t st);
-// part 0: lane end windows (jump-ahead); part 1: the backwards replay -> sample index lists
+// part 0: lane end windows (jump-ahead); part 1: the backwards replay -> selection bitmaps
 hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
-                          const uint32_t* w0, const double2* rtab, const BatchShape& sh,
-                          double sample_frac, uint32_t* wins, uint16_t* idx, int32_t* flags,
-                          hipStream_t st, int part);
-hipError_t launch_gram(const int32_t* counts, const double* pts, const uint16_t* idx,
+                          const uint32_t* w0, const BatchShape& sh, double sample_frac,
+                          uint32_t* wins, uint32_t* selw, int32_t* flags, hipStream_t st,
+                          int part);
+hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t* selw,
                        const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
                        hipStream_t st);
 hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,

@@ -382,28 +382,103 @@ __global__ __launch_bounds__(64) void sampler_window_kernel(
     }
 }
 
-// exact j = x mod d for x < 2^31, 1 <= d <= 65536.  1/d from v_rcp_f64 + one Newton step
-// (relative error << 2^-40), q0 = trunc(x/d) is then off by at most one, and the remainder
-// x - q0*d is exact in fp64 (fma), so a two-sided correction gives the exact result.
-// Everything stays in VALU: a table in memory would need SMEM/LDS loads whose lgkmcnt waits
-// also drain the replay's in-flight LDS atomics.
-__device__ __forceinline__ double recip_nr(double dd) {
+// exact j = x mod d for x < 2^31, 2 <= d <= 65536, from r = 1/d rounded UP to within
+// 2^-32 relative (rup_recip; both conditions are checked exactly with an fma residual and a
+// violation raises flag 4).  Then x*r >= x/d, and x*r - x/d < 2^-1/d, so trunc(fl(x*r)) =
+// floor(x/d): for an exact multiple k*d, fl(x*r) >= k (rounding is monotone and k is
+// representable); otherwise x/d <= k + 1 - 1/d leaves a margin far above the error.  The
+// remainder fma(-q, d, x) is then exact.  Everything stays in VALU (no SMEM/LDS table: their
+// lgkmcnt waits would also drain the replay's in-flight LDS atomics).
+__device__ __forceinline__ double rup_recip(double dd, bool* bad) {
     const double r0 = __builtin_amdgcn_rcp(dd);
-    return __builtin_fma(r0, __builtin_fma(-dd, r0, 1.0), r0);
+    double r = __builtin_fma(r0, __builtin_fma(-dd, r0, 1.0), r0);
+    r = __builtin_fma(r, 0x1p-40, r);                  // one-sided: NR error is ~2^-52
+    const double e = __builtin_fma(-dd, r, 1.0);       // exact residual 1 - d*r
+    *bad = !(e <= 0.0 && e > -0x1p-32);
+    return r;
 }
 
-__device__ __forceinline__ uint32_t mod_by_recip(uint32_t x, double rinv, double dd, uint32_t d) {
+__device__ __forceinline__ uint32_t mod_rup(uint32_t x, double r, double dd) {
     const double xd = (double)x;
-    const double q0 = __builtin_trunc(xd * rinv);
-    int32_t j = (int32_t)__builtin_fma(-q0, dd, xd);
-    j = j < 0 ? j + (int32_t)d : j;
-    return (uint32_t)j >= d ? (uint32_t)j - d : (uint32_t)j;
+    const double q = __builtin_trunc(xd * r);
+    return (uint32_t)(int32_t)__builtin_fma(-q, dd, xd);
 }
 
+__device__ __forceinline__ double bcast_f64(double v, int u) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, u);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), u);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// One block of 31 reverse steps i0, i0-1, ..., i0-30 of one lane's replay (ring = the 31-word
+// glibc window, advanced backwards in place).  Returns the block's selection word: bit u set
+// iff step i0-u's index ends in the sample.  bm = the lane's s-bit LDS bitmap, [word][lane].
+//   MODE 0 (every step i >= s):      valid = j < s;  old = bm[j] |= bit;     sel = valid && !old
+//   MODE 1 (every step 1 <= i < s):  old = bm[j]; bm[j] := bm[i];            sel = !old
+//   MODE 2 (mixed / steps below 1):  per-step choice of the two (dead steps do nothing)
+// (bm bit set = "resolved": for i >= s the position was taken by a later step; for i < s the
+// reverse-step set T of the header comment is the complement.)  The atomics' old values are
+// consumed after the block, so the LDS traffic streams without waits; MODE 1/2 read bm[i] from
+// registers mirroring the (at most two) words holding i0-30..i0.
+template <int MODE>
+__device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t* bm, int lane,
+                                                 int i0, int s, bool* bad) {
+    const int il = i0 - (lane < 31 ? lane : 0);
+    const double rl = rup_recip((double)(il >= 1 ? il + 1 : 2), bad);
+    int wA = 0, wB = 0;
+    uint32_t curA = 0, curB = 0;
+    if (MODE != 0) {
+        wA = i0 >> 5;
+        wB = (i0 - 30) > 0 ? (i0 - 30) >> 5 : 0;
+        curA = bm[wA * 64 + lane];
+        curB = bm[wB * 64 + lane];
+    }
+    uint32_t olds[31], sel[31];
+#pragma unroll
+    for (int u = 0; u < 31; u++) {
+        const int ii = i0 - u;  // uniform
+        const int slot = 30 - u;
+        const uint32_t rv = ring[slot];
+        ring[slot] = rv - ring[(slot + 28) % 31];
+        const bool live = MODE != 2 || ii >= 1;
+        const double dd = (double)(live ? ii + 1 : 2);
+        const uint32_t j = mod_rup(rv >> 1, bcast_f64(rl, u), dd);
+        const uint32_t bit = 1u << (j & 31);
+        const bool isB = MODE == 1 || (MODE == 2 && ii < s);
+        if (MODE == 0) {
+            const bool valid = j < (uint32_t)s;
+            const uint32_t orm = valid ? bit : 0u;
+            olds[u] = atomicOr(&bm[(valid ? (j >> 5) : 0u) * 64 + lane], orm);
+            sel[u] = orm;
+        } else {
+            const uint32_t cw = ((ii >> 5) == wA) ? curA : curB;
+            const uint32_t bi = (cw >> (ii & 31)) & 1u;
+            const bool validA = live && !isB && j < (uint32_t)s;
+            const bool validB = live && isB;
+            const uint32_t w = (validA || validB) ? (j >> 5) : 0u;
+            const uint32_t andm = validB ? ~bit : 0xffffffffu;
+            const uint32_t orm = validB ? (bi << (j & 31)) : (validA ? bit : 0u);
+            uint32_t* wp = &bm[w * 64 + lane];
+            olds[u] = atomicAnd(wp, andm);
+            atomicOr(wp, orm);
+            curA = (w == (uint32_t)wA) ? ((curA & andm) | orm) : curA;
+            curB = (w == (uint32_t)wB) ? ((curB & andm) | orm) : curB;
+            sel[u] = (validA || validB) ? bit : 0u;
+        }
+    }
+    uint32_t word = 0;
+#pragma unroll
+    for (int u = 0; u < 31; u++)
+        word |= (sel[u] != 0u && (olds[u] & sel[u]) == 0u) ? (1u << u) : 0u;
+    return word;
+}
+
+// One lane = one iteration; writes the iteration's selection bitmap in block space:
+// sel[p][w][b][lane] bit u <-> index i = M-1-31b-u (b = 0 .. (M-1)/31), exactly s bits set.
 __global__ __launch_bounds__(64) void sampler_kernel(
-    const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins,
-    const double2* __restrict__ rtab, int nwaves, int idx_stride, double sample_frac,
-    uint16_t* __restrict__ idx, int32_t* __restrict__ flags, int dbg) {
+    const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins, int nwaves, int nbw,
+    double sample_frac, uint32_t* __restrict__ selw, int32_t* __restrict__ flags) {
     extern __shared__ uint32_t bm[];  // [nwords][64]
     const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
     const int M = counts[p];
@@ -417,86 +492,42 @@ __global__ __launch_bounds__(64) void sampler_kernel(
 #pragma unroll
         for (int t = 0; t < 31; t++) ring[t] = wi[t * 64];
     }
-    uint16_t* my = idx + ((size_t)p * nwaves + w) * (size_t)idx_stride * 64 + lane;
-    int emitted = 0;
-    int i = M - 1;
-    // Every step runs the same branch-free sequence (phase A = i >= s, phase B = i < s):
-    //   A: valid = j < s;   seen[j] |= bit;                emit = valid && !old
-    //   B: valid = j != i;  seen[j] := !T[i] (and + or);   emit = valid ? !old : T[i]
-    // The old words of a block's 31 steps are consumed only after the block, so the LDS
-    // atomics stream without waits.  Phase B needs the bitmap words holding positions
-    // i0..i0-30 (at most two): they are read once at the block start and mirrored in
-    // registers (curA/curB) -- a read inside the block would wait for every in-flight atomic.
-    uint32_t last0 = 0;
+    uint32_t* out = selw + ((size_t)p * nwaves + w) * (size_t)nbw * 64 + lane;
+    const int b0 = (M - 1) / 31, u0 = (M - 1) % 31;  // slot of position 0
+    int i = M - 1, b = 0, emitted = 0;
+    uint32_t lastw = 0;
+    bool bad = false;
     while (i >= 1) {
-        const int i0 = i;
-        const int wA = i0 >> 5;
-        const int wB = (i0 - 30) > 0 ? (i0 - 30) >> 5 : 0;
-        uint32_t curA = 0, curB = 0;
-        if (i0 - 30 < s) {
-            curA = bm[wA * 64 + lane];
-            curB = bm[wB * 64 + lane];
-        }
-        uint32_t olds[31], bitsel[31];
-        uint32_t emask = 0, vmask = 0;
-#pragma unroll
-        for (int u = 0; u < 31; u++) {
-            const int ii = i0 - u;              // uniform
-            const bool live = ii >= 1;
-            const bool isB = ii < s;
-            const int slot = 30 - u;
-            const uint32_t rv = ring[slot];
-            ring[slot] = rv - ring[(slot + 28) % 31];
-            const int dv = live ? ii + 1 : 2;
-            const double dd = (double)dv;
-            const uint32_t j = mod_by_recip(rv >> 1, recip_nr(dd), dd, (uint32_t)dv);
-            const uint32_t cw = ((ii >> 5) == wA) ? curA : curB;
-            const bool bT = isB && live && !((cw >> (ii & 31)) & 1u);
-            const uint32_t bit = 1u << (j & 31);
-            const bool valid = live && (isB ? (j != (uint32_t)ii) : (j < (uint32_t)s));
-            const uint32_t andm = (valid && isB) ? ~bit : 0xffffffffu;
-            const uint32_t orm = valid ? (bT ? 0u : bit) : 0u;
-            const uint32_t w = valid ? (j >> 5) : 0u;
-            uint32_t* wp = &bm[w * 64 + lane];
-            olds[u] = atomicAnd(wp, andm);
-            atomicOr(wp, orm);
-            curA = (w == (uint32_t)wA) ? ((curA & andm) | orm) : curA;
-            curB = (w == (uint32_t)wB) ? ((curB & andm) | orm) : curB;
-            bitsel[u] = valid ? bit : 0u;
-            vmask |= valid ? (1u << u) : 0u;
-            emask |= (live && isB && j == (uint32_t)ii && bT) ? (1u << u) : 0u;
-        }
-        i = i0 - 31;
-        if (i < 1) last0 = (wB == 0) ? curB : curA;  // word 0 after the final block
-#pragma unroll
-        for (int u = 0; u < 31; u++) {
-            const bool em = (((vmask >> u) & 1u) && !(olds[u] & bitsel[u])) || ((emask >> u) & 1u);
-            if (em) {
-                if (emitted < idx_stride && !(dbg & 1)) my[(size_t)emitted * 64] = (uint16_t)(i0 - u);
-                emitted++;
-            }
-        }
+        uint32_t word;
+        if (i - 30 >= s)
+            word = replay_block<0>(ring, bm, lane, i, s, &bad);
+        else if (i < s && i - 30 >= 1)
+            word = replay_block<1>(ring, bm, lane, i, s, &bad);
+        else
+            word = replay_block<2>(ring, bm, lane, i, s, &bad);
+        emitted += __builtin_popcount(word);
+        if (b == b0) lastw = word;
+        else out[(size_t)b * 64] = word;
+        i -= 31;
+        b++;
     }
-    if (dbg & 1) my[0] = (uint16_t)emitted;
-    {
-        (void)last0;
-        const uint32_t word0 = bm[lane];  // position 0 (after every atomic of the replay)
-        if (!(word0 & 1u)) {
-            if (emitted < idx_stride) my[(size_t)emitted * 64] = 0;
-            emitted++;
-        }
+    if (!(bm[lane] & 1u)) {  // position 0 still unresolved: its value 0 stays in the prefix
+        lastw |= 1u << u0;
+        emitted++;
     }
+    out[(size_t)b0 * 64] = lastw;
     if (emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
+    if (bad) atomicOr(&flags[p], 4);
 }
 
-// Gram of each lane's s sampled rows; rows gathered 8 at a time so the index loads and the
-// 48-byte row gathers of a batch are all in flight together.  Row max_nq of pts is a zero
-// sentinel used to pad the last batch.
+// Gram of each lane's s sampled rows: the selection bitmap is walked with a per-lane cursor
+// (one word prefetched), rows gathered 8 at a time so their loads are all in flight together.
+// Row max_nq of pts is a zero sentinel used to pad the last batch.
 __global__ __launch_bounds__(64) void gram_kernel(const int32_t* __restrict__ counts,
                                                   const double* __restrict__ pts, int max_nq,
-                                                  int iters, int nwaves, int idx_stride,
+                                                  int iters, int nwaves, int nbw, int idx_stride,
                                                   double sample_frac,
-                                                  const uint16_t* __restrict__ idx,
+                                                  const uint32_t* __restrict__ selw,
                                                   double* __restrict__ gram,
                                                   int32_t* __restrict__ samples) {
     const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
@@ -504,17 +535,33 @@ __global__ __launch_bounds__(64) void gram_kernel(const int32_t* __restrict__ co
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;
     const int h = w * 64 + lane;
-    const uint16_t* my = idx + ((size_t)p * nwaves + w) * (size_t)idx_stride * 64 + lane;
+    const uint32_t* my = selw + ((size_t)p * nwaves + w) * (size_t)nbw * 64 + lane;
     const double2* P = reinterpret_cast<const double2*>(pts + (size_t)p * (max_nq + 1) * 6);
+    const int b0 = (M - 1) / 31;
+    int b = 0;
+    uint32_t cur = my[0];
+    uint32_t nxt = b0 >= 1 ? my[64] : 0u;
     double g[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) g[k] = 0.0;
-    const int n = min(s, idx_stride);
     constexpr int B = 8;
-    for (int k0 = 0; k0 < n; k0 += B) {
+    for (int k0 = 0; k0 < s; k0 += B) {
         int v[B];
 #pragma unroll
-        for (int u = 0; u < B; u++) v[u] = (k0 + u < n) ? (int)my[(size_t)(k0 + u) * 64] : max_nq;
+        for (int u = 0; u < B; u++) {
+            v[u] = max_nq;
+            if (k0 + u < s) {
+                while (cur == 0u && b < b0) {
+                    b++;
+                    cur = nxt;
+                    nxt = (b + 1 <= b0) ? my[(size_t)(b + 1) * 64] : 0u;
+                }
+                if (cur) {
+                    v[u] = M - 1 - 31 * b - __builtin_ctz(cur);
+                    cur &= cur - 1u;
+                }
+            }
+        }
         double2 a[B][3];
 #pragma unroll
         for (int u = 0; u < B; u++)
@@ -533,7 +580,7 @@ __global__ __launch_bounds__(64) void gram_kernel(const int32_t* __restrict__ co
                     g[6 * a6 + b6] = __builtin_fma(LL[a6], RR[b6], g[6 * a6 + b6]);
         }
         if (samples && h < iters)
-            for (int u = 0; u < B && k0 + u < n; u++)
+            for (int u = 0; u < B && k0 + u < s && k0 + u < idx_stride; u++)
                 samples[((size_t)p * iters + h) * idx_stride + k0 + u] = v[u];
     }
     if (h < iters) {
@@ -1114,7 +1161,7 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     r.min_dist = 0.0;
     const int fl = flags ? flags[p] : 0;
     if (fl & 1) r.status = ERP_TOO_FEW_POINTS;
-    else if (fl & 2)
+    else if (fl & 6)
         r.status = ERP_INTERNAL;
     else if (s < 1)
         r.status = ERP_TOO_FEW_POINTS;
@@ -1252,32 +1299,6 @@ hipError_t launch_set_i64x4(int64_t* p, int64_t a, int64_t b, int64_t c, int64_t
     hipLaunchKernelGGL(set_i64x4_kernel, dim3(1), dim3(1), 0, st, p, a, b, c, d);
     return hipGetLastError();
 }
-// ERP_DEBUG_MODE (timing ablations only, results are wrong when set): bit0 = sampler skips
-// its index stores
-static int debug_mode() {
-    static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("ERP_DEBUG_MODE");
-        v = e ? atoi(e) : 0;
-    }
-    return v;
-}
-
-// (1/d, d) for d = 0..65536 (the modulo divisors of random_shuffle), in device memory
-double2* make_recip_table() {
-    const int n = 65537;
-    double2* h = (double2*)malloc(sizeof(double2) * n);
-    for (int d = 0; d < n; d++) {
-        h[d].x = d ? 1.0 / (double)d : 0.0;
-        h[d].y = (double)d;
-    }
-    double2* dptr = nullptr;
-    if (hipMalloc(&dptr, sizeof(double2) * n) == hipSuccess)
-        (void)hipMemcpy(dptr, h, sizeof(double2) * n, hipMemcpyHostToDevice);
-    free(h);
-    return dptr;
-}
-
 void init_constants() {
     uint32_t red[30][31] = {};
     uint32_t v[31] = {};
@@ -1349,9 +1370,9 @@ hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_
 }
 
 hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
-                          const uint32_t* w0, const double2* rtab, const BatchShape& sh,
-                          double sample_frac, uint32_t* wins, uint16_t* idx, int32_t* flags,
-                          hipStream_t st, int part) {
+                          const uint32_t* w0, const BatchShape& sh, double sample_frac,
+                          uint32_t* wins, uint32_t* selw, int32_t* flags, hipStream_t st,
+                          int part) {
     const int nwaves = (sh.iters + 63) / 64;
     if (part == 0) {
         hipLaunchKernelGGL(sampler_window_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts,
@@ -1360,18 +1381,18 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         const int nwords = (sh.max_s + 31) / 32;
         const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
         hipLaunchKernelGGL(sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
-                           wins, rtab, nwaves, sh.idx_stride, sample_frac, idx, flags,
-                           debug_mode());
+                           wins, nwaves, sh.sel_words, sample_frac, selw, flags);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_gram(const int32_t* counts, const double* pts, const uint16_t* idx,
+hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t* selw,
                        const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
                        hipStream_t st) {
     const int nwaves = (sh.iters + 63) / 64;
     hipLaunchKernelGGL(gram_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, pts,
-                       sh.max_nq, sh.iters, nwaves, sh.idx_stride, sample_frac, idx, gram, samples);
+                       sh.max_nq, sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, selw,
+                       gram, samples);
     return hipGetLastError();
 }
 
