@@ -761,6 +761,14 @@ __device__ __forceinline__ float rdist(float xi, float yi, float zi, float xj, f
     return __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
 }
 
+// its square (same operations; sqrtf of it is the distance)
+__device__ __forceinline__ float rdist2(float xi, float yi, float zi, float xj, float yj, float zj) {
+    const float dx = xi - xj;
+    const float dy = yi - yj;
+    const float dz = zi - zj;
+    return dx * dx + dy * dy + dz * dz;
+}
+
 // find the bin holding `rank` in hist[0..2047] (block of 256); returns bin, writes #before
 __device__ int find_bin_2048(const uint32_t* hist, long rank, long* before, int* ws, int* res) {
     const int tid = threadIdx.x;
@@ -789,9 +797,11 @@ __device__ int find_bin_2048(const uint32_t* hist, long rank, long* before, int*
 }
 
 // Trimmed mean of row i: value at ranks [lo, hi) of the K distances, lo = (long)(K*0.2),
-// hi = (long)(K*0.8).  Exact order statistics by a 3-level radix select on the f32 bit
-// patterns (11+11+10 bits), then the window sum in fp64 (fixed order; the reference's sorted
-// sequential sum may differ in the last bits -- the final kernel re-scores near ties exactly).
+// hi = (long)(K*0.8).  Exact order statistics by a 3-level radix select (11+11+10 bits) on the
+// f32 bit patterns of the SQUARED distances s (sqrtf is monotone, so the sorted distances are
+// sqrtf of the sorted s: no square root in the selection passes), then the window sum of
+// sqrtf(s) in fp64 (fixed order; the reference's sorted sequential sum may differ in the last
+// bits -- the final kernel re-scores near ties exactly).
 __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __restrict__ kcount,
                                                              const float* __restrict__ rv,
                                                              int stride, double trim_lo,
@@ -822,7 +832,7 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     for (int k = tid; k < 2048; k += 256) histA[k] = 0;
     __syncthreads();
     for (int j = tid; j < K; j += 256) {
-        const uint32_t key = __float_as_uint(rdist(xi, yi, zi, X[j], Y[j], Z[j]));
+        const uint32_t key = __float_as_uint(rdist2(xi, yi, zi, X[j], Y[j], Z[j]));
         atomicAdd(&histA[key >> 21], 1u);
     }
     __syncthreads();
@@ -836,7 +846,7 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     }
     __syncthreads();
     for (int j = tid; j < K; j += 256) {
-        const uint32_t key = __float_as_uint(rdist(xi, yi, zi, X[j], Y[j], Z[j]));
+        const uint32_t key = __float_as_uint(rdist2(xi, yi, zi, X[j], Y[j], Z[j]));
         const uint32_t top = key >> 21;
         if (top == (uint32_t)ba) atomicAdd(&histA[(key >> 10) & 2047], 1u);
         if (top == (uint32_t)bb) atomicAdd(&histB[(key >> 10) & 2047], 1u);
@@ -854,7 +864,7 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     }
     __syncthreads();
     for (int j = tid; j < K; j += 256) {
-        const uint32_t key = __float_as_uint(rdist(xi, yi, zi, X[j], Y[j], Z[j]));
+        const uint32_t key = __float_as_uint(rdist2(xi, yi, zi, X[j], Y[j], Z[j]));
         const uint32_t top = key >> 10;
         if (top == pa) atomicAdd(&histA[key & 1023], 1u);
         if (top == pb) atomicAdd(&histB[key & 1023], 1u);
@@ -871,9 +881,8 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     // level 3: sum of the keys strictly between va and vb
     double acc = 0.0;
     for (int j = tid; j < K; j += 256) {
-        const float d = rdist(xi, yi, zi, X[j], Y[j], Z[j]);
-        const uint32_t key = __float_as_uint(d);
-        if (key > va && key < vb) acc += (double)d;
+        const uint32_t key = __float_as_uint(rdist2(xi, yi, zi, X[j], Y[j], Z[j]));
+        if (key > va && key < vb) acc += (double)__builtin_sqrtf(__uint_as_float(key));
     }
     red[tid] = acc;
     __syncthreads();
@@ -884,12 +893,12 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     if (tid == 0) {
         double sum;
         if (va == vb) {
-            sum = (double)(hi - lo) * (double)__uint_as_float(va);
+            sum = (double)(hi - lo) * (double)__builtin_sqrtf(__uint_as_float(va));
         } else {
             const long na = le_a - lo;   // ranks lo .. le_a-1 hold va
             const long nb = hi - lt_b;   // ranks lt_b .. hi-1 hold vb
-            sum = red[0] + (double)na * (double)__uint_as_float(va) +
-                  (double)nb * (double)__uint_as_float(vb);
+            sum = red[0] + (double)na * (double)__builtin_sqrtf(__uint_as_float(va)) +
+                  (double)nb * (double)__builtin_sqrtf(__uint_as_float(vb));
         }
         tmean[(size_t)p * stride + i] = sum / ((double)(hi - lo) * 1.0);
     }
@@ -946,28 +955,40 @@ __global__ __launch_bounds__(1024) void consensus_input_kernel(const float* __re
 }
 
 // ---- pruning by rigorous bounds -------------------------------------------------------
-// Every row's K distances (the reference's exact f32 values) are binned into NB geometric
-// bins (64 per binade over 20 binades below the set's diameter, underflow in bin 0).  From the
-// exact bin counts, the trimmed sum over ranks [lo, hi) is bracketed by
-//   LB = sum_b n_b(window) * lower_edge(b),  UB = sum_b n_b(window) * upper_edge(b)
+// Every row's K squared distances s_ij (the reference's exact f32 dx*dx + dy*dy + dz*dz, whose
+// correctly rounded sqrtf is its distance) are binned into NB geometric bins: 32 per binade of
+// s (= 64 per binade of the distance) over the 40 binades of s below the squared diameter of
+// the set, underflow in bin 0.  sqrtf is monotone, so a value in bin [E_b, E_b+1) has distance
+// in [sqrtf(E_b), sqrtf(E_b+1)] and, from the exact bin counts, the trimmed sum over ranks
+// [lo, hi) is bracketed by
+//   LB = sum_b n_b(window) * sqrtf(E_b),  UB = sum_b n_b(window) * sqrtf(E_b+1)
 // (relative width <= 2^-6).  A row whose LB exceeds the smallest UB cannot be the argmin; only
-// the survivors get the exact order statistics.  8 rows share each column load.
+// the survivors get the exact order statistics.  No square root in the K^2 loop.
+// Block = 8 rows x 256 columns at a time; lane l takes row (l + t) & 7 at step t, so one
+// atomic wave-instruction spreads over 8 rows (same-address conflicts <= 8-way instead of
+// 64-way for a concentrated row), and the row stride (== 4 mod 32 words) puts the same bin of
+// different rows in different banks.
 constexpr int kBoundRows = 8;
-constexpr int kBinsPerBinade = 64;
-constexpr int kBinades = 20;
+constexpr int kBinsPerBinade = 32;    // of s = d^2
+constexpr int kBinades = 40;          // of s
 constexpr int kNB = kBinsPerBinade * kBinades;  // 1280
+constexpr int kHistStride = kNB + 4;
 
+// first s-binade of the bins: the 40 binades ending with the one holding D^2 (D = dscale is
+// the bounding-box diagonal rounded up, >= every distance, so every s_ij <= D^2)
 __device__ __forceinline__ int bounds_elo(float D) {
-    int t = (int)(__float_as_uint(D) >> 23) + 1;
-    int e = t - kBinades;
+    const float D2 = D * D * (1.0f + 0x1p-20f);
+    const int t = (int)(__float_as_uint(D2) >> 23) + 1;
+    const int e = t - kBinades;
     return e < 1 ? 1 : e;
 }
-
+// distance bounds of bin b (rigorous: sqrtf of the s-edges; sqrtf is monotone)
 __device__ __forceinline__ float bin_lower(int elo, int b) {
-    return b == 0 ? 0.f : __uint_as_float((uint32_t)((elo << 6) + b) << 17);
+    return b == 0 ? 0.f : __builtin_sqrtf(__uint_as_float((uint32_t)((elo << 5) + b) << 18));
 }
 __device__ __forceinline__ float bin_upper(int elo, int b) {
-    return b == kNB - 1 ? kInf : __uint_as_float((uint32_t)((elo << 6) + b + 1) << 17);
+    return b == kNB - 1 ? kInf
+                        : __builtin_sqrtf(__uint_as_float((uint32_t)((elo << 5) + b + 1) << 18));
 }
 
 __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __restrict__ kcount,
@@ -977,8 +998,8 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
                                                                double trim_hi,
                                                                double* __restrict__ lb,
                                                                double* __restrict__ ub) {
-    __shared__ uint32_t hist[kBoundRows][kNB];
-    const int p = blockIdx.y, tid = threadIdx.x;
+    __shared__ uint32_t hist[kBoundRows * kHistStride];
+    const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
     const int r0 = blockIdx.x * kBoundRows;
     if (r0 >= K) return;
@@ -986,25 +1007,28 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     const float* Y = X + stride;
     const float* Z = Y + stride;
     const int elo = bounds_elo(dscale[p]);
-    const int base = elo << 6;
+    const int base = elo << 5;
     float xi[kBoundRows], yi[kBoundRows], zi[kBoundRows];
+    int hoff[kBoundRows];
 #pragma unroll
-    for (int r = 0; r < kBoundRows; r++) {
+    for (int t = 0; t < kBoundRows; t++) {
+        const int r = (lane + t) & (kBoundRows - 1);
         const int row = min(r0 + r, K - 1);
-        xi[r] = X[row];
-        yi[r] = Y[row];
-        zi[r] = Z[row];
+        xi[t] = X[row];
+        yi[t] = Y[row];
+        zi[t] = Z[row];
+        hoff[t] = r * kHistStride;
     }
-    for (int k = tid; k < kBoundRows * kNB; k += 256) (&hist[0][0])[k] = 0u;
+    for (int k = tid; k < kBoundRows * kHistStride; k += 256) hist[k] = 0u;
     __syncthreads();
     for (int j = tid; j < K; j += 256) {
         const float xj = X[j], yj = Y[j], zj = Z[j];
 #pragma unroll
-        for (int r = 0; r < kBoundRows; r++) {
-            const uint32_t key = __float_as_uint(rdist(xi[r], yi[r], zi[r], xj, yj, zj));
-            int b = (int)(key >> 17) - base;
-            b = b < 0 ? 0 : (b > kNB - 1 ? kNB - 1 : b);
-            atomicAdd(&hist[r][b], 1u);
+        for (int t = 0; t < kBoundRows; t++) {
+            const uint32_t key = __float_as_uint(rdist2(xi[t], yi[t], zi[t], xj, yj, zj));
+            int b = (int)(key >> 18) - base;
+            b = min(max(b, 0), kNB - 1);
+            atomicAdd(&hist[hoff[t] + b], 1u);
         }
     }
     __syncthreads();
@@ -1012,8 +1036,9 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     const long lo = (long)(K * trim_lo), hi = (long)(K * trim_hi);
     const int r = tid >> 5, sl = tid & 31;
     constexpr int per = kNB / 32;
+    const uint32_t* h = hist + r * kHistStride;
     uint32_t c = 0;
-    for (int b = sl * per; b < (sl + 1) * per; b++) c += hist[r][b];
+    for (int b = sl * per; b < (sl + 1) * per; b++) c += h[b];
     // exclusive scan over the 32 lanes of this row (within one wave half)
     uint32_t x = c;
 #pragma unroll
@@ -1024,7 +1049,7 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     long cum = (long)(x - c);
     double L = 0.0, U = 0.0;
     for (int b = sl * per; b < (sl + 1) * per; b++) {
-        const long n = hist[r][b];
+        const long n = h[b];
         const long a0 = cum > lo ? cum : lo;
         const long a1 = (cum + n) < hi ? (cum + n) : hi;
         if (a1 > a0) {
