@@ -30,6 +30,7 @@ sys.path.insert(0, ROOT)
 PEAK_FP32_VALU_UNFUSED = 157.3 / 2  # TFLOP/s: 157.3 counts an FMA as 2; sub/mul/add are 1 each
 PEAK_FP64_VALU = 78.6               # TFLOP/s (MI355X spec, FMA = 2)
 PEAK_HBM = 8000.0                   # GB/s
+PEAK_BF16_MFMA = 2516.6             # TFLOP/s dense (256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz)
 
 
 def parse():
@@ -74,12 +75,15 @@ def stage_work(stage, B, kpts, iters, res):
     M = res["M"].astype(np.float64)
     s = np.floor(M * 0.25)
     K = res["K"].astype(np.float64)
-    if stage == "knn2_partial":
-        flops = 3.0 * kpts * kpts * 64 * B  # sub, mul, add per element (flann::L2 order, no FMA)
-        return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", "3*N*T*64 fp32 ops per pair"
+    if stage in ("knn2_filter", "knn2_candidates"):
+        flops = 3 * 2.0 * kpts * kpts * 64 * B  # q_hi t_hi + q_hi t_lo + q_lo t_hi, bf16 MFMA
+        return flops, "TFLOP/s", PEAK_BF16_MFMA, "mfma", "3 bf16 MFMA products x 2*N*T*64 per pair"
     if stage == "gram":
         flops = float(np.sum(s * iters * (12 + 72)))  # 12 mul + 36 FMA per sampled row, fp64
         return flops, "TFLOP/s", PEAK_FP64_VALU, "valu", "84 fp64 flops per sampled row"
+    if stage == "consensus_bounds":
+        flops = float(np.sum(K * K * 8.0))  # 3 sub, 3 mul, 2 add per squared distance, K^2
+        return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", "8 fp32 ops per squared distance, K^2"
     if stage == "consensus_rows":
         flops = float(np.sum(K * K * 9.0))  # 3 sub, 3 mul, 2 add, 1 sqrt per distance
         return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", "9 fp32 ops per distance, K^2"

@@ -86,9 +86,9 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_eight_point_estimation", "erp_pair_batch_run", "erp_ctx_set_profiling",
             "erp_stage_name", "erp_ctx_stage_times", "erp_eight_point_hypotheses_dev",
             "erp_consensus_dev"]
-STAGES = ["knn2_partial", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
+STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
-          "consensus_select", "windows", "gram"]
+          "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore"]
 
 
 class ErpError(RuntimeError):

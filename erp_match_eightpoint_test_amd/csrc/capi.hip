@@ -68,7 +68,7 @@ struct erp_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
-    DevBuf part, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
+    DevBuf part, pu, ccount, cand, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins;
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -157,7 +157,8 @@ erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
 erp_status erp_ctx_destroy(erp_ctx* ctx) {
     if (!ctx) return ERP_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    DevBuf* all[] = {&ctx->part, &ctx->matches, &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
+    DevBuf* all[] = {&ctx->part, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->matches,
+                     &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
                      &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
                      &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
@@ -178,19 +179,55 @@ erp::BatchShape make_shape(int n_pairs, int max_nq, int max_nt, int iters, doubl
     sh.n_pairs = n_pairs;
     sh.max_nq = std::max(max_nq, 1);
     sh.max_nt = std::max(max_nt, 1);
-    const int qblocks = (sh.max_nq + 255) / 256;
-    const int tmax = (sh.max_nt + 63) / 64;
+    // matcher filter grid: 128 queries x one train chunk per block, >= ~2048 blocks
+    const int qblocks = (sh.max_nq + 127) / 128;
+    const int tmax = (sh.max_nt + 31) / 32;
     int chunks = (2048 + qblocks * n_pairs - 1) / (qblocks * n_pairs);
     chunks = std::max(1, std::min(chunks, tmax));
     int chunk_len = (sh.max_nt + chunks - 1) / chunks;
-    chunk_len = (chunk_len + 63) / 64 * 64;
-    sh.chunk_len = chunk_len;
-    sh.chunks = (sh.max_nt + chunk_len - 1) / chunk_len;
+    chunk_len = (chunk_len + 31) / 32 * 32;
+    sh.fchunk_len = chunk_len;
+    sh.fchunks = (sh.max_nt + chunk_len - 1) / chunk_len;
     sh.iters = std::max(iters, 1);
     sh.max_s = std::max((int)(sh.max_nq * frac), 1);
     sh.idx_stride = sh.max_s;
     sh.sel_words = (sh.max_nq + 30) / 31 + 1;
     return sh;
+}
+
+bool ensure_matcher(erp_ctx* c, const erp::BatchShape& sh) {
+    const size_t PQ = (size_t)sh.n_pairs * sh.max_nq;
+    return ensure(c->part, PQ * sizeof(erp::Top2)) &&
+           ensure(c->pu, PQ * sh.fchunks * sizeof(float2)) && ensure(c->ccount, PQ * 4) &&
+           ensure(c->cand, PQ * erp::kCandCap * 4);
+}
+
+// exact k=2 + ratio test: MFMA filter (upper bounds), candidates, exact rescoring, merge
+erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int64_t* oq,
+                       const int64_t* ot, const erp::BatchShape& sh, float ratio,
+                       erp_dmatch* matches, int32_t* counts, int32_t* flags, hipStream_t st) {
+    auto* pu = (float2*)ctx->pu.p;
+    auto* cc = (int32_t*)ctx->ccount.p;
+    auto* cand = (int32_t*)ctx->cand.p;
+    {
+        StageTimer _t(ctx, ERP_STAGE_KNN2_FILTER, st);
+        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, pu, cc, cand, 1, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_KNN2_CANDIDATES, st);
+        ERP_CK(hipMemsetAsync(cc, 0, (size_t)sh.n_pairs * sh.max_nq * 4, st));
+        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, pu, cc, cand, 2, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_KNN2_RESCORE, st);
+        ERP_CK(erp::launch_knn2_rescore(dq, dt, oq, ot, sh, cc, cand, (erp::Top2*)ctx->part.p, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_KNN2_MERGE, st);
+        ERP_CK(erp::launch_knn2_merge((erp::Top2*)ctx->part.p, oq, ot, sh, ratio, matches, counts,
+                                      flags, st));
+    }
+    return ERP_OK;
 }
 
 erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_batch_outputs* out) {
@@ -334,9 +371,9 @@ erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable) {
 
 const char* erp_stage_name(int32_t stage) {
     static const char* names[ERP_STAGE_COUNT] = {
-        "knn2_partial", "knn2_merge", "bearings", "jump_prep", "sampler",
+        "knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler",
         "eigen", "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
-        "consensus_select", "windows", "gram"};
+        "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore"};
     return (stage >= 0 && stage < ERP_STAGE_COUNT) ? names[stage] : "unknown";
 }
 
@@ -366,7 +403,7 @@ erp_status erp_ctx_reserve(erp_ctx* ctx, int32_t n_pairs, int32_t max_nq, int32_
     std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     const erp::BatchShape sh = make_shape(n_pairs, max_nq, max_nt, iters, 0.25);
-    if (!ensure(ctx->part, (size_t)n_pairs * sh.chunks * sh.max_nq * sizeof(erp::Top2)) ||
+    if (!ensure_matcher(ctx, sh) ||
         !ensure(ctx->matches, (size_t)n_pairs * sh.max_nq * sizeof(erp_dmatch)))
         return ERP_OUT_OF_MEMORY;
     return ensure_estimator(ctx, sh, nullptr);
@@ -385,8 +422,7 @@ erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* b, float ratio
     hipStream_t st = (hipStream_t)stream;
     const erp::BatchShape sh = make_shape(b->n_pairs, b->max_nq, b->max_nt, cfg->iters,
                                           cfg->sample_frac);
-    if (!ensure(ctx->part, (size_t)sh.n_pairs * sh.chunks * sh.max_nq * sizeof(erp::Top2)))
-        return ERP_OUT_OF_MEMORY;
+    if (!ensure_matcher(ctx, sh)) return ERP_OUT_OF_MEMORY;
     erp_dmatch* matches = out->matches;
     if (!matches) {
         if (!ensure(ctx->matches, (size_t)sh.n_pairs * sh.max_nq * sizeof(erp_dmatch)))
@@ -398,16 +434,9 @@ erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* b, float ratio
     es = upload_w0(ctx, cfg, st);
     if (es != ERP_OK) return es;
     ERP_CK(hipMemsetAsync(ctx->flags.p, 0, (size_t)sh.n_pairs * 4, st));
-    {
-        StageTimer _t(ctx, ERP_STAGE_KNN2_PARTIAL, st);
-        ERP_CK(erp::launch_knn2_partial(b->desc_l, b->desc_r, b->off_l, b->off_r, sh,
-                                        (erp::Top2*)ctx->part.p, st));
-    }
-    {
-        StageTimer _t(ctx, ERP_STAGE_KNN2_MERGE, st);
-        ERP_CK(erp::launch_knn2_merge((erp::Top2*)ctx->part.p, b->off_l, b->off_r, sh, ratio, matches,
-                                      (int32_t*)ctx->counts.p, (int32_t*)ctx->flags.p, st));
-    }
+    es = run_matcher(ctx, b->desc_l, b->desc_r, b->off_l, b->off_r, sh, ratio, matches,
+                     (int32_t*)ctx->counts.p, (int32_t*)ctx->flags.p, st);
+    if (es != ERP_OK) return es;
     {
         StageTimer _t(ctx, ERP_STAGE_BEARINGS, st);
         ERP_CK(erp::launch_bearings_from_matches(matches, (int32_t*)ctx->counts.p, b->kp_l, b->kp_r,
@@ -432,21 +461,13 @@ erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,
         return ERP_OK;
     }
     const erp::BatchShape sh = make_shape(1, nq, nt, 1, 0.25);
-    if (!ensure(ctx->part, (size_t)sh.chunks * sh.max_nq * sizeof(erp::Top2)) ||
-        !ensure(ctx->off, 4 * sizeof(int64_t)) || !ensure(ctx->flags, 16))
+    if (!ensure_matcher(ctx, sh) || !ensure(ctx->off, 4 * sizeof(int64_t)) ||
+        !ensure(ctx->flags, 16))
         return ERP_OUT_OF_MEMORY;
     ERP_CK(erp::launch_set_i64x4((int64_t*)ctx->off.p, 0, nq, 0, nt, st));
     const int64_t* oq = (const int64_t*)ctx->off.p;
-    {
-        StageTimer _t(ctx, ERP_STAGE_KNN2_PARTIAL, st);
-        ERP_CK(erp::launch_knn2_partial(d_query, d_train, oq, oq + 2, sh, (erp::Top2*)ctx->part.p, st));
-    }
-    {
-        StageTimer _t(ctx, ERP_STAGE_KNN2_MERGE, st);
-        ERP_CK(erp::launch_knn2_merge((erp::Top2*)ctx->part.p, oq, oq + 2, sh, ratio, d_out, d_count,
-                                      (int32_t*)ctx->flags.p, st));
-    }
-    return ERP_OK;
+    return run_matcher(ctx, d_query, d_train, oq, oq + 2, sh, ratio, d_out, d_count,
+                       (int32_t*)ctx->flags.p, st);
 }
 
 erp_status erp_match_two_image(erp_ctx* ctx, const float* h_desc1, int32_t n1, const float* h_desc2,

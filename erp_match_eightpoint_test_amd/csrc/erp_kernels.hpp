@@ -11,6 +11,7 @@ namespace erp {
 constexpr int kDim = 64;          // SURF descriptor length (extended=false)
 constexpr int kMaxQ = 24;         // jump polynomials x^(64(M-1)2^k): waves per pair < 2^24
 constexpr int kPolyWords = 31;    // glibc TYPE_3 degree
+constexpr int kCandCap = 64;      // matcher candidates kept per query (more: exact sweep)
 
 struct Top2 {                     // partial k=2 result of one train chunk for one query
     float d0;                     // best squared distance
@@ -20,7 +21,7 @@ struct Top2 {                     // partial k=2 result of one train chunk for o
 
 // scratch the pipeline needs for one batch (all device pointers, sized by the context)
 struct Workspace {
-    Top2* part;                   // [pairs][chunks][max_nq]
+    Top2* part;                   // [pairs][max_nq] exact k=2 per query
     erp_dmatch* matches;          // [pairs][max_nq]
     int32_t* counts;              // [pairs] M
     double* pts;                  // [pairs][max_nq + 1][6] bearings (l, r); last row = 0
@@ -40,7 +41,7 @@ struct Workspace {
 struct BatchShape {
     int n_pairs;
     int max_nq, max_nt;
-    int chunks, chunk_len;
+    int fchunks, fchunk_len;      // train chunks of the matcher's filter passes
     int iters;
     int max_s;                    // (int)(max_nq * sample_frac)
     int idx_stride;               // entries of one hypothesis in the debug samples output
@@ -52,9 +53,14 @@ hipError_t launch_set_i64x4(int64_t* p, int64_t a, int64_t b, int64_t c, int64_t
                             hipStream_t st);                                       // lifetime)
 void init_constants();            // reduction table for the jump polynomials (once per device)
 
-hipError_t launch_knn2_partial(const float* desc_q, const float* desc_t, const int64_t* off_q,
-                               const int64_t* off_t, const BatchShape& sh, Top2* part,
-                               hipStream_t st);
+// matcher: pass 1 (per-chunk top-2 upper bounds pu), pass 2 (candidates; ccount zeroed
+// before), rescore (exact Top2 per query into part[pairs][max_nq]), merge (ratio + compaction)
+hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                              const int64_t* off_t, const BatchShape& sh, float2* pu,
+                              int32_t* ccount, int32_t* cand, int pass, hipStream_t st);
+hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                               const int64_t* off_t, const BatchShape& sh, const int32_t* ccount,
+                               const int32_t* cand, Top2* part, hipStream_t st);
 hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
                              const BatchShape& sh, float ratio, erp_dmatch* matches,
                              int32_t* counts, int32_t* flags, hipStream_t st);

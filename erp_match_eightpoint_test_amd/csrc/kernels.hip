@@ -6,7 +6,7 @@
 // the fp64 Gram accumulation, which is parity-checked by tolerance).
 //
 // Stage                    reference                                   kernel
-// exact k=2 + ratio        src/feature_matcher.cpp:42-59               knn2_partial / knn2_merge
+// exact k=2 + ratio        src/feature_matcher.cpp:42-59               knn2_filter/_rescore/_merge
 // gather + pixel->bearing  src/spherical_surf.cpp:155-162,
 //                          src/eight_point.cpp:163-186                 bearings_*
 // random_array sampler     src/eight_point.hpp:30-59 (glibc replay)    jump_prep / sampler_gram
@@ -63,61 +63,242 @@ __device__ int block_exclusive_scan(int v, int* ws, int* total) {
 }
 
 // ===================================================================== matcher =========
-// One thread = one query descriptor held in VGPRs (64 f32); a 64-row tile of train
-// descriptors is staged in LDS and read as wave-uniform (broadcast) float4s.  Distance in the
-// flann::L2<float> order: per group of 4, acc += d0*d0 + d1*d1 + d2*d2 + d3*d3 (no FMA).
-// Each block covers 256 queries x one train chunk; knn2_merge folds the chunks in order.
-__global__ __launch_bounds__(256) void knn2_partial_kernel(const float* __restrict__ dq,
-                                                           const float* __restrict__ dt,
-                                                           const int64_t* __restrict__ off_q,
-                                                           const int64_t* __restrict__ off_t,
-                                                           int chunk_len, int chunks, int max_nq,
-                                                           Top2* __restrict__ part) {
-    __shared__ float4 tile[64 * 16];
+// Exact k=2 in three steps (the result is identical to a brute-force sweep in the flann::L2
+// order, lowest train index winning ties):
+//  1. knn2_filter<1>: approximate squared distances a = |q|^2 + |t|^2 - 2 q.t with the dot
+//     product on bf16 MFMA in three terms (q_hi t_hi + q_hi t_lo + q_lo t_hi, q = q_hi + q_lo
+//     split exactly in bf16 pieces, residual <= 2^-16 |q| per component; f32 accumulation).
+//     For every pair |a - e| <= eps(q,t) = 2^-12 (|q|^2 + |t|^2), e = the reference's exact
+//     f32 value (the error budget -- split residuals, MFMA f32 accumulation of 192 products, the
+//     norms, and e's own rounding against the real distance -- stays below half of eps even if
+//     every rounding truncates).  Each query keeps the two smallest u = a + eps per chunk.
+//  2. knn2_filter<2>: U2 = the second smallest u over all chunks bounds e of the true second
+//     neighbour from above; every train row with l = a - eps <= U2 (which includes every row
+//     with e <= e_(2), i.e. both true neighbours and all their ties) is a candidate.
+//  3. knn2_rescore: exact flann::L2 distances of the candidates (a full exact sweep if a query
+//     ever has more than kCandCap), giving (d0, j0, d1) exactly.
+// Matrix layout for v_mfma_f32_32x32x16_bf16: A = 32 train rows x 16 dims (LDS, staged and
+// split per 32-row tile), B = 16 dims x 32 queries (registers, split once), D = 32 x 32 with
+// the query on the lane (col = lane & 31) and 16 train rows in the registers
+// (row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)).  Block = 4 waves x 32 queries x one train chunk.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kFQ = 128;            // queries per block
+constexpr int kFT = 32;             // train rows per tile
+constexpr int kFRow = 72;           // bf16 per LDS row: 64 + 8 pad (conflict-free b128 reads)
+constexpr float kFEps = 0x1p-12f;
+constexpr float kFTiny = 0x1p-100f; // absolute floor (flushed denormals)
+
+struct FilterLds {
+    bf16x8 hi[2][kFT * kFRow / 8];
+    bf16x8 lo[2][kFT * kFRow / 8];
+    float tt[2][kFT];
+};
+
+__device__ __forceinline__ void split8(const float4 a, const float4 b, bf16x8& hi, bf16x8& lo) {
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const __bf16 h = (__bf16)v[k];
+        hi[k] = h;
+        lo[k] = (__bf16)(v[k] - (float)h);
+    }
+}
+
+__device__ __forceinline__ float sq8(const float4 a, const float4 b) {
+    return a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z +
+           b.w * b.w;
+}
+
+template <int PASS>
+__global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restrict__ dq,
+                                                          const float* __restrict__ dt,
+                                                          const int64_t* __restrict__ off_q,
+                                                          const int64_t* __restrict__ off_t,
+                                                          int chunk_len, int chunks, int max_nq,
+                                                          float2* __restrict__ pu,
+                                                          int32_t* __restrict__ ccount,
+                                                          int32_t* __restrict__ cand) {
+    __shared__ FilterLds sm;
     const int p = blockIdx.z;
     const int64_t qbase = off_q[p];
     const int nq = (int)(off_q[p + 1] - qbase);
     const int64_t tbase = off_t[p];
     const int nt = (int)(off_t[p + 1] - tbase);
-    const int q0 = blockIdx.x * 256;
+    const int q0 = blockIdx.x * kFQ;
     const int t0 = blockIdx.y * chunk_len;
-    if (q0 >= nq || t0 >= nt) return;
+    if (q0 >= nq || t0 >= nt) return;  // uniform over the block
     const int t1 = min(t0 + chunk_len, nt);
-    const int q = q0 + threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
+    const int q = q0 + (tid >> 6) * 32 + (lane & 31);
     const bool qv = q < nq;
-    float4 qr[16];
-    const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + (qv ? q : 0)) * kDim);
+    // query fragments (B operand): dims 16c + 8h .. +7 of query q, split once
+    bf16x8 qh[4], ql[4];
+    float qq = 0.f;
+    {
+        const float* qp = dq + (qbase + (qv ? q : 0)) * kDim + 8 * h;
 #pragma unroll
-    for (int c = 0; c < 16; c++) qr[c] = qp[c];
-    float b0 = kInf, b1 = kInf;
-    int j0 = -1;
-    for (int tt = t0; tt < t1; tt += 64) {
-        const int n = min(64, t1 - tt);
+        for (int c = 0; c < 4; c++) {
+            const float4 a = *reinterpret_cast<const float4*>(qp + 16 * c);
+            const float4 b = *reinterpret_cast<const float4*>(qp + 16 * c + 4);
+            qq += sq8(a, b);
+            split8(a, b, qh[c], ql[c]);
+        }
+        qq += __shfl_xor(qq, 32, 64);
+    }
+    float U2 = 0.f;
+    if (PASS == 2) {
+        const int nch = (nt + chunk_len - 1) / chunk_len;
+        float m1 = kInf, m2 = kInf;
+        for (int c = 0; c < nch; c++) {
+            const float2 v = pu[((size_t)p * chunks + c) * max_nq + (qv ? q : 0)];
+            m2 = fminf(fmaxf(m1, v.x), fminf(m2, v.y));
+            m1 = fminf(m1, v.x);
+        }
+        U2 = m2;
+    }
+    float m1 = kInf, m2 = kInf;
+    // staging: thread -> train row tid >> 3 of the tile, floats 8 (tid & 7) .. +7
+    const int srow = tid >> 3, scol = 8 * (tid & 7);
+    float4 ga = make_float4(0.f, 0.f, 0.f, 0.f), gb = ga;
+    auto gload = [&](int tile0) {
+        const int j = tile0 + srow;
+        if (j < t1) {
+            const float* tp = dt + (tbase + j) * kDim + scol;
+            ga = *reinterpret_cast<const float4*>(tp);
+            gb = *reinterpret_cast<const float4*>(tp + 4);
+        } else {
+            ga = make_float4(0.f, 0.f, 0.f, 0.f);
+            gb = ga;
+        }
+    };
+    const int ntiles = (t1 - t0 + kFT - 1) / kFT;
+    gload(t0);
+    const int r = lane & 31;
+    for (int k = 0; k < ntiles; k++) {
+        const int buf = k & 1, tile0 = t0 + k * kFT;
+        {
+            bf16x8 hi, lo;
+            split8(ga, gb, hi, lo);
+            float ss = sq8(ga, gb);
+            ss += __shfl_xor(ss, 1, 64);
+            ss += __shfl_xor(ss, 2, 64);
+            ss += __shfl_xor(ss, 4, 64);
+            sm.hi[buf][(srow * kFRow + scol) / 8] = hi;
+            sm.lo[buf][(srow * kFRow + scol) / 8] = lo;
+            if ((tid & 7) == 0) sm.tt[buf][srow] = (tile0 + srow < t1) ? ss : kInf;
+        }
         __syncthreads();
-        const float4* tp = reinterpret_cast<const float4*>(dt + (tbase + tt) * kDim);
-        for (int k = threadIdx.x; k < n * 16; k += 256) tile[k] = tp[k];
-        __syncthreads();
-        for (int v = 0; v < n; v++) {
-            float acc = 0.f;
+        if (k + 1 < ntiles) gload(tile0 + kFT);
+        f32x16 acc = {};
 #pragma unroll
-            for (int c = 0; c < 16; c++) {
-                const float4 tv = tile[v * 16 + c];
-                const float d0 = qr[c].x - tv.x;
-                const float d1 = qr[c].y - tv.y;
-                const float d2 = qr[c].z - tv.z;
-                const float d3 = qr[c].w - tv.w;
-                acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
-            }
-            if (acc < b0) {
-                b1 = b0;
-                b0 = acc;
-                j0 = tt + v;
-            } else if (acc < b1) {
-                b1 = acc;
+        for (int c = 0; c < 4; c++) {
+            const bf16x8 ah = sm.hi[buf][(r * kFRow + 16 * c + 8 * h) / 8];
+            const bf16x8 al = sm.lo[buf][(r * kFRow + 16 * c + 8 * h) / 8];
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, qh[c], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ql[c], acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, qh[c], acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const float4 t4 = *reinterpret_cast<const float4*>(&sm.tt[buf][8 * g + 4 * h]);
+            const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const float st = qq + tv[e];
+                const float a = __builtin_fmaf(-2.f, acc[4 * g + e], st);
+                if (PASS == 1) {
+                    const float u = __builtin_fmaf(kFEps, st, a) + kFTiny;
+                    m2 = __builtin_amdgcn_fmed3f(m1, m2, u);
+                    m1 = fminf(m1, u);
+                } else {
+                    const float l = __builtin_fmaf(-kFEps, st, a) - kFTiny;
+                    if (l <= U2 && qv) {  // NaN (rows past the chunk: inf - inf) never passes
+                        const int slot = atomicAdd(&ccount[(size_t)p * max_nq + q], 1);
+                        if (slot < kCandCap)
+                            cand[((size_t)p * max_nq + q) * kCandCap + slot] =
+                                tile0 + 8 * g + 4 * h + e;
+                    }
+                }
             }
         }
     }
-    if (qv) part[((size_t)p * chunks + blockIdx.y) * max_nq + q] = Top2{b0, j0, b1};
+    if (PASS == 1) {
+        const float o1 = __shfl_xor(m1, 32, 64), o2 = __shfl_xor(m2, 32, 64);
+        const float n2 = fminf(fmaxf(m1, o1), fminf(m2, o2));
+        const float n1 = fminf(m1, o1);
+        if (h == 0 && qv) pu[((size_t)p * chunks + blockIdx.y) * max_nq + q] = make_float2(n1, n2);
+    }
+}
+
+// exact squared distance in the flann::L2<float> order: per group of 4,
+// acc += d0*d0 + d1*d1 + d2*d2 + d3*d3 (no FMA)
+__device__ __forceinline__ float exact_l2(const float4* qr, const float4* __restrict__ tp) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        const float4 tv = tp[c];
+        const float d0 = qr[c].x - tv.x;
+        const float d1 = qr[c].y - tv.y;
+        const float d2 = qr[c].z - tv.z;
+        const float d3 = qr[c].w - tv.w;
+        acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    }
+    return acc;
+}
+
+// one wave per query: exact distances of its candidates (or of every train row when the
+// candidate list overflowed), then the k=2 result with the sweep's tie rule
+__global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restrict__ dq,
+                                                           const float* __restrict__ dt,
+                                                           const int64_t* __restrict__ off_q,
+                                                           const int64_t* __restrict__ off_t,
+                                                           int max_nq,
+                                                           const int32_t* __restrict__ ccount,
+                                                           const int32_t* __restrict__ cand,
+                                                           Top2* __restrict__ part) {
+    const int p = blockIdx.y, lane = wave_lane();
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t qbase = off_q[p];
+    const int nq = (int)(off_q[p + 1] - qbase);
+    const int64_t tbase = off_t[p];
+    const int nt = (int)(off_t[p + 1] - tbase);
+    if (q >= nq) return;
+    float4 qr[16];
+    const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
+#pragma unroll
+    for (int c = 0; c < 16; c++) qr[c] = qp[c];
+    const int n = ccount[(size_t)p * max_nq + q];
+    float b0 = kInf, b1 = kInf;
+    int j0 = 0x7fffffff;
+    auto consider = [&](int j) {
+        const float acc = exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim));
+        if (acc < b0 || (acc == b0 && j < j0)) {
+            b1 = b0;
+            b0 = acc;
+            j0 = j;
+        } else if (acc < b1) {
+            b1 = acc;
+        }
+    };
+    if (n <= kCandCap) {
+        if (lane < n) consider(cand[((size_t)p * max_nq + q) * kCandCap + lane]);
+    } else {
+        for (int j = lane; j < nt; j += 64) consider(j);
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const float ob0 = __shfl_xor(b0, o, 64), ob1 = __shfl_xor(b1, o, 64);
+        const int oj = __shfl_xor(j0, o, 64);
+        if (ob0 < b0 || (ob0 == b0 && oj < j0)) {
+            b1 = fminf(b0, ob1);
+            b0 = ob0;
+            j0 = oj;
+        } else {
+            b1 = fminf(b1, ob0);
+        }
+    }
+    if (lane == 0) part[(size_t)p * max_nq + q] = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
 }
 
 // Fold chunk partials in train order (lowest index wins ties), apply the ratio test
@@ -1342,20 +1523,34 @@ void init_constants() {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_red), red, sizeof(red));
 }
 
-hipError_t launch_knn2_partial(const float* desc_q, const float* desc_t, const int64_t* off_q,
-                               const int64_t* off_t, const BatchShape& sh, Top2* part,
-                               hipStream_t st) {
-    dim3 grid((sh.max_nq + 255) / 256, sh.chunks, sh.n_pairs);
-    hipLaunchKernelGGL(knn2_partial_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
-                       sh.chunk_len, sh.chunks, sh.max_nq, part);
+hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                              const int64_t* off_t, const BatchShape& sh, float2* pu,
+                              int32_t* ccount, int32_t* cand, int pass, hipStream_t st) {
+    dim3 grid((sh.max_nq + kFQ - 1) / kFQ, sh.fchunks, sh.n_pairs);
+    if (pass == 1)
+        hipLaunchKernelGGL(knn2_filter_kernel<1>, grid, dim3(256), 0, st, desc_q, desc_t, off_q,
+                           off_t, sh.fchunk_len, sh.fchunks, sh.max_nq, pu, ccount, cand);
+    else
+        hipLaunchKernelGGL(knn2_filter_kernel<2>, grid, dim3(256), 0, st, desc_q, desc_t, off_q,
+                           off_t, sh.fchunk_len, sh.fchunks, sh.max_nq, pu, ccount, cand);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                               const int64_t* off_t, const BatchShape& sh, const int32_t* ccount,
+                               const int32_t* cand, Top2* part, hipStream_t st) {
+    dim3 grid((sh.max_nq + 3) / 4, sh.n_pairs);
+    hipLaunchKernelGGL(knn2_rescore_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
+                       sh.max_nq, ccount, cand, part);
     return hipGetLastError();
 }
 
 hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
                              const BatchShape& sh, float ratio, erp_dmatch* matches,
                              int32_t* counts, int32_t* flags, hipStream_t st) {
+    // the rescored Top2 are one "chunk" spanning the whole train set
     hipLaunchKernelGGL(knn2_merge_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, part, off_q, off_t,
-                       sh.chunk_len, sh.chunks, sh.max_nq, ratio, matches, counts, flags);
+                       max(sh.max_nt, 1), 1, sh.max_nq, ratio, matches, counts, flags);
     return hipGetLastError();
 }
 

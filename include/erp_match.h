@@ -159,7 +159,7 @@ erp_status erp_ctx_reserve(erp_ctx* ctx, int32_t n_pairs, int32_t max_nq, int32_
 /* ---- stage timing (the reference's START_TIME/STOP_TIME, src/debug_print.h:9-13, applied to
    the hot path): HIP events recorded around every kernel on the pipeline's stream. ---- */
 typedef enum erp_stage {
-    ERP_STAGE_KNN2_PARTIAL = 0, /* exact k=2 distance sweep (dominant matcher kernel) */
+    ERP_STAGE_KNN2_FILTER = 0,  /* MFMA pass 1: per-query upper bounds of the 2nd neighbour */
     ERP_STAGE_KNN2_MERGE = 1,   /* chunk fold + ratio test + compaction */
     ERP_STAGE_BEARINGS = 2,     /* gather + pixel -> bearing */
     ERP_STAGE_JUMP_PREP = 3,    /* glibc jump-ahead polynomials */
@@ -172,7 +172,9 @@ typedef enum erp_stage {
     ERP_STAGE_CONSENSUS_SELECT = 10,
     ERP_STAGE_WINDOWS = 11,         /* per-iteration glibc end windows (jump-ahead) */
     ERP_STAGE_GRAM = 12,            /* A^T A of every sample (fp64) */
-    ERP_STAGE_COUNT = 13
+    ERP_STAGE_KNN2_CANDIDATES = 13, /* MFMA pass 2: candidate train rows per query */
+    ERP_STAGE_KNN2_RESCORE = 14,    /* exact flann::L2 distances of the candidates */
+    ERP_STAGE_COUNT = 15
 } erp_stage;
 erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable);
 const char* erp_stage_name(int32_t stage);

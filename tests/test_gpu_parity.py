@@ -66,6 +66,58 @@ def test_match_ties_and_ratio_boundary(ctx, oracle):
     assert np.array_equal(mt.view(np.uint32), ref.view(np.uint32))
 
 
+def _all_queries_vs_oracle(ctx, oracle, q, t):
+    """every query's exact k=2 through the matcher: ratio 1e30 keeps every query (checks
+    trainIdx = j0 and distance = sqrtf(d0) bit-exactly), ratio 1.0 drops exactly the queries
+    whose two nearest distances tie (checks d1 == d0 detection), ratio 0.3 = the reference."""
+    from erp_match_eightpoint_test_amd import feature_matcher
+    fm = feature_matcher(ctx=ctx)
+    for ratio in (1e30, 1.0, 0.3):
+        ref, _, _, _ = oracle.match_two_image(q, t, ratio=ratio)
+        mt = fm.match_two_image(q, t, ratio=ratio)
+        assert len(mt) == len(ref), ratio
+        assert np.array_equal(mt.view(np.uint32), ref.view(np.uint32)), ratio
+
+
+def test_match_filter_candidate_overflow(ctx, oracle):
+    """>64 train rows inside the filter's error window of one query (near-duplicates differing
+    in the last bits): the candidate list overflows and the exact sweep path must decide."""
+    rng = np.random.default_rng(11)
+    t = synth.random_descriptors(rng, 1200)
+    base = t[7].copy()
+    for k in range(300):
+        v = base.copy()
+        v[k % 64] = np.nextafter(v[k % 64], np.float32(2.0) if k % 2 else np.float32(-2.0))
+        t[100 + k] = v
+    q = np.concatenate([base[None, :], t[50:90], synth.random_descriptors(rng, 100)])
+    _all_queries_vs_oracle(ctx, oracle, q, t)
+
+
+def test_match_filter_near_ties_unnormalised(ctx, oracle):
+    """distances equal up to rounding, unnormalised magnitudes (1e-3 .. 1e2) and zero rows: the
+    filter's error bound scales with |q|^2 + |t|^2 and must never drop a true neighbour."""
+    rng = np.random.default_rng(12)
+    t = synth.random_descriptors(rng, 900).astype(np.float32)
+    scale = np.exp(rng.uniform(np.log(1e-3), np.log(1e2), size=(900, 1))).astype(np.float32)
+    t = (t * scale).astype(np.float32)
+    t[3] = 0.0
+    t[4] = 0.0
+    q = t[rng.integers(0, 900, 200)] + rng.normal(0, 1e-6, (200, 64)).astype(np.float32)
+    q[0] = 0.0
+    # two train rows at the same distance from a query but on different sides
+    q[1] = t[10]
+    d = rng.normal(0, 1e-3, 64).astype(np.float32)
+    t[11] = t[10] + d
+    t[12] = t[10] - d
+    _all_queries_vs_oracle(ctx, oracle, q.astype(np.float32), t)
+
+
+@pytest.mark.parametrize("nq,nt", [(300, 4097), (4096, 4096)])
+def test_match_all_queries_vs_oracle(ctx, oracle, nq, nt):
+    p = synth.make_pair(nq * 3 + nt, n_kpts=nq, n_train=nt)
+    _all_queries_vs_oracle(ctx, oracle, p["desc_l"], p["desc_r"])
+
+
 def test_match_edge_counts(ctx):
     from erp_match_eightpoint_test_amd import ErpError, feature_matcher
     fm = feature_matcher(ctx=ctx)
