@@ -68,7 +68,7 @@ struct erp_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
-    DevBuf part, pu, ccount, cand, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
+    DevBuf part, pu, ccount, cand, bsel, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins;
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -157,7 +157,7 @@ erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
 erp_status erp_ctx_destroy(erp_ctx* ctx) {
     if (!ctx) return ERP_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    DevBuf* all[] = {&ctx->part, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->matches,
+    DevBuf* all[] = {&ctx->part, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->matches,
                      &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
                      &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
@@ -243,6 +243,7 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result)) &&
               ensure(c->dscale, P * 4) && ensure(c->lb, P * 2 * sh.iters * 8) &&
               ensure(c->ub, P * 2 * sh.iters * 8) && ensure(c->surv, P * 2 * sh.iters * 4) &&
+              ensure(c->bsel, P * 2 * sh.iters * 8) &&
               ensure(c->nsurv, P * 4);
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
@@ -327,7 +328,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
         ERP_CK(erp::launch_consensus_bounds((int32_t*)c->kcount.p, (float*)c->rv.p,
                                             (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
-                                            (double*)c->lb.p, (double*)c->ub.p, st));
+                                            (double*)c->lb.p, (double*)c->ub.p,
+                                            (int32_t*)c->bsel.p, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
@@ -337,9 +339,10 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_ROWS, st);
-        ERP_CK(erp::launch_consensus_rows((int32_t*)c->kcount.p, (float*)c->rv.p, sh, cfg->trim_lo,
-                                          cfg->trim_hi, (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
-                                          tmean, st));
+        ERP_CK(erp::launch_consensus_rows((int32_t*)c->kcount.p, (float*)c->rv.p,
+                                          (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
+                                          (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
+                                          (int32_t*)c->bsel.p, tmean, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_FINAL, st);

@@ -91,15 +91,17 @@ hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyp
 hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream_t st);
 hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, int stride, float* rv,
                                   float* tv, int32_t* kcount, float* dscale, hipStream_t st);
+// per-row [LB, UB] of the trimmed mean and the bins holding ranks lo / hi-1 (bsel[row][2])
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    const BatchShape& sh, double trim_lo, double trim_hi, double* lb,
-                                   double* ub, hipStream_t st);
+                                   double* ub, int32_t* bsel, hipStream_t st);
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
                                    const BatchShape& sh, double trim_lo, double trim_hi,
                                    int32_t* surv, int32_t* nsurv, double* tmean, hipStream_t st);
-hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const BatchShape& sh,
-                                 double trim_lo, double trim_hi, const int32_t* surv,
-                                 const int32_t* nsurv, double* tmean, hipStream_t st);
+hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const float* dscale,
+                                 const BatchShape& sh, double trim_lo, double trim_hi,
+                                 const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
+                                 double* tmean, hipStream_t st);
 hipError_t launch_consensus_final(const int32_t* counts, const int32_t* kcount, const float* rv,
                                   const float* tv, const double* tmean, const int32_t* flags,
                                   const int32_t* nsurv, const BatchShape& sh, double sample_frac,

@@ -950,20 +950,27 @@ __device__ __forceinline__ float rdist2(float xi, float yi, float zi, float xj, 
     return dx * dx + dy * dy + dz * dz;
 }
 
-// find the bin holding `rank` in hist[0..2047] (block of 256); returns bin, writes #before
-__device__ int find_bin_2048(const uint32_t* hist, long rank, long* before, int* ws, int* res) {
+// find the bin holding `rank` in hist[0..N-1] (block of 256); returns bin, writes #before
+template <int N>
+__device__ int find_bin(const uint32_t* hist, long rank, long* before, int* ws, int* res) {
+    constexpr int PER = N / 256;
     const int tid = threadIdx.x;
     uint32_t loc = 0;
 #pragma unroll
-    for (int k = 0; k < 8; k++) loc += hist[tid * 8 + k];
+    for (int k = 0; k < PER; k++) loc += hist[tid * PER + k];
     int total;
     const int ex = block_exclusive_scan<256>((int)loc, ws, &total);
+    if (tid == 0) {
+        res[0] = -1;
+        res[1] = 0;
+    }
+    __syncthreads();
     if ((long)ex <= rank && rank < (long)ex + (long)loc) {
         long c = ex;
-        for (int k = 0; k < 8; k++) {
-            const long nc = c + hist[tid * 8 + k];
+        for (int k = 0; k < PER; k++) {
+            const long nc = c + hist[tid * PER + k];
             if (rank < nc) {
-                res[0] = tid * 8 + k;
+                res[0] = tid * PER + k;
                 res[1] = (int)c;
                 break;
             }
@@ -977,39 +984,41 @@ __device__ int find_bin_2048(const uint32_t* hist, long rank, long* before, int*
     return bin;
 }
 
-// Trimmed mean of row i: value at ranks [lo, hi) of the K distances, lo = (long)(K*0.2),
-// hi = (long)(K*0.8).  Exact order statistics by a 3-level radix select (11+11+10 bits) on the
-// f32 bit patterns of the SQUARED distances s (sqrtf is monotone, so the sorted distances are
-// sqrtf of the sorted s: no square root in the selection passes), then the window sum of
-// sqrtf(s) in fp64 (fixed order; the reference's sorted sequential sum may differ in the last
-// bits -- the final kernel re-scores near ties exactly).
-__global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __restrict__ kcount,
-                                                             const float* __restrict__ rv,
-                                                             int stride, double trim_lo,
-                                                             double trim_hi,
-                                                             const int32_t* __restrict__ surv,
-                                                             const int32_t* __restrict__ nsurv,
-                                                             double* __restrict__ tmean) {
-    __shared__ uint32_t histA[2048], histB[2048];
-    __shared__ int ws[8];
-    __shared__ int res[2];
-    __shared__ double red[256];
-    const int p = blockIdx.y, tid = threadIdx.x;
-    const int K = kcount[p];
-    if ((int)blockIdx.x >= nsurv[p]) return;
-    const int i = surv[(size_t)p * stride + blockIdx.x];
-    const float* X = rv + (size_t)p * 3 * stride;
-    const float* Y = X + stride;
-    const float* Z = Y + stride;
-    const float xi = X[i], yi = Y[i], zi = Z[i];
-    const long lo = (long)(K * trim_lo);
-    const long hi = (long)(K * trim_hi);
-    if (hi <= lo) {
-        if (tid == 0) tmean[(size_t)p * stride + i] = __builtin_nan("");
-        return;
-    }
+__device__ double block_sum_f64(double v, double* red) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6] = v;
+    __syncthreads();
+    const double s = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return s;
+}
+
+__device__ long block_sum_i64(long v, double* red) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    long* r = reinterpret_cast<long*>(red);
+    __syncthreads();
+    if ((tid & 63) == 0) r[tid >> 6] = v;
+    __syncthreads();
+    const long s = r[0] + r[1] + r[2] + r[3];
+    __syncthreads();
+    return s;
+}
+
+// Window sum of row i (ranks [lo, hi)) by a 3-level radix select (11+11+10 bits) on the f32
+// bit patterns of the squared distances s (sqrtf is monotone, so the sorted distances are
+// sqrtf of the sorted s), then the sum of sqrtf(s) in fp64.  Four passes over the row; the
+// general fallback of consensus_rows.  Returns the sum on every thread.
+__device__ double radix_window_sum(const float* X, const float* Y, const float* Z, int K,
+                                   float xi, float yi, float zi, long lo, long hi,
+                                   uint32_t* histA, uint32_t* histB, int* ws, int* res,
+                                   double* red) {
+    const int tid = threadIdx.x;
     const long ra = lo, rb = hi - 1;
-    // level 0
     for (int k = tid; k < 2048; k += 256) histA[k] = 0;
     __syncthreads();
     for (int j = tid; j < K; j += 256) {
@@ -1018,9 +1027,8 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     }
     __syncthreads();
     long ca, cb;
-    const int ba = find_bin_2048(histA, ra, &ca, ws, res);
-    const int bb = find_bin_2048(histA, rb, &cb, ws, res);
-    // level 1
+    const int ba = find_bin<2048>(histA, ra, &ca, ws, res);
+    const int bb = find_bin<2048>(histA, rb, &cb, ws, res);
     for (int k = tid; k < 2048; k += 256) {
         histA[k] = 0;
         histB[k] = 0;
@@ -1034,11 +1042,10 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     }
     __syncthreads();
     long ca1, cb1;
-    const int ba1 = find_bin_2048(histA, ra - ca, &ca1, ws, res);
-    const int bb1 = find_bin_2048(histB, rb - cb, &cb1, ws, res);
+    const int ba1 = find_bin<2048>(histA, ra - ca, &ca1, ws, res);
+    const int bb1 = find_bin<2048>(histB, rb - cb, &cb1, ws, res);
     const uint32_t pa = ((uint32_t)ba << 11) | (uint32_t)ba1;  // key >> 10
     const uint32_t pb = ((uint32_t)bb << 11) | (uint32_t)bb1;
-    // level 2 (10 bits)
     for (int k = tid; k < 2048; k += 256) {
         histA[k] = 0;
         histB[k] = 0;
@@ -1052,37 +1059,22 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     }
     __syncthreads();
     long ca2, cb2;
-    const int ba2 = find_bin_2048(histA, ra - ca - ca1, &ca2, ws, res);
-    const int bb2 = find_bin_2048(histB, rb - cb - cb1, &cb2, ws, res);
+    const int ba2 = find_bin<2048>(histA, ra - ca - ca1, &ca2, ws, res);
+    const int bb2 = find_bin<2048>(histB, rb - cb - cb1, &cb2, ws, res);
     const uint32_t va = (pa << 10) | (uint32_t)ba2;  // key at rank lo
     const uint32_t vb = (pb << 10) | (uint32_t)bb2;  // key at rank hi-1
     const long lt_a = ca + ca1 + ca2;                // #keys < va
     const long le_a = lt_a + histA[ba2];             // #keys <= va
     const long lt_b = cb + cb1 + cb2;                // #keys < vb
-    // level 3: sum of the keys strictly between va and vb
     double acc = 0.0;
     for (int j = tid; j < K; j += 256) {
         const uint32_t key = __float_as_uint(rdist2(xi, yi, zi, X[j], Y[j], Z[j]));
         if (key > va && key < vb) acc += (double)__builtin_sqrtf(__uint_as_float(key));
     }
-    red[tid] = acc;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (tid < o) red[tid] += red[tid + o];
-        __syncthreads();
-    }
-    if (tid == 0) {
-        double sum;
-        if (va == vb) {
-            sum = (double)(hi - lo) * (double)__builtin_sqrtf(__uint_as_float(va));
-        } else {
-            const long na = le_a - lo;   // ranks lo .. le_a-1 hold va
-            const long nb = hi - lt_b;   // ranks lt_b .. hi-1 hold vb
-            sum = red[0] + (double)na * (double)__builtin_sqrtf(__uint_as_float(va)) +
-                  (double)nb * (double)__builtin_sqrtf(__uint_as_float(vb));
-        }
-        tmean[(size_t)p * stride + i] = sum / ((double)(hi - lo) * 1.0);
-    }
+    const double inner = block_sum_f64(acc, red);
+    if (va == vb) return (double)(hi - lo) * (double)__builtin_sqrtf(__uint_as_float(va));
+    return inner + (double)(le_a - lo) * (double)__builtin_sqrtf(__uint_as_float(va)) +
+           (double)(hi - lt_b) * (double)__builtin_sqrtf(__uint_as_float(vb));
 }
 
 // consensus-only entry: AoS R/T lists -> SoA rv, tv, kcount, dscale (one block)
@@ -1136,13 +1128,14 @@ __global__ __launch_bounds__(1024) void consensus_input_kernel(const float* __re
 }
 
 // ---- pruning by rigorous bounds -------------------------------------------------------
-// Every row's K squared distances s_ij (the reference's exact f32 dx*dx + dy*dy + dz*dz, whose
-// correctly rounded sqrtf is its distance) are binned into NB geometric bins: 32 per binade of
-// s (= 64 per binade of the distance) over the 40 binades of s below the squared diameter of
-// the set, underflow in bin 0.  sqrtf is monotone, so a value in bin [E_b, E_b+1) has distance
-// in [sqrtf(E_b), sqrtf(E_b+1)] and, from the exact bin counts, the trimmed sum over ranks
-// [lo, hi) is bracketed by
-//   LB = sum_b n_b(window) * sqrtf(E_b),  UB = sum_b n_b(window) * sqrtf(E_b+1)
+// Every row's K squared distances are binned into NB geometric bins: 32 per binade of s = d^2
+// (= 64 per binade of the distance d) over the 40 binades of s below the squared diameter of
+// the set, underflow in bin 0.  The binned value is s' = fma(dz, dz, fma(dy, dy, dx * dx)),
+// within 2 * gamma_3 < 2^-21 (relative) of the reference's s = dx*dx + dy*dy + dz*dz (same dx,
+// dy, dz; all terms >= 0), and d = sqrtf(s) is monotone in s, so a value in bin
+// [E_b, E_b+1) has d in [sqrtf(E_b (1 - 2^-20)), sqrtf(E_b+1 (1 + 2^-20))].  From the exact
+// bin counts the trimmed sum over ranks [lo, hi) is bracketed by
+//   LB = sum_b n_b(window) * lower_b,  UB = sum_b n_b(window) * upper_b
 // (relative width <= 2^-6).  A row whose LB exceeds the smallest UB cannot be the argmin; only
 // the survivors get the exact order statistics.  No square root in the K^2 loop.
 // Block = 8 rows x 256 columns at a time; lane l takes row (l + t) & 7 at step t, so one
@@ -1156,20 +1149,16 @@ constexpr int kNB = kBinsPerBinade * kBinades;  // 1280
 constexpr int kHistStride = kNB + 4;
 
 // first s-binade of the bins: the 40 binades ending with the one holding D^2 (D = dscale is
-// the bounding-box diagonal rounded up, >= every distance, so every s_ij <= D^2)
+// the bounding-box diagonal rounded up, >= every distance, so every s <= D^2)
 __device__ __forceinline__ int bounds_elo(float D) {
-    const float D2 = D * D * (1.0f + 0x1p-20f);
+    const float D2 = D * D * (1.0f + 0x1p-18f);
     const int t = (int)(__float_as_uint(D2) >> 23) + 1;
     const int e = t - kBinades;
     return e < 1 ? 1 : e;
 }
-// distance bounds of bin b (rigorous: sqrtf of the s-edges; sqrtf is monotone)
-__device__ __forceinline__ float bin_lower(int elo, int b) {
-    return b == 0 ? 0.f : __builtin_sqrtf(__uint_as_float((uint32_t)((elo << 5) + b) << 18));
-}
-__device__ __forceinline__ float bin_upper(int elo, int b) {
-    return b == kNB - 1 ? kInf
-                        : __builtin_sqrtf(__uint_as_float((uint32_t)((elo << 5) + b + 1) << 18));
+// d-space edge e of the bins (e = 1 .. NB-1: lower edge of bin e = upper edge of bin e-1)
+__device__ __forceinline__ float bin_edge_s(int elo, int e) {
+    return __uint_as_float((uint32_t)((elo << 5) + e) << 18);
 }
 
 __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __restrict__ kcount,
@@ -1178,8 +1167,10 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
                                                                int stride, double trim_lo,
                                                                double trim_hi,
                                                                double* __restrict__ lb,
-                                                               double* __restrict__ ub) {
+                                                               double* __restrict__ ub,
+                                                               int32_t* __restrict__ bsel) {
     __shared__ uint32_t hist[kBoundRows * kHistStride];
+    __shared__ float elow[kNB], eupp[kNB];  // d-space bounds of each bin
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
     const int r0 = blockIdx.x * kBoundRows;
@@ -1198,18 +1189,24 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
         xi[t] = X[row];
         yi[t] = Y[row];
         zi[t] = Z[row];
-        hoff[t] = r * kHistStride;
+        hoff[t] = r * kHistStride - base;  // hist index = hoff + clamp(key, base, base+NB-1)
     }
     for (int k = tid; k < kBoundRows * kHistStride; k += 256) hist[k] = 0u;
+    for (int b = tid; b < kNB; b += 256) {
+        elow[b] = b == 0 ? 0.f : __builtin_sqrtf(bin_edge_s(elo, b) * (1.0f - 0x1p-20f));
+        eupp[b] = b == kNB - 1 ? kInf : __builtin_sqrtf(bin_edge_s(elo, b + 1) * (1.0f + 0x1p-20f));
+    }
     __syncthreads();
+    const int bmax = base + kNB - 1;
+#pragma unroll 2
     for (int j = tid; j < K; j += 256) {
         const float xj = X[j], yj = Y[j], zj = Z[j];
 #pragma unroll
         for (int t = 0; t < kBoundRows; t++) {
-            const uint32_t key = __float_as_uint(rdist2(xi[t], yi[t], zi[t], xj, yj, zj));
-            int b = (int)(key >> 18) - base;
-            b = min(max(b, 0), kNB - 1);
-            atomicAdd(&hist[hoff[t] + b], 1u);
+            const float dx = xi[t] - xj, dy = yi[t] - yj, dz = zi[t] - zj;
+            const float s = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+            const int key = (int)(__float_as_uint(s) >> 18);
+            atomicAdd(&hist[hoff[t] + min(max(key, base), bmax)], 1u);
         }
     }
     __syncthreads();
@@ -1228,29 +1225,179 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
         if (sl >= o) x += y;
     }
     long cum = (long)(x - c);
+    const int row = r0 + r;
     double L = 0.0, U = 0.0;
-    for (int b = sl * per; b < (sl + 1) * per; b++) {
-        const long n = h[b];
-        const long a0 = cum > lo ? cum : lo;
-        const long a1 = (cum + n) < hi ? (cum + n) : hi;
-        if (a1 > a0) {
-            L += (double)(a1 - a0) * (double)bin_lower(elo, b);
-            U += (double)(a1 - a0) * (double)bin_upper(elo, b);
+    int sel_a = -1, sel_b = -1;  // bins holding ranks lo and hi-1 (for the exact pass)
+    if (cum < hi && cum + (long)c > lo) {
+#pragma unroll 1
+        for (int b = sl * per; b < (sl + 1) * per; b++) {
+            const long n = h[b];
+            const long a0 = cum > lo ? cum : lo;
+            const long a1 = (cum + n) < hi ? (cum + n) : hi;
+            if (a1 > a0) {
+                L += (double)(a1 - a0) * (double)elow[b];
+                U += (double)(a1 - a0) * (double)eupp[b];
+            }
+            sel_a = (cum <= lo && lo < cum + n) ? b : sel_a;
+            sel_b = (cum <= hi - 1 && hi - 1 < cum + n) ? b : sel_b;
+            cum += n;
         }
-        cum += n;
+    }
+    if (row < K) {
+        if (sel_a >= 0) bsel[((size_t)p * stride + row) * 2] = sel_a;
+        if (sel_b >= 0) bsel[((size_t)p * stride + row) * 2 + 1] = sel_b;
     }
 #pragma unroll
     for (int o = 16; o > 0; o >>= 1) {
         L += __shfl_xor(L, o, 32);
         U += __shfl_xor(U, o, 32);
     }
-    const int row = r0 + r;
     if (sl == 0 && row < K) {
         const double w = (double)(hi - lo);
         // margins cover the reference's own rounding of its sorted sequential sum
         lb[(size_t)p * stride + row] = hi > lo ? (L / w) * (1.0 - 1e-9) : 0.0;
         ub[(size_t)p * stride + row] = hi > lo ? (U / w) * (1.0 + 1e-9) : 0.0;
     }
+}
+
+// Trimmed mean of a surviving row i, ranks [lo, hi), lo = (long)(K*0.2), hi = (long)(K*0.8).
+// The bounds kernel already located the (s'-)bins b_a, b_b holding ranks lo and hi-1; here
+//   pass 1: exact s = dx*dx + dy*dy + dz*dz for every column; fp64 sum of sqrtf(s) over the
+//           bins strictly between b_a and b_b, exact counts below them, and for the two bins
+//           512-way sub-histograms (key bits 17..9) with their fp64 sums of sqrtf(s);
+//   pass 2: 512-way histograms of the two sub-bins holding the ranks (key bits 8..0, i.e.
+//           exact values) -> the exact keys va, vb at ranks lo and hi-1 and their
+//           multiplicities.
+// Sum = sum over keys strictly between va and vb (assembled from the levels) + the boundary
+// multiplicities.  (The sort order of the distances is the order of s: sqrtf is monotone.)
+// When a bin edge moved an element between the s' and s binnings across a rank, or a rank
+// sits in the under/overflow bin, the row takes the 4-pass radix path instead.  The sum is
+// not the reference's sorted sequential one in the last bits; consensus_final re-scores near
+// ties exactly.
+__global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __restrict__ kcount,
+                                                             const float* __restrict__ rv,
+                                                             const float* __restrict__ dscale,
+                                                             int stride, double trim_lo,
+                                                             double trim_hi,
+                                                             const int32_t* __restrict__ surv,
+                                                             const int32_t* __restrict__ nsurv,
+                                                             const int32_t* __restrict__ bsel,
+                                                             double* __restrict__ tmean) {
+    __shared__ uint32_t histA[2048], histB[2048];  // radix fallback; level counts alias it
+    __shared__ double sA[512], sB[512];
+    __shared__ int ws[8];
+    __shared__ int res[2];
+    __shared__ double red[8];
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const int K = kcount[p];
+    if ((int)blockIdx.x >= nsurv[p]) return;
+    const int i = surv[(size_t)p * stride + blockIdx.x];
+    const float* X = rv + (size_t)p * 3 * stride;
+    const float* Y = X + stride;
+    const float* Z = Y + stride;
+    const float xi = X[i], yi = Y[i], zi = Z[i];
+    const long lo = (long)(K * trim_lo);
+    const long hi = (long)(K * trim_hi);
+    if (hi <= lo) {
+        if (tid == 0) tmean[(size_t)p * stride + i] = __builtin_nan("");
+        return;
+    }
+    const int base = bounds_elo(dscale[p]) << 5;
+    const int ba = bsel[((size_t)p * stride + i) * 2], bb = bsel[((size_t)p * stride + i) * 2 + 1];
+    bool fast = ba > 0 && bb < kNB - 1 && ba <= bb;
+    double sum = 0.0;
+    uint32_t* cA = histA;        // level-2 counts of bin b_a
+    uint32_t* cB = histA + 512;  // of bin b_b (unused when b_a == b_b)
+    uint32_t* tA = histB;        // level-3 counts of the sub-bin holding rank lo
+    uint32_t* tB = histB + 512;  //                           and rank hi-1
+    if (fast) {
+        for (int k = tid; k < 512; k += 256) {
+            cA[k] = 0;
+            cB[k] = 0;
+            tA[k] = 0;
+            tB[k] = 0;
+            sA[k] = 0.0;
+            sB[k] = 0.0;
+        }
+        __syncthreads();
+        double acc = 0.0;
+        long belowA = 0, belowB = 0;
+#pragma unroll 4
+        for (int j = tid; j < K; j += 256) {
+            const float s = rdist2(xi, yi, zi, X[j], Y[j], Z[j]);
+            const uint32_t key = __float_as_uint(s);
+            const int e = min(max((int)(key >> 18) - base, 0), kNB - 1);
+            belowA += e < ba;
+            belowB += e < bb;
+            if (e > ba && e < bb) {
+                acc += (double)__builtin_sqrtf(s);
+            } else if (e == ba || e == bb) {
+                const int sub = (int)((key >> 9) & 511u);
+                const double d = (double)__builtin_sqrtf(s);
+                if (e == ba) {
+                    atomicAdd(&cA[sub], 1u);
+                    atomicAdd(&sA[sub], d);
+                } else {
+                    atomicAdd(&cB[sub], 1u);
+                    atomicAdd(&sB[sub], d);
+                }
+            }
+        }
+        const double inner = block_sum_f64(acc, red);
+        const long cumA = block_sum_i64(belowA, red);
+        const long cumB = block_sum_i64(belowB, red);
+        const uint32_t* cX = (ba == bb) ? cA : cB;
+        const double* sX = (ba == bb) ? sA : sB;
+        long befA, befB;
+        const int sa = find_bin<512>(cA, lo - cumA, &befA, ws, res);
+        const int sb = find_bin<512>(cX, hi - 1 - cumB, &befB, ws, res);
+        fast = lo >= cumA && hi - 1 >= cumB && sa >= 0 && sb >= 0;  // uniform
+        if (fast) {
+            const uint32_t prefA = ((uint32_t)(base + ba) << 9) | (uint32_t)sa;  // key >> 9
+            const uint32_t prefB = ((uint32_t)(base + bb) << 9) | (uint32_t)sb;
+#pragma unroll 4
+            for (int j = tid; j < K; j += 256) {
+                const uint32_t key = __float_as_uint(rdist2(xi, yi, zi, X[j], Y[j], Z[j]));
+                if ((key >> 9) == prefA) atomicAdd(&tA[key & 511u], 1u);
+                if ((key >> 9) == prefB) atomicAdd(&tB[key & 511u], 1u);
+            }
+            __syncthreads();
+            long befA3, befB3;
+            const int ta = find_bin<512>(tA, lo - cumA - befA, &befA3, ws, res);
+            const int tb = find_bin<512>(tB, hi - 1 - cumB - befB, &befB3, ws, res);
+            const uint32_t va = (prefA << 9) | (uint32_t)ta, vb = (prefB << 9) | (uint32_t)tb;
+            const long le_a = cumA + befA + befA3 + tA[ta];  // #keys <= va
+            const long lt_b = cumB + befB + befB3;           // #keys <  vb
+            // keys strictly between va and vb
+            double part = 0.0;
+            for (int k = tid; k < 512; k += 256) {
+                const double dA = (double)__builtin_sqrtf(__uint_as_float((prefA << 9) | k));
+                const double dB = (double)__builtin_sqrtf(__uint_as_float((prefB << 9) | k));
+                if (ba != bb) {
+                    if (k > sa) part += sA[k];
+                    if (k < sb) part += sX[k];
+                    if (k > ta) part += (double)tA[k] * dA;
+                    if (k < tb) part += (double)tB[k] * dB;
+                } else if (sa != sb) {
+                    if (k > sa && k < sb) part += sA[k];
+                    if (k > ta) part += (double)tA[k] * dA;
+                    if (k < tb) part += (double)tB[k] * dB;
+                } else {
+                    if (k > ta && k < tb) part += (double)tA[k] * dA;
+                }
+            }
+            const double mid = block_sum_f64(part, red);
+            if (va == vb)
+                sum = (double)(hi - lo) * (double)__builtin_sqrtf(__uint_as_float(va));
+            else
+                sum = inner + mid +
+                      (double)(le_a - lo) * (double)__builtin_sqrtf(__uint_as_float(va)) +
+                      (double)(hi - lt_b) * (double)__builtin_sqrtf(__uint_as_float(vb));
+        }
+        __syncthreads();
+    }
+    if (!fast) sum = radix_window_sum(X, Y, Z, K, xi, yi, zi, lo, hi, histA, histB, ws, res, red);
+    if (tid == 0) tmean[(size_t)p * stride + i] = sum / ((double)(hi - lo) * 1.0);
 }
 
 // survivors: rows with LB <= min UB, in row order; pruned rows get tmean = +inf
@@ -1647,10 +1794,10 @@ hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, i
 
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    const BatchShape& sh, double trim_lo, double trim_hi, double* lb,
-                                   double* ub, hipStream_t st) {
+                                   double* ub, int32_t* bsel, hipStream_t st) {
     dim3 grid((2 * sh.iters + kBoundRows - 1) / kBoundRows, sh.n_pairs);
     hipLaunchKernelGGL(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
-                       2 * sh.iters, trim_lo, trim_hi, lb, ub);
+                       2 * sh.iters, trim_lo, trim_hi, lb, ub, bsel);
     return hipGetLastError();
 }
 
@@ -1662,12 +1809,13 @@ hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, cons
     return hipGetLastError();
 }
 
-hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const BatchShape& sh,
-                                 double trim_lo, double trim_hi, const int32_t* surv,
-                                 const int32_t* nsurv, double* tmean, hipStream_t st) {
+hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const float* dscale,
+                                 const BatchShape& sh, double trim_lo, double trim_hi,
+                                 const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
+                                 double* tmean, hipStream_t st) {
     dim3 grid(2 * sh.iters, sh.n_pairs);
-    hipLaunchKernelGGL(consensus_rows_kernel, grid, dim3(256), 0, st, kcount, rv, 2 * sh.iters,
-                       trim_lo, trim_hi, surv, nsurv, tmean);
+    hipLaunchKernelGGL(consensus_rows_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
+                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, tmean);
     return hipGetLastError();
 }
 

@@ -364,3 +364,39 @@ def test_consensus_bimodal_many_survivors(ctx, oracle):
     rc, mi, d = oracle.consensus(rv)
     res = D.gpu_consensus(ctx, "cuda")(rv, tv)
     assert res["min_idx"] == mi or np.array_equal(rv[res["min_idx"]], rv[mi])
+
+
+def test_consensus_heavy_duplicates(ctx, oracle):
+    """few distinct R vectors repeated many times: zero distances put the window ranks in the
+    underflow bin, which takes the radix fallback of consensus_rows."""
+    from erp_match_eightpoint_test_amd import dist as D
+    rng = np.random.default_rng(21)
+    base = (rng.standard_normal((5, 3)) * 0.01).astype(np.float32)
+    rv = base[rng.integers(0, 5, 1500)]
+    tv = rng.standard_normal((1500, 3)).astype(np.float32)
+    rc, mi, d = oracle.consensus(rv)
+    res = D.gpu_consensus(ctx, "cuda")(rv, tv)
+    assert res["status"] == 0
+    assert res["min_idx"] == mi
+
+
+def test_consensus_survivor_means_bimodal_pair(ctx, oracle):
+    """a full-size synthetic pair whose R1 and R2 are both valid in every iteration (K = 2I):
+    thousands of consensus survivors; their trimmed means must match the oracle's."""
+    from erp_match_eightpoint_test_amd import PairBatchRunner, results_to_numpy
+    import torch
+    p = synth.make_pair(20200423 + 8, n_kpts=4096)
+    run = PairBatchRunner(ctx=ctx, iters=1500)
+    outs = run.run(*_batch([p]), want=("rvec", "dist"))
+    torch.cuda.synchronize()
+    res = results_to_numpy(outs["results"])[0]
+    K = int(res["K"])
+    assert K == 3000 and res["survivors"] > 100   # the bimodal regime this test is about
+    rv = outs["rvec"][0, :K].cpu().numpy()
+    _, mi, dref = oracle.consensus(rv)
+    assert mi == res["min_idx"] or np.array_equal(rv[mi], rv[res["min_idx"]])
+    d = outs["dist"][0, :K].cpu().numpy()
+    live = np.isfinite(d)
+    assert live.sum() == res["survivors"]
+    assert np.all(dref[~live] >= dref.min())
+    assert np.allclose(d[live], dref[live], rtol=1e-12, atol=0)
