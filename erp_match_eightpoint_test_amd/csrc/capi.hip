@@ -68,7 +68,7 @@ struct erp_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
-    DevBuf part, pu, ccount, cand, bsel, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
+    DevBuf part, pu, ccount, cand, bsel, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins;
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -157,7 +157,8 @@ erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
 erp_status erp_ctx_destroy(erp_ctx* ctx) {
     if (!ctx) return ERP_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    DevBuf* all[] = {&ctx->part, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->matches,
+    DevBuf* all[] = {&ctx->part, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->gfin,
+                     &ctx->matches,
                      &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
                      &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
@@ -238,7 +239,8 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->wins, P * nwaves * 31 * 64 * 4) && ensure(c->polyR, P * 65 * 31 * 4) &&
               ensure(c->polyQ, P * erp::kMaxQ * 31 * 4) &&
               ensure(c->idx, P * nwaves * (size_t)sh.sel_words * 64 * 4) &&
-              ensure(c->gram, P * sh.iters * 36 * 8) && ensure(c->rv, P * 6 * sh.iters * 4) &&
+              ensure(c->gram, P * erp::gram_chunks_max(sh.max_nq) * sh.iters * 36 * 8) &&
+              ensure(c->gfin, P * sh.iters * 36 * 8) && ensure(c->rv, P * 6 * sh.iters * 4) &&
               ensure(c->kcount, P * 4) && ensure(c->sortbuf, P * (size_t)erp::sortbuf_len(sh.iters) * 4) &&
               ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result)) &&
               ensure(c->dscale, P * 4) && ensure(c->lb, P * 2 * sh.iters * 8) &&
@@ -301,8 +303,8 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
     }
     {
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
-        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac, cfg->valid_abs, hyps,
-                                 st));
+        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, erp::gram_chunks_max(sh.max_nq), sh,
+                                 cfg->sample_frac, cfg->valid_abs, (double*)c->gfin.p, hyps, st));
     }
     return ERP_OK;
 }
@@ -649,7 +651,8 @@ erp_status erp_eight_point_estimation(erp_ctx* ctx, const double* h_bl, const do
     if (m < 1) return ERP_TOO_FEW_POINTS;
     std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
-    if (!ensure(ctx->in_d, (size_t)m * 48 + 36 * 8 + sizeof(erp_hypothesis) + 64)) return ERP_OUT_OF_MEMORY;
+    if (!ensure(ctx->in_d, (size_t)m * 48 + 36 * 8 * 2 + sizeof(erp_hypothesis) + 64))
+        return ERP_OUT_OF_MEMORY;
     std::vector<double> pts((size_t)m * 6);
     for (int32_t i = 0; i < m; i++)
         for (int k = 0; k < 3; k++) {
@@ -659,13 +662,14 @@ erp_status erp_eight_point_estimation(erp_ctx* ctx, const double* h_bl, const do
     char* base = (char*)ctx->in_d.p;
     double* d_pts = (double*)base;
     double* d_gram = (double*)(base + (size_t)m * 48);
-    int32_t* d_cnt = (int32_t*)(base + (size_t)m * 48 + 36 * 8);
-    erp_hypothesis* d_h = (erp_hypothesis*)(base + (size_t)m * 48 + 36 * 8 + 16);
+    double* d_gfin = (double*)(base + (size_t)m * 48 + 36 * 8);
+    int32_t* d_cnt = (int32_t*)(base + (size_t)m * 48 + 36 * 8 * 2);
+    erp_hypothesis* d_h = (erp_hypothesis*)(base + (size_t)m * 48 + 36 * 8 * 2 + 16);
     ERP_CK(hipMemcpy(d_pts, pts.data(), pts.size() * 8, hipMemcpyHostToDevice));
     ERP_CK(hipMemcpy(d_cnt, &m, 4, hipMemcpyHostToDevice));
     ERP_CK(erp::launch_gram_all(d_pts, m, d_gram, nullptr));
     erp::BatchShape sh = make_shape(1, m, m, 1, 1.0);
-    ERP_CK(erp::launch_eigen(d_cnt, d_gram, sh, 1.0, 1.57, d_h, nullptr));
+    ERP_CK(erp::launch_eigen(d_cnt, d_gram, 1, sh, 1.0, 1.57, d_gfin, d_h, nullptr));
     ERP_CK(hipMemcpy(h_out, d_h, sizeof(erp_hypothesis), hipMemcpyDeviceToHost));
     return ERP_OK;
 }

@@ -411,4 +411,139 @@ ERP_HD inline void gram_jacobi9(const double* G_in, int32_t s, double* e) {
     }
 }
 
+// ---- s >= 9: the smallest eigenvector without accumulating V ---------------------------
+// For s >= 9 the selected Vt row is the eigenvector of G's smallest eigenvalue.  The same
+// cyclic Jacobi sweeps run on the upper triangle only (no V: 45 instead of 162 doubles live,
+// so the kernel keeps several waves per SIMD), giving lambda_min to ~eps*trace(G); then two
+// steps of inverse iteration with (G - mu I), mu = lambda_min - 8 eps trace(G), factored as
+// L D L^T (symmetric positive definite by construction; Cholesky-type factorizations of SPD
+// matrices are backward stable without pivoting).  The vector agrees with the rotation-
+// accumulated one to O(eps * trace / gap) -- the accuracy either has -- and its sign is
+// arbitrary, as the reference's is (E and -E decompose to the same R, T).
+ERP_HD ERP_INLINE constexpr int ut9(int i, int j) {
+    return i <= j ? i * 9 - i * (i - 1) / 2 + (j - i) : j * 9 - j * (j - 1) / 2 + (i - j);
+}
+
+// g36[k * stride + h]: the 36 distinct Gram values (base uniform across a wave, h the lane
+// part, so the device loads use a scalar base and a 32-bit lane offset)
+ERP_HD ERP_INLINE void gram36_to_ut(const double* g36, int stride, int h, double* S) {
+#pragma unroll
+    for (int a = 0; a < 9; a++)
+#pragma unroll
+        for (int b = a; b < 9; b++) {
+            const int i = a / 3, j = a % 3, k = b / 3, l = b % 3;
+            S[ut9(a, b)] = g36[(6 * sym3(i, k) + sym3(j, l)) * stride + h];
+        }
+}
+
+ERP_HD inline void gram_min_eigvec9(const double* g36, int stride, int h, double* e) {
+    double S[45];
+    gram36_to_ut(g36, stride, h, S);
+    double tr = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) tr += S[ut9(i, i)];
+    const double eps = kDblEps * 10;
+    const double floor_abs = 4 * kDblEps * tr;
+    for (int sweep = 0; sweep < 40; sweep++) {
+        bool changed = false;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+#pragma unroll
+            for (int j = i + 1; j < 9; j++) {
+                const double a = S[ut9(i, i)], b = S[ut9(j, j)], p = S[ut9(i, j)];
+                const double ap = fabs(p);
+                if (ap <= eps * sqrt(fabs(a * b)) || ap <= floor_abs) continue;
+                const double p2 = 2 * p;
+                const double beta = a - b, gamma = hypot(p2, beta);
+                double c, s;
+                if (beta < 0) {
+                    const double delta = (gamma - beta) * 0.5;
+                    s = sqrt(delta / gamma);
+                    c = p2 / (gamma * s * 2);
+                } else {
+                    c = sqrt((gamma + beta) / (gamma * 2));
+                    s = p2 / (gamma * c * 2);
+                }
+#pragma unroll
+                for (int k = 0; k < 9; k++) {
+                    if (k == i || k == j) continue;
+                    const double gik = S[ut9(i, k)], gjk = S[ut9(j, k)];
+                    S[ut9(i, k)] = c * gik + s * gjk;
+                    S[ut9(j, k)] = -s * gik + c * gjk;
+                }
+                const double cs2p = 2 * c * s * p;
+                S[ut9(i, i)] = c * c * a + cs2p + s * s * b;
+                S[ut9(j, j)] = s * s * a - cs2p + c * c * b;
+                S[ut9(i, j)] = 0;
+                changed = true;
+            }
+        }
+        if (!changed) break;
+    }
+    double lmin = S[0];
+#pragma unroll
+    for (int i = 1; i < 9; i++) lmin = fmin(lmin, S[ut9(i, i)]);
+    const double tiny = kDblEps * (tr > 0 ? tr : 1.0);
+    const double mu = lmin - 8 * tiny;
+    // L D L^T of B = G - mu I, in place (L below the diagonal, stored at ut9(j, i), D on it).
+    // G is read again from memory, not kept live through the sweeps: the barrier stops the
+    // compiler from reusing the first loads (72 VGPRs of occupancy).
+    __asm__ volatile("" ::: "memory");
+    gram36_to_ut(g36, stride, h, S);
+#pragma unroll
+    for (int i = 0; i < 9; i++) S[ut9(i, i)] -= mu;
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+        double d = S[ut9(j, j)];
+#pragma unroll
+        for (int k = 0; k < j; k++) d -= S[ut9(k, j)] * S[ut9(k, j)] * S[ut9(k, k)];
+        d = d > tiny * 1e-3 ? d : tiny * 1e-3;  // rounding can only touch the last pivots
+        S[ut9(j, j)] = d;
+        const double inv = 1.0 / d;
+#pragma unroll
+        for (int i = j + 1; i < 9; i++) {
+            double v = S[ut9(j, i)];
+#pragma unroll
+            for (int k = 0; k < j; k++) v -= S[ut9(k, i)] * S[ut9(k, j)] * S[ut9(k, k)];
+            S[ut9(j, i)] = v * inv;  // L[i][j]
+        }
+    }
+    double x[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) x[i] = 1.0;
+#pragma unroll
+    for (int it = 0; it < 2; it++) {
+#pragma unroll
+        for (int i = 0; i < 9; i++)  // L y = x
+#pragma unroll
+            for (int k = 0; k < i; k++) x[i] -= S[ut9(k, i)] * x[k];
+#pragma unroll
+        for (int i = 0; i < 9; i++) x[i] /= S[ut9(i, i)];
+#pragma unroll
+        for (int i = 8; i >= 0; i--)  // L^T x = z
+#pragma unroll
+            for (int k = i + 1; k < 9; k++) x[i] -= S[ut9(i, k)] * x[k];
+        double nrm = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) nrm += x[i] * x[i];
+        const double inv = 1.0 / sqrt(nrm);
+#pragma unroll
+        for (int i = 0; i < 9; i++) x[i] *= inv;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) e[i] = x[i];
+}
+
+// the selected Vt row for any s: rotation-accumulated Jacobi for the thin case (s < 9,
+// where the row is not the smallest eigenvector), the V-free path otherwise
+ERP_HD inline void gram_select_vec(const double* g36, int32_t s, double* e) {
+    if (s >= 9) {
+        gram_min_eigvec9(g36, 1, 0, e);
+    } else {
+        double G[81];
+        gram36_to_full(g36, G);
+        gram_jacobi9(G, s, e);
+    }
+}
+
 }  // namespace erp

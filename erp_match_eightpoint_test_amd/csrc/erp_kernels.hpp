@@ -79,12 +79,15 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
                           const uint32_t* w0, const BatchShape& sh, double sample_frac,
                           uint32_t* wins, uint32_t* selw, int32_t* flags, hipStream_t st,
                           int part);
+int gram_chunks_max(int max_nq);  // partial-Gram chunks per iteration for max_nq rows
 hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t* selw,
                        const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
                        hipStream_t st);
-hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
-                        double sample_frac, double valid_abs, erp_hypothesis* hyps,
-                        hipStream_t st);
+// selected singular vector per iteration from the nchunk partial Grams gram[p][c][36][iters]
+// (summed into gfin[p][h][36], which then also holds the vector), then the estimate
+hipError_t launch_eigen(const int32_t* counts, const double* gram, int nchunk,
+                        const BatchShape& sh, double sample_frac, double valid_abs,
+                        double* gfin, erp_hypothesis* hyps, hipStream_t st);
 hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyps,
                                 const BatchShape& sh, double sample_frac, float* rv, float* tv,
                                 int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st);

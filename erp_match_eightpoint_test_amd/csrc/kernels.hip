@@ -701,57 +701,82 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     if (bad) atomicOr(&flags[p], 4);
 }
 
-// Gram of each lane's s sampled rows: the selection bitmap is walked with a per-lane cursor
-// (one word prefetched), rows gathered 8 at a time so their loads are all in flight together.
-// Row max_nq of pts is a zero sentinel used to pad the last batch.
-__global__ __launch_bounds__(64) void gram_kernel(const int32_t* __restrict__ counts,
-                                                  const double* __restrict__ pts, int max_nq,
-                                                  int iters, int nwaves, int nbw, int idx_stride,
-                                                  double sample_frac,
-                                                  const uint32_t* __restrict__ selw,
-                                                  double* __restrict__ gram,
-                                                  int32_t* __restrict__ samples) {
-    const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
+// Gram of each iteration's s sampled rows, as partial sums over row chunks.  A block = 4
+// waves (256 iterations of one pair) x one chunk of kGramChunk selection words (31 rows
+// each): the chunk's rows (<= 620 x 48 B) are staged in LDS with coalesced loads, each
+// lane's selection words too, and every lane walks its own set bits with a cursor, reading
+// its rows from LDS (random 16-B global gathers per lane would be served one cache line at a
+// time).  Partial Grams gpart[p][chunk][36][iters] are summed in a fixed order by the eigen
+// kernels.  An exhausted lane reads the zero row (slot kGramRows).
+constexpr int kGramChunk = 20;
+constexpr int kGramRows = kGramChunk * 31;
+
+__device__ __forceinline__ int gram_chunks(int M) { return ((M - 1) / 31 + kGramChunk) / kGramChunk; }
+
+__global__ __launch_bounds__(256) void gram_kernel(const int32_t* __restrict__ counts,
+                                                   const double* __restrict__ pts, int max_nq,
+                                                   int iters, int nwaves, int nbw, int nchunk,
+                                                   int idx_stride, double sample_frac,
+                                                   const uint32_t* __restrict__ selw,
+                                                   double* __restrict__ gpart,
+                                                   int32_t* __restrict__ samples) {
+    __shared__ double2 rows[(kGramRows + 1) * 3];
+    __shared__ uint32_t wds[kGramChunk * 256];
+    const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+    const int c = blockIdx.x % nchunk, wg = blockIdx.x / nchunk;
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;
-    const int h = w * 64 + lane;
-    const uint32_t* my = selw + ((size_t)p * nwaves + w) * (size_t)nbw * 64 + lane;
+    const int nb = (M - 1) / 31 + 1;
+    const int b_lo = c * kGramChunk;
+    if (b_lo >= nb) return;  // uniform over the block
+    const int nw = min(b_lo + kGramChunk, nb) - b_lo;
+    const int i_hi = M - 1 - 31 * b_lo;          // row of slot 0 (slot = i_hi - i)
+    const int nrows = min(31 * nw, i_hi + 1);
     const double2* P = reinterpret_cast<const double2*>(pts + (size_t)p * (max_nq + 1) * 6);
-    const int b0 = (M - 1) / 31;
-    int b = 0;
-    uint32_t cur = my[0];
-    uint32_t nxt = b0 >= 1 ? my[64] : 0u;
+    for (int t = tid; t < nrows * 3; t += 256) rows[t] = P[(size_t)(i_hi - t / 3) * 3 + t % 3];
+    if (tid < 3) rows[kGramRows * 3 + tid] = make_double2(0.0, 0.0);
+    const int wv = wg * 4 + (tid >> 6);          // wave index of these 64 iterations
+    const int h = wv * 64 + lane;
+    const uint32_t* my = selw + ((size_t)p * nwaves + (wv < nwaves ? wv : 0)) * (size_t)nbw * 64 + lane;
+    int cnt = 0;
+    for (int k = 0; k < nw; k++) {
+        const uint32_t v = wv < nwaves ? my[(size_t)(b_lo + k) * 64] : 0u;
+        wds[k * 256 + tid] = v;
+        cnt += __builtin_popcount(v);
+    }
+    __syncthreads();
+    int mx = cnt;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+    int before = 0;  // samples in earlier chunks (debug output only)
+    if (samples)
+        for (int k = 0; k < b_lo; k++) before += __builtin_popcount(wv < nwaves ? my[(size_t)k * 64] : 0u);
     double g[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) g[k] = 0.0;
-    constexpr int B = 8;
-    for (int k0 = 0; k0 < s; k0 += B) {
-        int v[B];
+    int wi = 0;
+    uint32_t cur = wds[tid];
+    constexpr int B = 4;
+    for (int k0 = 0; k0 < mx; k0 += B) {
+        int slot[B];
 #pragma unroll
         for (int u = 0; u < B; u++) {
-            v[u] = max_nq;
-            if (k0 + u < s) {
-                while (cur == 0u && b < b0) {
-                    b++;
-                    cur = nxt;
-                    nxt = (b + 1 <= b0) ? my[(size_t)(b + 1) * 64] : 0u;
-                }
-                if (cur) {
-                    v[u] = M - 1 - 31 * b - __builtin_ctz(cur);
-                    cur &= cur - 1u;
-                }
+            while (cur == 0u && wi + 1 < nw) {
+                wi++;
+                cur = wds[wi * 256 + tid];
+            }
+            slot[u] = kGramRows;
+            if (cur) {
+                slot[u] = 31 * wi + __builtin_ctz(cur);
+                cur &= cur - 1u;
             }
         }
-        double2 a[B][3];
-#pragma unroll
-        for (int u = 0; u < B; u++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) a[u][c] = P[(size_t)v[u] * 3 + c];
 #pragma unroll
         for (int u = 0; u < B; u++) {
-            const double l0 = a[u][0].x, l1 = a[u][0].y, l2 = a[u][1].x;
-            const double r0 = a[u][1].y, r1 = a[u][2].x, r2 = a[u][2].y;
+            const double2 a0 = rows[slot[u] * 3], a1 = rows[slot[u] * 3 + 1], a2 = rows[slot[u] * 3 + 2];
+            const double l0 = a0.x, l1 = a0.y, l2 = a1.x;
+            const double r0 = a1.y, r1 = a2.x, r2 = a2.y;
             const double LL[6] = {l0 * l0, l0 * l1, l0 * l2, l1 * l1, l1 * l2, l2 * l2};
             const double RR[6] = {r0 * r0, r0 * r1, r0 * r2, r1 * r1, r1 * r2, r2 * r2};
 #pragma unroll
@@ -761,13 +786,14 @@ __global__ __launch_bounds__(64) void gram_kernel(const int32_t* __restrict__ co
                     g[6 * a6 + b6] = __builtin_fma(LL[a6], RR[b6], g[6 * a6 + b6]);
         }
         if (samples && h < iters)
-            for (int u = 0; u < B && k0 + u < s && k0 + u < idx_stride; u++)
-                samples[((size_t)p * iters + h) * idx_stride + k0 + u] = v[u];
+            for (int u = 0; u < B; u++)
+                if (slot[u] != kGramRows && before + k0 + u < idx_stride)
+                    samples[((size_t)p * iters + h) * idx_stride + before + k0 + u] = i_hi - slot[u];
     }
-    if (h < iters) {
-        double* go = gram + ((size_t)p * iters + h) * 36;
+    if (h < iters) {  // [p][chunk][k][h]: coalesced over the lanes
+        double* go = gpart + ((size_t)p * nchunk + c) * 36 * iters + h;
 #pragma unroll
-        for (int k = 0; k < 36; k++) go[k] = g[k];
+        for (int k = 0; k < 36; k++) go[(size_t)k * iters] = g[k];
     }
 }
 
@@ -802,21 +828,58 @@ __global__ __launch_bounds__(256) void gram_all_kernel(const double* __restrict_
 }
 
 // ========================================================= per-hypothesis solve ==========
+// THIN = false: pairs with s >= 9 (V-free eigenvector); THIN = true: pairs with s < 9
+// (rotation-accumulated Jacobi).  Two instantiations so the common case is not sized by the
+// thin path's 162 live doubles; each returns at once for the other class of pairs.  The
+// selected vector overwrites the first 9 doubles of the iteration's Gram record; the
+// estimate (rank-2 fix, decomposition, Euler angles) runs in estimate_kernel.
+template <bool THIN>
 __global__ __launch_bounds__(64) void eigen_kernel(const int32_t* __restrict__ counts,
                                                    const double* __restrict__ gram, int iters,
-                                                   double sample_frac, double valid_abs,
-                                                   erp_hypothesis* __restrict__ hyps) {
+                                                   int nchunk, double sample_frac,
+                                                   double* __restrict__ gfin) {
+    const int p = blockIdx.y;
+    const int h = blockIdx.x * 64 + threadIdx.x;
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || h >= iters || (s < 9) != THIN) return;
+    // gram[p][chunk][36][iters]: partial Grams of the row chunks, summed in chunk order into
+    // the iteration's own record gfin[p][h][36], which then also receives the vector
+    const double* gi = gram + (size_t)p * nchunk * 36 * iters + h;
+    double* gf = gfin + ((size_t)p * iters + h) * 36;
+    const int nc = min(nchunk, gram_chunks(M));
+    for (int k = 0; k < 36; k++) {
+        double v = gi[(size_t)k * iters];
+        for (int c = 1; c < nc; c++) v += gi[((size_t)c * 36 + k) * iters];
+        gf[k] = v;
+    }
+    double e[9];
+    if (THIN) {
+        double g36[36], G[81];
+#pragma unroll
+        for (int k = 0; k < 36; k++) g36[k] = gf[k];
+        gram36_to_full(g36, G);
+        gram_jacobi9(G, s, e);
+    } else {
+        gram_min_eigvec9(gf, 1, 0, e);
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) gf[k] = e[k];
+}
+
+__global__ __launch_bounds__(64) void estimate_kernel(const int32_t* __restrict__ counts,
+                                                      const double* __restrict__ gfin, int iters,
+                                                      double sample_frac, double valid_abs,
+                                                      erp_hypothesis* __restrict__ hyps) {
     const int p = blockIdx.y;
     const int h = blockIdx.x * 64 + threadIdx.x;
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || h >= iters) return;
-    const double* gi = gram + ((size_t)p * iters + h) * 36;
-    double g36[36], G[81], e[9];
+    const double* gi = gfin + ((size_t)p * iters + h) * 36;
+    double e[9];
 #pragma unroll
-    for (int k = 0; k < 36; k++) g36[k] = gi[k];
-    gram36_to_full(g36, G);
-    gram_jacobi9(G, s, e);
+    for (int k = 0; k < 9; k++) e[k] = gi[k];
     Hyp hy;
     estimate_from_e(e, valid_abs, hy);
     erp_hypothesis* o = hyps + (size_t)p * iters + h;
@@ -1753,13 +1816,17 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
     return hipGetLastError();
 }
 
+int gram_chunks_max(int max_nq) { return ((max_nq + 30) / 31 + kGramChunk) / kGramChunk; }
+
 hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t* selw,
                        const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
                        hipStream_t st) {
     const int nwaves = (sh.iters + 63) / 64;
-    hipLaunchKernelGGL(gram_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, pts,
-                       sh.max_nq, sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, selw,
-                       gram, samples);
+    const int nchunk = gram_chunks_max(sh.max_nq);
+    dim3 grid(((nwaves + 3) / 4) * nchunk, sh.n_pairs);
+    hipLaunchKernelGGL(gram_kernel, grid, dim3(256), 0, st, counts, pts, sh.max_nq, sh.iters,
+                       nwaves, sh.sel_words, nchunk, sh.idx_stride, sample_frac, selw, gram,
+                       samples);
     return hipGetLastError();
 }
 
@@ -1768,12 +1835,17 @@ hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream
     return hipGetLastError();
 }
 
-hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
-                        double sample_frac, double valid_abs, erp_hypothesis* hyps,
-                        hipStream_t st) {
+hipError_t launch_eigen(const int32_t* counts, const double* gram, int nchunk,
+                        const BatchShape& sh, double sample_frac, double valid_abs,
+                        double* gfin, erp_hypothesis* hyps, hipStream_t st) {
     dim3 grid((sh.iters + 63) / 64, sh.n_pairs);
-    hipLaunchKernelGGL(eigen_kernel, grid, dim3(64), 0, st, counts, gram, sh.iters, sample_frac,
-                       valid_abs, hyps);
+    hipLaunchKernelGGL(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters, nchunk,
+                       sample_frac, gfin);
+    // (M is only known on the device: the thin instantiation returns at once for s >= 9)
+    hipLaunchKernelGGL(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters, nchunk,
+                       sample_frac, gfin);
+    hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, gfin, sh.iters,
+                       sample_frac, valid_abs, hyps);
     return hipGetLastError();
 }
 

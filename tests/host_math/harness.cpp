@@ -21,13 +21,20 @@ void erph_gram36(const double* bl, const double* br, int32_t m, double* g36) {
 
 int erph_estimate(const double* bl, const double* br, int32_t m, double valid_abs, erp::Hyp* out) {
     if (m < 1) return -2;
-    double g36[36], G[81], e[9];
+    double g36[36], e[9];
     erph_gram36(bl, br, m, g36);
-    erp::gram36_to_full(g36, G);
-    erp::gram_jacobi9(G, m, e);
+    erp::gram_select_vec(g36, m, e);
     erp::estimate_from_e(e, valid_abs, *out);
     return 0;
 }
+
+// selected vector by the rotation-accumulated Jacobi (any s) and by the V-free path (s >= 9)
+void erph_vec_jacobi(const double* g36, int32_t s, double* e) {
+    double G[81];
+    erp::gram36_to_full(g36, G);
+    erp::gram_jacobi9(G, s, e);
+}
+void erph_vec_fast(const double* g36, double* e) { erp::gram_min_eigvec9(g36, 1, 0, e); }
 
 void erph_svd3(const double* src, double* w, double* u, double* vt) { erp::svd3_opencv(src, w, u, vt); }
 

@@ -75,3 +75,25 @@ def test_gram_estimator_vs_oracle(oracle, harness, s):
         assert min(same, swap) <= 2e-6, (s, trial)
         assert np.abs(ho["T"] - h["T"]).max() <= 2e-6
     assert worst_e < 1e-8
+
+
+@pytest.mark.parametrize("s", [9, 12, 50, 670])
+def test_vfree_eigvec_matches_rotation_accumulated(oracle, harness, s):
+    """s >= 9: the V-free path (Jacobi eigenvalues + inverse iteration) gives the same vector
+    as the rotation-accumulated Jacobi, up to sign, including near-exact (noise-free) data."""
+    bl, br = _bearings(oracle, 33, 2048)
+    rng = np.random.default_rng(100 + s)
+    worst = 0.0
+    for trial in range(40):
+        idx = rng.choice(len(bl), s, replace=False)
+        a = np.ascontiguousarray(bl[idx])
+        b = np.ascontiguousarray(br[idx])
+        g36 = np.zeros(36)
+        harness.erph_gram36(_p(a), _p(b), s, _p(g36))
+        e1 = np.zeros(9)
+        e2 = np.zeros(9)
+        harness.erph_vec_jacobi(_p(g36), s, _p(e1))
+        harness.erph_vec_fast(_p(g36), _p(e2))
+        assert abs(np.linalg.norm(e2) - 1.0) < 1e-12
+        worst = max(worst, min(np.abs(e1 - e2).max(), np.abs(e1 + e2).max()))
+    assert worst < 1e-9, worst
