@@ -408,74 +408,82 @@ __global__ void bearings_direct_kernel(const erp_point2f* __restrict__ kl,
 // 31-word window r[n..n+30] to r[n+d..n+d+30].  One wave per pair computes
 //   R_l = x^(l(M-1)) (l = 0..64) and Q_k = x^(64(M-1) 2^k),
 // the hops from a wave's first hypothesis to each lane's hypothesis and between waves.
-__device__ void pmul(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t* tmp) {
+// One wave: out = a * b mod P (31 coefficients each, in LDS).  Lane n < 61 forms the
+// convolution coefficient c_n; lanes t < 31 then fold c_31..c_60 with the reduction table
+// column they hold in registers (cred[d] = c_red[d][t]).  out may alias neither a nor b.
+__device__ __forceinline__ void pmul_wave(const uint32_t* a, const uint32_t* b, uint32_t* out,
+                                          const uint32_t (&cred)[30]) {
     const int lane = wave_lane();
-    if (lane < 61) {
-        const int lo = lane > 30 ? lane - 30 : 0, hi = lane < 30 ? lane : 30;
-        uint32_t c = 0;
-        for (int i = lo; i <= hi; i++) c += a[i] * b[lane - i];
-        tmp[lane] = c;
-    }
-    __syncthreads();
-    if (lane < 31) {
-        uint32_t acc = tmp[lane];
+    uint32_t c = 0;
 #pragma unroll
-        for (int d = 0; d < 30; d++) acc += tmp[31 + d] * c_red[d][lane];
-        out[lane] = acc;
+    for (int i = 0; i < 31; i++) {
+        const int j = lane - i;
+        const uint32_t bj = (j >= 0 && j <= 30) ? b[j < 0 ? 0 : (j > 30 ? 30 : j)] : 0u;
+        c += a[i] * bj;
     }
-    __syncthreads();
+    uint32_t r = c;
+#pragma unroll
+    for (int d = 0; d < 30; d++) r += (uint32_t)__builtin_amdgcn_readlane((int)c, 31 + d) * cred[d];
+    if (lane < 31) out[lane] = r;
 }
 
-__global__ __launch_bounds__(64) void jump_prep_kernel(const int32_t* __restrict__ counts,
-                                                       double sample_frac, int nq_needed,
-                                                       uint32_t* __restrict__ polyR,
-                                                       uint32_t* __restrict__ polyQ) {
-    __shared__ uint32_t res[32], base[32], r1[32], t2[32], tmp[64];
-    const int p = blockIdx.x, lane = wave_lane();
+// glibc jump-ahead polynomials of one pair (one block of 16 waves):
+//   R_l = x^(l(M-1)) mod P (l = 0..64) and Q_k = x^(64(M-1) 2^k) (k < nq_needed).
+// R_1 by left-to-right square-and-shift (multiplying by x is a shift plus one fold), R_2..R_64
+// in six doubling levels (R_{h+j} = R_h R_j, the level's products spread over the waves),
+// the Q_k by repeated squaring: ~26 dependent products instead of ~95.
+__global__ __launch_bounds__(1024) void jump_prep_kernel(const int32_t* __restrict__ counts,
+                                                         double sample_frac, int nq_needed,
+                                                         uint32_t* __restrict__ polyR,
+                                                         uint32_t* __restrict__ polyQ) {
+    __shared__ uint32_t Rl[65][32];
+    __shared__ uint32_t tq[2][32];
+    const int p = blockIdx.x, lane = wave_lane(), wid = threadIdx.x >> 6;
     const int M = counts[p];
     if ((int)(M * sample_frac) < 1 || M < 2) return;
-    if (lane < 31) {
-        res[lane] = lane == 0 ? 1u : 0u;
-        base[lane] = lane == 1 ? 1u : 0u;
-    }
-    __syncthreads();
-    uint32_t e = (uint32_t)(M - 1);
-    while (e) {
-        if (e & 1u) {
-            pmul(res, base, t2, tmp);
-            if (lane < 31) res[lane] = t2[lane];
-            __syncthreads();
+    uint32_t cred[30];
+#pragma unroll
+    for (int d = 0; d < 30; d++) cred[d] = lane < 31 ? c_red[d][lane] : 0u;
+    // R_1 (wave 0)
+    if (wid == 0) {
+        const uint32_t e = (uint32_t)(M - 1);
+        const int top = 31 - __builtin_clz(e);
+        int cur = 0;  // result lives in tq[cur]
+        if (lane < 31) tq[0][lane] = lane == 1 ? 1u : 0u;  // x^1 (top bit)
+        for (int bit = top - 1; bit >= 0; bit--) {
+            pmul_wave(tq[cur], tq[cur], tq[cur ^ 1], cred);
+            cur ^= 1;
+            if ((e >> bit) & 1u) {
+                const uint32_t hi = tq[cur][30];
+                const uint32_t v = lane == 0 ? 0u : tq[cur][lane - 1 < 0 ? 0 : lane - 1];
+                const uint32_t add = (lane == 0 || lane == 28) ? hi : 0u;
+                if (lane < 31) tq[cur ^ 1][lane] = v + add;
+                cur ^= 1;
+            }
         }
-        e >>= 1;
-        if (e) {
-            pmul(base, base, t2, tmp);
-            if (lane < 31) base[lane] = t2[lane];
-            __syncthreads();
-        }
-    }
-    uint32_t* R = polyR + (size_t)p * 65 * 31;
-    if (lane < 31) {
-        R[lane] = lane == 0 ? 1u : 0u;
-        R[31 + lane] = res[lane];
-        r1[lane] = res[lane];
-    }
-    __syncthreads();
-    for (int l = 2; l <= 64; l++) {
-        pmul(res, r1, t2, tmp);
         if (lane < 31) {
-            res[lane] = t2[lane];
-            R[l * 31 + lane] = t2[lane];
+            Rl[0][lane] = lane == 0 ? 1u : 0u;
+            Rl[1][lane] = tq[cur][lane];
         }
+    }
+    __syncthreads();
+    for (int have = 1; have < 64; have *= 2) {  // R_{have+1 .. 2 have}
+        for (int j = wid; j < have; j += 16) pmul_wave(Rl[have], Rl[j + 1], Rl[have + 1 + j], cred);
         __syncthreads();
     }
-    uint32_t* Q = polyQ + (size_t)p * kMaxQ * 31;
-    for (int k = 0; k < nq_needed; k++) {
-        if (k > 0) {
-            pmul(res, res, t2, tmp);
-            if (lane < 31) res[lane] = t2[lane];
-            __syncthreads();
+    uint32_t* R = polyR + (size_t)p * 65 * 31;
+    for (int t = threadIdx.x; t < 65 * 31; t += 1024) R[t] = Rl[t / 31][t % 31];
+    if (wid == 0) {
+        uint32_t* Q = polyQ + (size_t)p * kMaxQ * 31;
+        if (lane < 31) tq[0][lane] = Rl[64][lane];
+        int cur = 0;
+        for (int k = 0; k < nq_needed; k++) {
+            if (k > 0) {
+                pmul_wave(tq[cur], tq[cur], tq[cur ^ 1], cred);
+                cur ^= 1;
+            }
+            if (lane < 31) Q[k * 31 + lane] = tq[cur][lane];
         }
-        if (lane < 31) Q[k * 31 + lane] = res[lane];
     }
 }
 
@@ -1794,7 +1802,7 @@ hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_
                             uint32_t* polyQ, hipStream_t st) {
     // sample_frac is only used to skip pairs with sample_n < 1; pass a tiny positive value so
     // every pair with M >= 2 gets polynomials (the sampler decides on its own)
-    hipLaunchKernelGGL(jump_prep_kernel, dim3(sh.n_pairs), dim3(64), 0, st, counts, 1.0,
+    hipLaunchKernelGGL(jump_prep_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, 1.0,
                        q_needed(sh.iters), polyR, polyQ);
     return hipGetLastError();
 }
