@@ -88,7 +88,8 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_consensus_dev"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
-          "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore"]
+          "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
+          "consensus_refine"]
 
 
 class ErpError(RuntimeError):

@@ -337,7 +337,23 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
         ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, (double*)c->lb.p,
                                             (double*)c->ub.p, sh, cfg->trim_lo, cfg->trim_hi,
-                                            (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, st));
+                                            (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, 0,
+                                            st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_CONSENSUS_REFINE, st);
+        ERP_CK(erp::launch_consensus_refine((int32_t*)c->kcount.p, (float*)c->rv.p,
+                                            (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
+                                            (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
+                                            (int32_t*)c->bsel.p, (double*)c->lb.p,
+                                            (double*)c->ub.p, st));
+    }
+    {
+        StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
+        ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, (double*)c->lb.p,
+                                            (double*)c->ub.p, sh, cfg->trim_lo, cfg->trim_hi,
+                                            (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, 1,
+                                            st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_ROWS, st);
@@ -378,7 +394,8 @@ const char* erp_stage_name(int32_t stage) {
     static const char* names[ERP_STAGE_COUNT] = {
         "knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler",
         "eigen", "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
-        "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore"};
+        "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
+        "consensus_refine"};
     return (stage >= 0 && stage < ERP_STAGE_COUNT) ? names[stage] : "unknown";
 }
 

@@ -98,9 +98,16 @@ hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, i
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    const BatchShape& sh, double trim_lo, double trim_hi, double* lb,
                                    double* ub, int32_t* bsel, hipStream_t st);
+// survivors = rows with LB <= min UB (again = 1: only pairs the refine pass touched)
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
                                    const BatchShape& sh, double trim_lo, double trim_hi,
-                                   int32_t* surv, int32_t* nsurv, double* tmean, hipStream_t st);
+                                   int32_t* surv, int32_t* nsurv, double* tmean, int again,
+                                   hipStream_t st);
+// tighter [LB, UB] for the current survivors (exact inner sums + sub-bins of the boundary bins)
+hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const float* dscale,
+                                   const BatchShape& sh, double trim_lo, double trim_hi,
+                                   const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
+                                   double* lb, double* ub, hipStream_t st);
 hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const float* dscale,
                                  const BatchShape& sh, double trim_lo, double trim_hi,
                                  const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,

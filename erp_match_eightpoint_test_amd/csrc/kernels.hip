@@ -1218,6 +1218,7 @@ constexpr int kBinsPerBinade = 32;    // of s = d^2
 constexpr int kBinades = 40;          // of s
 constexpr int kNB = kBinsPerBinade * kBinades;  // 1280
 constexpr int kHistStride = kNB + 4;
+constexpr int kRefineMin = 256;  // survivors per pair below which refining does not pay
 
 // first s-binade of the bins: the 40 binades ending with the one holding D^2 (D = dscale is
 // the bounding-box diagonal rounded up, >= every distance, so every s <= D^2)
@@ -1362,6 +1363,160 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
         // sequential sum
         lb[(size_t)p * stride + row] = hi > lo ? ((double)L / w) * (1.0 - 2e-4) : 0.0;
         ub[(size_t)p * stride + row] = hi > lo ? ((double)U / w) * (1.0 + 2e-4) : 0.0;
+    }
+}
+
+// Tighter bounds for the surviving rows (8 per block, lanes rotating over the rows as in the
+// bounds kernel).  For each row: the exact s of every column (the reference's expression),
+// an fp64 sum of sqrtf(s) over the bins strictly between b_a and b_b (the bins of ranks lo and
+// hi-1 from the bounds kernel), exact counts below them, and 512-way sub-histograms (key bits
+// 17..9) of the two boundary bins.  The window's part inside a boundary bin is bracketed with
+// sub-bin resolution (2^-15 relative instead of 2^-6), so the bounds tighten by ~500x and the
+// next selection keeps only genuine near-ties -- this is what makes a two-cluster row set
+// (R1 and R2 valid in every iteration: every row's mean within 1 % of the minimum) cheap.
+// A row whose ranks do not fall into b_a / b_b under the exact binning keeps its old bounds.
+__global__ __launch_bounds__(256) void consensus_refine_kernel(const int32_t* __restrict__ kcount,
+                                                               const float* __restrict__ rv,
+                                                               const float* __restrict__ dscale,
+                                                               int stride, double trim_lo,
+                                                               double trim_hi,
+                                                               const int32_t* __restrict__ surv,
+                                                               const int32_t* __restrict__ nsurv,
+                                                               const int32_t* __restrict__ bsel,
+                                                               double* __restrict__ lb,
+                                                               double* __restrict__ ub) {
+    __shared__ uint32_t sub[kBoundRows][2][512];
+    __shared__ double inner[kBoundRows];
+    __shared__ int below[kBoundRows][2];
+    const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
+    const int K = kcount[p];
+    const int ns = nsurv[p];
+    const int s0 = blockIdx.x * kBoundRows;
+    if (s0 >= ns || ns <= kRefineMin) return;  // few survivors: the exact pass is cheaper
+    const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
+    if (hi <= lo) return;
+    const float* X = rv + (size_t)p * 3 * stride;
+    const float* Y = X + stride;
+    const float* Z = Y + stride;
+    const int base = bounds_elo(dscale[p]) << 5;
+    const int32_t* S = surv + (size_t)p * stride;
+    float xi[kBoundRows], yi[kBoundRows], zi[kBoundRows];
+    int ba[kBoundRows], bb[kBoundRows];
+    double acc[kBoundRows];
+    int bel_a[kBoundRows], bel_b[kBoundRows];
+#pragma unroll
+    for (int t = 0; t < kBoundRows; t++) {
+        const int r = (lane + t) & (kBoundRows - 1);
+        const int row = S[min(s0 + r, ns - 1)];
+        xi[t] = X[row];
+        yi[t] = Y[row];
+        zi[t] = Z[row];
+        ba[t] = bsel[((size_t)p * stride + row) * 2] + base;   // as key >> 18
+        bb[t] = bsel[((size_t)p * stride + row) * 2 + 1] + base;
+        acc[t] = 0.0;
+        bel_a[t] = 0;
+        bel_b[t] = 0;
+    }
+    for (int q = tid; q < kBoundRows * 2 * 512; q += 256) (&sub[0][0][0])[q] = 0u;
+    if (tid < kBoundRows) {
+        inner[tid] = 0.0;
+        below[tid][0] = 0;
+        below[tid][1] = 0;
+    }
+    __syncthreads();
+    for (int j = tid; j < K; j += 256) {
+        const float xj = X[j], yj = Y[j], zj = Z[j];
+#pragma unroll
+        for (int t = 0; t < kBoundRows; t++) {
+            const float s = rdist2(xi[t], yi[t], zi[t], xj, yj, zj);
+            const uint32_t key = __float_as_uint(s);
+            const int e = (int)(key >> 18);
+            bel_a[t] += e < ba[t];
+            bel_b[t] += e < bb[t];
+            if (e > ba[t] && e < bb[t]) {
+                acc[t] += (double)__builtin_sqrtf(s);
+            } else if (e == ba[t] || e == bb[t]) {
+                const int r = (lane + t) & (kBoundRows - 1);
+                atomicAdd(&sub[r][e == ba[t] ? 0 : 1][(key >> 9) & 511u], 1u);
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < kBoundRows; t++) {
+        const int r = (lane + t) & (kBoundRows - 1);
+        atomicAdd(&inner[r], acc[t]);
+        atomicAdd(&below[r][0], bel_a[t]);
+        atomicAdd(&below[r][1], bel_b[t]);
+    }
+    __syncthreads();
+    // per row (32 threads): bracket the window's part inside the two boundary bins
+    const int r = tid >> 5, sl = tid & 31;
+    if (s0 + r >= ns) return;
+    const int row = S[s0 + r];
+    const int bA = bsel[((size_t)p * stride + row) * 2] + base;
+    const int bB = bsel[((size_t)p * stride + row) * 2 + 1] + base;
+    const int cA = below[r][0], cB = below[r][1];
+    // sub-bin k of bin b (as key >> 18) covers keys [((b << 9) | k) << 9, ... + 512)
+    auto sub_lo = [&](int b, int k) { return (double)__builtin_sqrtf(__uint_as_float((uint32_t)((b << 9) | k) << 9)); };
+    auto sub_hi = [&](int b, int k) {
+        return (double)__builtin_sqrtf(__uint_as_float(((uint32_t)((b << 9) | k) << 9) + 511u));
+    };
+    // the window's ranks inside bin A: [max(lo, cA), min(hi, cA + nA)); inside bin B (when
+    // distinct): [cB, hi).  Count per sub-bin, clipped to those rank ranges, times the
+    // sub-bin's d-range gives the bounds.
+    double L = 0.0, U = 0.0;
+    int nA = 0, nB = 0;
+    for (int k = sl; k < 512; k += 32) {
+        nA += (int)sub[r][0][k];
+        nB += (int)sub[r][1][k];
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        nA += __shfl_xor(nA, o, 32);
+        nB += __shfl_xor(nB, o, 32);
+    }
+    const bool same = bA == bB;
+    bool ok = cA <= lo && lo < cA + nA && (same ? (hi - 1 < cA + nA) : (cB <= hi - 1 && hi - 1 < cB + nB));
+    if (ok) {
+        // sub-bins of A in ascending order: thread sl owns k = 16 sl .. 16 sl + 15
+        for (int part = 0; part < (same ? 1 : 2); part++) {
+            const uint32_t* hh = sub[r][part];
+            const int b = part ? bB : bA;
+            const int c0 = part ? cB : cA;
+            int cnt = 0;
+            for (int q = 0; q < 16; q++) cnt += (int)hh[16 * sl + q];
+            int x = cnt;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                const int y = __shfl_up(x, o, 32);
+                if (sl >= o) x += y;
+            }
+            int cum = c0 + x - cnt;
+            for (int q = 0; q < 16; q++) {
+                const int k = 16 * sl + q;
+                const int n = (int)hh[k];
+                const int a0 = max(cum, lo), a1 = min(cum + n, hi);
+                if (a1 > a0) {
+                    L += (double)(a1 - a0) * sub_lo(b, k);
+                    U += (double)(a1 - a0) * sub_hi(b, k);
+                }
+                cum += n;
+            }
+        }
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        L += __shfl_xor(L, o, 32);
+        U += __shfl_xor(U, o, 32);
+    }
+    if (sl == 0 && ok) {
+        const double w = (double)(hi - lo);
+        const double in = inner[r];
+        const double nl = ((in + L) / w) * (1.0 - 1e-9), nu = ((in + U) / w) * (1.0 + 1e-9);
+        double* lp = lb + (size_t)p * stride + row;
+        double* up = ub + (size_t)p * stride + row;
+        *lp = fmax(*lp, nl);
+        *up = fmin(*up, nu);
     }
 }
 
@@ -1513,11 +1668,13 @@ __global__ __launch_bounds__(1024) void consensus_select_kernel(const int32_t* _
                                                                 double trim_hi,
                                                                 int32_t* __restrict__ surv,
                                                                 int32_t* __restrict__ nsurv,
-                                                                double* __restrict__ tmean) {
+                                                                double* __restrict__ tmean,
+                                                                int again) {
     __shared__ double sm[16];
     __shared__ int ws[16];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int K = kcount[p];
+    if (again && nsurv[p] <= kRefineMin) return;  // not refined: the list stands
     const double* L = lb + (size_t)p * stride;
     const double* U = ub + (size_t)p * stride;
     double* Tm = tmean + (size_t)p * stride;
@@ -1917,9 +2074,20 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
 
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
                                    const BatchShape& sh, double trim_lo, double trim_hi,
-                                   int32_t* surv, int32_t* nsurv, double* tmean, hipStream_t st) {
+                                   int32_t* surv, int32_t* nsurv, double* tmean, int again,
+                                   hipStream_t st) {
     hipLaunchKernelGGL(consensus_select_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, kcount, lb, ub,
-                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, tmean);
+                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, tmean, again);
+    return hipGetLastError();
+}
+
+hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const float* dscale,
+                                   const BatchShape& sh, double trim_lo, double trim_hi,
+                                   const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
+                                   double* lb, double* ub, hipStream_t st) {
+    dim3 grid((2 * sh.iters + kBoundRows - 1) / kBoundRows, sh.n_pairs);
+    hipLaunchKernelGGL(consensus_refine_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
+                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub);
     return hipGetLastError();
 }
 

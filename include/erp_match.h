@@ -174,7 +174,8 @@ typedef enum erp_stage {
     ERP_STAGE_GRAM = 12,            /* A^T A of every sample (fp64) */
     ERP_STAGE_KNN2_CANDIDATES = 13, /* MFMA pass 2: candidate train rows per query */
     ERP_STAGE_KNN2_RESCORE = 14,    /* exact flann::L2 distances of the candidates */
-    ERP_STAGE_COUNT = 15
+    ERP_STAGE_CONSENSUS_REFINE = 15, /* tighter bounds for the survivors (sub-bins) */
+    ERP_STAGE_COUNT = 16
 } erp_stage;
 erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable);
 const char* erp_stage_name(int32_t stage);
