@@ -199,6 +199,7 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ql[c], acc, 0, 0, 0);
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, qh[c], acc, 0, 0, 0);
         }
+        uint32_t cmask = 0;  // pass 2: candidate rows of this tile (bit 4g + e)
 #pragma unroll
         for (int g = 0; g < 4; g++) {
             const float4 t4 = *reinterpret_cast<const float4*>(&sm.tt[buf][8 * g + 4 * h]);
@@ -212,13 +213,22 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
                     m2 = __builtin_amdgcn_fmed3f(m1, m2, u);
                     m1 = fminf(m1, u);
                 } else {
+                    // NaN (rows past the chunk: inf - inf) never passes
                     const float l = __builtin_fmaf(-kFEps, st, a) - kFTiny;
-                    if (l <= U2 && qv) {  // NaN (rows past the chunk: inf - inf) never passes
-                        const int slot = atomicAdd(&ccount[(size_t)p * max_nq + q], 1);
-                        if (slot < kCandCap)
-                            cand[((size_t)p * max_nq + q) * kCandCap + slot] =
-                                tile0 + 8 * g + 4 * h + e;
-                    }
+                    cmask |= (l <= U2) ? (1u << (4 * g + e)) : 0u;
+                }
+            }
+        }
+        if (PASS == 2) {
+            if (!qv) cmask = 0;
+            if (__builtin_amdgcn_ballot_w64(cmask != 0)) {  // rare: most tiles have none
+                while (cmask) {
+                    const int bit = __builtin_ctz(cmask);
+                    cmask &= cmask - 1u;
+                    const int slot = atomicAdd(&ccount[(size_t)p * max_nq + q], 1);
+                    if (slot < kCandCap)
+                        cand[((size_t)p * max_nq + q) * kCandCap + slot] =
+                            tile0 + 8 * (bit >> 2) + 4 * h + (bit & 3);
                 }
             }
         }
@@ -913,68 +923,50 @@ __global__ __launch_bounds__(1024) void valid_compact_kernel(const int32_t* __re
                                                              float* __restrict__ rv_aos,
                                                              float* __restrict__ dscale) {
     __shared__ int ws[16];
-    const int p = blockIdx.x;
+    __shared__ float red6[6][16];
+    const int p = blockIdx.x, tid = threadIdx.x;
     const int M = counts[p];
     if ((int)(M * sample_frac) < 1) {
-        if (threadIdx.x == 0) kcount[p] = 0;
+        if (tid == 0) kcount[p] = 0;
         return;
     }
     const erp_hypothesis* H = hyps + (size_t)p * iters;
-    const int per = (iters + 1023) / 1024;
-    const int ha = min(iters, (int)threadIdx.x * per), hb = min(iters, ha + per);
-    int cnt = 0;
-    for (int h = ha; h < hb; h++) cnt += (H[h].R1_valid != 0) + (H[h].R2_valid != 0);
-    int total;
-    int pos = block_exclusive_scan<1024>(cnt, ws, &total);
     const int stride = 2 * iters;
     float* X = rv + (size_t)p * 3 * stride;
     float* T = tv + (size_t)p * 3 * stride;
     float* A = rv_aos ? rv_aos + (size_t)p * 3 * stride : nullptr;
-    for (int h = ha; h < hb; h++) {
-        const erp_hypothesis hy = H[h];
-        if (hy.R1_valid) {
-            X[pos] = hy.R1[0];
-            X[stride + pos] = hy.R1[1];
-            X[2 * stride + pos] = hy.R1[2];
-            if (A) {
-                A[3 * pos] = hy.R1[0];
-                A[3 * pos + 1] = hy.R1[1];
-                A[3 * pos + 2] = hy.R1[2];
+    float mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+    int base = 0;
+    // chunks of 1024 consecutive iterations (one per thread, coalesced record reads); the
+    // block scan of each chunk keeps the reference's push order (iteration, then R1, R2)
+    for (int h0 = 0; h0 < iters; h0 += 1024) {
+        const int h = h0 + tid;
+        erp_hypothesis hy;
+        hy.R1_valid = 0;
+        hy.R2_valid = 0;
+        if (h < iters) hy = H[h];
+        const int cnt = (hy.R1_valid != 0) + (hy.R2_valid != 0);
+        int total;
+        int pos = base + block_exclusive_scan<1024>(cnt, ws, &total);
+#pragma unroll
+        for (int which = 0; which < 2; which++) {
+            if (!(which ? hy.R2_valid : hy.R1_valid)) continue;
+            const float* R = which ? hy.R2 : hy.R1;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                X[c * stride + pos] = R[c];
+                mn[c] = fminf(mn[c], R[c]);
+                mx[c] = fmaxf(mx[c], R[c]);
+                T[3 * pos + c] = hy.T[c];
+                if (A) A[3 * pos + c] = R[c];
             }
-            T[3 * pos] = hy.T[0];
-            T[3 * pos + 1] = hy.T[1];
-            T[3 * pos + 2] = hy.T[2];
             pos++;
         }
-        if (hy.R2_valid) {
-            X[pos] = hy.R2[0];
-            X[stride + pos] = hy.R2[1];
-            X[2 * stride + pos] = hy.R2[2];
-            if (A) {
-                A[3 * pos] = hy.R2[0];
-                A[3 * pos + 1] = hy.R2[1];
-                A[3 * pos + 2] = hy.R2[2];
-            }
-            T[3 * pos] = hy.T[0];
-            T[3 * pos + 1] = hy.T[1];
-            T[3 * pos + 2] = hy.T[2];
-            pos++;
-        }
+        base += total;
     }
-    if (threadIdx.x == 0) kcount[p] = total;
+    if (tid == 0) kcount[p] = base;
     // bounding-box diagonal of the valid R set (>= every pairwise distance): the scale of
     // the consensus bounds histogram
-    __syncthreads();
-    float mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
-    for (int k = threadIdx.x; k < total; k += 1024) {
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            const float v = X[c * stride + k];
-            mn[c] = fminf(mn[c], v);
-            mx[c] = fmaxf(mx[c], v);
-        }
-    }
-    __shared__ float red6[6][16];
 #pragma unroll
     for (int c = 0; c < 3; c++) {
         float a = mn[c], b = mx[c];
@@ -983,13 +975,13 @@ __global__ __launch_bounds__(1024) void valid_compact_kernel(const int32_t* __re
             a = fminf(a, __shfl_xor(a, o, 64));
             b = fmaxf(b, __shfl_xor(b, o, 64));
         }
-        if ((threadIdx.x & 63) == 0) {
-            red6[c][threadIdx.x >> 6] = a;
-            red6[3 + c][threadIdx.x >> 6] = b;
+        if ((tid & 63) == 0) {
+            red6[c][tid >> 6] = a;
+            red6[3 + c][tid >> 6] = b;
         }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (tid == 0) {
         double d2 = 0;
         for (int c = 0; c < 3; c++) {
             float a = kInf, b = -kInf;
@@ -997,7 +989,7 @@ __global__ __launch_bounds__(1024) void valid_compact_kernel(const int32_t* __re
                 a = fminf(a, red6[c][w]);
                 b = fmaxf(b, red6[3 + c][w]);
             }
-            const double e = total > 0 ? (double)b - (double)a : 0.0;
+            const double e = base > 0 ? (double)b - (double)a : 0.0;
             d2 += e * e;
         }
         dscale[p] = (float)(sqrt(d2) * (1.0 + 1e-6));
