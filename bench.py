@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=8, help="pairs per step per GPU")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="independent sub-batches (own context + HIP stream) per step")
     ap.add_argument("--iters", type=int, default=10000)
     ap.add_argument("--kpts", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=20200423)
@@ -141,42 +143,64 @@ def main():
 
     from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
     pairs = make_batch(rank, args.pairs, args.kpts, args.seed)
-    b = to_device(pairs, dev)
-    ctx = Context(local)
-    runner = PairBatchRunner(ctx=ctx, iters=args.iters)
-    runner.reserve(args.pairs, b["max_nq"], b["max_nt"])
-    call = lambda: runner.run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"],  # noqa
-                              b["off_r"], b["width"], b["height"], b["max_nq"], b["max_nt"])
+    S = max(1, min(args.streams, args.pairs))
+    parts = [pairs[i * args.pairs // S:(i + 1) * args.pairs // S] for i in range(S)]
+    subs = []
+    for part in parts:  # one context (scratch) and one HIP stream per sub-batch
+        b = to_device(part, dev)
+        ctx = Context(local)
+        runner = PairBatchRunner(ctx=ctx, iters=args.iters)
+        runner.reserve(len(part), b["max_nq"], b["max_nt"])
+        subs.append(dict(b=b, ctx=ctx, runner=runner, stream=torch.cuda.Stream(dev),
+                         res=torch.empty((len(part), 64), dtype=torch.uint8, device=dev)))
+
+    def call():
+        for sb in subs:
+            b = sb["b"]
+            with torch.cuda.stream(sb["stream"]):
+                out = sb["runner"].run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"],
+                                       b["off_r"], b["width"], b["height"], b["max_nq"],
+                                       b["max_nt"], stream=sb["stream"].cuda_stream)
+                sb["res"].copy_(out["results"])
+        for sb in subs:
+            torch.cuda.current_stream(dev).wait_stream(sb["stream"])
+        return torch.cat([sb["res"] for sb in subs])
+
     gathered = None
     if dist is not None:
         gathered = torch.empty((world, args.pairs, 64), dtype=torch.uint8, device=dev)
     for _ in range(args.warmup):
         out = call()
         if dist is not None:
-            dist.all_gather_into_tensor(gathered, out["results"])
+            dist.all_gather_into_tensor(gathered, out)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
-    ctx.set_profiling(True)
-    ctx.stage_times()  # clear
+    for sb in subs:
+        sb["ctx"].set_profiling(True)
+        sb["ctx"].stage_times()  # clear
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = call()
         if dist is not None:
-            dist.all_gather_into_tensor(gathered, out["results"])
+            dist.all_gather_into_tensor(gathered, out)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
-    stages = ctx.stage_times()
-    ctx.set_profiling(False)
+    stages = {}
+    for sb in subs:
+        for k, (ms, n) in sb["ctx"].stage_times().items():
+            a = stages.get(k, (0.0, 0))
+            stages[k] = (a[0] + ms, a[1] + n)
+        sb["ctx"].set_profiling(False)
     elapsed = t1 - t0
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    res = results_to_numpy(out["results"])
+    res = results_to_numpy(out)
     ok = bool(np.all(res["status"] == 0))
     err_deg = [float(np.degrees(np.abs(r["R"] - p["euler_gt"])).mean()) for r, p in zip(res, pairs)]
     if rank != 0:
@@ -208,6 +232,7 @@ def main():
         "config": {"workload": "configs[1] shape: 4096x4096 kpts/pair, 10k initial_guess iters, "
                                f"batch of {args.pairs} independent pairs per step per GPU",
                    "kpts": args.kpts, "iters": args.iters, "pairs_per_step_per_gpu": args.pairs,
+                   "streams": S,
                    "parallelism": f"pair-sharded x{world}", "sampler": "glibc replay (seed 1)"},
         "roofline": roof,
         "cpu_baseline": cpu,

@@ -1206,11 +1206,17 @@ __global__ __launch_bounds__(1024) void consensus_input_kernel(const float* __re
 // 64-way for a concentrated row), and the row stride (== 4 mod 32 words) puts the same bin of
 // different rows in different banks.
 constexpr int kBoundRows = 8;
-constexpr int kBinsPerBinade = 32;    // of s = d^2
+constexpr int kBinShift = 19;         // bin = key >> 19: 16 bins per binade of s = d^2
+constexpr int kMantBits = 23 - kBinShift;
+constexpr int kBinsPerBinade = 1 << kMantBits;  // (= 32 per binade of the distance)
 constexpr int kBinades = 40;          // of s
-constexpr int kNB = kBinsPerBinade * kBinades;  // 1280
+constexpr int kNB = kBinsPerBinade * kBinades;  // 640
+constexpr int kSubBits = 10;          // 1024 sub-bins per bin (refine / exact pass) ...
+constexpr int kNS = 1 << kSubBits;
+constexpr int kLowBits = kBinShift - kSubBits;  // ... and below them the exact values
+constexpr int kRefineRows = 4;        // rows per refine block
 constexpr int kHistStride = kNB + 4;
-constexpr int kRefineMin = 256;  // survivors per pair below which refining does not pay
+constexpr int kRefineMin = 32;   // survivors per pair below which refining does not pay
 
 // first s-binade of the bins: the 40 binades ending with the one holding D^2 (D = dscale is
 // the bounding-box diagonal rounded up, >= every distance, so every s <= D^2)
@@ -1222,7 +1228,7 @@ __device__ __forceinline__ int bounds_elo(float D) {
 }
 // d-space edge e of the bins (e = 1 .. NB-1: lower edge of bin e = upper edge of bin e-1)
 __device__ __forceinline__ float bin_edge_s(int elo, int e) {
-    return __uint_as_float((uint32_t)((elo << 5) + e) << 18);
+    return __uint_as_float((uint32_t)((elo << kMantBits) + e) << kBinShift);
 }
 
 __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __restrict__ kcount,
@@ -1243,7 +1249,7 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     const float* Y = X + stride;
     const float* Z = Y + stride;
     const int elo = bounds_elo(dscale[p]);
-    const int base = elo << 5;
+    const int base = elo << kMantBits;
     float xi[kBoundRows], yi[kBoundRows], zi[kBoundRows];
     int hoff[kBoundRows];
 #pragma unroll
@@ -1289,7 +1295,7 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
         for (int t = 0; t < kBoundRows; t++) {
             const float dx = xi[t] - xj, dy = yi[t] - yj, dz = zi[t] - zj;
             const float s = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
-            const int key = (int)(__float_as_uint(s) >> 18);
+            const int key = (int)(__float_as_uint(s) >> kBinShift);
             atomicAdd(&hist[hoff[t] + min(max(key, base), bmax)], 1u);
         }
     }
@@ -1358,59 +1364,57 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     }
 }
 
-// Tighter bounds for the surviving rows (8 per block, lanes rotating over the rows as in the
+// Tighter bounds for the surviving rows (4 per block, lanes rotating over the rows as in the
 // bounds kernel).  For each row: the exact s of every column (the reference's expression),
 // an fp64 sum of sqrtf(s) over the bins strictly between b_a and b_b (the bins of ranks lo and
-// hi-1 from the bounds kernel), exact counts below them, and 512-way sub-histograms (key bits
-// 17..9) of the two boundary bins.  The window's part inside a boundary bin is bracketed with
-// sub-bin resolution (2^-15 relative instead of 2^-6), so the bounds tighten by ~500x and the
+// hi-1 from the bounds kernel), exact counts below them, and 1024-way sub-histograms (key bits
+// 18..9) of the two boundary bins.  The window's part inside a boundary bin is bracketed with
+// sub-bin resolution (2^-15 relative instead of 2^-5), so the bounds tighten by ~1000x and the
 // next selection keeps only genuine near-ties -- this is what makes a two-cluster row set
 // (R1 and R2 valid in every iteration: every row's mean within 1 % of the minimum) cheap.
 // A row whose ranks do not fall into b_a / b_b under the exact binning keeps its old bounds.
-__global__ __launch_bounds__(256) void consensus_refine_kernel(const int32_t* __restrict__ kcount,
-                                                               const float* __restrict__ rv,
-                                                               const float* __restrict__ dscale,
-                                                               int stride, double trim_lo,
-                                                               double trim_hi,
-                                                               const int32_t* __restrict__ surv,
-                                                               const int32_t* __restrict__ nsurv,
-                                                               const int32_t* __restrict__ bsel,
-                                                               double* __restrict__ lb,
-                                                               double* __restrict__ ub) {
-    __shared__ uint32_t sub[kBoundRows][2][512];
-    __shared__ double inner[kBoundRows];
-    __shared__ int below[kBoundRows][2];
-    const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
+__device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
+                                       const float* __restrict__ rv,
+                                       const float* __restrict__ dscale, int stride,
+                                       double trim_lo, double trim_hi,
+                                       const int32_t* __restrict__ surv,
+                                       const int32_t* __restrict__ nsurv,
+                                       const int32_t* __restrict__ bsel, double* __restrict__ lb,
+                                       double* __restrict__ ub, int p, int vb) {
+    __shared__ uint32_t sub[kRefineRows][2][kNS];
+    __shared__ double inner[kRefineRows];
+    __shared__ int below[kRefineRows][2];
+    const int tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
     const int ns = nsurv[p];
-    const int s0 = blockIdx.x * kBoundRows;
+    const int s0 = vb * kRefineRows;
     if (s0 >= ns || ns <= kRefineMin) return;  // few survivors: the exact pass is cheaper
     const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
     if (hi <= lo) return;
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
-    const int base = bounds_elo(dscale[p]) << 5;
+    const int base = bounds_elo(dscale[p]) << kMantBits;
     const int32_t* S = surv + (size_t)p * stride;
-    float xi[kBoundRows], yi[kBoundRows], zi[kBoundRows];
-    int ba[kBoundRows], bb[kBoundRows];
-    double acc[kBoundRows];
-    int bel_a[kBoundRows], bel_b[kBoundRows];
+    float xi[kRefineRows], yi[kRefineRows], zi[kRefineRows];
+    int ba[kRefineRows], bb[kRefineRows];
+    double acc[kRefineRows];
+    int bel_a[kRefineRows], bel_b[kRefineRows];
 #pragma unroll
-    for (int t = 0; t < kBoundRows; t++) {
-        const int r = (lane + t) & (kBoundRows - 1);
+    for (int t = 0; t < kRefineRows; t++) {
+        const int r = (lane + t) & (kRefineRows - 1);
         const int row = S[min(s0 + r, ns - 1)];
         xi[t] = X[row];
         yi[t] = Y[row];
         zi[t] = Z[row];
-        ba[t] = bsel[((size_t)p * stride + row) * 2] + base;   // as key >> 18
+        ba[t] = bsel[((size_t)p * stride + row) * 2] + base;   // as key >> kBinShift
         bb[t] = bsel[((size_t)p * stride + row) * 2 + 1] + base;
         acc[t] = 0.0;
         bel_a[t] = 0;
         bel_b[t] = 0;
     }
-    for (int q = tid; q < kBoundRows * 2 * 512; q += 256) (&sub[0][0][0])[q] = 0u;
-    if (tid < kBoundRows) {
+    for (int q = tid; q < kRefineRows * 2 * kNS; q += 256) (&sub[0][0][0])[q] = 0u;
+    if (tid < kRefineRows) {
         inner[tid] = 0.0;
         below[tid][0] = 0;
         below[tid][1] = 0;
@@ -1419,58 +1423,62 @@ __global__ __launch_bounds__(256) void consensus_refine_kernel(const int32_t* __
     for (int j = tid; j < K; j += 256) {
         const float xj = X[j], yj = Y[j], zj = Z[j];
 #pragma unroll
-        for (int t = 0; t < kBoundRows; t++) {
+        for (int t = 0; t < kRefineRows; t++) {
             const float s = rdist2(xi[t], yi[t], zi[t], xj, yj, zj);
             const uint32_t key = __float_as_uint(s);
-            const int e = (int)(key >> 18);
+            const int e = (int)(key >> kBinShift);
             bel_a[t] += e < ba[t];
             bel_b[t] += e < bb[t];
             if (e > ba[t] && e < bb[t]) {
                 acc[t] += (double)__builtin_sqrtf(s);
             } else if (e == ba[t] || e == bb[t]) {
-                const int r = (lane + t) & (kBoundRows - 1);
-                atomicAdd(&sub[r][e == ba[t] ? 0 : 1][(key >> 9) & 511u], 1u);
+                const int r = (lane + t) & (kRefineRows - 1);
+                atomicAdd(&sub[r][e == ba[t] ? 0 : 1][(key >> kLowBits) & (kNS - 1u)], 1u);
             }
         }
     }
 #pragma unroll
-    for (int t = 0; t < kBoundRows; t++) {
-        const int r = (lane + t) & (kBoundRows - 1);
+    for (int t = 0; t < kRefineRows; t++) {
+        const int r = (lane + t) & (kRefineRows - 1);
         atomicAdd(&inner[r], acc[t]);
         atomicAdd(&below[r][0], bel_a[t]);
         atomicAdd(&below[r][1], bel_b[t]);
     }
     __syncthreads();
-    // per row (32 threads): bracket the window's part inside the two boundary bins
-    const int r = tid >> 5, sl = tid & 31;
+    // per row (one wave): bracket the window's part inside the two boundary bins
+    const int r = tid >> 6, sl = tid & 63;
     if (s0 + r >= ns) return;
     const int row = S[s0 + r];
     const int bA = bsel[((size_t)p * stride + row) * 2] + base;
     const int bB = bsel[((size_t)p * stride + row) * 2 + 1] + base;
     const int cA = below[r][0], cB = below[r][1];
-    // sub-bin k of bin b (as key >> 18) covers keys [((b << 9) | k) << 9, ... + 512)
-    auto sub_lo = [&](int b, int k) { return (double)__builtin_sqrtf(__uint_as_float((uint32_t)((b << 9) | k) << 9)); };
+    // sub-bin k of bin b (as key >> kBinShift) covers keys [((b << kSubBits) | k) << kLowBits,
+    // + 2^kLowBits)
+    auto sub_lo = [&](int b, int k) {
+        return (double)__builtin_sqrtf(__uint_as_float((uint32_t)((b << kSubBits) | k) << kLowBits));
+    };
     auto sub_hi = [&](int b, int k) {
-        return (double)__builtin_sqrtf(__uint_as_float(((uint32_t)((b << 9) | k) << 9) + 511u));
+        return (double)__builtin_sqrtf(__uint_as_float(
+            ((uint32_t)((b << kSubBits) | k) << kLowBits) + ((1u << kLowBits) - 1u)));
     };
     // the window's ranks inside bin A: [max(lo, cA), min(hi, cA + nA)); inside bin B (when
     // distinct): [cB, hi).  Count per sub-bin, clipped to those rank ranges, times the
     // sub-bin's d-range gives the bounds.
     double L = 0.0, U = 0.0;
     int nA = 0, nB = 0;
-    for (int k = sl; k < 512; k += 32) {
+    for (int k = sl; k < kNS; k += 64) {
         nA += (int)sub[r][0][k];
         nB += (int)sub[r][1][k];
     }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-        nA += __shfl_xor(nA, o, 32);
-        nB += __shfl_xor(nB, o, 32);
+    for (int o = 32; o > 0; o >>= 1) {
+        nA += __shfl_xor(nA, o, 64);
+        nB += __shfl_xor(nB, o, 64);
     }
     const bool same = bA == bB;
     bool ok = cA <= lo && lo < cA + nA && (same ? (hi - 1 < cA + nA) : (cB <= hi - 1 && hi - 1 < cB + nB));
     if (ok) {
-        // sub-bins of A in ascending order: thread sl owns k = 16 sl .. 16 sl + 15
+        // sub-bins in ascending order: thread sl owns k = 16 sl .. 16 sl + 15
         for (int part = 0; part < (same ? 1 : 2); part++) {
             const uint32_t* hh = sub[r][part];
             const int b = part ? bB : bA;
@@ -1479,8 +1487,8 @@ __global__ __launch_bounds__(256) void consensus_refine_kernel(const int32_t* __
             for (int q = 0; q < 16; q++) cnt += (int)hh[16 * sl + q];
             int x = cnt;
 #pragma unroll
-            for (int o = 1; o < 32; o <<= 1) {
-                const int y = __shfl_up(x, o, 32);
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(x, o, 64);
                 if (sl >= o) x += y;
             }
             int cum = c0 + x - cnt;
@@ -1497,9 +1505,9 @@ __global__ __launch_bounds__(256) void consensus_refine_kernel(const int32_t* __
         }
     }
 #pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-        L += __shfl_xor(L, o, 32);
-        U += __shfl_xor(U, o, 32);
+    for (int o = 32; o > 0; o >>= 1) {
+        L += __shfl_xor(L, o, 64);
+        U += __shfl_xor(U, o, 64);
     }
     if (sl == 0 && ok) {
         const double w = (double)(hi - lo);
@@ -1512,11 +1520,50 @@ __global__ __launch_bounds__(256) void consensus_refine_kernel(const int32_t* __
     }
 }
 
+// Work items of all pairs flattened: item g of the batch = (pair p, unit u); the per-pair unit
+// counts are only known on the device, so every block forms their prefix sums and strides
+// over the items (one launch of a fixed grid, no empty blocks, pairs balanced).
+template <typename UNITS>
+__device__ bool item_to_pair(int g, int n_pairs, UNITS units, int* p_out, int* u_out) {
+    int base = 0;
+    for (int p = 0; p < n_pairs; p++) {
+        const int n = units(p);
+        if (g < base + n) {
+            *p_out = p;
+            *u_out = g - base;
+            return true;
+        }
+        base += n;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(256) void consensus_refine_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv,
+    const float* __restrict__ dscale, int stride, double trim_lo, double trim_hi,
+    const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
+    const int32_t* __restrict__ bsel, double* __restrict__ lb, double* __restrict__ ub,
+    int n_pairs) {
+    auto units = [&](int p) {
+        const int ns = nsurv[p];
+        return ns > kRefineMin ? (ns + kRefineRows - 1) / kRefineRows : 0;
+    };
+    int total = 0;
+    for (int p = 0; p < n_pairs; p++) total += units(p);
+    for (int g = blockIdx.x; g < total; g += gridDim.x) {
+        int p, u;
+        item_to_pair(g, n_pairs, units, &p, &u);
+        __syncthreads();  // the previous item's LDS readers are done
+        consensus_refine_block(kcount, rv, dscale, stride, trim_lo, trim_hi, surv, nsurv, bsel,
+                               lb, ub, p, u);
+    }
+}
+
 // Trimmed mean of a surviving row i, ranks [lo, hi), lo = (long)(K*0.2), hi = (long)(K*0.8).
 // The bounds kernel already located the (s'-)bins b_a, b_b holding ranks lo and hi-1; here
 //   pass 1: exact s = dx*dx + dy*dy + dz*dz for every column; fp64 sum of sqrtf(s) over the
 //           bins strictly between b_a and b_b, exact counts below them, and for the two bins
-//           512-way sub-histograms (key bits 17..9) with their fp64 sums of sqrtf(s);
+//           1024-way sub-histograms (key bits 18..9) with their fp64 sums of sqrtf(s);
 //   pass 2: 512-way histograms of the two sub-bins holding the ranks (key bits 8..0, i.e.
 //           exact values) -> the exact keys va, vb at ranks lo and hi-1 and their
 //           multiplicities.
@@ -1526,24 +1573,22 @@ __global__ __launch_bounds__(256) void consensus_refine_kernel(const int32_t* __
 // sits in the under/overflow bin, the row takes the 4-pass radix path instead.  The sum is
 // not the reference's sorted sequential one in the last bits; consensus_final re-scores near
 // ties exactly.
-__global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __restrict__ kcount,
-                                                             const float* __restrict__ rv,
-                                                             const float* __restrict__ dscale,
-                                                             int stride, double trim_lo,
-                                                             double trim_hi,
-                                                             const int32_t* __restrict__ surv,
-                                                             const int32_t* __restrict__ nsurv,
-                                                             const int32_t* __restrict__ bsel,
-                                                             double* __restrict__ tmean) {
+__device__ void consensus_rows_block(const int32_t* __restrict__ kcount,
+                                     const float* __restrict__ rv,
+                                     const float* __restrict__ dscale, int stride, double trim_lo,
+                                     double trim_hi, const int32_t* __restrict__ surv,
+                                     const int32_t* __restrict__ nsurv,
+                                     const int32_t* __restrict__ bsel,
+                                     double* __restrict__ tmean, int p, int vb) {
     __shared__ uint32_t histA[2048], histB[2048];  // radix fallback; level counts alias it
-    __shared__ double sA[512], sB[512];
+    __shared__ double sA[kNS], sB[kNS];
     __shared__ int ws[8];
     __shared__ int res[2];
     __shared__ double red[8];
-    const int p = blockIdx.y, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const int K = kcount[p];
-    if ((int)blockIdx.x >= nsurv[p]) return;
-    const int i = surv[(size_t)p * stride + blockIdx.x];
+    if (vb >= nsurv[p]) return;
+    const int i = surv[(size_t)p * stride + vb];
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
@@ -1554,22 +1599,25 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
         if (tid == 0) tmean[(size_t)p * stride + i] = __builtin_nan("");
         return;
     }
-    const int base = bounds_elo(dscale[p]) << 5;
+    const int base = bounds_elo(dscale[p]) << kMantBits;
     const int ba = bsel[((size_t)p * stride + i) * 2], bb = bsel[((size_t)p * stride + i) * 2 + 1];
     bool fast = ba > 0 && bb < kNB - 1 && ba <= bb;
     double sum = 0.0;
+    constexpr int NL = 1 << kLowBits;  // exact values per sub-bin
     uint32_t* cA = histA;        // level-2 counts of bin b_a
-    uint32_t* cB = histA + 512;  // of bin b_b (unused when b_a == b_b)
+    uint32_t* cB = histA + kNS;  // of bin b_b (unused when b_a == b_b)
     uint32_t* tA = histB;        // level-3 counts of the sub-bin holding rank lo
-    uint32_t* tB = histB + 512;  //                           and rank hi-1
+    uint32_t* tB = histB + NL;   //                           and rank hi-1
     if (fast) {
-        for (int k = tid; k < 512; k += 256) {
+        for (int k = tid; k < kNS; k += 256) {
             cA[k] = 0;
             cB[k] = 0;
-            tA[k] = 0;
-            tB[k] = 0;
             sA[k] = 0.0;
             sB[k] = 0.0;
+        }
+        for (int k = tid; k < NL; k += 256) {
+            tA[k] = 0;
+            tB[k] = 0;
         }
         __syncthreads();
         double acc = 0.0;
@@ -1578,13 +1626,13 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
         for (int j = tid; j < K; j += 256) {
             const float s = rdist2(xi, yi, zi, X[j], Y[j], Z[j]);
             const uint32_t key = __float_as_uint(s);
-            const int e = min(max((int)(key >> 18) - base, 0), kNB - 1);
+            const int e = min(max((int)(key >> kBinShift) - base, 0), kNB - 1);
             belowA += e < ba;
             belowB += e < bb;
             if (e > ba && e < bb) {
                 acc += (double)__builtin_sqrtf(s);
             } else if (e == ba || e == bb) {
-                const int sub = (int)((key >> 9) & 511u);
+                const int sub = (int)((key >> kLowBits) & (kNS - 1u));
                 const double d = (double)__builtin_sqrtf(s);
                 if (e == ba) {
                     atomicAdd(&cA[sub], 1u);
@@ -1601,37 +1649,40 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
         const uint32_t* cX = (ba == bb) ? cA : cB;
         const double* sX = (ba == bb) ? sA : sB;
         long befA, befB;
-        const int sa = find_bin<512>(cA, lo - cumA, &befA, ws, res);
-        const int sb = find_bin<512>(cX, hi - 1 - cumB, &befB, ws, res);
+        const int sa = find_bin<kNS>(cA, lo - cumA, &befA, ws, res);
+        const int sb = find_bin<kNS>(cX, hi - 1 - cumB, &befB, ws, res);
         fast = lo >= cumA && hi - 1 >= cumB && sa >= 0 && sb >= 0;  // uniform
         if (fast) {
-            const uint32_t prefA = ((uint32_t)(base + ba) << 9) | (uint32_t)sa;  // key >> 9
-            const uint32_t prefB = ((uint32_t)(base + bb) << 9) | (uint32_t)sb;
+            const uint32_t prefA = ((uint32_t)(base + ba) << kSubBits) | (uint32_t)sa;  // key >> kLowBits
+            const uint32_t prefB = ((uint32_t)(base + bb) << kSubBits) | (uint32_t)sb;
 #pragma unroll 4
             for (int j = tid; j < K; j += 256) {
                 const uint32_t key = __float_as_uint(rdist2(xi, yi, zi, X[j], Y[j], Z[j]));
-                if ((key >> 9) == prefA) atomicAdd(&tA[key & 511u], 1u);
-                if ((key >> 9) == prefB) atomicAdd(&tB[key & 511u], 1u);
+                if ((key >> kLowBits) == prefA) atomicAdd(&tA[key & (NL - 1u)], 1u);
+                if ((key >> kLowBits) == prefB) atomicAdd(&tB[key & (NL - 1u)], 1u);
             }
             __syncthreads();
             long befA3, befB3;
-            const int ta = find_bin<512>(tA, lo - cumA - befA, &befA3, ws, res);
-            const int tb = find_bin<512>(tB, hi - 1 - cumB - befB, &befB3, ws, res);
-            const uint32_t va = (prefA << 9) | (uint32_t)ta, vb = (prefB << 9) | (uint32_t)tb;
+            const int ta = find_bin<NL>(tA, lo - cumA - befA, &befA3, ws, res);
+            const int tb = find_bin<NL>(tB, hi - 1 - cumB - befB, &befB3, ws, res);
+            const uint32_t va = (prefA << kLowBits) | (uint32_t)ta;
+            const uint32_t vb = (prefB << kLowBits) | (uint32_t)tb;
             const long le_a = cumA + befA + befA3 + tA[ta];  // #keys <= va
             const long lt_b = cumB + befB + befB3;           // #keys <  vb
             // keys strictly between va and vb
             double part = 0.0;
-            for (int k = tid; k < 512; k += 256) {
-                const double dA = (double)__builtin_sqrtf(__uint_as_float((prefA << 9) | k));
-                const double dB = (double)__builtin_sqrtf(__uint_as_float((prefB << 9) | k));
+            for (int k = tid; k < kNS; k += 256) {  // whole sub-bins
                 if (ba != bb) {
                     if (k > sa) part += sA[k];
                     if (k < sb) part += sX[k];
-                    if (k > ta) part += (double)tA[k] * dA;
-                    if (k < tb) part += (double)tB[k] * dB;
                 } else if (sa != sb) {
                     if (k > sa && k < sb) part += sA[k];
+                }
+            }
+            for (int k = tid; k < NL; k += 256) {  // exact values inside the rank sub-bins
+                const double dA = (double)__builtin_sqrtf(__uint_as_float((prefA << kLowBits) | k));
+                const double dB = (double)__builtin_sqrtf(__uint_as_float((prefB << kLowBits) | k));
+                if (prefA != prefB) {
                     if (k > ta) part += (double)tA[k] * dA;
                     if (k < tb) part += (double)tB[k] * dB;
                 } else {
@@ -1650,6 +1701,23 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(const int32_t* __re
     }
     if (!fast) sum = radix_window_sum(X, Y, Z, K, xi, yi, zi, lo, hi, histA, histB, ws, res, red);
     if (tid == 0) tmean[(size_t)p * stride + i] = sum / ((double)(hi - lo) * 1.0);
+}
+
+__global__ __launch_bounds__(256) void consensus_rows_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv,
+    const float* __restrict__ dscale, int stride, double trim_lo, double trim_hi,
+    const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
+    const int32_t* __restrict__ bsel, double* __restrict__ tmean, int n_pairs) {
+    auto units = [&](int p) { return nsurv[p]; };
+    int total = 0;
+    for (int p = 0; p < n_pairs; p++) total += units(p);
+    for (int g = blockIdx.x; g < total; g += gridDim.x) {
+        int p, u;
+        item_to_pair(g, n_pairs, units, &p, &u);
+        __syncthreads();  // the previous row's LDS readers are done
+        consensus_rows_block(kcount, rv, dscale, stride, trim_lo, trim_hi, surv, nsurv, bsel,
+                             tmean, p, u);
+    }
 }
 
 // survivors: rows with LB <= min UB, in row order; pruned rows get tmean = +inf
@@ -2077,9 +2145,8 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
                                    const BatchShape& sh, double trim_lo, double trim_hi,
                                    const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
                                    double* lb, double* ub, hipStream_t st) {
-    dim3 grid((2 * sh.iters + kBoundRows - 1) / kBoundRows, sh.n_pairs);
-    hipLaunchKernelGGL(consensus_refine_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
-                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub);
+    hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
+                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, sh.n_pairs);
     return hipGetLastError();
 }
 
@@ -2087,9 +2154,8 @@ hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const f
                                  const BatchShape& sh, double trim_lo, double trim_hi,
                                  const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
                                  double* tmean, hipStream_t st) {
-    dim3 grid(2 * sh.iters, sh.n_pairs);
-    hipLaunchKernelGGL(consensus_rows_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
-                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, tmean);
+    hipLaunchKernelGGL(consensus_rows_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
+                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, tmean, sh.n_pairs);
     return hipGetLastError();
 }
 
