@@ -4,10 +4,11 @@
 Workload (BASELINE.json configs[1] shape): synthetic ERP pairs of 4096 x 4096 64-D SURF-like
 descriptors + keypoints (W x H = 5376 x 2688), exact k=2 + ratio-0.3 match -> gather ->
 eight_point::find with 10 000 initial_guess iterations (glibc-replay sampler, reference
-defaults otherwise).  A step = one erp_pair_batch_run over a batch of B such pairs resident
-in HBM; every step recomputes everything (no cached outputs).
+defaults otherwise).  A step = B such pairs resident in HBM, split into S independent
+sub-batches (own context + HIP stream each, so one sub-batch's latency-bound kernels overlap
+the other's); every step recomputes everything (no cached outputs).  Defaults B = 128, S = 1.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs B] [--iters I] [--kpts N]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs B] [--streams S] [--iters I]
 
 N > 1: launched by torch.distributed.run, one rank per GPU; each rank runs its own B pairs
 (weak scaling, independent pairs = the reference's per-pair process) and the per-pair result
@@ -38,14 +39,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs", type=int, default=8, help="pairs per step per GPU")
+    ap.add_argument("--pairs", type=int, default=128, help="pairs per step per GPU")
     ap.add_argument("--streams", type=int, default=1,
                     help="independent sub-batches (own context + HIP stream) per step")
     ap.add_argument("--iters", type=int, default=10000)
     ap.add_argument("--kpts", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=20200423)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--profile-tag", default="r01")
     return ap.parse_args()
 

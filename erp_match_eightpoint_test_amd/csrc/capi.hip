@@ -239,7 +239,7 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->wins, P * nwaves * 31 * 64 * 4) && ensure(c->polyR, P * 65 * 31 * 4) &&
               ensure(c->polyQ, P * erp::kMaxQ * 31 * 4) &&
               ensure(c->idx, P * nwaves * (size_t)sh.sel_words * 64 * 4) &&
-              ensure(c->gram, P * erp::gram_chunks_max(sh.max_nq) * sh.iters * 36 * 8) &&
+              ensure(c->gram, P * erp::gram_split(sh) * sh.iters * 36 * 8) &&
               ensure(c->gfin, P * sh.iters * 36 * 8) && ensure(c->rv, P * 6 * sh.iters * 4) &&
               ensure(c->kcount, P * 4) && ensure(c->sortbuf, P * (size_t)erp::sortbuf_len(sh.iters) * 4) &&
               ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result)) &&
@@ -303,7 +303,7 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
     }
     {
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
-        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, erp::gram_chunks_max(sh.max_nq), sh,
+        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, erp::gram_split(sh), sh,
                                  cfg->sample_frac, cfg->valid_abs, (double*)c->gfin.p, hyps, st));
     }
     return ERP_OK;

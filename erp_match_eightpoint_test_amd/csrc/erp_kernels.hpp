@@ -79,7 +79,8 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
                           const uint32_t* w0, const BatchShape& sh, double sample_frac,
                           uint32_t* wins, uint32_t* selw, int32_t* flags, hipStream_t st,
                           int part);
-int gram_chunks_max(int max_nq);  // partial-Gram chunks per iteration for max_nq rows
+int gram_chunks_max(int max_nq);  // Gram row chunks per iteration for max_nq rows
+int gram_split(const BatchShape& sh);  // partial Grams per iteration (chunks split over blocks)
 hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t* selw,
                        const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
                        hipStream_t st);

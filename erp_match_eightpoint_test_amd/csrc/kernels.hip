@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -719,13 +721,14 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     if (bad) atomicOr(&flags[p], 4);
 }
 
-// Gram of each iteration's s sampled rows, as partial sums over row chunks.  A block = 4
-// waves (256 iterations of one pair) x one chunk of kGramChunk selection words (31 rows
-// each): the chunk's rows (<= 620 x 48 B) are staged in LDS with coalesced loads, each
-// lane's selection words too, and every lane walks its own set bits with a cursor, reading
-// its rows from LDS (random 16-B global gathers per lane would be served one cache line at a
-// time).  Partial Grams gpart[p][chunk][36][iters] are summed in a fixed order by the eigen
-// kernels.  An exhausted lane reads the zero row (slot kGramRows).
+// Gram of each iteration's s sampled rows.  A block = 4 waves (256 iterations of one pair);
+// it walks row chunks of kGramChunk selection words (31 rows each): the chunk's rows (<= 620 x
+// 48 B) are staged in LDS with coalesced loads, each lane's selection words too, and every
+// lane walks its own set bits with a cursor, reading its rows from LDS (random 16-B global
+// gathers per lane would be served one cache line at a time).  When the batch is small the
+// chunks are split over csplit blocks (block cs takes chunks cs, cs + csplit, ...) and their
+// partial Grams gpart[p][cs][36][iters] are summed in a fixed order by the eigen kernels; for
+// large batches csplit = 1 and nothing is re-read.  An exhausted lane reads the zero row.
 constexpr int kGramChunk = 20;
 constexpr int kGramRows = kGramChunk * 31;
 
@@ -733,7 +736,7 @@ __device__ __forceinline__ int gram_chunks(int M) { return ((M - 1) / 31 + kGram
 
 __global__ __launch_bounds__(256) void gram_kernel(const int32_t* __restrict__ counts,
                                                    const double* __restrict__ pts, int max_nq,
-                                                   int iters, int nwaves, int nbw, int nchunk,
+                                                   int iters, int nwaves, int nbw, int csplit,
                                                    int idx_stride, double sample_frac,
                                                    const uint32_t* __restrict__ selw,
                                                    double* __restrict__ gpart,
@@ -741,75 +744,84 @@ __global__ __launch_bounds__(256) void gram_kernel(const int32_t* __restrict__ c
     __shared__ double2 rows[(kGramRows + 1) * 3];
     __shared__ uint32_t wds[kGramChunk * 256];
     const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
-    const int c = blockIdx.x % nchunk, wg = blockIdx.x / nchunk;
+    const int cs = blockIdx.x % csplit, wg = blockIdx.x / csplit;
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;
     const int nb = (M - 1) / 31 + 1;
-    const int b_lo = c * kGramChunk;
-    if (b_lo >= nb) return;  // uniform over the block
-    const int nw = min(b_lo + kGramChunk, nb) - b_lo;
-    const int i_hi = M - 1 - 31 * b_lo;          // row of slot 0 (slot = i_hi - i)
-    const int nrows = min(31 * nw, i_hi + 1);
+    if (cs * kGramChunk >= nb) return;  // uniform over the block (this partial is not read)
     const double2* P = reinterpret_cast<const double2*>(pts + (size_t)p * (max_nq + 1) * 6);
-    for (int t = tid; t < nrows * 3; t += 256) rows[t] = P[(size_t)(i_hi - t / 3) * 3 + t % 3];
-    if (tid < 3) rows[kGramRows * 3 + tid] = make_double2(0.0, 0.0);
     const int wv = wg * 4 + (tid >> 6);          // wave index of these 64 iterations
     const int h = wv * 64 + lane;
     const uint32_t* my = selw + ((size_t)p * nwaves + (wv < nwaves ? wv : 0)) * (size_t)nbw * 64 + lane;
-    int cnt = 0;
-    for (int k = 0; k < nw; k++) {
-        const uint32_t v = wv < nwaves ? my[(size_t)(b_lo + k) * 64] : 0u;
-        wds[k * 256 + tid] = v;
-        cnt += __builtin_popcount(v);
-    }
-    __syncthreads();
-    int mx = cnt;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
-    int before = 0;  // samples in earlier chunks (debug output only)
-    if (samples)
-        for (int k = 0; k < b_lo; k++) before += __builtin_popcount(wv < nwaves ? my[(size_t)k * 64] : 0u);
     double g[36];
 #pragma unroll
     for (int k = 0; k < 36; k++) g[k] = 0.0;
-    int wi = 0;
-    uint32_t cur = wds[tid];
-    constexpr int B = 4;
-    for (int k0 = 0; k0 < mx; k0 += B) {
-        int slot[B];
-#pragma unroll
-        for (int u = 0; u < B; u++) {
-            while (cur == 0u && wi + 1 < nw) {
-                wi++;
-                cur = wds[wi * 256 + tid];
-            }
-            slot[u] = kGramRows;
-            if (cur) {
-                slot[u] = 31 * wi + __builtin_ctz(cur);
-                cur &= cur - 1u;
-            }
+    int before = 0;  // samples in earlier chunks (debug output only)
+    if (samples)
+        for (int k = 0; k < cs * kGramChunk; k++)
+            before += __builtin_popcount(wv < nwaves ? my[(size_t)k * 64] : 0u);
+    for (int c = cs; c * kGramChunk < nb; c += csplit) {
+        const int b_lo = c * kGramChunk;
+        const int nw = min(b_lo + kGramChunk, nb) - b_lo;
+        const int i_hi = M - 1 - 31 * b_lo;      // row of slot 0 (slot = i_hi - i)
+        const int nrows = min(31 * nw, i_hi + 1);
+        __syncthreads();                         // previous chunk's LDS readers are done
+        for (int t = tid; t < nrows * 3; t += 256) rows[t] = P[(size_t)(i_hi - t / 3) * 3 + t % 3];
+        if (tid < 3) rows[kGramRows * 3 + tid] = make_double2(0.0, 0.0);
+        int cnt = 0;
+        for (int k = 0; k < nw; k++) {
+            const uint32_t v = wv < nwaves ? my[(size_t)(b_lo + k) * 64] : 0u;
+            wds[k * 256 + tid] = v;
+            cnt += __builtin_popcount(v);
         }
+        __syncthreads();
+        int mx = cnt;
 #pragma unroll
-        for (int u = 0; u < B; u++) {
-            const double2 a0 = rows[slot[u] * 3], a1 = rows[slot[u] * 3 + 1], a2 = rows[slot[u] * 3 + 2];
-            const double l0 = a0.x, l1 = a0.y, l2 = a1.x;
-            const double r0 = a1.y, r1 = a2.x, r2 = a2.y;
-            const double LL[6] = {l0 * l0, l0 * l1, l0 * l2, l1 * l1, l1 * l2, l2 * l2};
-            const double RR[6] = {r0 * r0, r0 * r1, r0 * r2, r1 * r1, r1 * r2, r2 * r2};
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+        int wi = 0;
+        uint32_t cur = wds[tid];
+        constexpr int B = 4;
+        for (int k0 = 0; k0 < mx; k0 += B) {
+            int slot[B];
 #pragma unroll
-            for (int a6 = 0; a6 < 6; a6++)
+            for (int u = 0; u < B; u++) {
+                while (cur == 0u && wi + 1 < nw) {
+                    wi++;
+                    cur = wds[wi * 256 + tid];
+                }
+                slot[u] = kGramRows;
+                if (cur) {
+                    slot[u] = 31 * wi + __builtin_ctz(cur);
+                    cur &= cur - 1u;
+                }
+            }
 #pragma unroll
-                for (int b6 = 0; b6 < 6; b6++)
-                    g[6 * a6 + b6] = __builtin_fma(LL[a6], RR[b6], g[6 * a6 + b6]);
+            for (int u = 0; u < B; u++) {
+                const double2 a0 = rows[slot[u] * 3], a1 = rows[slot[u] * 3 + 1], a2 = rows[slot[u] * 3 + 2];
+                const double l0 = a0.x, l1 = a0.y, l2 = a1.x;
+                const double r0 = a1.y, r1 = a2.x, r2 = a2.y;
+                const double LL[6] = {l0 * l0, l0 * l1, l0 * l2, l1 * l1, l1 * l2, l2 * l2};
+                const double RR[6] = {r0 * r0, r0 * r1, r0 * r2, r1 * r1, r1 * r2, r2 * r2};
+#pragma unroll
+                for (int a6 = 0; a6 < 6; a6++)
+#pragma unroll
+                    for (int b6 = 0; b6 < 6; b6++)
+                        g[6 * a6 + b6] = __builtin_fma(LL[a6], RR[b6], g[6 * a6 + b6]);
+            }
+            if (samples && h < iters)
+                for (int u = 0; u < B; u++)
+                    if (slot[u] != kGramRows && before + k0 + u < idx_stride)
+                        samples[((size_t)p * iters + h) * idx_stride + before + k0 + u] = i_hi - slot[u];
         }
-        if (samples && h < iters)
-            for (int u = 0; u < B; u++)
-                if (slot[u] != kGramRows && before + k0 + u < idx_stride)
-                    samples[((size_t)p * iters + h) * idx_stride + before + k0 + u] = i_hi - slot[u];
+        if (samples) {  // samples of the chunks between this one and the next one taken
+            before += cnt;
+            for (int k = b_lo + kGramChunk; k < min((c + csplit) * kGramChunk, nb); k++)
+                before += __builtin_popcount(wv < nwaves ? my[(size_t)k * 64] : 0u);
+        }
     }
-    if (h < iters) {  // [p][chunk][k][h]: coalesced over the lanes
-        double* go = gpart + ((size_t)p * nchunk + c) * 36 * iters + h;
+    if (h < iters) {  // [p][cs][k][h]: coalesced over the lanes
+        double* go = gpart + ((size_t)p * csplit + cs) * 36 * iters + h;
 #pragma unroll
         for (int k = 0; k < 36; k++) go[(size_t)k * iters] = g[k];
     }
@@ -2077,14 +2089,20 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
 
 int gram_chunks_max(int max_nq) { return ((max_nq + 30) / 31 + kGramChunk) / kGramChunk; }
 
+int gram_split(const BatchShape& sh) {
+    const int blocks = ((sh.iters + 255) / 256) * sh.n_pairs;
+    const int want = (2048 + blocks - 1) / blocks;  // enough blocks to fill the chip
+    return std::max(1, std::min(want, gram_chunks_max(sh.max_nq)));
+}
+
 hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t* selw,
                        const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
                        hipStream_t st) {
     const int nwaves = (sh.iters + 63) / 64;
-    const int nchunk = gram_chunks_max(sh.max_nq);
-    dim3 grid(((nwaves + 3) / 4) * nchunk, sh.n_pairs);
+    const int csplit = gram_split(sh);
+    dim3 grid(((nwaves + 3) / 4) * csplit, sh.n_pairs);
     hipLaunchKernelGGL(gram_kernel, grid, dim3(256), 0, st, counts, pts, sh.max_nq, sh.iters,
-                       nwaves, sh.sel_words, nchunk, sh.idx_stride, sample_frac, selw, gram,
+                       nwaves, sh.sel_words, csplit, sh.idx_stride, sample_frac, selw, gram,
                        samples);
     return hipGetLastError();
 }
