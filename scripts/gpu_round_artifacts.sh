@@ -15,3 +15,5 @@ echo "== rocprofv3 kernel-trace stats" && timeout -k 10 600 rocprofv3 --kernel-t
 echo "== pmc FETCH_SIZE" && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch_${TAG} -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/pmc_fetch_${TAG}.log 2>&1 || { tail -20 gpurun_out/pmc_fetch_${TAG}.log; exit 1; }
 echo "== pmc WRITE_SIZE" && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write_${TAG} -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/pmc_write_${TAG}.log 2>&1 || { tail -20 gpurun_out/pmc_write_${TAG}.log; exit 1; }
 find gpurun_out/prof_${TAG} gpurun_out/pmc_fetch_${TAG} gpurun_out/pmc_write_${TAG} -name "*.csv" | head -20
+# then, in the container: python scripts/pmc_summarize.py --tag $TAG --stats gpurun_out/prof_$TAG \
+#   --fetch gpurun_out/pmc_fetch_$TAG --write gpurun_out/pmc_write_$TAG   (-> profiles/)
