@@ -68,7 +68,7 @@ struct erp_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
-    DevBuf part, pu, ccount, cand, bsel, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
+    DevBuf part, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins;
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -157,7 +157,7 @@ erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
 erp_status erp_ctx_destroy(erp_ctx* ctx) {
     if (!ctx) return ERP_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    DevBuf* all[] = {&ctx->part, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->gfin,
+    DevBuf* all[] = {&ctx->part, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->edges, &ctx->gfin,
                      &ctx->matches,
                      &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
                      &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
@@ -240,12 +240,12 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->polyQ, P * erp::kMaxQ * 31 * 4) &&
               ensure(c->idx, P * nwaves * (size_t)sh.sel_words * 64 * 4) &&
               ensure(c->gram, P * erp::gram_split(sh) * sh.iters * 36 * 8) &&
-              ensure(c->gfin, P * sh.iters * 36 * 8) && ensure(c->rv, P * 6 * sh.iters * 4) &&
+              ensure(c->gfin, P * sh.iters * 9 * 8) && ensure(c->rv, P * 6 * sh.iters * 4) &&
               ensure(c->kcount, P * 4) && ensure(c->sortbuf, P * (size_t)erp::sortbuf_len(sh.iters) * 4) &&
               ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result)) &&
               ensure(c->dscale, P * 4) && ensure(c->lb, P * 2 * sh.iters * 8) &&
               ensure(c->ub, P * 2 * sh.iters * 8) && ensure(c->surv, P * 2 * sh.iters * 4) &&
-              ensure(c->bsel, P * 2 * sh.iters * 8) &&
+              ensure(c->bsel, P * 2 * sh.iters * 8) && ensure(c->edges, erp::consensus_edges_bytes((int)P)) &&
               ensure(c->nsurv, P * 4);
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
@@ -316,7 +316,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                          bool from_hyps) {
     erp_ctx* ctx = c;
     auto* counts = from_hyps ? (int32_t*)c->counts.p : nullptr;
-    auto* flags = from_hyps ? (int32_t*)c->flags.p : nullptr;
+    auto* flags = (int32_t*)c->flags.p;  // consensus-only: set by consensus_input (non-finite)
     auto* hyps = (out && out->hyps) ? out->hyps : (erp_hypothesis*)c->hyps.p;
     auto* tv = (out && out->tvec) ? out->tvec : (float*)c->tv.p;
     auto* tmean = (out && out->dist) ? out->dist : (double*)c->tmean.p;
@@ -329,7 +329,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
         ERP_CK(erp::launch_consensus_bounds((int32_t*)c->kcount.p, (float*)c->rv.p,
-                                            (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
+                                            (float*)c->dscale.p, (float*)c->edges.p, sh,
+                                            cfg->trim_lo, cfg->trim_hi,
                                             (double*)c->lb.p, (double*)c->ub.p,
                                             (int32_t*)c->bsel.p, st));
     }
@@ -593,7 +594,7 @@ erp_status erp_consensus_dev(erp_ctx* ctx, const float* d_rvec, const float* d_t
     if (es != ERP_OK) return es;
     ERP_CK(erp::launch_consensus_input(d_rvec, d_tvec, K, 2 * sh.iters, (float*)ctx->rv.p,
                                        (float*)ctx->tv.p, (int32_t*)ctx->kcount.p,
-                                       (float*)ctx->dscale.p, st));
+                                       (float*)ctx->dscale.p, (int32_t*)ctx->flags.p, st));
     return run_consensus(ctx, sh, &cfg, nullptr, d_result, st, false);
 }
 

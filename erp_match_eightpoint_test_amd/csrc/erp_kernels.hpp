@@ -85,20 +85,23 @@ hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t*
                        const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
                        hipStream_t st);
 // selected singular vector per iteration from the nchunk partial Grams gram[p][c][36][iters]
-// (summed into gfin[p][h][36], which then also holds the vector), then the estimate
-hipError_t launch_eigen(const int32_t* counts, const double* gram, int nchunk,
+// (summed in place into chunk 0), vectors to evec[p][9][iters], then the estimate
+hipError_t launch_eigen(const int32_t* counts, double* gram, int nchunk,
                         const BatchShape& sh, double sample_frac, double valid_abs,
-                        double* gfin, erp_hypothesis* hyps, hipStream_t st);
+                        double* evec, erp_hypothesis* hyps, hipStream_t st);
 hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyps,
                                 const BatchShape& sh, double sample_frac, float* rv, float* tv,
                                 int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st);
 hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream_t st);
 hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, int stride, float* rv,
-                                  float* tv, int32_t* kcount, float* dscale, hipStream_t st);
+                                  float* tv, int32_t* kcount, float* dscale, int32_t* flags,
+                                  hipStream_t st);
 // per-row [LB, UB] of the trimmed mean and the bins holding ranks lo / hi-1 (bsel[row][2])
+size_t consensus_edges_bytes(int n_pairs);
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
-                                   const BatchShape& sh, double trim_lo, double trim_hi, double* lb,
-                                   double* ub, int32_t* bsel, hipStream_t st);
+                                   float* edges, const BatchShape& sh, double trim_lo,
+                                   double trim_hi, double* lb, double* ub, int32_t* bsel,
+                                   hipStream_t st);
 // survivors = rows with LB <= min UB (again = 1: only pairs the refine pass touched)
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
                                    const BatchShape& sh, double trim_lo, double trim_hi,

@@ -865,40 +865,43 @@ __global__ __launch_bounds__(256) void gram_all_kernel(const double* __restrict_
 // estimate (rank-2 fix, decomposition, Euler angles) runs in estimate_kernel.
 template <bool THIN>
 __global__ __launch_bounds__(64) void eigen_kernel(const int32_t* __restrict__ counts,
-                                                   const double* __restrict__ gram, int iters,
+                                                   double* __restrict__ gram, int iters,
                                                    int nchunk, double sample_frac,
-                                                   double* __restrict__ gfin) {
+                                                   double* __restrict__ evec) {
     const int p = blockIdx.y;
     const int h = blockIdx.x * 64 + threadIdx.x;
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || h >= iters || (s < 9) != THIN) return;
     // gram[p][chunk][36][iters]: partial Grams of the row chunks, summed in chunk order into
-    // the iteration's own record gfin[p][h][36], which then also receives the vector
-    const double* gi = gram + (size_t)p * nchunk * 36 * iters + h;
-    double* gf = gfin + ((size_t)p * iters + h) * 36;
+    // chunk 0's slice (in place, coalesced over the lanes); the solve then reads the 36 values
+    // with stride iters and the vector goes to evec[p][9][iters]
+    double* gi = gram + (size_t)p * nchunk * 36 * iters + h;
     const int nc = min(nchunk, gram_chunks(M));
-    for (int k = 0; k < 36; k++) {
-        double v = gi[(size_t)k * iters];
-        for (int c = 1; c < nc; c++) v += gi[((size_t)c * 36 + k) * iters];
-        gf[k] = v;
+    if (nc > 1) {
+        for (int k = 0; k < 36; k++) {
+            double v = gi[(size_t)k * iters];
+            for (int c = 1; c < nc; c++) v += gi[((size_t)c * 36 + k) * iters];
+            gi[(size_t)k * iters] = v;
+        }
     }
     double e[9];
     if (THIN) {
         double g36[36], G[81];
 #pragma unroll
-        for (int k = 0; k < 36; k++) g36[k] = gf[k];
+        for (int k = 0; k < 36; k++) g36[k] = gi[(size_t)k * iters];
         gram36_to_full(g36, G);
         gram_jacobi9(G, s, e);
     } else {
-        gram_min_eigvec9(gf, 1, 0, e);
+        gram_min_eigvec9(gi, iters, 0, e);
     }
+    double* eo = evec + (size_t)p * 9 * iters + h;
 #pragma unroll
-    for (int k = 0; k < 9; k++) gf[k] = e[k];
+    for (int k = 0; k < 9; k++) eo[(size_t)k * iters] = e[k];
 }
 
 __global__ __launch_bounds__(64) void estimate_kernel(const int32_t* __restrict__ counts,
-                                                      const double* __restrict__ gfin, int iters,
+                                                      const double* __restrict__ evec, int iters,
                                                       double sample_frac, double valid_abs,
                                                       erp_hypothesis* __restrict__ hyps) {
     const int p = blockIdx.y;
@@ -906,10 +909,10 @@ __global__ __launch_bounds__(64) void estimate_kernel(const int32_t* __restrict_
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || h >= iters) return;
-    const double* gi = gfin + ((size_t)p * iters + h) * 36;
+    const double* ei = evec + (size_t)p * 9 * iters + h;
     double e[9];
 #pragma unroll
-    for (int k = 0; k < 9; k++) e[k] = gi[k];
+    for (int k = 0; k < 9; k++) e[k] = ei[(size_t)k * iters];
     Hyp hy;
     estimate_from_e(e, valid_abs, hy);
     erp_hypothesis* o = hyps + (size_t)p * iters + h;
@@ -1159,18 +1162,36 @@ __global__ __launch_bounds__(1024) void consensus_input_kernel(const float* __re
                                                                float* __restrict__ rv,
                                                                float* __restrict__ tv,
                                                                int32_t* __restrict__ kcount,
-                                                               float* __restrict__ dscale) {
+                                                               float* __restrict__ dscale,
+                                                               int32_t* __restrict__ flags) {
     __shared__ float red6[6][16];
+    __shared__ int bad;
+    if (threadIdx.x == 0) bad = 0;
+    __syncthreads();
     float mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+    bool fin = true;
     for (int k = threadIdx.x; k < K; k += 1024) {
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             const float v = rvec[3 * (size_t)k + c];
             rv[c * (size_t)stride + k] = v;
             tv[3 * (size_t)k + c] = tvec[3 * (size_t)k + c];
+            fin = fin && __builtin_isfinite(v);
             mn[c] = fminf(mn[c], v);
             mx[c] = fmaxf(mx[c], v);
         }
+    }
+    // a non-finite rotation vector has no place in the binned distance space (the pipeline's
+    // valid hypotheses are finite by construction: |Euler| < valid_abs): ERP_INVALID_ARG
+    if (!fin) bad = 1;
+    __syncthreads();
+    if (bad) {
+        if (threadIdx.x == 0) {
+            kcount[0] = 0;
+            dscale[0] = 1.f;
+            flags[0] = 8;
+        }
+        return;
     }
 #pragma unroll
     for (int c = 0; c < 3; c++) {
@@ -1199,35 +1220,46 @@ __global__ __launch_bounds__(1024) void consensus_input_kernel(const float* __re
         }
         dscale[0] = (float)(sqrt(d2) * (1.0 + 1e-6));
         kcount[0] = K;
+        flags[0] = 0;
     }
 }
 
 // ---- pruning by rigorous bounds -------------------------------------------------------
-// Every row's K squared distances are binned into NB geometric bins: 32 per binade of s = d^2
-// (= 64 per binade of the distance d) over the 40 binades of s below the squared diameter of
-// the set, underflow in bin 0.  The binned value is s' = fma(dz, dz, fma(dy, dy, dx * dx)),
-// within 2 * gamma_3 < 2^-21 (relative) of the reference's s = dx*dx + dy*dy + dz*dz (same dx,
-// dy, dz; all terms >= 0), and d = sqrtf(s) is monotone in s, so a value in bin
-// [E_b, E_b+1) has d in [sqrtf(E_b (1 - 2^-20)), sqrtf(E_b+1 (1 + 2^-20))].  From the exact
-// bin counts the trimmed sum over ranks [lo, hi) is bracketed by
+// Every row's K squared distances are binned into NB geometric bins: 16 per binade of s = d^2
+// (= 32 per binade of the distance d) over the 36 binades of s below the squared diameter of
+// the set, underflow in bin 0.  The binned value is s' = fma(dz, dz, fma(dy, dy, dx * dx)):
+// with S = dx^2 + dy^2 + dz^2 exactly (the reference's dx = fl(x_i - x_j), identical here), s'
+// is within (1 +- 3.0001 u) of S (three correctly rounded operations on non-negative terms,
+// u = 2^-24) and so is the reference's s = dx*dx + dy*dy + dz*dz, so s' in bin [E_b, E_b+1)
+// puts the reference's d = sqrtf(s) in
+//   [sqrt(E_b (1 - 2^-20)) (1 - 2^-20), sqrt(E_b+1 (1 + 2^-20)) (1 + 2^-20)]
+// (the 2^-20 factors absorb the 6u of both roundings and sqrtf).  From the exact bin counts
+// the trimmed sum over ranks [lo, hi) is bracketed by
 //   LB = sum_b n_b(window) * lower_b,  UB = sum_b n_b(window) * upper_b
-// (relative width <= 2^-6).  A row whose LB exceeds the smallest UB cannot be the argmin; only
-// the survivors get the exact order statistics.  No square root in the K^2 loop.
-// Block = 8 rows x 256 columns at a time; lane l takes row (l + t) & 7 at step t, so one
-// atomic wave-instruction spreads over 8 rows (same-address conflicts <= 8-way instead of
-// 64-way for a concentrated row), and the row stride (== 4 mod 32 words) puts the same bin of
-// different rows in different banks.
-constexpr int kBoundRows = 8;
+// (relative width <= 2^-5; valid because the bins are ordered: the order statistics of the
+// per-element lower bounds lower_bin(e) <= d_e are <= those of d).  A row whose LB exceeds the
+// smallest UB cannot be the argmin; only the survivors get the exact order statistics.  No
+// square root in the K^2 loop.
+// Block = 16 rows x 256 columns at a time.  The histograms are laid out [bin][row] (one 4-B
+// word per (bin, row)), so row r's bins all live in LDS banks r and r + 16; at step t lane l
+// takes row (l + t) & 15, so the 32 lanes of an LDS lane group hit each row twice and collide
+// at most 2-way (a random scatter of 32 lanes over 32 banks, the [row][bin] layout, costs ~3.5x:
+// that was 2/3 of the kernel's LDS time).  Rows t, t+1 share packed f32 instructions
+// (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 with the column broadcast), the key is clamped
+// to the first bin (v_max_u32) and the LDS byte address is one v_lshl_add_u32 of it: six VALU
+// instructions and one ds_add_u32 per distance.  Four
+// blocks (39 KB of histograms each) per CU.  The d-space bin edges are per pair
+// (consensus_edges_kernel); the epilogue holds its slice's edges in registers.
+constexpr int kBoundRows = 16;       // rows per bounds block
 constexpr int kBinShift = 19;         // bin = key >> 19: 16 bins per binade of s = d^2
 constexpr int kMantBits = 23 - kBinShift;
 constexpr int kBinsPerBinade = 1 << kMantBits;  // (= 32 per binade of the distance)
-constexpr int kBinades = 40;          // of s
-constexpr int kNB = kBinsPerBinade * kBinades;  // 640
+constexpr int kBinades = 36;          // of s (576 bins: 4 blocks of 39 KB per CU)
+constexpr int kNB = kBinsPerBinade * kBinades;  // 576
 constexpr int kSubBits = 10;          // 1024 sub-bins per bin (refine / exact pass) ...
 constexpr int kNS = 1 << kSubBits;
 constexpr int kLowBits = kBinShift - kSubBits;  // ... and below them the exact values
 constexpr int kRefineRows = 4;        // rows per refine block
-constexpr int kHistStride = kNB + 4;
 constexpr int kRefineMin = 32;   // survivors per pair below which refining does not pay
 
 // first s-binade of the bins: the 40 binades ending with the one holding D^2 (D = dscale is
@@ -1243,102 +1275,160 @@ __device__ __forceinline__ float bin_edge_s(int elo, int e) {
     return __uint_as_float((uint32_t)((elo << kMantBits) + e) << kBinShift);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// (key << 2) + base as ONE v_lshl_add_u32 (the compiler otherwise rewrites (x >> 19) << 2 as
+// (x >> 17) & ~3 and adds: three instructions in the K^2 loop)
+__device__ __forceinline__ uint32_t lshl2_add(uint32_t key, uint32_t base) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 2, %2" : "=v"(r) : "v"(key), "v"(base));
+    return r;
+}
+__device__ __forceinline__ void lds_inc(uint32_t byte_addr) {
+    __hip_atomic_fetch_add((lds_u32*)(size_t)byte_addr, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// d-space bounds of the reference's d for a key in bin b (header comment above), in f32:
+// E_b (1 -+ 2^-20) rounds by <= u, sqrtf adds u, the final product u: <= 3u < 2^-19, so the
+// (1 -+ 2^-19) factors keep the bounds outward.  Bin 0 also holds every s below E_1.
+__device__ __forceinline__ float bin_lower_d(int elo, int b) {
+    if (b == 0) return 0.f;
+    return __builtin_sqrtf(bin_edge_s(elo, b) * (1.0f - 0x1p-20f)) * (1.0f - 0x1p-19f);
+}
+__device__ __forceinline__ float bin_upper_d(int elo, int b) {
+    if (b == kNB - 1) return kInf;
+    return __builtin_sqrtf(bin_edge_s(elo, b + 1) * (1.0f + 0x1p-20f)) * (1.0f + 0x1p-19f);
+}
+
+// lshl_add with shift 6: the [bin][16 rows] histogram address (bin * 64 + row * 4 + base)
+__device__ __forceinline__ uint32_t lshl6_add(uint32_t key, uint32_t base) {
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 6, %2" : "=v"(r) : "v"(key), "v"(base));
+    return r;
+}
+
+// d-space bounds of the bins of pair p (the same for every block of the pair):
+// edges[p][0][b] = lower bound, edges[p][1][b] = upper bound of the reference's d in bin b
+__global__ __launch_bounds__(256) void consensus_edges_kernel(const float* __restrict__ dscale,
+                                                              float* __restrict__ edges) {
+    const int p = blockIdx.x;
+    const int elo = bounds_elo(dscale[p]);
+    float* ed = edges + (size_t)p * 2 * kNB;
+    for (int b = threadIdx.x; b < kNB; b += 256) {
+        ed[b] = bin_lower_d(elo, b);
+        ed[kNB + b] = bin_upper_d(elo, b);
+    }
+}
+
 __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __restrict__ kcount,
                                                                const float* __restrict__ rv,
                                                                const float* __restrict__ dscale,
+                                                               const float* __restrict__ edges,
                                                                int stride, double trim_lo,
                                                                double trim_hi,
                                                                double* __restrict__ lb,
                                                                double* __restrict__ ub,
                                                                int32_t* __restrict__ bsel) {
-    __shared__ __align__(16) uint32_t hist[kBoundRows * kHistStride];
-    __shared__ float elow[kNB], eupp[kNB];  // d-space bounds of each bin
+    constexpr int R = kBoundRows;
+    constexpr int NS = 256 / R;        // epilogue slices per row
+    constexpr int per = kNB / NS;      // bins per slice
+    static_assert(kNB % NS == 0, "slices");
+    __shared__ __align__(16) uint32_t hist[kNB * R];  // [bin][row]
+    __shared__ int part[NS][R];                       // per-slice counts
+    __shared__ float partL[NS][R], partU[NS][R];
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
-    const int r0 = blockIdx.x * kBoundRows;
+    const int r0 = blockIdx.x * R;
     if (r0 >= K) return;
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
     const int elo = bounds_elo(dscale[p]);
     const int base = elo << kMantBits;
-    float xi[kBoundRows], yi[kBoundRows], zi[kBoundRows];
-    int hoff[kBoundRows];
+    constexpr int kPairs = R / 2;
+    f32x2 xi[kPairs], yi[kPairs], zi[kPairs];
+    uint32_t hoff[R];  // LDS byte address of (bin 0 - base, row)
+    const uint32_t hist_addr = (uint32_t)(size_t)(lds_u32*)hist;
 #pragma unroll
-    for (int t = 0; t < kBoundRows; t++) {
-        const int r = (lane + t) & (kBoundRows - 1);
+    for (int t = 0; t < R; t++) {
+        const int r = (lane + t) & (R - 1);
         const int row = min(r0 + r, K - 1);
-        xi[t] = X[row];
-        yi[t] = Y[row];
-        zi[t] = Z[row];
-        hoff[t] = r * kHistStride - base;  // hist index = hoff + clamp(key, base, base+NB-1)
+        xi[t >> 1][t & 1] = X[row];
+        yi[t >> 1][t & 1] = Y[row];
+        zi[t >> 1][t & 1] = Z[row];
+        hoff[t] = hist_addr + 4u * (uint32_t)r - 64u * (uint32_t)base;
     }
-    for (int k = tid; k < kBoundRows * kHistStride / 4; k += 256)
+    for (int k = tid; k < kNB * R / 4; k += 256)
         reinterpret_cast<uint4*>(hist)[k] = make_uint4(0u, 0u, 0u, 0u);
-    for (int b = tid; b < kNB; b += 256) {
-        elow[b] = b == 0 ? 0.f : __builtin_sqrtf(bin_edge_s(elo, b) * (1.0f - 0x1p-20f));
-        eupp[b] = b == kNB - 1 ? kInf : __builtin_sqrtf(bin_edge_s(elo, b + 1) * (1.0f + 0x1p-20f));
-    }
     __syncthreads();
-    const int bmax = base + kNB - 1;
-    // columns prefetched two iterations ahead (the loop body is shorter than an L2 round trip)
-    float xa = 0.f, ya = 0.f, za = 0.f, xb = 0.f, yb = 0.f, zb = 0.f;
-    if (tid < K) {
-        xa = X[tid];
-        ya = Y[tid];
-        za = Z[tid];
+    const uint32_t ubase = (uint32_t)base;  // keys below the first bin go to bin 0
+    // columns in batches of 4 per lane (j0 + 256 c + tid, c < 4: every load coalesced), the next
+    // batch loaded while this one is binned (4 x 32 distances of VALU work hide the L2 latency)
+    constexpr int CB = 4;
+    float cx[CB], cy[CB], cz[CB], nx[CB], ny[CB], nz[CB];
+#pragma unroll
+    for (int c = 0; c < CB; c++) {
+        const int j = min(c * 256 + tid, K - 1);
+        cx[c] = X[j];
+        cy[c] = Y[j];
+        cz[c] = Z[j];
     }
-    if (tid + 256 < K) {
-        xb = X[tid + 256];
-        yb = Y[tid + 256];
-        zb = Z[tid + 256];
-    }
-    for (int j = tid; j < K; j += 256) {
-        const float xj = xa, yj = ya, zj = za;
-        xa = xb;
-        ya = yb;
-        za = zb;
-        if (j + 512 < K) {
-            xb = X[j + 512];
-            yb = Y[j + 512];
-            zb = Z[j + 512];
+    for (int j0 = 0; j0 < K; j0 += CB * 256) {
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            const int j = min(j0 + CB * 256 + c * 256 + tid, K - 1);
+            nx[c] = X[j];
+            ny[c] = Y[j];
+            nz[c] = Z[j];
         }
 #pragma unroll
-        for (int t = 0; t < kBoundRows; t++) {
-            const float dx = xi[t] - xj, dy = yi[t] - yj, dz = zi[t] - zj;
-            const float s = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
-            const int key = (int)(__float_as_uint(s) >> kBinShift);
-            atomicAdd(&hist[hoff[t] + min(max(key, base), bmax)], 1u);
+        for (int c = 0; c < CB; c++) {
+            if (j0 + c * 256 + tid < K) {
+                const float xj = cx[c], yj = cy[c], zj = cz[c];
+#pragma unroll
+                for (int t = 0; t < kPairs; t++) {
+                    const f32x2 dx = xi[t] - xj, dy = yi[t] - yj, dz = zi[t] - zj;
+                    f32x2 s = dx * dx;
+                    s = __builtin_elementwise_fma(dy, dy, s);
+                    s = __builtin_elementwise_fma(dz, dz, s);
+                    const uint32_t k0 = max(__float_as_uint(s[0]) >> kBinShift, ubase);
+                    const uint32_t k1 = max(__float_as_uint(s[1]) >> kBinShift, ubase);
+                    lds_inc(lshl6_add(k0, hoff[2 * t]));
+                    lds_inc(lshl6_add(k1, hoff[2 * t + 1]));
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            cx[c] = nx[c];
+            cy[c] = ny[c];
+            cz[c] = nz[c];
         }
     }
     __syncthreads();
-    // per row: 32 threads x 40 bins.  Window-clipped counts w_b = clip(cum_b + n_b) -
-    // clip(cum_b) (clip to [lo, hi]); L, U accumulate w_b * edge in f32 (<= 1280 non-negative
-    // terms: relative error < 1280 * 2^-24, covered by the 2e-4 margins below).
+    // per row: NS slices of `per` consecutive bins, thread = slice * R + row; the slice's bin
+    // counts and edges in registers.  Window-clipped counts w_b = clip(cum_b + n_b) -
+    // clip(cum_b) (clip to [lo, hi]); L, U accumulate w_b * edge in f32 (<= kNB non-negative
+    // terms: relative error < kNB * 2^-24, covered by the 2e-4 margins below).
     const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
-    const int r = tid >> 5, sl = tid & 31;
-    constexpr int per = kNB / 32;
-    const uint32_t* h = hist + r * kHistStride + sl * per;
-    uint32_t n[per];
-#pragma unroll
-    for (int q = 0; q < per / 4; q++) {
-        const uint4 v = reinterpret_cast<const uint4*>(h)[q];
-        n[4 * q] = v.x;
-        n[4 * q + 1] = v.y;
-        n[4 * q + 2] = v.z;
-        n[4 * q + 3] = v.w;
-    }
+    const int r = tid & (R - 1), sl = tid / R;
+    const float* ed = edges + (size_t)p * 2 * kNB + sl * per;
+    float el[per], eu[per];
+    int n[per];
     int c = 0;
 #pragma unroll
-    for (int q = 0; q < per; q++) c += (int)n[q];
-    // exclusive scan over the 32 lanes of this row (within one wave half)
-    int x = c;
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-        const int y = __shfl_up(x, o, 32);
-        if (sl >= o) x += y;
+    for (int q = 0; q < per; q++) {
+        el[q] = ed[q];
+        eu[q] = ed[kNB + q];
+        n[q] = (int)hist[(sl * per + q) * R + r];
+        c += n[q];
     }
-    int cum = x - c;
+    part[sl][r] = c;
+    __syncthreads();
+    int cum = 0;
+    for (int q = 0; q < sl; q++) cum += part[q][r];
     const int row = r0 + r;
     float L = 0.f, U = 0.f;
     int sel_a = -1, sel_b = -1;  // bins holding ranks lo and hi-1 (for the exact pass)
@@ -1346,14 +1436,13 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
         int c0 = min(max(cum, lo), hi);
 #pragma unroll
         for (int q = 0; q < per; q++) {
-            const int b = sl * per + q;
-            const int nc = cum + (int)n[q];
+            const int nc = cum + n[q];
             const int c1 = min(max(nc, lo), hi);
             const float w = (float)(c1 - c0);
-            L = __builtin_fmaf(w, elow[b], L);
-            U = __builtin_fmaf(w, eupp[b], U);
-            sel_a = (cum <= lo && lo < nc) ? b : sel_a;
-            sel_b = (cum <= hi - 1 && hi - 1 < nc) ? b : sel_b;
+            L = __builtin_fmaf(w, el[q], L);
+            U = __builtin_fmaf(w, eu[q], U);
+            sel_a = (cum <= lo && lo < nc) ? sl * per + q : sel_a;
+            sel_b = (cum <= hi - 1 && hi - 1 < nc) ? sl * per + q : sel_b;
             cum = nc;
             c0 = c1;
         }
@@ -1362,12 +1451,14 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
         if (sel_a >= 0) bsel[((size_t)p * stride + row) * 2] = sel_a;
         if (sel_b >= 0) bsel[((size_t)p * stride + row) * 2 + 1] = sel_b;
     }
-#pragma unroll
-    for (int o = 16; o > 0; o >>= 1) {
-        L += __shfl_xor(L, o, 32);
-        U += __shfl_xor(U, o, 32);
-    }
+    partL[sl][r] = L;
+    partU[sl][r] = U;
+    __syncthreads();
     if (sl == 0 && row < K) {
+        for (int q = 1; q < NS; q++) {
+            L += partL[q][r];
+            U += partU[q][r];
+        }
         const double w = (double)(hi - lo);
         // margins: the f32 accumulation above and the reference's own rounding of its sorted
         // sequential sum
@@ -1848,6 +1939,8 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     r.min_dist = 0.0;
     const int fl = flags ? flags[p] : 0;
     if (fl & 1) r.status = ERP_TOO_FEW_POINTS;
+    else if (fl & 8)
+        r.status = ERP_INVALID_ARG;
     else if (fl & 6)
         r.status = ERP_INTERNAL;
     else if (s < 1)
@@ -2112,16 +2205,16 @@ hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream
     return hipGetLastError();
 }
 
-hipError_t launch_eigen(const int32_t* counts, const double* gram, int nchunk,
+hipError_t launch_eigen(const int32_t* counts, double* gram, int nchunk,
                         const BatchShape& sh, double sample_frac, double valid_abs,
-                        double* gfin, erp_hypothesis* hyps, hipStream_t st) {
+                        double* evec, erp_hypothesis* hyps, hipStream_t st) {
     dim3 grid((sh.iters + 63) / 64, sh.n_pairs);
     hipLaunchKernelGGL(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters, nchunk,
-                       sample_frac, gfin);
+                       sample_frac, evec);
     // (M is only known on the device: the thin instantiation returns at once for s >= 9)
     hipLaunchKernelGGL(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters, nchunk,
-                       sample_frac, gfin);
-    hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, gfin, sh.iters,
+                       sample_frac, evec);
+    hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
                        sample_frac, valid_abs, hyps);
     return hipGetLastError();
 }
@@ -2135,17 +2228,22 @@ hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyp
 }
 
 hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, int stride, float* rv,
-                                  float* tv, int32_t* kcount, float* dscale, hipStream_t st) {
+                                  float* tv, int32_t* kcount, float* dscale, int32_t* flags,
+                                  hipStream_t st) {
     hipLaunchKernelGGL(consensus_input_kernel, dim3(1), dim3(1024), 0, st, rvec, tvec, K, stride, rv,
-                       tv, kcount, dscale);
+                       tv, kcount, dscale, flags);
     return hipGetLastError();
 }
 
+size_t consensus_edges_bytes(int n_pairs) { return (size_t)n_pairs * 2 * kNB * sizeof(float); }
+
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
-                                   const BatchShape& sh, double trim_lo, double trim_hi, double* lb,
-                                   double* ub, int32_t* bsel, hipStream_t st) {
+                                   float* edges, const BatchShape& sh, double trim_lo,
+                                   double trim_hi, double* lb, double* ub, int32_t* bsel,
+                                   hipStream_t st) {
+    hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     dim3 grid((2 * sh.iters + kBoundRows - 1) / kBoundRows, sh.n_pairs);
-    hipLaunchKernelGGL(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
+    hipLaunchKernelGGL(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale, edges,
                        2 * sh.iters, trim_lo, trim_hi, lb, ub, bsel);
     return hipGetLastError();
 }

@@ -401,3 +401,44 @@ def test_consensus_survivor_means_bimodal_pair(ctx, oracle):
     assert live.sum() == res["survivors"]
     assert np.all(dref[~live] >= dref.min())
     assert np.allclose(d[live], dref[live], rtol=1e-12, atol=0)
+
+
+def test_consensus_nonfinite_input_is_invalid_arg(ctx):
+    """a NaN / inf rotation vector handed to the consensus-only entry is rejected
+    (ERP_INVALID_ARG) instead of being binned."""
+    from erp_match_eightpoint_test_amd import dist as D
+    rng = np.random.default_rng(5)
+    for bad in (np.nan, np.inf, -np.inf):
+        rv = (rng.standard_normal((300, 3)) * 0.01).astype(np.float32)
+        rv[137, 1] = bad
+        res = D.gpu_consensus(ctx, "cuda")(rv, np.zeros_like(rv))
+        assert res["status"] == 1, res
+    rv = (rng.standard_normal((300, 3)) * 0.01).astype(np.float32)  # the context recovers
+    assert D.gpu_consensus(ctx, "cuda")(rv, np.zeros_like(rv))["status"] == 0
+
+
+@pytest.mark.parametrize("case", ["wide_range", "dup_block", "tiny_cluster"])
+def test_consensus_bounds_wide_dynamic_range(ctx, oracle, case):
+    """binned-distance bounds when the window's ranks sit in the lowest binades of the
+    40-binade range (tight cluster + rotations near the validity limit, many exact duplicates):
+    the winner and every survivor's mean stay exact."""
+    from erp_match_eightpoint_test_amd import dist as D
+    rng = np.random.default_rng({"wide_range": 1, "dup_block": 2, "tiny_cluster": 3}[case])
+    K = 2500
+    if case == "wide_range":
+        rv = rng.standard_normal((K, 3)) * 1e-5 + 0.3
+        far = rng.choice(K, 40, replace=False)
+        rv[far] = rng.uniform(-1.56, 1.56, (40, 3))
+    elif case == "dup_block":
+        rv = rng.standard_normal((K, 3)) * 2e-3
+        rv[rng.choice(K, 900, replace=False)] = rv[7]
+        rv[rng.choice(K, 30, replace=False)] = rng.uniform(-1.5, 1.5, (30, 3))
+    else:
+        rv = rng.standard_normal((K, 3)) * 1e-7 + np.array([1.0, -0.5, 0.25])
+    rv = rv.astype(np.float32)
+    tv = rng.standard_normal((K, 3)).astype(np.float32)
+    _, mi, dref = oracle.consensus(rv)
+    res = D.gpu_consensus(ctx, "cuda")(rv, tv)
+    assert res["status"] == 0 and res["K"] == K
+    assert res["min_idx"] == mi or np.array_equal(rv[res["min_idx"]], rv[mi])
+    assert abs(res["min_dist"] - dref[mi]) <= 1e-12 * abs(dref[mi])
