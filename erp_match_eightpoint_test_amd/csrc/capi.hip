@@ -69,7 +69,9 @@ struct erp_ctx {
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
     DevBuf part, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
-        sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins;
+        sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
+        rtab;
+    bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
     uint64_t w0_offset = 0;
@@ -163,7 +165,8 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
                      &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
-                     &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins};
+                     &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins,
+                     &ctx->rtab};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
@@ -250,7 +253,19 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
     if (ok && !(out && out->dist)) ok = ensure(c->tmean, P * 2 * sh.iters * 8);
-    return ok ? ERP_OK : ERP_OUT_OF_MEMORY;
+    if (!ok) return ERP_OUT_OF_MEMORY;
+    if (!c->rtab_valid) {  // once per context: the reciprocal table, verified exactly
+        constexpr int n = erp::kRecipTable;
+        if (!ensure(c->rtab, (size_t)n * 8 + 8)) return ERP_OUT_OF_MEMORY;
+        int32_t* d_bad = (int32_t*)((char*)c->rtab.p + (size_t)n * 8);
+        ERP_CK(hipMemset(d_bad, 0, 4));
+        ERP_CK(erp::launch_recip_table(n, (double*)c->rtab.p, d_bad, nullptr));
+        int32_t bad = 0;
+        ERP_CK(hipMemcpy(&bad, d_bad, 4, hipMemcpyDeviceToHost));
+        if (bad) return ERP_INTERNAL;
+        c->rtab_valid = true;
+    }
+    return ERP_OK;
 }
 
 erp_status upload_w0(erp_ctx* c, const erp_ransac_cfg* cfg, hipStream_t st) {
@@ -286,14 +301,14 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
     {
         StageTimer _t(ctx, ERP_STAGE_WINDOWS, st);
         ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
-                                   (uint32_t*)c->w0.p, sh, cfg->sample_frac, (uint32_t*)c->wins.p,
-                                   (uint32_t*)c->idx.p, flags, st, 0));
+                                   (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
+                                   (uint32_t*)c->wins.p, (uint32_t*)c->idx.p, flags, st, 0));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
         ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
-                                   (uint32_t*)c->w0.p, sh, cfg->sample_frac, (uint32_t*)c->wins.p,
-                                   (uint32_t*)c->idx.p, flags, st, 1));
+                                   (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
+                                   (uint32_t*)c->wins.p, (uint32_t*)c->idx.p, flags, st, 1));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_GRAM, st);

@@ -77,8 +77,12 @@ hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_
 // part 0: lane end windows (jump-ahead); part 1: the backwards replay -> selection bitmaps
 hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
                           const uint32_t* w0, const BatchShape& sh, double sample_frac,
-                          uint32_t* wins, uint32_t* selw, int32_t* flags, hipStream_t st,
-                          int part);
+                          const double* rtab, uint32_t* wins, uint32_t* selw, int32_t* flags,
+                          hipStream_t st, int part);
+// rtab[d] = 1/d rounded up, d < kRecipTable (the sampler's exact modulo); *bad counts entries
+// whose one-sided error bound fails (never, by construction; checked once per context)
+constexpr int kRecipTable = 65538;
+hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st);
 int gram_chunks_max(int max_nq);  // Gram row chunks per iteration for max_nq rows
 int gram_split(const BatchShape& sh);  // partial Grams per iteration (chunks split over blocks)
 hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t* selw,

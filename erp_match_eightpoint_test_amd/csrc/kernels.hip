@@ -584,12 +584,14 @@ __global__ __launch_bounds__(64) void sampler_window_kernel(
 }
 
 // exact j = x mod d for x < 2^31, 2 <= d <= 65536, from r = 1/d rounded UP to within
-// 2^-32 relative (rup_recip; both conditions are checked exactly with an fma residual and a
-// violation raises flag 4).  Then x*r >= x/d, and x*r - x/d < 2^-1/d, so trunc(fl(x*r)) =
-// floor(x/d): for an exact multiple k*d, fl(x*r) >= k (rounding is monotone and k is
-// representable); otherwise x/d <= k + 1 - 1/d leaves a margin far above the error.  The
-// remainder fma(-q, d, x) is then exact.  Everything stays in VALU (no SMEM/LDS table: their
-// lgkmcnt waits would also drain the replay's in-flight LDS atomics).
+// 2^-32 relative (rup_recip; both conditions are checked exactly with an fma residual when the
+// table is built, recip_table_kernel).  Then x*r >= x/d, and x*r - x/d < 2^-1/d, so
+// trunc(fl(x*r)) = floor(x/d): for an exact multiple k*d, fl(x*r) >= k (rounding is monotone
+// and k is representable); otherwise x/d <= k + 1 - 1/d leaves a margin far above the error.
+// The remainder x - q*d is then exact: fma(-q, d, x) in fp64, or for d >= 256 (q < 2^23) one
+// v_mad_i32_i24.  The reciprocals come from a table indexed by the step (uniform across the
+// wave): scalar loads, issued one block ahead, whose lgkmcnt wait coincides with the block's
+// own wait for its LDS atomics.
 __device__ __forceinline__ double rup_recip(double dd, bool* bad) {
     const double r0 = __builtin_amdgcn_rcp(dd);
     double r = __builtin_fma(r0, __builtin_fma(-dd, r0, 1.0), r0);
@@ -599,17 +601,27 @@ __device__ __forceinline__ double rup_recip(double dd, bool* bad) {
     return r;
 }
 
+// rtab[d] = rup_recip(d), d = 0 .. n-1 (entries 0, 1 unused: 1.0); *bad counts violations
+__global__ __launch_bounds__(256) void recip_table_kernel(int n, double* __restrict__ rtab,
+                                                          int32_t* __restrict__ bad) {
+    const int d = blockIdx.x * 256 + threadIdx.x;
+    if (d >= n) return;
+    bool b = false;
+    rtab[d] = d >= 2 ? rup_recip((double)d, &b) : 1.0;
+    if (b) atomicAdd(bad, 1);
+}
+
 __device__ __forceinline__ uint32_t mod_rup(uint32_t x, double r, double dd) {
     const double xd = (double)x;
     const double q = __builtin_trunc(xd * r);
     return (uint32_t)(int32_t)__builtin_fma(-q, dd, xd);
 }
-
-__device__ __forceinline__ double bcast_f64(double v, int u) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, u);
-    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), u);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+// d >= 256: q = floor(x/d) < 2^23, so x - q*d is one 24-bit multiply-add
+__device__ __forceinline__ uint32_t mod_rup_i24(uint32_t x, double r, int d) {
+    const int q = (int)((double)x * r);  // v_cvt_i32_f64 truncates
+    int j;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(j) : "v"(q), "s"(-d), "v"(x));
+    return (uint32_t)j;
 }
 
 // One block of 31 reverse steps i0, i0-1, ..., i0-30 of one lane's replay (ring = the 31-word
@@ -622,11 +634,12 @@ __device__ __forceinline__ double bcast_f64(double v, int u) {
 // reverse-step set T of the header comment is the complement.)  The atomics' old values are
 // consumed after the block, so the LDS traffic streams without waits; MODE 1/2 read bm[i] from
 // registers mirroring the (at most two) words holding i0-30..i0.
-template <int MODE>
+template <int MODE, bool I24>
 __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t* bm, int lane,
-                                                 int i0, int s, bool* bad) {
-    const int il = i0 - (lane < 31 ? lane : 0);
-    const double rl = rup_recip((double)(il >= 1 ? il + 1 : 2), bad);
+                                                 int i0, int s, const double* __restrict__ rtab) {
+    double rt[31];  // 1/(i+1) of the block's steps: scalar loads (uniform index)
+#pragma unroll
+    for (int u = 0; u < 31; u++) rt[u] = rtab[max(i0 - u, 1) + 1];
     int wA = 0, wB = 0;
     uint32_t curA = 0, curB = 0;
     if (MODE != 0) {
@@ -643,8 +656,8 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
         const uint32_t rv = ring[slot];
         ring[slot] = rv - ring[(slot + 28) % 31];
         const bool live = MODE != 2 || ii >= 1;
-        const double dd = (double)(live ? ii + 1 : 2);
-        const uint32_t j = mod_rup(rv >> 1, bcast_f64(rl, u), dd);
+        const int d = live ? ii + 1 : 2;
+        const uint32_t j = I24 ? mod_rup_i24(rv >> 1, rt[u], d) : mod_rup(rv >> 1, rt[u], (double)d);
         const uint32_t bit = 1u << (j & 31);
         const bool isB = MODE == 1 || (MODE == 2 && ii < s);
         if (MODE == 0) {
@@ -679,7 +692,8 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
 // sel[p][w][b][lane] bit u <-> index i = M-1-31b-u (b = 0 .. (M-1)/31), exactly s bits set.
 __global__ __launch_bounds__(64) void sampler_kernel(
     const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins, int nwaves, int nbw,
-    double sample_frac, uint32_t* __restrict__ selw, int32_t* __restrict__ flags) {
+    double sample_frac, const double* __restrict__ rtab, uint32_t* __restrict__ selw,
+    int32_t* __restrict__ flags) {
     extern __shared__ uint32_t bm[];  // [nwords][64]
     const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
     const int M = counts[p];
@@ -697,15 +711,16 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     const int b0 = (M - 1) / 31, u0 = (M - 1) % 31;  // slot of position 0
     int i = M - 1, b = 0, emitted = 0;
     uint32_t lastw = 0;
-    bool bad = false;
     while (i >= 1) {
         uint32_t word;
-        if (i - 30 >= s)
-            word = replay_block<0>(ring, bm, lane, i, s, &bad);
+        if (i - 30 >= s && i - 30 >= 255)
+            word = replay_block<0, true>(ring, bm, lane, i, s, rtab);
+        else if (i - 30 >= s)
+            word = replay_block<0, false>(ring, bm, lane, i, s, rtab);
         else if (i < s && i - 30 >= 1)
-            word = replay_block<1>(ring, bm, lane, i, s, &bad);
+            word = replay_block<1, false>(ring, bm, lane, i, s, rtab);
         else
-            word = replay_block<2>(ring, bm, lane, i, s, &bad);
+            word = replay_block<2, false>(ring, bm, lane, i, s, rtab);
         emitted += __builtin_popcount(word);
         if (b == b0) lastw = word;
         else out[(size_t)b * 64] = word;
@@ -718,7 +733,6 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     }
     out[(size_t)b0 * 64] = lastw;
     if (emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
-    if (bad) atomicOr(&flags[p], 4);
 }
 
 // Gram of each iteration's s sampled rows.  A block = 4 waves (256 iterations of one pair);
@@ -2165,8 +2179,8 @@ hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_
 
 hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const uint32_t* polyQ,
                           const uint32_t* w0, const BatchShape& sh, double sample_frac,
-                          uint32_t* wins, uint32_t* selw, int32_t* flags, hipStream_t st,
-                          int part) {
+                          const double* rtab, uint32_t* wins, uint32_t* selw, int32_t* flags,
+                          hipStream_t st, int part) {
     const int nwaves = (sh.iters + 63) / 64;
     if (part == 0) {
         hipLaunchKernelGGL(sampler_window_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts,
@@ -2175,8 +2189,13 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         const int nwords = (sh.max_s + 31) / 32;
         const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
         hipLaunchKernelGGL(sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
-                           wins, nwaves, sh.sel_words, sample_frac, selw, flags);
+                           wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st) {
+    hipLaunchKernelGGL(recip_table_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, rtab, bad);
     return hipGetLastError();
 }
 
