@@ -70,7 +70,7 @@ struct erp_ctx {
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
     DevBuf part, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
-        rtab;
+        rtab, limbs;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -166,7 +166,7 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
                      &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
                      &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins,
-                     &ctx->rtab};
+                     &ctx->rtab, &ctx->limbs};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
@@ -242,7 +242,7 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->wins, P * nwaves * 31 * 64 * 4) && ensure(c->polyR, P * 65 * 31 * 4) &&
               ensure(c->polyQ, P * erp::kMaxQ * 31 * 4) &&
               ensure(c->idx, P * nwaves * (size_t)sh.sel_words * 64 * 4) &&
-              ensure(c->gram, P * erp::gram_split(sh) * sh.iters * 36 * 8) &&
+              ensure(c->gram, P * sh.iters * 36 * 8) && ensure(c->limbs, erp::gram_limbs_bytes(sh)) &&
               ensure(c->gfin, P * sh.iters * 9 * 8) && ensure(c->rv, P * 6 * sh.iters * 4) &&
               ensure(c->kcount, P * 4) && ensure(c->sortbuf, P * (size_t)erp::sortbuf_len(sh.iters) * 4) &&
               ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result)) &&
@@ -312,13 +312,13 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
     }
     {
         StageTimer _t(ctx, ERP_STAGE_GRAM, st);
-        ERP_CK(erp::launch_gram(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
-                                cfg->sample_frac, (double*)c->gram.p, out ? out->samples : nullptr,
-                                st));
+        ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
+                                     cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
+                                     out ? out->samples : nullptr, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
-        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, erp::gram_split(sh), sh,
+        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh,
                                  cfg->sample_frac, cfg->valid_abs, (double*)c->gfin.p, hyps, st));
     }
     return ERP_OK;
@@ -702,7 +702,7 @@ erp_status erp_eight_point_estimation(erp_ctx* ctx, const double* h_bl, const do
     ERP_CK(hipMemcpy(d_cnt, &m, 4, hipMemcpyHostToDevice));
     ERP_CK(erp::launch_gram_all(d_pts, m, d_gram, nullptr));
     erp::BatchShape sh = make_shape(1, m, m, 1, 1.0);
-    ERP_CK(erp::launch_eigen(d_cnt, d_gram, 1, sh, 1.0, 1.57, d_gfin, d_h, nullptr));
+    ERP_CK(erp::launch_eigen(d_cnt, d_gram, sh, 1.0, 1.57, d_gfin, d_h, nullptr));
     ERP_CK(hipMemcpy(h_out, d_h, sizeof(erp_hypothesis), hipMemcpyDeviceToHost));
     return ERP_OK;
 }

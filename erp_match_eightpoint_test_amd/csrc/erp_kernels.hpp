@@ -83,16 +83,18 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
 // whose one-sided error bound fails (never, by construction; checked once per context)
 constexpr int kRecipTable = 65538;
 hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st);
-int gram_chunks_max(int max_nq);  // Gram row chunks per iteration for max_nq rows
-int gram_split(const BatchShape& sh);  // partial Grams per iteration (chunks split over blocks)
-hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t* selw,
-                       const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
-                       hipStream_t st);
-// selected singular vector per iteration from the nchunk partial Grams gram[p][c][36][iters]
-// (summed in place into chunk 0), vectors to evec[p][9][iters], then the estimate
-hipError_t launch_eigen(const int32_t* counts, double* gram, int nchunk,
-                        const BatchShape& sh, double sample_frac, double valid_abs,
-                        double* evec, erp_hypothesis* hyps, hipStream_t st);
+// Gram of every iteration's sample on int8 MFMA (exact fixed-point sums) -> gram[p][36][iters];
+// limbs = scratch of gram_limbs_bytes(sh); samples (debug, may be NULL) = the sampled indices
+size_t gram_limbs_bytes(const BatchShape& sh);
+hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint32_t* selw,
+                            const BatchShape& sh, double sample_frac, int8_t* limbs,
+                            double* gram, int32_t* samples, hipStream_t st);
+
+// selected singular vector per iteration from the Grams gram[p][36][iters] -> evec[p][9][iters],
+// then the estimate (rank-2 fix, decomposition, Euler angles, validity) -> hyps
+hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
+                        double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
+                        hipStream_t st);
 hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyps,
                                 const BatchShape& sh, double sample_frac, float* rv, float* tv,
                                 int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st);

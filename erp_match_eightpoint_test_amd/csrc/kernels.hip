@@ -9,11 +9,13 @@
 // exact k=2 + ratio        src/feature_matcher.cpp:42-59               knn2_filter/_rescore/_merge
 // gather + pixel->bearing  src/spherical_surf.cpp:155-162,
 //                          src/eight_point.cpp:163-186                 bearings_*
-// random_array sampler     src/eight_point.hpp:30-59 (glibc replay)    jump_prep / sampler_gram
-// A^T A of the sample      src/eight_point.cpp:22-39                   sampler_gram
-// SVD, rank 2, decompose   src/eight_point.cpp:39-84                   eigen
+// random_array sampler     src/eight_point.hpp:30-59 (glibc replay)    jump_prep / sampler_window /
+//                                                                      sampler
+// A^T A of the sample      src/eight_point.cpp:22-39                   gram_limbs / gram_mfma
+// SVD, rank 2, decompose   src/eight_point.cpp:39-84                   eigen / estimate
 // push valid R1/R2         src/eight_point.cpp:113-126                 valid_compact
-// trimmed-mean consensus   src/eight_point.cpp:129-149                 consensus_rows / _final
+// trimmed-mean consensus   src/eight_point.cpp:129-149                 consensus_bounds / _select /
+//                                                                      _refine / _rows / _final
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -735,109 +737,180 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     if (emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
 }
 
-// Gram of each iteration's s sampled rows.  A block = 4 waves (256 iterations of one pair);
-// it walks row chunks of kGramChunk selection words (31 rows each): the chunk's rows (<= 620 x
-// 48 B) are staged in LDS with coalesced loads, each lane's selection words too, and every
-// lane walks its own set bits with a cursor, reading its rows from LDS (random 16-B global
-// gathers per lane would be served one cache line at a time).  When the batch is small the
-// chunks are split over csplit blocks (block cs takes chunks cs, cs + csplit, ...) and their
-// partial Grams gpart[p][cs][36][iters] are summed in a fixed order by the eigen kernels; for
-// large batches csplit = 1 and nothing is re-read.  An exhausted lane reads the zero row.
-constexpr int kGramChunk = 20;
-constexpr int kGramRows = kGramChunk * 31;
+// ---- Gram on int8 MFMA: exact fixed-point sums -------------------------------------------
+// G_h = sum over the sampled rows i of P_i, P_i = (l l^T) x (r r^T) (36 distinct values), is a
+// product of the 0/1 selection matrix (iterations x rows) with P (rows x 36).  Each P_i value
+// (|P| <= 1) is rounded ONCE to the fixed point q = rint(P 2^44) and split into 6 balanced
+// base-256 digits (int8), so G_h 2^44 = sum_limb 256^limb * (selection x digits_limb) is
+// computed EXACTLY by v_mfma_i32_32x32x32_i8 (the int32 sums stay below 65536 * 128 < 2^31)
+// and recombined in int64; the only roundings are the per-row quantisation (<= 2^-45 per
+// value, <= s 2^-45 per Gram entry: below the fp64 FMA chain's own s-step accumulation error)
+// and the final conversion to double.  Sums are order-independent and deterministic.
+// K order = the sampler's selection words: k = 32 b + u <-> row M-1-31b-u (u < 31; u = 31 is
+// a zero pad), so the A operand is the selection word itself, expanded 4 bits -> 4 bytes by
+// one 24-bit multiply and a mask.  Columns: tile t < 6 holds limb t of entries c = 0..31 (one
+// entry per lane: its 6 limbs recombine in registers), tile 6 holds the 6 limbs of entries
+// 32..35 (column 4 limb + c - 32; recombined by lane shuffles).
+constexpr int kGramLimbs = 6;
+constexpr int kGramTiles = 7;                 // 32-column MFMA tiles
+constexpr int kGramN = kGramTiles * 32;
+constexpr int kGramLdsCol = 48;               // LDS bytes per staged column (conflict-free b128)
+constexpr double kGramScale = 0x1p44;
 
-__device__ __forceinline__ int gram_chunks(int M) { return ((M - 1) / 31 + kGramChunk) / kGramChunk; }
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
 
-__global__ __launch_bounds__(256) void gram_kernel(const int32_t* __restrict__ counts,
-                                                   const double* __restrict__ pts, int max_nq,
-                                                   int iters, int nwaves, int nbw, int csplit,
-                                                   int idx_stride, double sample_frac,
-                                                   const uint32_t* __restrict__ selw,
-                                                   double* __restrict__ gpart,
-                                                   int32_t* __restrict__ samples) {
-    __shared__ double2 rows[(kGramRows + 1) * 3];
-    __shared__ uint32_t wds[kGramChunk * 256];
-    const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
-    const int cs = blockIdx.x % csplit, wg = blockIdx.x / csplit;
+__device__ __forceinline__ int gram_col(int limb, int c) {
+    return c < 32 ? limb * 32 + c : 192 + limb * 4 + (c - 32);
+}
+
+// limbs[p][b][n][32 bytes]: byte u of column n = gram_col(limb, c) = digit of row M-1-31b-u
+__global__ __launch_bounds__(256) void gram_limbs_kernel(const int32_t* __restrict__ counts,
+                                                         const double* __restrict__ pts,
+                                                         int max_nq, int nbw,
+                                                         int8_t* __restrict__ limbs) {
+    __shared__ __align__(16) int8_t tile[kGramN * 32];
+    const int p = blockIdx.y, b = blockIdx.x, tid = threadIdx.x;
+    const int M = counts[p];
+    if (M < 2 || b > (M - 1) / 31) return;
+    for (int k = tid; k < kGramN * 32 / 16; k += 256)
+        reinterpret_cast<uint4*>(tile)[k] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    const double* P = pts + (size_t)p * (max_nq + 1) * 6;
+    for (int item = tid; item < 31 * 36; item += 256) {
+        const int u = item / 36, c = item - 36 * (item / 36);
+        const int i = M - 1 - 31 * b - u;
+        if (i < 0) continue;
+        const double* pr = P + (size_t)i * 6;
+        const int a = c / 6, e = c - 6 * (c / 6);
+        // (l l^T) and (r r^T) index pairs 00 01 02 11 12 22 (entry c = 6 a + e)
+        const int ai = a < 3 ? 0 : (a < 5 ? 1 : 2), aj = a < 3 ? a : (a < 5 ? a - 2 : 2);
+        const int ei = e < 3 ? 0 : (e < 5 ? 1 : 2), ej = e < 3 ? e : (e < 5 ? e - 2 : 2);
+        const double LL = pr[ai] * pr[aj], RR = pr[3 + ei] * pr[3 + ej];
+        long long q = __double2ll_rn((LL * RR) * kGramScale);
+#pragma unroll
+        for (int k = 0; k < kGramLimbs; k++) {
+            const int d = (int)(int8_t)(q & 0xff);
+            tile[gram_col(k, c) * 32 + u] = (int8_t)d;
+            q = (q - d) >> 8;
+        }
+    }
+    __syncthreads();
+    uint4* o = reinterpret_cast<uint4*>(limbs + ((size_t)p * nbw + b) * kGramN * 32);
+    for (int k = tid; k < kGramN * 32 / 16; k += 256) o[k] = reinterpret_cast<const uint4*>(tile)[k];
+}
+
+// Block = 4 waves x 32 iterations (one MFMA row tile each); K loop over the pair's selection
+// words with the 7 KB limb tile of the next word staged into LDS (double buffer) while the
+// current one feeds 7 MFMAs per wave.  gram[p][36][iters] (SoA, the eigen kernels' layout).
+__global__ __launch_bounds__(256, 2) void gram_mfma_kernel(const int32_t* __restrict__ counts,
+                                                        const int8_t* __restrict__ limbs,
+                                                        const uint32_t* __restrict__ selw,
+                                                        int iters, int nwaves, int nbw,
+                                                        double sample_frac,
+                                                        double* __restrict__ gram) {
+    __shared__ __align__(16) int8_t bs[2][kGramN * kGramLdsCol];
+    const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;
+    const int hb = blockIdx.x * 128;
+    if (hb >= iters) return;  // uniform over the block
     const int nb = (M - 1) / 31 + 1;
-    if (cs * kGramChunk >= nb) return;  // uniform over the block (this partial is not read)
-    const double2* P = reinterpret_cast<const double2*>(pts + (size_t)p * (max_nq + 1) * 6);
-    const int wv = wg * 4 + (tid >> 6);          // wave index of these 64 iterations
-    const int h = wv * 64 + lane;
-    const uint32_t* my = selw + ((size_t)p * nwaves + (wv < nwaves ? wv : 0)) * (size_t)nbw * 64 + lane;
-    double g[36];
+    const int h0 = hb + wv * 32;
+    const int r = lane & 31, hh = lane >> 5;
+    const int h = h0 + r;
+    const bool hv = h < iters;
+    const uint32_t* sp = selw + ((size_t)p * nwaves + (hv ? h >> 6 : 0)) * (size_t)nbw * 64 + (h & 63);
+    const uint4* lg = reinterpret_cast<const uint4*>(limbs + (size_t)p * nbw * kGramN * 32);
+    // staging: the 448 16-B pieces of a word's tile, piece q -> column q >> 1, half q & 1
+    constexpr int kPieces = kGramN * 2;
+    uint4 st0 = make_uint4(0u, 0u, 0u, 0u), st1 = st0;
+    auto stage_load = [&](int b) {
+        st0 = lg[(size_t)b * kPieces + tid];
+        if (tid + 256 < kPieces) st1 = lg[(size_t)b * kPieces + tid + 256];
+    };
+    auto stage_store = [&](int buf) {
+        *reinterpret_cast<uint4*>(&bs[buf][(tid >> 1) * kGramLdsCol + (tid & 1) * 16]) = st0;
+        if (tid + 256 < kPieces)
+            *reinterpret_cast<uint4*>(&bs[buf][((tid + 256) >> 1) * kGramLdsCol + (tid & 1) * 16]) = st1;
+    };
+    i32x16 acc[kGramTiles];
 #pragma unroll
-    for (int k = 0; k < 36; k++) g[k] = 0.0;
-    int before = 0;  // samples in earlier chunks (debug output only)
-    if (samples)
-        for (int k = 0; k < cs * kGramChunk; k++)
-            before += __builtin_popcount(wv < nwaves ? my[(size_t)k * 64] : 0u);
-    for (int c = cs; c * kGramChunk < nb; c += csplit) {
-        const int b_lo = c * kGramChunk;
-        const int nw = min(b_lo + kGramChunk, nb) - b_lo;
-        const int i_hi = M - 1 - 31 * b_lo;      // row of slot 0 (slot = i_hi - i)
-        const int nrows = min(31 * nw, i_hi + 1);
-        __syncthreads();                         // previous chunk's LDS readers are done
-        for (int t = tid; t < nrows * 3; t += 256) rows[t] = P[(size_t)(i_hi - t / 3) * 3 + t % 3];
-        if (tid < 3) rows[kGramRows * 3 + tid] = make_double2(0.0, 0.0);
-        int cnt = 0;
-        for (int k = 0; k < nw; k++) {
-            const uint32_t v = wv < nwaves ? my[(size_t)(b_lo + k) * 64] : 0u;
-            wds[k * 256 + tid] = v;
-            cnt += __builtin_popcount(v);
+    for (int t = 0; t < kGramTiles; t++)
+#pragma unroll
+        for (int k = 0; k < 16; k++) acc[t][k] = 0;
+    stage_load(0);
+    stage_store(0);
+    uint32_t wcur = hv ? sp[0] : 0u;
+    __syncthreads();
+    for (int b = 0; b < nb; b++) {
+        const int buf = b & 1;
+        const bool more = b + 1 < nb;
+        uint32_t wnext = 0u;
+        if (more) {
+            stage_load(b + 1);
+            wnext = hv ? sp[(size_t)(b + 1) * 64] : 0u;
         }
+        const uint32_t bits = (wcur >> (16 * hh)) & 0xffffu;
+        i32x4 a;
+#pragma unroll
+        for (int v = 0; v < 4; v++)
+            a[v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
+        const int8_t* bt = &bs[buf][r * kGramLdsCol + hh * 16];
+#pragma unroll
+        for (int t = 0; t < kGramTiles; t++) {
+            const i32x4 bf = *reinterpret_cast<const i32x4*>(bt + t * 32 * kGramLdsCol);
+            acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf, acc[t], 0, 0, 0);
+        }
+        if (more) stage_store(buf ^ 1);
+        wcur = wnext;
         __syncthreads();
-        int mx = cnt;
+    }
+    // recombine: row = (k & 3) + 8 (k >> 2) + 4 hh; entry r from tiles 0..5 of this lane,
+    // entries 32..35 from tile 6 (lane 4 limb + e)
+    double* go = gram + (size_t)p * 36 * iters;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
-        int wi = 0;
-        uint32_t cur = wds[tid];
-        constexpr int B = 4;
-        for (int k0 = 0; k0 < mx; k0 += B) {
-            int slot[B];
+    for (int k = 0; k < 16; k++) {
+        const int row = (k & 3) + 8 * (k >> 2) + 4 * hh;
+        long long v = 0;
 #pragma unroll
-            for (int u = 0; u < B; u++) {
-                while (cur == 0u && wi + 1 < nw) {
-                    wi++;
-                    cur = wds[wi * 256 + tid];
-                }
-                slot[u] = kGramRows;
-                if (cur) {
-                    slot[u] = 31 * wi + __builtin_ctz(cur);
-                    cur &= cur - 1u;
-                }
-            }
+        for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[t][k] << (8 * t);
+        long long v2 = 0;
+        const int x = acc[kGramLimbs][k];
 #pragma unroll
-            for (int u = 0; u < B; u++) {
-                const double2 a0 = rows[slot[u] * 3], a1 = rows[slot[u] * 3 + 1], a2 = rows[slot[u] * 3 + 2];
-                const double l0 = a0.x, l1 = a0.y, l2 = a1.x;
-                const double r0 = a1.y, r1 = a2.x, r2 = a2.y;
-                const double LL[6] = {l0 * l0, l0 * l1, l0 * l2, l1 * l1, l1 * l2, l2 * l2};
-                const double RR[6] = {r0 * r0, r0 * r1, r0 * r2, r1 * r1, r1 * r2, r2 * r2};
-#pragma unroll
-                for (int a6 = 0; a6 < 6; a6++)
-#pragma unroll
-                    for (int b6 = 0; b6 < 6; b6++)
-                        g[6 * a6 + b6] = __builtin_fma(LL[a6], RR[b6], g[6 * a6 + b6]);
-            }
-            if (samples && h < iters)
-                for (int u = 0; u < B; u++)
-                    if (slot[u] != kGramRows && before + k0 + u < idx_stride)
-                        samples[((size_t)p * iters + h) * idx_stride + before + k0 + u] = i_hi - slot[u];
-        }
-        if (samples) {  // samples of the chunks between this one and the next one taken
-            before += cnt;
-            for (int k = b_lo + kGramChunk; k < min((c + csplit) * kGramChunk, nb); k++)
-                before += __builtin_popcount(wv < nwaves ? my[(size_t)k * 64] : 0u);
+        for (int t = 0; t < kGramLimbs; t++)
+            v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
+        if (h0 + row < iters) {
+            go[(size_t)r * iters + h0 + row] = (double)v * (1.0 / kGramScale);
+            if (r < 4) go[(size_t)(32 + r) * iters + h0 + row] = (double)v2 * (1.0 / kGramScale);
         }
     }
-    if (h < iters) {  // [p][cs][k][h]: coalesced over the lanes
-        double* go = gpart + ((size_t)p * csplit + cs) * 36 * iters + h;
-#pragma unroll
-        for (int k = 0; k < 36; k++) go[(size_t)k * iters] = g[k];
+}
+
+// debug output: the sampled match indices of every iteration (as a set, descending), from the
+// selection words
+__global__ __launch_bounds__(64) void samples_kernel(const int32_t* __restrict__ counts,
+                                                     const uint32_t* __restrict__ selw, int iters,
+                                                     int nwaves, int nbw, int idx_stride,
+                                                     double sample_frac,
+                                                     int32_t* __restrict__ samples) {
+    const int p = blockIdx.y, lane = wave_lane();
+    const int h = blockIdx.x * 64 + lane;
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || M < 2 || h >= iters) return;
+    const uint32_t* sp = selw + ((size_t)p * nwaves + blockIdx.x) * (size_t)nbw * 64 + lane;
+    int32_t* o = samples + ((size_t)p * iters + h) * idx_stride;
+    int n = 0;
+    for (int b = 0; b <= (M - 1) / 31; b++) {
+        uint32_t w = sp[(size_t)b * 64];
+        while (w) {
+            const int u = __builtin_ctz(w);
+            w &= w - 1u;
+            if (n < idx_stride) o[n] = M - 1 - 31 * b - u;
+            n++;
+        }
     }
 }
 
@@ -879,26 +952,17 @@ __global__ __launch_bounds__(256) void gram_all_kernel(const double* __restrict_
 // estimate (rank-2 fix, decomposition, Euler angles) runs in estimate_kernel.
 template <bool THIN>
 __global__ __launch_bounds__(64) void eigen_kernel(const int32_t* __restrict__ counts,
-                                                   double* __restrict__ gram, int iters,
-                                                   int nchunk, double sample_frac,
+                                                   const double* __restrict__ gram, int iters,
+                                                   double sample_frac,
                                                    double* __restrict__ evec) {
     const int p = blockIdx.y;
     const int h = blockIdx.x * 64 + threadIdx.x;
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || h >= iters || (s < 9) != THIN) return;
-    // gram[p][chunk][36][iters]: partial Grams of the row chunks, summed in chunk order into
-    // chunk 0's slice (in place, coalesced over the lanes); the solve then reads the 36 values
-    // with stride iters and the vector goes to evec[p][9][iters]
-    double* gi = gram + (size_t)p * nchunk * 36 * iters + h;
-    const int nc = min(nchunk, gram_chunks(M));
-    if (nc > 1) {
-        for (int k = 0; k < 36; k++) {
-            double v = gi[(size_t)k * iters];
-            for (int c = 1; c < nc; c++) v += gi[((size_t)c * 36 + k) * iters];
-            gi[(size_t)k * iters] = v;
-        }
-    }
+    // gram[p][36][iters] (SoA): the solve reads the 36 values with stride iters, the vector
+    // goes to evec[p][9][iters]
+    const double* gi = gram + (size_t)p * 36 * iters + h;
     double e[9];
     if (THIN) {
         double g36[36], G[81];
@@ -2199,23 +2263,21 @@ hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st)
     return hipGetLastError();
 }
 
-int gram_chunks_max(int max_nq) { return ((max_nq + 30) / 31 + kGramChunk) / kGramChunk; }
-
-int gram_split(const BatchShape& sh) {
-    const int blocks = ((sh.iters + 255) / 256) * sh.n_pairs;
-    const int want = (2048 + blocks - 1) / blocks;  // enough blocks to fill the chip
-    return std::max(1, std::min(want, gram_chunks_max(sh.max_nq)));
+size_t gram_limbs_bytes(const BatchShape& sh) {
+    return (size_t)sh.n_pairs * sh.sel_words * kGramN * 32;
 }
 
-hipError_t launch_gram(const int32_t* counts, const double* pts, const uint32_t* selw,
-                       const BatchShape& sh, double sample_frac, double* gram, int32_t* samples,
-                       hipStream_t st) {
+hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint32_t* selw,
+                            const BatchShape& sh, double sample_frac, int8_t* limbs,
+                            double* gram, int32_t* samples, hipStream_t st) {
     const int nwaves = (sh.iters + 63) / 64;
-    const int csplit = gram_split(sh);
-    dim3 grid(((nwaves + 3) / 4) * csplit, sh.n_pairs);
-    hipLaunchKernelGGL(gram_kernel, grid, dim3(256), 0, st, counts, pts, sh.max_nq, sh.iters,
-                       nwaves, sh.sel_words, csplit, sh.idx_stride, sample_frac, selw, gram,
-                       samples);
+    hipLaunchKernelGGL(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
+                       pts, sh.max_nq, sh.sel_words, limbs);
+    hipLaunchKernelGGL(gram_mfma_kernel, dim3((sh.iters + 127) / 128, sh.n_pairs), dim3(256), 0, st,
+                       counts, limbs, selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram);
+    if (samples)
+        hipLaunchKernelGGL(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
+                           sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);
     return hipGetLastError();
 }
 
@@ -2224,14 +2286,14 @@ hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream
     return hipGetLastError();
 }
 
-hipError_t launch_eigen(const int32_t* counts, double* gram, int nchunk,
-                        const BatchShape& sh, double sample_frac, double valid_abs,
-                        double* evec, erp_hypothesis* hyps, hipStream_t st) {
+hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
+                        double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
+                        hipStream_t st) {
     dim3 grid((sh.iters + 63) / 64, sh.n_pairs);
-    hipLaunchKernelGGL(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters, nchunk,
+    hipLaunchKernelGGL(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters,
                        sample_frac, evec);
     // (M is only known on the device: the thin instantiation returns at once for s >= 9)
-    hipLaunchKernelGGL(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters, nchunk,
+    hipLaunchKernelGGL(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters,
                        sample_frac, evec);
     hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
                        sample_frac, valid_abs, hyps);
