@@ -70,7 +70,7 @@ struct erp_ctx {
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
     DevBuf part, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
-        rtab, limbs;
+        rtab, limbs, tsplit, ovf;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -166,7 +166,7 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
                      &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
                      &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins,
-                     &ctx->rtab, &ctx->limbs};
+                     &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
@@ -203,7 +203,8 @@ bool ensure_matcher(erp_ctx* c, const erp::BatchShape& sh) {
     const size_t PQ = (size_t)sh.n_pairs * sh.max_nq;
     return ensure(c->part, PQ * sizeof(erp::Top2)) &&
            ensure(c->pu, PQ * sh.fchunks * sizeof(float2)) && ensure(c->ccount, PQ * 4) &&
-           ensure(c->cand, PQ * erp::kCandCap * 4);
+           ensure(c->cand, PQ * erp::kCandCap * 4) &&
+           ensure(c->tsplit, erp::knn2_split_bytes(sh)) && ensure(c->ovf, 4 + 8 * PQ);
 }
 
 // exact k=2 + ratio test: MFMA filter (upper bounds), candidates, exact rescoring, merge
@@ -215,16 +216,17 @@ erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int
     auto* cand = (int32_t*)ctx->cand.p;
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_FILTER, st);
-        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, pu, cc, cand, 1, st));
+        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand, 1, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_CANDIDATES, st);
         ERP_CK(hipMemsetAsync(cc, 0, (size_t)sh.n_pairs * sh.max_nq * 4, st));
-        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, pu, cc, cand, 2, st));
+        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand, 2, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_RESCORE, st);
-        ERP_CK(erp::launch_knn2_rescore(dq, dt, oq, ot, sh, cc, cand, (erp::Top2*)ctx->part.p, st));
+        ERP_CK(erp::launch_knn2_rescore(dq, dt, oq, ot, sh, cc, cand, (erp::Top2*)ctx->part.p,
+                                        (int32_t*)ctx->ovf.p, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_MERGE, st);

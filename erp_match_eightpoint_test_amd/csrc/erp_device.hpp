@@ -436,7 +436,7 @@ ERP_HD ERP_INLINE void gram36_to_ut(const double* g36, int stride, int h, double
         }
 }
 
-ERP_HD inline void gram_min_eigvec9(const double* g36, int stride, int h, double* e) {
+ERP_HD inline void gram_min_eigvec9_jacobi(const double* g36, int stride, int h, double* e) {
     double S[45];
     gram36_to_ut(g36, stride, h, S);
     double tr = 0;
@@ -529,6 +529,93 @@ ERP_HD inline void gram_min_eigvec9(const double* g36, int stride, int h, double
         const double inv = 1.0 / sqrt(nrm);
 #pragma unroll
         for (int i = 0; i < 9; i++) x[i] *= inv;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) e[i] = x[i];
+}
+
+// L D L^T of B = G - mu I from the 36 Gram values, in place in S (L below the diagonal, stored
+// at ut9(j, i); D on the diagonal, clamped at floor_d)
+ERP_HD ERP_INLINE void gram_ldlt9(const double* g36, int stride, int h, double mu, double floor_d,
+                                  double* S) {
+    gram36_to_ut(g36, stride, h, S);
+#pragma unroll
+    for (int i = 0; i < 9; i++) S[ut9(i, i)] -= mu;
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+        double d = S[ut9(j, j)];
+#pragma unroll
+        for (int k = 0; k < j; k++) d -= S[ut9(k, j)] * S[ut9(k, j)] * S[ut9(k, k)];
+        d = d > floor_d ? d : floor_d;
+        S[ut9(j, j)] = d;
+        const double inv = 1.0 / d;
+#pragma unroll
+        for (int i = j + 1; i < 9; i++) {
+            double v = S[ut9(j, i)];
+#pragma unroll
+            for (int k = 0; k < j; k++) v -= S[ut9(k, i)] * S[ut9(k, j)] * S[ut9(k, k)];
+            S[ut9(j, i)] = v * inv;  // L[i][j]
+        }
+    }
+}
+
+// s >= 9: the eigenvector of G's smallest eigenvalue by inverse iteration on G itself (shift
+// mu = -16 eps tr(G): G - mu I is positive definite, so L D L^T needs no pivoting).  The
+// eight-point Grams have lambda_1 / lambda_2 ~ 1e-5 (every sampled correspondence nearly
+// satisfies the same epipolar constraint), so each step gains ~5 digits: the loop stops one
+// step after the iterate moves by < 1e-12 and the vector is then at rounding level.  A lane
+// whose iterate has not settled after kInvIt steps (near-degenerate lambda_1 ~ lambda_2) takes
+// the Jacobi path (eigenvalue shift + inverse iteration, gram_min_eigvec9_jacobi).
+ERP_HD inline void gram_min_eigvec9(const double* g36, int stride, int h, double* e) {
+    constexpr int kInvIt = 10;
+    double S[45];
+    double tr = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) tr += g36[(6 * sym3(i / 3, i / 3) + sym3(i % 3, i % 3)) * stride + h];
+    const double tiny = kDblEps * (tr > 0 ? tr : 1.0);
+    gram_ldlt9(g36, stride, h, -16 * tiny, tiny * 1e-3, S);
+    double dinv[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) dinv[i] = 1.0 / S[ut9(i, i)];
+    double x[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) x[i] = 1.0 / 3.0;
+    int settled = -1;  // step at which the iterate stopped moving
+    for (int it = 0; it < kInvIt; it++) {
+        double y[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {  // L y = x
+            double v = x[i];
+#pragma unroll
+            for (int k = 0; k < i; k++) v -= S[ut9(k, i)] * y[k];
+            y[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 9; i++) y[i] *= dinv[i];
+#pragma unroll
+        for (int i = 8; i >= 0; i--)  // L^T z = y
+#pragma unroll
+            for (int k = i + 1; k < 9; k++) y[i] -= S[ut9(i, k)] * y[k];
+        double nrm = 0, dot = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            nrm += y[i] * y[i];
+            dot += y[i] * x[i];
+        }
+        const double inv = (dot < 0 ? -1.0 : 1.0) / sqrt(nrm);  // keep the sign: no flip-flop
+        double dlt = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            const double v = y[i] * inv;
+            dlt = fmax(dlt, fabs(v - x[i]));
+            x[i] = v;
+        }
+        if (settled >= 0) break;     // one more step after settling
+        if (dlt < 1e-12) settled = it;
+    }
+    if (settled < 0) {
+        gram_min_eigvec9_jacobi(g36, stride, h, e);
+        return;
     }
 #pragma unroll
     for (int i = 0; i < 9; i++) e[i] = x[i];

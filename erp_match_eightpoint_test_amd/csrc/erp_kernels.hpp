@@ -55,12 +55,17 @@ void init_constants();            // reduction table for the jump polynomials (o
 
 // matcher: pass 1 (per-chunk top-2 upper bounds pu), pass 2 (candidates; ccount zeroed
 // before), rescore (exact Top2 per query into part[pairs][max_nq]), merge (ratio + compaction)
+// split = scratch of knn2_split_bytes(sh): the train rows as bf16 hi / lo pieces + norms
+// (pass 1 fills it)
+size_t knn2_split_bytes(const BatchShape& sh);
 hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
-                              const int64_t* off_t, const BatchShape& sh, float2* pu,
-                              int32_t* ccount, int32_t* cand, int pass, hipStream_t st);
+                              const int64_t* off_t, const BatchShape& sh, void* split,
+                              float2* pu, int32_t* ccount, int32_t* cand, int pass,
+                              hipStream_t st);
+// ovf = scratch of 4 + 8 * n_pairs * max_nq bytes: overflow list for the exact sweep
 hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
                                const int64_t* off_t, const BatchShape& sh, const int32_t* ccount,
-                               const int32_t* cand, Top2* part, hipStream_t st);
+                               const int32_t* cand, Top2* part, int32_t* ovf, hipStream_t st);
 hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
                              const BatchShape& sh, float ratio, erp_dmatch* matches,
                              int32_t* counts, int32_t* flags, hipStream_t st);

@@ -33,6 +33,8 @@ namespace {
 
 constexpr float kInf = __builtin_huge_valf();
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 // x^(31+d) mod (x^31 - x^28 - 1), d = 0..29: reduction of a 61-coefficient product
 __constant__ uint32_t c_red[30][31];
 
@@ -69,44 +71,51 @@ __device__ int block_exclusive_scan(int v, int* ws, int* total) {
 // ===================================================================== matcher =========
 // Exact k=2 in three steps (the result is identical to a brute-force sweep in the flann::L2
 // order, lowest train index winning ties):
-//  1. knn2_filter<1>: approximate squared distances a = |q|^2 + |t|^2 - 2 q.t with the dot
-//     product on bf16 MFMA in three terms (q_hi t_hi + q_hi t_lo + q_lo t_hi, q = q_hi + q_lo
-//     split exactly in bf16 pieces, residual <= 2^-16 |q| per component; f32 accumulation).
-//     For every pair |a - e| <= eps(q,t) = 2^-12 (|q|^2 + |t|^2), e = the reference's exact
-//     f32 value (the error budget -- split residuals, MFMA f32 accumulation of 192 products, the
-//     norms, and e's own rounding against the real distance -- stays below half of eps even if
-//     every rounding truncates).  Each query keeps the two smallest u = a + eps per chunk.
+//  1. knn2_filter<1>: approximate squared distances a = |q|^2 + |t|^2 - 2 qh.th from ONE bf16
+//     MFMA product of the rounded rows (qh = bf16(q), th = bf16(t); f32 accumulation).
+//     Bound: with |q_i - qh_i| <= 2^-8 |q_i| (bf16 round-to-nearest, 8 significant bits),
+//     |q.t - qh.th| <= sum |qh_i||t_i - th_i| + |q_i - qh_i||t_i| <= 2^-7 (1 + 2^-9) |q||t|
+//     <= 2^-8 (1 + 2^-9) (|q|^2 + |t|^2); the MFMA's f32 accumulation of 64 exact products,
+//     the f32 norms and the reference's own rounding of e add < 2^-16 (|q|^2 + |t|^2).  So
+//     |a - e| <= 2^-6.98 (|q|^2 + |t|^2) < eps(q,t) = 2^-6 (|q|^2 + |t|^2) for the
+//     reference's exact f32 value e.  Each query keeps the two smallest u = a + eps per chunk.
 //  2. knn2_filter<2>: U2 = the second smallest u over all chunks bounds e of the true second
 //     neighbour from above; every train row with l = a - eps <= U2 (which includes every row
-//     with e <= e_(2), i.e. both true neighbours and all their ties) is a candidate.
+//     with e <= e_(2), i.e. both true neighbours and all their ties) is a candidate (a few per
+//     query on SURF-like data: the rows within 4 eps of the second neighbour).
 //  3. knn2_rescore: exact flann::L2 distances of the candidates (a full exact sweep if a query
 //     ever has more than kCandCap), giving (d0, j0, d1) exactly.
-// Matrix layout for v_mfma_f32_32x32x16_bf16: A = 32 train rows x 16 dims (LDS, staged and
-// split per 32-row tile), B = 16 dims x 32 queries (registers, split once), D = 32 x 32 with
-// the query on the lane (col = lane & 31) and 16 train rows in the registers
-// (row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)).  Block = 4 waves x 32 queries x one train chunk.
+// The train rows are rounded to bf16 ONCE per batch (knn2_split: bf16 rows and |t|^2, dense
+// [pair][row] layout) and staged per 32-row tile into LDS by plain copies.
+// Matrix layout for v_mfma_f32_32x32x16_bf16: A = 32 train rows x 16 dims (LDS), B = 16 dims x
+// 32 queries (registers, rounded once), D = 32 x 32 with the query on the lane (col = lane & 31)
+// and 16 train rows in the registers (row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)).  Block = 4
+// waves x 32 queries x one train chunk.  The bounds are formed with packed f32 math:
+//   u = fma(-2, qh.th, qu + tu),  qu = |q|^2 (1 + eps) + tiny,  tu = |t|^2 (1 + eps)
+//   l = fma(-2, qh.th, ql + tl),  ql = |q|^2 (1 - eps) - tiny,  tl = |t|^2 (1 - eps)
+// (= a +- (eps (|q|^2 + |t|^2) + tiny) up to four more f32 roundings, <= 2^-21 (|q|^2 + |t|^2),
+// inside the bound's slack).  Pass 1 keeps the two smallest u per query (v_med3 / v_min);
+// pass 2 takes the minimum l of the lane's 16 rows and only builds the candidate mask when it
+// reaches U2 (rare).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kFQ = 128;            // queries per block
 constexpr int kFT = 32;             // train rows per tile
 constexpr int kFRow = 72;           // bf16 per LDS row: 64 + 8 pad (conflict-free b128 reads)
-constexpr float kFEps = 0x1p-12f;
+constexpr float kFEps = 0x1p-6f;
 constexpr float kFTiny = 0x1p-100f; // absolute floor (flushed denormals)
 
 struct FilterLds {
     bf16x8 hi[2][kFT * kFRow / 8];
-    bf16x8 lo[2][kFT * kFRow / 8];
-    float tt[2][kFT];
+    float tb[2][kFT];               // tu (pass 1) or tl (pass 2) of the tile's rows
 };
 
-__device__ __forceinline__ void split8(const float4 a, const float4 b, bf16x8& hi, bf16x8& lo) {
+__device__ __forceinline__ bf16x8 round8(const float4 a, const float4 b) {
     const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    bf16x8 h;
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-        const __bf16 h = (__bf16)v[k];
-        hi[k] = h;
-        lo[k] = (__bf16)(v[k] - (float)h);
-    }
+    for (int k = 0; k < 8; k++) h[k] = (__bf16)v[k];
+    return h;
 }
 
 __device__ __forceinline__ float sq8(const float4 a, const float4 b) {
@@ -114,12 +123,39 @@ __device__ __forceinline__ float sq8(const float4 a, const float4 b) {
            b.w * b.w;
 }
 
+// train rows -> thi [pair][max_nt][64] bf16 (round to nearest) and tn [pair][max_nt] = |t|^2;
+// four threads per row (16 dims each)
+__global__ __launch_bounds__(256) void knn2_split_kernel(const float* __restrict__ dt,
+                                                         const int64_t* __restrict__ off_t,
+                                                         int max_nt, bf16x8* __restrict__ thi,
+                                                         float* __restrict__ tn) {
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const int j = blockIdx.x * 64 + (tid >> 2), part = tid & 3;
+    const int64_t tbase = off_t[p];
+    const int nt = (int)(off_t[p + 1] - tbase);
+    if (blockIdx.x * 64 >= nt) return;  // uniform
+    float ss = 0.f;
+    const size_t o = ((size_t)p * max_nt + j) * 8 + 2 * part;  // in bf16x8 units
+    if (j < nt) {
+        const float4* tp = reinterpret_cast<const float4*>(dt + (tbase + j) * kDim + 16 * part);
+        const float4 a = tp[0], b = tp[1], c = tp[2], d = tp[3];
+        thi[o] = round8(a, b);
+        thi[o + 1] = round8(c, d);
+        ss = sq8(a, b) + sq8(c, d);
+    }
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    if (part == 0 && j < nt) tn[(size_t)p * max_nt + j] = ss;
+}
+
 template <int PASS>
 __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restrict__ dq,
-                                                          const float* __restrict__ dt,
+                                                          const bf16x8* __restrict__ thi,
+                                                          const float* __restrict__ tn,
                                                           const int64_t* __restrict__ off_q,
                                                           const int64_t* __restrict__ off_t,
                                                           int chunk_len, int chunks, int max_nq,
+                                                          int max_nt,
                                                           float2* __restrict__ pu,
                                                           int32_t* __restrict__ ccount,
                                                           int32_t* __restrict__ cand) {
@@ -127,8 +163,7 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     const int p = blockIdx.z;
     const int64_t qbase = off_q[p];
     const int nq = (int)(off_q[p + 1] - qbase);
-    const int64_t tbase = off_t[p];
-    const int nt = (int)(off_t[p + 1] - tbase);
+    const int nt = (int)(off_t[p + 1] - off_t[p]);
     const int q0 = blockIdx.x * kFQ;
     const int t0 = blockIdx.y * chunk_len;
     if (q0 >= nq || t0 >= nt) return;  // uniform over the block
@@ -136,8 +171,8 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
     const int q = q0 + (tid >> 6) * 32 + (lane & 31);
     const bool qv = q < nq;
-    // query fragments (B operand): dims 16c + 8h .. +7 of query q, split once
-    bf16x8 qh[4], ql[4];
+    // query fragments (B operand): dims 16c + 8h .. +7 of query q, rounded once
+    bf16x8 qh[4];
     float qq = 0.f;
     {
         const float* qp = dq + (qbase + (qv ? q : 0)) * kDim + 8 * h;
@@ -146,10 +181,14 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
             const float4 a = *reinterpret_cast<const float4*>(qp + 16 * c);
             const float4 b = *reinterpret_cast<const float4*>(qp + 16 * c + 4);
             qq += sq8(a, b);
-            split8(a, b, qh[c], ql[c]);
+            qh[c] = round8(a, b);
         }
         qq += __shfl_xor(qq, 32, 64);
     }
+    const float qb = PASS == 1 ? __builtin_fmaf(qq, kFEps, qq) + kFTiny
+                               : __builtin_fmaf(qq, -kFEps, qq) - kFTiny;
+    const f32x2 qb2 = {qb, qb};
+    const f32x2 m2x = {-2.f, -2.f};
     float U2 = 0.f;
     if (PASS == 2) {
         const int nch = (nt + chunk_len - 1) / chunk_len;
@@ -162,18 +201,21 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
         U2 = m2;
     }
     float m1 = kInf, m2 = kInf;
-    // staging: thread -> train row tid >> 3 of the tile, floats 8 (tid & 7) .. +7
-    const int srow = tid >> 3, scol = 8 * (tid & 7);
-    float4 ga = make_float4(0.f, 0.f, 0.f, 0.f), gb = ga;
+    // staging: thread -> train row tid >> 3 of the tile, 16 bytes (tid & 7) of it
+    const int srow = tid >> 3, spart = tid & 7;
+    const bf16x8* thp = thi + (size_t)p * max_nt * 8;
+    const float* tnp = tn + (size_t)p * max_nt;
+    const bf16x8 z8 = {};
+    bf16x8 gh = z8;
+    float gn = kInf;
     auto gload = [&](int tile0) {
         const int j = tile0 + srow;
         if (j < t1) {
-            const float* tp = dt + (tbase + j) * kDim + scol;
-            ga = *reinterpret_cast<const float4*>(tp);
-            gb = *reinterpret_cast<const float4*>(tp + 4);
+            gh = thp[(size_t)j * 8 + spart];
+            if (spart == 0) gn = tnp[j];
         } else {
-            ga = make_float4(0.f, 0.f, 0.f, 0.f);
-            gb = ga;
+            gh = z8;
+            gn = kInf;
         }
     };
     const int ntiles = (t1 - t0 + kFT - 1) / kFT;
@@ -181,53 +223,51 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     const int r = lane & 31;
     for (int k = 0; k < ntiles; k++) {
         const int buf = k & 1, tile0 = t0 + k * kFT;
-        {
-            bf16x8 hi, lo;
-            split8(ga, gb, hi, lo);
-            float ss = sq8(ga, gb);
-            ss += __shfl_xor(ss, 1, 64);
-            ss += __shfl_xor(ss, 2, 64);
-            ss += __shfl_xor(ss, 4, 64);
-            sm.hi[buf][(srow * kFRow + scol) / 8] = hi;
-            sm.lo[buf][(srow * kFRow + scol) / 8] = lo;
-            if ((tid & 7) == 0) sm.tt[buf][srow] = (tile0 + srow < t1) ? ss : kInf;
-        }
+        sm.hi[buf][(srow * kFRow) / 8 + spart] = gh;
+        if (spart == 0)
+            sm.tb[buf][srow] = gn == kInf ? kInf
+                                          : __builtin_fmaf(gn, PASS == 1 ? kFEps : -kFEps, gn);
         __syncthreads();
         if (k + 1 < ntiles) gload(tile0 + kFT);
         f32x16 acc = {};
 #pragma unroll
         for (int c = 0; c < 4; c++) {
             const bf16x8 ah = sm.hi[buf][(r * kFRow + 16 * c + 8 * h) / 8];
-            const bf16x8 al = sm.lo[buf][(r * kFRow + 16 * c + 8 * h) / 8];
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, qh[c], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, ql[c], acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, qh[c], acc, 0, 0, 0);
         }
-        uint32_t cmask = 0;  // pass 2: candidate rows of this tile (bit 4g + e)
+        f32x2 b2[8];
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            const float4 t4 = *reinterpret_cast<const float4*>(&sm.tt[buf][8 * g + 4 * h]);
-            const float tv[4] = {t4.x, t4.y, t4.z, t4.w};
+            const float4 t4 = *reinterpret_cast<const float4*>(&sm.tb[buf][8 * g + 4 * h]);
+            const f32x2 ta = {t4.x, t4.y}, tb = {t4.z, t4.w};
+            const f32x2 a0 = {acc[4 * g], acc[4 * g + 1]}, a1 = {acc[4 * g + 2], acc[4 * g + 3]};
+            b2[2 * g] = __builtin_elementwise_fma(m2x, a0, qb2 + ta);
+            b2[2 * g + 1] = __builtin_elementwise_fma(m2x, a1, qb2 + tb);
+        }
+        if (PASS == 1) {
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
-                const float st = qq + tv[e];
-                const float a = __builtin_fmaf(-2.f, acc[4 * g + e], st);
-                if (PASS == 1) {
-                    const float u = __builtin_fmaf(kFEps, st, a) + kFTiny;
+            for (int e = 0; e < 8; e++) {
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    const float u = b2[e][c];
                     m2 = __builtin_amdgcn_fmed3f(m1, m2, u);
                     m1 = fminf(m1, u);
-                } else {
-                    // NaN (rows past the chunk: inf - inf) never passes
-                    const float l = __builtin_fmaf(-kFEps, st, a) - kFTiny;
-                    cmask |= (l <= U2) ? (1u << (4 * g + e)) : 0u;
                 }
             }
-        }
-        if (PASS == 2) {
-            if (!qv) cmask = 0;
-            if (__builtin_amdgcn_ballot_w64(cmask != 0)) {  // rare: most tiles have none
+        } else {
+            float mn = kInf;
+#pragma unroll
+            for (int e = 0; e < 8; e++) mn = fminf(mn, fminf(b2[e][0], b2[e][1]));
+            const bool any = qv && mn <= U2;
+            if (__builtin_amdgcn_ballot_w64(any)) {  // rare: most tiles have no candidate
+                uint32_t cmask = 0;  // element 2e + c <-> register 4 (e >> 1) + 2 (e & 1) + c
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+#pragma unroll
+                    for (int c = 0; c < 2; c++)
+                        cmask |= (qv && b2[e][c] <= U2) ? (1u << (2 * e + c)) : 0u;
                 while (cmask) {
-                    const int bit = __builtin_ctz(cmask);
+                    const int bit = __builtin_ctz(cmask);  // = accumulator register index
                     cmask &= cmask - 1u;
                     const int slot = atomicAdd(&ccount[(size_t)p * max_nq + q], 1);
                     if (slot < kCandCap)
@@ -261,8 +301,19 @@ __device__ __forceinline__ float exact_l2(const float4* qr, const float4* __rest
     return acc;
 }
 
-// one wave per query: exact distances of its candidates (or of every train row when the
-// candidate list overflowed), then the k=2 result with the sweep's tie rule
+// k=2 update with the sweep's tie rule (lowest train index first among equal distances)
+__device__ __forceinline__ void top2_consider(float acc, int j, float& b0, int& j0, float& b1) {
+    if (acc < b0 || (acc == b0 && j < j0)) {
+        b1 = b0;
+        b0 = acc;
+        j0 = j;
+    } else if (acc < b1) {
+        b1 = acc;
+    }
+}
+
+// one lane per query: exact distances of its candidates (~2 on SURF-like data); a query whose
+// candidate list overflowed goes to the overflow list (exact sweep, knn2_sweep_kernel)
 __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restrict__ dq,
                                                            const float* __restrict__ dt,
                                                            const int64_t* __restrict__ off_q,
@@ -270,49 +321,73 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                                                            int max_nq,
                                                            const int32_t* __restrict__ ccount,
                                                            const int32_t* __restrict__ cand,
-                                                           Top2* __restrict__ part) {
-    const int p = blockIdx.y, lane = wave_lane();
-    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                           Top2* __restrict__ part,
+                                                           int32_t* __restrict__ ovf) {
+    const int p = blockIdx.y;
+    const int q = blockIdx.x * 256 + threadIdx.x;
     const int64_t qbase = off_q[p];
     const int nq = (int)(off_q[p + 1] - qbase);
     const int64_t tbase = off_t[p];
-    const int nt = (int)(off_t[p + 1] - tbase);
     if (q >= nq) return;
+    const int n = ccount[(size_t)p * max_nq + q];
+    if (n > kCandCap) {
+        const int slot = atomicAdd(&ovf[0], 1);
+        ovf[1 + 2 * slot] = p;
+        ovf[2 + 2 * slot] = q;
+        return;
+    }
     float4 qr[16];
     const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
 #pragma unroll
     for (int c = 0; c < 16; c++) qr[c] = qp[c];
-    const int n = ccount[(size_t)p * max_nq + q];
     float b0 = kInf, b1 = kInf;
     int j0 = 0x7fffffff;
-    auto consider = [&](int j) {
-        const float acc = exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim));
-        if (acc < b0 || (acc == b0 && j < j0)) {
-            b1 = b0;
-            b0 = acc;
-            j0 = j;
-        } else if (acc < b1) {
-            b1 = acc;
-        }
-    };
-    if (n <= kCandCap) {
-        if (lane < n) consider(cand[((size_t)p * max_nq + q) * kCandCap + lane]);
-    } else {
-        for (int j = lane; j < nt; j += 64) consider(j);
+    const int32_t* cl = cand + ((size_t)p * max_nq + q) * kCandCap;
+    for (int k = 0; k < n; k++) {
+        const int j = cl[k];
+        top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim)), j, b0,
+                      j0, b1);
     }
+    part[(size_t)p * max_nq + q] = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
+}
+
+// exact sweep over every train row for the overflow queries: one wave per query, a fixed grid
+// striding over the list
+__global__ __launch_bounds__(256) void knn2_sweep_kernel(const float* __restrict__ dq,
+                                                         const float* __restrict__ dt,
+                                                         const int64_t* __restrict__ off_q,
+                                                         const int64_t* __restrict__ off_t,
+                                                         int max_nq, const int32_t* __restrict__ ovf,
+                                                         Top2* __restrict__ part) {
+    const int lane = wave_lane();
+    const int nov = ovf[0];
+    for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < nov; w += gridDim.x * 4) {
+        const int p = ovf[1 + 2 * w], q = ovf[2 + 2 * w];
+        const int64_t qbase = off_q[p], tbase = off_t[p];
+        const int nt = (int)(off_t[p + 1] - tbase);
+        float4 qr[16];
+        const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const float ob0 = __shfl_xor(b0, o, 64), ob1 = __shfl_xor(b1, o, 64);
-        const int oj = __shfl_xor(j0, o, 64);
-        if (ob0 < b0 || (ob0 == b0 && oj < j0)) {
-            b1 = fminf(b0, ob1);
-            b0 = ob0;
-            j0 = oj;
-        } else {
-            b1 = fminf(b1, ob0);
+        for (int c = 0; c < 16; c++) qr[c] = qp[c];
+        float b0 = kInf, b1 = kInf;
+        int j0 = 0x7fffffff;
+        for (int j = lane; j < nt; j += 64)
+            top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim)), j,
+                          b0, j0, b1);
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const float ob0 = __shfl_xor(b0, o, 64), ob1 = __shfl_xor(b1, o, 64);
+            const int oj = __shfl_xor(j0, o, 64);
+            if (ob0 < b0 || (ob0 == b0 && oj < j0)) {
+                b1 = fminf(b0, ob1);
+                b0 = ob0;
+                j0 = oj;
+            } else {
+                b1 = fminf(b1, ob0);
+            }
         }
+        if (lane == 0) part[(size_t)p * max_nq + q] = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
     }
-    if (lane == 0) part[(size_t)p * max_nq + q] = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
 }
 
 // Fold chunk partials in train order (lowest index wins ties), apply the ratio test
@@ -1353,7 +1428,6 @@ __device__ __forceinline__ float bin_edge_s(int elo, int e) {
     return __uint_as_float((uint32_t)((elo << kMantBits) + e) << kBinShift);
 }
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // (key << 2) + base as ONE v_lshl_add_u32 (the compiler otherwise rewrites (x >> 19) << 2 as
@@ -1996,7 +2070,7 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     __shared__ double sv[1024];
     __shared__ int si[1024];
     __shared__ int cand[64];
-    __shared__ int ncand;
+    __shared__ int ws[16];
     __shared__ double sres[1];
     const int p = blockIdx.x, tid = threadIdx.x;
     const int K = kcount[p];
@@ -2067,33 +2141,20 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
         best = si[0];
         bv = sv[0];
         __syncthreads();
-        // near ties: rows within 1e-9 (relative) of the approximate minimum
-        if (tid == 0) ncand = 0;
-        __syncthreads();
+        // near ties: rows within 1e-9 (relative) of the approximate minimum; the first 64 of
+        // them in row order (contiguous row ranges per thread + an ordered scan: deterministic,
+        // and the lowest index of a run of identical rows is always kept)
         const double tol = 1e-9 * fabs(bv) + 1e-300;
-        for (int k = tid; k < K; k += 1024) {
-            if (Tm[k] <= bv + tol) {
-                const int slot = atomicAdd(&ncand, 1);
-                if (slot < 64) cand[slot] = k;
-            }
-        }
+        const int per = (K + 1023) / 1024;
+        const int ka = min(K, tid * per), kb = min(K, ka + per);
+        int cnt = 0;
+        for (int k = ka; k < kb; k++) cnt += Tm[k] <= bv + tol;
+        int nc;
+        int pos = block_exclusive_scan<1024>(cnt, ws, &nc);
+        for (int k = ka; k < kb && pos < 64; k++)
+            if (Tm[k] <= bv + tol) cand[pos++] = k;
         __syncthreads();
-        const int nc = ncand;
         if (nc > 1) {
-            // sort candidate indices (few) ascending
-            if (tid == 0) {
-                const int n = nc < 64 ? nc : 64;
-                for (int a = 1; a < n; a++) {
-                    const int key = cand[a];
-                    int b = a - 1;
-                    while (b >= 0 && cand[b] > key) {
-                        cand[b + 1] = cand[b];
-                        b--;
-                    }
-                    cand[b + 1] = key;
-                }
-            }
-            __syncthreads();
             const int n = nc < 64 ? nc : 64;
             const long lo = (long)(K * trim_lo), hi = (long)(K * trim_hi);
             float* buf = sortbuf + (size_t)p * npow2;
@@ -2175,25 +2236,40 @@ void init_constants() {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_red), red, sizeof(red));
 }
 
+size_t knn2_split_bytes(const BatchShape& sh) {
+    return (size_t)sh.n_pairs * sh.max_nt * (kDim * sizeof(__bf16) + sizeof(float));
+}
+
 hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
-                              const int64_t* off_t, const BatchShape& sh, float2* pu,
-                              int32_t* ccount, int32_t* cand, int pass, hipStream_t st) {
+                              const int64_t* off_t, const BatchShape& sh, void* split,
+                              float2* pu, int32_t* ccount, int32_t* cand, int pass,
+                              hipStream_t st) {
+    bf16x8* thi = (bf16x8*)split;
+    float* tn = (float*)(thi + (size_t)sh.n_pairs * sh.max_nt * 8);
+    if (pass == 1)
+        hipLaunchKernelGGL(knn2_split_kernel, dim3((sh.max_nt + 63) / 64, sh.n_pairs), dim3(256), 0,
+                           st, desc_t, off_t, sh.max_nt, thi, tn);
     dim3 grid((sh.max_nq + kFQ - 1) / kFQ, sh.fchunks, sh.n_pairs);
     if (pass == 1)
-        hipLaunchKernelGGL(knn2_filter_kernel<1>, grid, dim3(256), 0, st, desc_q, desc_t, off_q,
-                           off_t, sh.fchunk_len, sh.fchunks, sh.max_nq, pu, ccount, cand);
+        hipLaunchKernelGGL(knn2_filter_kernel<1>, grid, dim3(256), 0, st, desc_q, thi, tn,
+                           off_q, off_t, sh.fchunk_len, sh.fchunks, sh.max_nq, sh.max_nt, pu,
+                           ccount, cand);
     else
-        hipLaunchKernelGGL(knn2_filter_kernel<2>, grid, dim3(256), 0, st, desc_q, desc_t, off_q,
-                           off_t, sh.fchunk_len, sh.fchunks, sh.max_nq, pu, ccount, cand);
+        hipLaunchKernelGGL(knn2_filter_kernel<2>, grid, dim3(256), 0, st, desc_q, thi, tn,
+                           off_q, off_t, sh.fchunk_len, sh.fchunks, sh.max_nq, sh.max_nt, pu,
+                           ccount, cand);
     return hipGetLastError();
 }
 
 hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
                                const int64_t* off_t, const BatchShape& sh, const int32_t* ccount,
-                               const int32_t* cand, Top2* part, hipStream_t st) {
-    dim3 grid((sh.max_nq + 3) / 4, sh.n_pairs);
+                               const int32_t* cand, Top2* part, int32_t* ovf, hipStream_t st) {
+    hipLaunchKernelGGL(set_i32_kernel, dim3(1), dim3(1), 0, st, ovf, 0);
+    dim3 grid((sh.max_nq + 255) / 256, sh.n_pairs);
     hipLaunchKernelGGL(knn2_rescore_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
-                       sh.max_nq, ccount, cand, part);
+                       sh.max_nq, ccount, cand, part, ovf);
+    hipLaunchKernelGGL(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
+                       sh.max_nq, ovf, part);
     return hipGetLastError();
 }
 

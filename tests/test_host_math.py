@@ -97,3 +97,30 @@ def test_vfree_eigvec_matches_rotation_accumulated(oracle, harness, s):
         assert abs(np.linalg.norm(e2) - 1.0) < 1e-12
         worst = max(worst, min(np.abs(e1 - e2).max(), np.abs(e1 + e2).max()))
     assert worst < 1e-9, worst
+
+
+@pytest.mark.parametrize("s", [9, 10, 40])
+def test_min_eigvec_unstructured_grams(harness, s):
+    """Grams of random, unrelated bearing pairs (no common epipolar constraint: lambda_1 is not
+    small against lambda_2, so the direct inverse iteration may not settle and the Jacobi path
+    takes over): the vector is still the smallest eigenvector, as LAPACK's, up to sign."""
+    rng = np.random.default_rng(s)
+    worst = 0.0
+    for trial in range(60):
+        a = rng.standard_normal((s, 3))
+        b = rng.standard_normal((s, 3))
+        a /= np.linalg.norm(a, axis=1, keepdims=True)
+        b /= np.linalg.norm(b, axis=1, keepdims=True)
+        a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+        g36 = np.zeros(36)
+        harness.erph_gram36(_p(a), _p(b), s, _p(g36))
+        A = np.einsum("ni,nj->nij", a, b).reshape(s, 9)
+        w, v = np.linalg.eigh(A.T @ A)
+        if (w[1] - w[0]) < 1e-6 * w[-1]:
+            continue  # degenerate: the smallest eigenvector is not defined
+        e = np.zeros(9)
+        harness.erph_vec_fast(_p(g36), _p(e))
+        ref = v[:, 0]
+        err = min(np.abs(e - ref).max(), np.abs(e + ref).max())
+        worst = max(worst, err * (w[1] - w[0]) / w[-1])  # scale by the conditioning
+    assert worst < 1e-12, worst
