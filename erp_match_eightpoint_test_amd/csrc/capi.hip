@@ -202,8 +202,9 @@ erp::BatchShape make_shape(int n_pairs, int max_nq, int max_nt, int iters, doubl
 bool ensure_matcher(erp_ctx* c, const erp::BatchShape& sh) {
     const size_t PQ = (size_t)sh.n_pairs * sh.max_nq;
     return ensure(c->part, PQ * sizeof(erp::Top2)) &&
-           ensure(c->pu, PQ * sh.fchunks * sizeof(float2)) && ensure(c->ccount, PQ * 4) &&
-           ensure(c->cand, PQ * erp::kCandCap * 4) &&
+           ensure(c->pu, PQ * sh.fchunks * sizeof(float2)) &&
+           ensure(c->ccount, PQ * sh.fchunks * 2 * 4) &&
+           ensure(c->cand, PQ * sh.fchunks * 2 * erp::kCandSub * 4) &&
            ensure(c->tsplit, erp::knn2_split_bytes(sh)) && ensure(c->ovf, 4 + 8 * PQ);
 }
 
@@ -220,7 +221,6 @@ erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int
     }
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_CANDIDATES, st);
-        ERP_CK(hipMemsetAsync(cc, 0, (size_t)sh.n_pairs * sh.max_nq * 4, st));
         ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand, 2, st));
     }
     {

@@ -11,7 +11,8 @@ namespace erp {
 constexpr int kDim = 64;          // SURF descriptor length (extended=false)
 constexpr int kMaxQ = 24;         // jump polynomials x^(64(M-1)2^k): waves per pair < 2^24
 constexpr int kPolyWords = 31;    // glibc TYPE_3 degree
-constexpr int kCandCap = 64;      // matcher candidates kept per query (more: exact sweep)
+constexpr int kCandSub = 32;      // matcher candidates kept per (query, train chunk, lane half)
+                                  // (more: exact sweep of the query)
 
 struct Top2 {                     // partial k=2 result of one train chunk for one query
     float d0;                     // best squared distance

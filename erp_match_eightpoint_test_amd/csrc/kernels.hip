@@ -76,15 +76,18 @@ __device__ int block_exclusive_scan(int v, int* ws, int* total) {
 //     Bound: with |q_i - qh_i| <= 2^-8 |q_i| (bf16 round-to-nearest, 8 significant bits),
 //     |q.t - qh.th| <= sum |qh_i||t_i - th_i| + |q_i - qh_i||t_i| <= 2^-7 (1 + 2^-9) |q||t|
 //     <= 2^-8 (1 + 2^-9) (|q|^2 + |t|^2); the MFMA's f32 accumulation of 64 exact products,
-//     the f32 norms and the reference's own rounding of e add < 2^-16 (|q|^2 + |t|^2).  So
-//     |a - e| <= 2^-6.98 (|q|^2 + |t|^2) < eps(q,t) = 2^-6 (|q|^2 + |t|^2) for the
-//     reference's exact f32 value e.  Each query keeps the two smallest u = a + eps per chunk.
+//     the f32 norms, the reference's own rounding of e (64 f32 squares summed: <= 2^-16.9 S)
+//     and the bound's own f32 formation add < 1.7e-5 (|q|^2 + |t|^2).  So
+//     |a - e| <= 0.0078444 (|q|^2 + |t|^2) < eps(q,t) = 0x1.08p-7 (|q|^2 + |t|^2) = 0.0080566
+//     (|q|^2 + |t|^2) for the reference's exact f32 value e.  Each query keeps the two
+//     smallest u = a + eps per chunk.
 //  2. knn2_filter<2>: U2 = the second smallest u over all chunks bounds e of the true second
 //     neighbour from above; every train row with l = a - eps <= U2 (which includes every row
 //     with e <= e_(2), i.e. both true neighbours and all their ties) is a candidate (a few per
-//     query on SURF-like data: the rows within 4 eps of the second neighbour).
+//     query on SURF-like data: the rows within 4 eps of the second neighbour).  Candidates go
+//     to per-(query, chunk, lane half) lists with a register counter: no atomics.
 //  3. knn2_rescore: exact flann::L2 distances of the candidates (a full exact sweep if a query
-//     ever has more than kCandCap), giving (d0, j0, d1) exactly.
+//     ever has more than kCandSub in one list), giving (d0, j0, d1) exactly.
 // The train rows are rounded to bf16 ONCE per batch (knn2_split: bf16 rows and |t|^2, dense
 // [pair][row] layout) and staged per 32-row tile into LDS by plain copies.
 // Matrix layout for v_mfma_f32_32x32x16_bf16: A = 32 train rows x 16 dims (LDS), B = 16 dims x
@@ -102,7 +105,7 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kFQ = 128;            // queries per block
 constexpr int kFT = 32;             // train rows per tile
 constexpr int kFRow = 72;           // bf16 per LDS row: 64 + 8 pad (conflict-free b128 reads)
-constexpr float kFEps = 0x1p-6f;
+constexpr float kFEps = 0x1.08p-7f;
 constexpr float kFTiny = 0x1p-100f; // absolute floor (flushed denormals)
 
 struct FilterLds {
@@ -201,6 +204,10 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
         U2 = m2;
     }
     float m1 = kInf, m2 = kInf;
+    // pass 2: this lane's candidate list (query q, this chunk, lane half h)
+    const size_t cl = (((size_t)p * max_nq + (qv ? q : 0)) * chunks + blockIdx.y) * 2 + h;
+    int32_t* clist = cand + cl * kCandSub;
+    int ncand = 0;
     // staging: thread -> train row tid >> 3 of the tile, 16 bytes (tid & 7) of it
     const int srow = tid >> 3, spart = tid & 7;
     const bf16x8* thp = thi + (size_t)p * max_nt * 8;
@@ -259,7 +266,7 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
 #pragma unroll
             for (int e = 0; e < 8; e++) mn = fminf(mn, fminf(b2[e][0], b2[e][1]));
             const bool any = qv && mn <= U2;
-            if (__builtin_amdgcn_ballot_w64(any)) {  // rare: most tiles have no candidate
+            if (__builtin_amdgcn_ballot_w64(any)) {  // most tiles have no candidate
                 uint32_t cmask = 0;  // element 2e + c <-> register 4 (e >> 1) + 2 (e & 1) + c
 #pragma unroll
                 for (int e = 0; e < 8; e++)
@@ -269,10 +276,8 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
                 while (cmask) {
                     const int bit = __builtin_ctz(cmask);  // = accumulator register index
                     cmask &= cmask - 1u;
-                    const int slot = atomicAdd(&ccount[(size_t)p * max_nq + q], 1);
-                    if (slot < kCandCap)
-                        cand[((size_t)p * max_nq + q) * kCandCap + slot] =
-                            tile0 + 8 * (bit >> 2) + 4 * h + (bit & 3);
+                    if (ncand < kCandSub) clist[ncand] = tile0 + 8 * (bit >> 2) + 4 * h + (bit & 3);
+                    ncand++;
                 }
             }
         }
@@ -282,6 +287,8 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
         const float n2 = fminf(fmaxf(m1, o1), fminf(m2, o2));
         const float n1 = fminf(m1, o1);
         if (h == 0 && qv) pu[((size_t)p * chunks + blockIdx.y) * max_nq + q] = make_float2(n1, n2);
+    } else if (qv) {
+        ccount[cl] = ncand;
     }
 }
 
@@ -318,7 +325,7 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                                                            const float* __restrict__ dt,
                                                            const int64_t* __restrict__ off_q,
                                                            const int64_t* __restrict__ off_t,
-                                                           int max_nq,
+                                                           int max_nq, int chunk_len, int chunks,
                                                            const int32_t* __restrict__ ccount,
                                                            const int32_t* __restrict__ cand,
                                                            Top2* __restrict__ part,
@@ -329,8 +336,12 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
     const int nq = (int)(off_q[p + 1] - qbase);
     const int64_t tbase = off_t[p];
     if (q >= nq) return;
-    const int n = ccount[(size_t)p * max_nq + q];
-    if (n > kCandCap) {
+    const int nt = (int)(off_t[p + 1] - tbase);
+    const int nl = 2 * ((nt + chunk_len - 1) / chunk_len);  // lists of this query
+    const size_t l0 = ((size_t)p * max_nq + q) * chunks * 2;
+    bool over = false;
+    for (int l = 0; l < nl; l++) over = over || ccount[l0 + l] > kCandSub;
+    if (over) {
         const int slot = atomicAdd(&ovf[0], 1);
         ovf[1 + 2 * slot] = p;
         ovf[2 + 2 * slot] = q;
@@ -342,11 +353,14 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
     for (int c = 0; c < 16; c++) qr[c] = qp[c];
     float b0 = kInf, b1 = kInf;
     int j0 = 0x7fffffff;
-    const int32_t* cl = cand + ((size_t)p * max_nq + q) * kCandCap;
-    for (int k = 0; k < n; k++) {
-        const int j = cl[k];
-        top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim)), j, b0,
-                      j0, b1);
+    for (int l = 0; l < nl; l++) {
+        const int n = ccount[l0 + l];
+        const int32_t* cl = cand + (l0 + l) * kCandSub;
+        for (int k = 0; k < n; k++) {
+            const int j = cl[k];
+            top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim)), j,
+                          b0, j0, b1);
+        }
     }
     part[(size_t)p * max_nq + q] = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
 }
@@ -2267,7 +2281,7 @@ hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const i
     hipLaunchKernelGGL(set_i32_kernel, dim3(1), dim3(1), 0, st, ovf, 0);
     dim3 grid((sh.max_nq + 255) / 256, sh.n_pairs);
     hipLaunchKernelGGL(knn2_rescore_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
-                       sh.max_nq, ccount, cand, part, ovf);
+                       sh.max_nq, sh.fchunk_len, sh.fchunks, ccount, cand, part, ovf);
     hipLaunchKernelGGL(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
                        sh.max_nq, ovf, part);
     return hipGetLastError();

@@ -80,7 +80,7 @@ def _all_queries_vs_oracle(ctx, oracle, q, t):
 
 
 def test_match_filter_candidate_overflow(ctx, oracle):
-    """>64 train rows inside the filter's error window of one query (near-duplicates differing
+    """>32 train rows inside the filter's error window of one query (near-duplicates differing
     in the last bits): the candidate list overflows and the exact sweep path must decide."""
     rng = np.random.default_rng(11)
     t = synth.random_descriptors(rng, 1200)
