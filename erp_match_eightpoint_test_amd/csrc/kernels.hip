@@ -890,15 +890,21 @@ __global__ __launch_bounds__(256) void gram_limbs_kernel(const int32_t* __restri
 }
 
 // Block = 4 waves x 32 iterations (one MFMA row tile each); K loop over the pair's selection
-// words with the 7 KB limb tile of the next word staged into LDS (double buffer) while the
-// current one feeds 7 MFMAs per wave.  gram[p][36][iters] (SoA, the eigen kernels' layout).
+// words, two words (64 rows, 14 MFMAs per wave) per step.  The next step's limb tiles (2 x 7 KB)
+// are loaded into registers while the current step's feed the MFMAs, and written to the other
+// LDS buffer after them (one barrier per step).  gram[p][36][iters] (SoA, the eigen layout).
+constexpr int kGramWords = 2;                                 // selection words per K step
+constexpr int kGramStepPieces = kGramWords * kGramN * 2;      // 16-B pieces per step (896)
+constexpr int kGramPiecesPerThread = (kGramStepPieces + 255) / 256;
+constexpr int kGramLdsWord = kGramN * kGramLdsCol;            // LDS bytes per staged word
+
 __global__ __launch_bounds__(256, 2) void gram_mfma_kernel(const int32_t* __restrict__ counts,
-                                                        const int8_t* __restrict__ limbs,
-                                                        const uint32_t* __restrict__ selw,
-                                                        int iters, int nwaves, int nbw,
-                                                        double sample_frac,
-                                                        double* __restrict__ gram) {
-    __shared__ __align__(16) int8_t bs[2][kGramN * kGramLdsCol];
+                                                           const int8_t* __restrict__ limbs,
+                                                           const uint32_t* __restrict__ selw,
+                                                           int iters, int nwaves, int nbw,
+                                                           double sample_frac,
+                                                           double* __restrict__ gram) {
+    __shared__ __align__(16) int8_t bs[2][kGramWords * kGramLdsWord];
     const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
@@ -906,54 +912,77 @@ __global__ __launch_bounds__(256, 2) void gram_mfma_kernel(const int32_t* __rest
     const int hb = blockIdx.x * 128;
     if (hb >= iters) return;  // uniform over the block
     const int nb = (M - 1) / 31 + 1;
+    const int nsteps = (nb + kGramWords - 1) / kGramWords;
     const int h0 = hb + wv * 32;
     const int r = lane & 31, hh = lane >> 5;
     const int h = h0 + r;
     const bool hv = h < iters;
     const uint32_t* sp = selw + ((size_t)p * nwaves + (hv ? h >> 6 : 0)) * (size_t)nbw * 64 + (h & 63);
     const uint4* lg = reinterpret_cast<const uint4*>(limbs + (size_t)p * nbw * kGramN * 32);
-    // staging: the 448 16-B pieces of a word's tile, piece q -> column q >> 1, half q & 1
-    constexpr int kPieces = kGramN * 2;
-    uint4 st0 = make_uint4(0u, 0u, 0u, 0u), st1 = st0;
-    auto stage_load = [&](int b) {
-        st0 = lg[(size_t)b * kPieces + tid];
-        if (tid + 256 < kPieces) st1 = lg[(size_t)b * kPieces + tid + 256];
+    // staging piece q of a step: word q / (2 kGramN), column (q >> 1) % kGramN, half q & 1
+    uint4 stg[kGramPiecesPerThread];
+    auto stage_load = [&](int step) {
+#pragma unroll
+        for (int i = 0; i < kGramPiecesPerThread; i++) {
+            const int q = tid + 256 * i;
+            const int w = step * kGramWords + q / (2 * kGramN);
+            stg[i] = (q < kGramStepPieces && w < nb)
+                         ? lg[(size_t)step * kGramStepPieces + q]
+                         : make_uint4(0u, 0u, 0u, 0u);
+        }
     };
     auto stage_store = [&](int buf) {
-        *reinterpret_cast<uint4*>(&bs[buf][(tid >> 1) * kGramLdsCol + (tid & 1) * 16]) = st0;
-        if (tid + 256 < kPieces)
-            *reinterpret_cast<uint4*>(&bs[buf][((tid + 256) >> 1) * kGramLdsCol + (tid & 1) * 16]) = st1;
+#pragma unroll
+        for (int i = 0; i < kGramPiecesPerThread; i++) {
+            const int q = tid + 256 * i;
+            if (q < kGramStepPieces) {
+                const int w = q / (2 * kGramN), col = (q >> 1) % kGramN;
+                *reinterpret_cast<uint4*>(
+                    &bs[buf][w * kGramLdsWord + col * kGramLdsCol + (q & 1) * 16]) = stg[i];
+            }
+        }
+    };
+    auto sel_load = [&](int step, uint32_t (&w)[kGramWords]) {
+#pragma unroll
+        for (int i = 0; i < kGramWords; i++) {
+            const int b = step * kGramWords + i;
+            w[i] = (hv && b < nb) ? sp[(size_t)b * 64] : 0u;
+        }
     };
     i32x16 acc[kGramTiles];
 #pragma unroll
     for (int t = 0; t < kGramTiles; t++)
 #pragma unroll
         for (int k = 0; k < 16; k++) acc[t][k] = 0;
+    uint32_t wcur[kGramWords], wnext[kGramWords];
     stage_load(0);
     stage_store(0);
-    uint32_t wcur = hv ? sp[0] : 0u;
+    sel_load(0, wcur);
+    if (nsteps > 1) stage_load(1);
     __syncthreads();
-    for (int b = 0; b < nb; b++) {
-        const int buf = b & 1;
-        const bool more = b + 1 < nb;
-        uint32_t wnext = 0u;
-        if (more) {
-            stage_load(b + 1);
-            wnext = hv ? sp[(size_t)(b + 1) * 64] : 0u;
-        }
-        const uint32_t bits = (wcur >> (16 * hh)) & 0xffffu;
-        i32x4 a;
+    for (int st = 0; st < nsteps; st++) {
+        const int buf = st & 1;
+        if (st + 1 < nsteps) sel_load(st + 1, wnext);
 #pragma unroll
-        for (int v = 0; v < 4; v++)
-            a[v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
-        const int8_t* bt = &bs[buf][r * kGramLdsCol + hh * 16];
+        for (int i = 0; i < kGramWords; i++) {
+            const uint32_t bits = (wcur[i] >> (16 * hh)) & 0xffffu;
+            i32x4 a;
 #pragma unroll
-        for (int t = 0; t < kGramTiles; t++) {
-            const i32x4 bf = *reinterpret_cast<const i32x4*>(bt + t * 32 * kGramLdsCol);
-            acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf, acc[t], 0, 0, 0);
+            for (int v = 0; v < 4; v++)
+                a[v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
+            const int8_t* bt = &bs[buf][i * kGramLdsWord + r * kGramLdsCol + hh * 16];
+#pragma unroll
+            for (int t = 0; t < kGramTiles; t++) {
+                const i32x4 bf = *reinterpret_cast<const i32x4*>(bt + t * 32 * kGramLdsCol);
+                acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf, acc[t], 0, 0, 0);
+            }
         }
-        if (more) stage_store(buf ^ 1);
-        wcur = wnext;
+        if (st + 1 < nsteps) {
+            stage_store(buf ^ 1);                   // tile st+1 (loaded during step st-1)
+            if (st + 2 < nsteps) stage_load(st + 2);
+#pragma unroll
+            for (int i = 0; i < kGramWords; i++) wcur[i] = wnext[i];
+        }
         __syncthreads();
     }
     // recombine: row = (k & 3) + 8 (k >> 2) + 4 hh; entry r from tiles 0..5 of this lane,
