@@ -32,6 +32,8 @@ PEAK_FP32_VALU_UNFUSED = 157.3 / 2  # TFLOP/s: 157.3 counts an FMA as 2; sub/mul
 PEAK_FP64_VALU = 78.6               # TFLOP/s (MI355X spec, FMA = 2)
 PEAK_HBM = 8000.0                   # GB/s
 PEAK_BF16_MFMA = 2516.6             # TFLOP/s dense (256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz)
+PEAK_I8_MFMA = 2 * PEAK_BF16_MFMA   # TOP/s dense (32x32x32 i8 = the cycles of 32x32x16 bf16)
+PEAK_VALU_OPS = 256 * 64 * 2.4e9 / 1e12  # T lane-ops/s: 64 VALU lanes per CU per clock
 
 
 def parse():
@@ -47,7 +49,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=20200423)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--profile-tag", default="r01c")
+    ap.add_argument("--profile-tag", default="r01d")
     return ap.parse_args()
 
 
@@ -73,26 +75,23 @@ def to_device(pairs, dev):
 
 
 def stage_work(stage, B, kpts, iters, res):
-    """algorithmic work of ONE launch of `stage` over the batch (SURVEY.md §8d):
+    """algorithmic work of ONE launch of `stage` over the batch (SURVEY.md §8d, DESIGN.md §3):
     returns (amount, unit, peak, bound, note)."""
     M = res["M"].astype(np.float64)
-    s = np.floor(M * 0.25)
     K = res["K"].astype(np.float64)
     if stage in ("knn2_filter", "knn2_candidates"):
-        flops = 3 * 2.0 * kpts * kpts * 64 * B  # q_hi t_hi + q_hi t_lo + q_lo t_hi, bf16 MFMA
-        return flops, "TFLOP/s", PEAK_BF16_MFMA, "mfma", "3 bf16 MFMA products x 2*N*T*64 per pair"
+        flops = 2.0 * kpts * kpts * 64 * B  # one bf16 product qh.th per (query, train) pair
+        return flops, "TFLOP/s", PEAK_BF16_MFMA, "mfma", "2*N*T*64 bf16 MFMA flops per pair"
     if stage == "gram":
-        flops = float(np.sum(s * iters * (12 + 72)))  # 12 mul + 36 FMA per sampled row, fp64
-        return flops, "TFLOP/s", PEAK_FP64_VALU, "valu", "84 fp64 flops per sampled row"
+        nb = np.floor((M - 1) / 31) + 1  # selection words (31 rows + 1 pad each)
+        ops = float(np.sum(2.0 * iters * 32 * nb * 216))  # 6 int8 limbs x 36 Gram entries
+        return ops, "TOP/s", PEAK_I8_MFMA, "mfma", "2*I*32*nb*216 int8 MFMA ops per pair"
     if stage == "consensus_bounds":
         flops = float(np.sum(K * K * 8.0))  # 3 sub, 3 mul, 2 add per squared distance, K^2
         return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", "8 fp32 ops per squared distance, K^2"
-    if stage == "consensus_rows":
-        flops = float(np.sum(K * K * 9.0))  # 3 sub, 3 mul, 2 add, 1 sqrt per distance
-        return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", "9 fp32 ops per distance, K^2"
-    if stage == "eigen":
-        flops = float(iters * B * 40000.0)
-        return flops, "TFLOP/s", PEAK_FP64_VALU, "valu", "~4e4 fp64 flops per 9x9 Jacobi"
+    if stage == "sampler":
+        ops = float(np.sum((M - 1) * iters * 4.0))  # per draw: recurrence, shift, remainder, test
+        return ops, "Top/s", PEAK_VALU_OPS, "valu", "4 int/fp64 ops per rand() draw (floor)"
     return None
 
 
@@ -221,6 +220,16 @@ def main():
         roof = {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
                 "frac": achieved / peak, "traffic": load_pmc(args.profile_tag, dom),
                 "avg_launch_ms": avg_s * 1e3, "work_per_launch": amount, "work_note": note}
+    stage_roofs = {}
+    for k in stages:
+        w = stage_work(k, args.pairs, args.kpts, args.iters, res)
+        if w is None or stages[k][1] == 0:
+            continue
+        amount, unit, peak, bound, note = w
+        avg_s = stages[k][0] / stages[k][1] / 1e3
+        stage_roofs[k] = {"bound": bound, "achieved": amount / avg_s / 1e12, "peak": peak,
+                          "unit": unit, "frac": amount / avg_s / 1e12 / peak,
+                          "avg_launch_ms": avg_s * 1e3}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(pairs, args.iters, args.cpu_seconds)
@@ -236,6 +245,7 @@ def main():
                    "streams": S,
                    "parallelism": f"pair-sharded x{world}", "sampler": "glibc replay (seed 1)"},
         "roofline": roof,
+        "roofline_stages": stage_roofs,
         "cpu_baseline": cpu,
         "stages_ms_per_step": {k: v[0] / max(args.steps, 1) for k, v in stages.items()},
         "check": {"all_status_ok": ok, "mean_abs_euler_err_deg_max": max(err_deg),

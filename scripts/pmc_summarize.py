@@ -32,8 +32,8 @@ STAGE_KERNEL = {
     "knn2_filter": "knn2_filter_kernel<1>", "knn2_candidates": "knn2_filter_kernel<2>",
     "knn2_rescore": "knn2_rescore_kernel", "knn2_merge": "knn2_merge_kernel",
     "bearings": "bearings_from_matches_kernel", "jump_prep": "jump_prep_kernel",
-    "windows": "sampler_window_kernel", "sampler": "sampler_kernel", "gram": "gram_kernel",
-    "eigen": "eigen_kernel", "valid_compact": "valid_compact_kernel",
+    "windows": "sampler_window_kernel", "sampler": "sampler_kernel", "gram": "gram_mfma_kernel",
+    "eigen": "eigen_kernel<false>", "valid_compact": "valid_compact_kernel",
     "consensus_bounds": "consensus_bounds_kernel", "consensus_select": "consensus_select_kernel",
     "consensus_refine": "consensus_refine_kernel", "consensus_rows": "consensus_rows_kernel",
     "consensus_final": "consensus_final_kernel",
@@ -41,12 +41,16 @@ STAGE_KERNEL = {
 
 
 def short(name: str) -> str:
-    """'erp::(anonymous namespace)::knn2_filter_kernel<1>(float const*, ...)' -> 'knn2_filter_kernel<1>'"""
-    n = name.split("(")[0] if "(" in name and not name.startswith("void ") else name
-    n = re.sub(r"^void\s+", "", n)
-    n = n.split("(")[0]
+    """'erp::(anonymous namespace)::knn2_filter_kernel<1>(float const*, ...)' or its mangled form
+    '_ZN3erp12_GLOBAL__N_118knn2_filter_kernelILi1EEEv...' -> 'knn2_filter_kernel<1>'"""
+    m = re.search(r"([a-z][a-z0-9_]*_kernel)(?:IL([ib])(\d+)E)?", name) if name.startswith("_Z") else None
+    if m:
+        if not m.group(2):
+            return m.group(1)
+        v = m.group(3) if m.group(2) == "i" else ("true" if m.group(3) == "1" else "false")
+        return f"{m.group(1)}<{v}>"
     m = re.search(r"([A-Za-z0-9_]+_kernel(?:<[^>]*>)?)", name)
-    return m.group(1) if m else n.split("::")[-1]
+    return m.group(1) if m else name.split("(")[0].split("::")[-1]
 
 
 def find_csv(d: str, suffix: str) -> str | None:

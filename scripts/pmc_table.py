@@ -17,8 +17,14 @@ acc = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
 for d in args:
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(path)):
-            m = re.search(r"([A-Za-z0-9_]+_kernel(?:<[^>]*>)?)", row["Kernel_Name"])
-            k = m.group(1) if m else row["Kernel_Name"][:40]
+            nm = row["Kernel_Name"]
+            m = re.search(r"([a-z][a-z0-9_]*_kernel)(?:IL([ib])(\d+)E)?", nm) if nm.startswith("_Z") else None
+            if m:
+                v = "" if not m.group(2) else (m.group(3) if m.group(2) == "i" else ("true" if m.group(3) == "1" else "false"))
+                k = m.group(1) + (f"<{v}>" if v else "")
+            else:
+                m = re.search(r"([A-Za-z0-9_]+_kernel(?:<[^>]*>)?)", nm)
+                k = m.group(1) if m else nm[:40]
             acc[k][row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
 for k, cs in sorted(acc.items()):
     if filt and not any(f in k for f in filt):
