@@ -21,6 +21,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -213,29 +214,34 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     const bf16x8* thp = thi + (size_t)p * max_nt * 8;
     const float* tnp = tn + (size_t)p * max_nt;
     const bf16x8 z8 = {};
-    bf16x8 gh = z8;
-    float gn = kInf;
-    auto gload = [&](int tile0) {
+    // two tiles in flight: tile k+2 is loaded while tile k is computed (one tile of work is
+    // shorter than an L2 round trip)
+    bf16x8 gh[2] = {z8, z8};
+    float gn[2] = {kInf, kInf};
+    auto gload = [&](int tile0, int slot) {
         const int j = tile0 + srow;
         if (j < t1) {
-            gh = thp[(size_t)j * 8 + spart];
-            if (spart == 0) gn = tnp[j];
+            gh[slot] = thp[(size_t)j * 8 + spart];
+            if (spart == 0) gn[slot] = tnp[j];
         } else {
-            gh = z8;
-            gn = kInf;
+            gh[slot] = z8;
+            gn[slot] = kInf;
         }
     };
     const int ntiles = (t1 - t0 + kFT - 1) / kFT;
-    gload(t0);
+    gload(t0, 0);
+    if (ntiles > 1) gload(t0 + kFT, 1);
     const int r = lane & 31;
-    for (int k = 0; k < ntiles; k++) {
-        const int buf = k & 1, tile0 = t0 + k * kFT;
-        sm.hi[buf][(srow * kFRow) / 8 + spart] = gh;
+    auto tile_step = [&](int k, auto slot_c) {
+        constexpr int buf = decltype(slot_c)::value;
+        const int tile0 = t0 + k * kFT;
+        sm.hi[buf][(srow * kFRow) / 8 + spart] = gh[buf];
         if (spart == 0)
-            sm.tb[buf][srow] = gn == kInf ? kInf
-                                          : __builtin_fmaf(gn, PASS == 1 ? kFEps : -kFEps, gn);
+            sm.tb[buf][srow] = gn[buf] == kInf
+                                   ? kInf
+                                   : __builtin_fmaf(gn[buf], PASS == 1 ? kFEps : -kFEps, gn[buf]);
         __syncthreads();
-        if (k + 1 < ntiles) gload(tile0 + kFT);
+        if (k + 2 < ntiles) gload(tile0 + 2 * kFT, buf);
         f32x16 acc = {};
 #pragma unroll
         for (int c = 0; c < 4; c++) {
@@ -281,6 +287,10 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
                 }
             }
         }
+    };
+    for (int k = 0; k < ntiles; k += 2) {
+        tile_step(k, std::integral_constant<int, 0>{});
+        if (k + 1 < ntiles) tile_step(k + 1, std::integral_constant<int, 1>{});
     }
     if (PASS == 1) {
         const float o1 = __shfl_xor(m1, 32, 64), o2 = __shfl_xor(m2, 32, 64);
