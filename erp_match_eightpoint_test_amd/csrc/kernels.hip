@@ -98,9 +98,9 @@ __device__ int block_exclusive_scan(int v, int* ws, int* total) {
 //   u = fma(-2, qh.th, qu + tu),  qu = |q|^2 (1 + eps) + tiny,  tu = |t|^2 (1 + eps)
 //   l = fma(-2, qh.th, ql + tl),  ql = |q|^2 (1 - eps) - tiny,  tl = |t|^2 (1 - eps)
 // (= a +- (eps (|q|^2 + |t|^2) + tiny) up to four more f32 roundings, <= 2^-21 (|q|^2 + |t|^2),
-// inside the bound's slack).  Pass 1 keeps the two smallest u per query (v_med3 / v_min);
-// pass 2 takes the minimum l of the lane's 16 rows and only builds the candidate mask when it
-// reaches U2 (rare).
+// inside the bound's slack).  Pass 1 keeps two group minima of u per lane (v_min3), whose top-2
+// over the query's lanes and chunks bounds its second smallest u; pass 2 takes the minimum l of
+// the lane's 16 rows and only builds the candidate mask when it reaches U2.
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kFQ = 128;            // queries per block
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
         }
         U2 = m2;
     }
-    float m1 = kInf, m2 = kInf;
+    float gm0 = kInf, gm1 = kInf;  // pass 1: group minima
     // pass 2: this lane's candidate list (query q, this chunk, lane half h)
     const size_t cl = (((size_t)p * max_nq + (qv ? q : 0)) * chunks + blockIdx.y) * 2 + h;
     int32_t* clist = cand + cl * kCandSub;
@@ -258,14 +258,15 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
             b2[2 * g + 1] = __builtin_elementwise_fma(m2x, a1, qb2 + tb);
         }
         if (PASS == 1) {
+            // two running group minima per lane (elements c = 0 / c = 1 of the packed pairs):
+            // minima of different groups are different rows, so the second smallest of the
+            // query's group minima (4 per chunk: 2 lanes x 2 groups) bounds the second smallest
+            // u from above -- as tight unless both nearest rows fall into one group.  One
+            // v_min3 per two elements instead of v_med3 + v_min per element.
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-#pragma unroll
-                for (int c = 0; c < 2; c++) {
-                    const float u = b2[e][c];
-                    m2 = __builtin_amdgcn_fmed3f(m1, m2, u);
-                    m1 = fminf(m1, u);
-                }
+            for (int e = 0; e < 8; e += 2) {
+                gm0 = fminf(gm0, fminf(b2[e][0], b2[e + 1][0]));
+                gm1 = fminf(gm1, fminf(b2[e][1], b2[e + 1][1]));
             }
         } else {
             float mn = kInf;
@@ -293,6 +294,8 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
         if (k + 1 < ntiles) tile_step(k + 1, std::integral_constant<int, 1>{});
     }
     if (PASS == 1) {
+        // top-2 of the query's four group minima (this lane's two and the other half's two)
+        const float m1 = fminf(gm0, gm1), m2 = fmaxf(gm0, gm1);
         const float o1 = __shfl_xor(m1, 32, 64), o2 = __shfl_xor(m2, 32, 64);
         const float n2 = fminf(fmaxf(m1, o1), fminf(m2, o2));
         const float n1 = fminf(m1, o1);
