@@ -1677,7 +1677,8 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
 
 // Tighter bounds for the surviving rows (4 per block, lanes rotating over the rows as in the
 // bounds kernel).  For each row: the exact s of every column (the reference's expression),
-// an fp64 sum of sqrtf(s) over the bins strictly between b_a and b_b (the bins of ranks lo and
+// an fp64 sum of sqrt(s) (raw v_sqrt_f32, bracketed by its 2^-22 error bound) over the bins
+// strictly between b_a and b_b (the bins of ranks lo and
 // hi-1 from the bounds kernel), exact counts below them, and 1024-way sub-histograms (key bits
 // 18..9) of the two boundary bins.  The window's part inside a boundary bin is bracketed with
 // sub-bin resolution (2^-15 relative instead of 2^-5), so the bounds tighten by ~1000x and the
@@ -1741,7 +1742,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
             bel_a[t] += e < ba[t];
             bel_b[t] += e < bb[t];
             if (e > ba[t] && e < bb[t]) {
-                acc[t] += (double)__builtin_sqrtf(s);
+                acc[t] += (double)__builtin_amdgcn_sqrtf(s);  // raw v_sqrt_f32, <= 1 ulp
             } else if (e == ba[t] || e == bb[t]) {
                 const int r = (lane + t) & (kRefineRows - 1);
                 atomicAdd(&sub[r][e == ba[t] ? 0 : 1][(key >> kLowBits) & (kNS - 1u)], 1u);
@@ -1823,7 +1824,10 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     if (sl == 0 && ok) {
         const double w = (double)(hi - lo);
         const double in = inner[r];
-        const double nl = ((in + L) / w) * (1.0 - 1e-9), nu = ((in + U) / w) * (1.0 + 1e-9);
+        // the inner sum used the raw v_sqrt_f32 (<= 2^-23 relative, flushes below 2^-126):
+        // bracket it by 2^-22 relative plus 2^-63 per term (the inner count is at most K)
+        const double inl = in * (1.0 - 0x1p-22), inu = in * (1.0 + 0x1p-22) + (double)K * 0x1p-63;
+        const double nl = ((inl + L) / w) * (1.0 - 1e-9), nu = ((inu + U) / w) * (1.0 + 1e-9);
         double* lp = lb + (size_t)p * stride + row;
         double* up = ub + (size_t)p * stride + row;
         *lp = fmax(*lp, nl);
