@@ -1436,12 +1436,13 @@ __global__ __launch_bounds__(1024) void consensus_input_kernel(const float* __re
 // ---- pruning by rigorous bounds -------------------------------------------------------
 // Every row's K squared distances are binned into NB geometric bins: 16 per binade of s = d^2
 // (= 32 per binade of the distance d) over the 36 binades of s below the squared diameter of
-// the set, underflow in bin 0.  The binned value is s' = fma(dz, dz, fma(dy, dy, dx * dx)):
-// with S = dx^2 + dy^2 + dz^2 exactly (the reference's dx = fl(x_i - x_j), identical here), s'
-// is within (1 +- 3.0001 u) of S (three correctly rounded operations on non-negative terms,
-// u = 2^-24) and so is the reference's s = dx*dx + dy*dy + dz*dz, so s' in bin [E_b, E_b+1)
-// puts the reference's d = sqrtf(s) in
-//   [sqrt(E_b (1 - 2^-20)) (1 - 2^-20), sqrt(E_b+1 (1 + 2^-20)) (1 + 2^-20)]
+// the set, underflow in bin 0.  The binned value is the biased s' = fma(dz, dz, fma(dy, dy,
+// fma(dx, dx, E0g))) (E0g: bounds_bias below): with S = dx^2 + dy^2 + dz^2 exactly (the
+// reference's dx = fl(x_i - x_j), identical here), s' is within (1 +- 3.0001 u) of S + E0g
+// (three correctly rounded operations on non-negative terms, u = 2^-24) and so is the
+// reference's s = dx*dx + dy*dy + dz*dz of S, so s' in bin [E_b, E_b+1) puts the reference's
+// d = sqrtf(s) in
+//   [sqrt(E_b (1 - 2^-20) - E0g) (1 - 2^-20), sqrt(E_b+1 (1 + 2^-20)) (1 + 2^-20)]
 // (the 2^-20 factors absorb the 6u of both roundings and sqrtf).  From the exact bin counts
 // the trimmed sum over ranks [lo, hi) is bracketed by
 //   LB = sum_b n_b(window) * lower_b,  UB = sum_b n_b(window) * upper_b
@@ -1454,8 +1455,8 @@ __global__ __launch_bounds__(1024) void consensus_input_kernel(const float* __re
 // takes row (l + t) & 15, so the 32 lanes of an LDS lane group hit each row twice and collide
 // at most 2-way (a random scatter of 32 lanes over 32 banks, the [row][bin] layout, costs ~3.5x:
 // that was 2/3 of the kernel's LDS time).  Rows t, t+1 share packed f32 instructions
-// (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 with the column broadcast), the key is clamped
-// to the first bin (v_max_u32) and the LDS byte address is one v_lshl_add_u32 of it: six VALU
+// (v_pk_add_f32 / v_pk_fma_f32 with the column broadcast), the bias keeps every key >= the
+// first guard bin, and the LDS byte address is one v_lshl_add_u32 of the key: five VALU
 // instructions and one ds_add_u32 per distance.  Four
 // blocks (39 KB of histograms each) per CU.  The d-space bin edges are per pair
 // (consensus_edges_kernel); the epilogue holds its slice's edges in registers.
@@ -1498,12 +1499,24 @@ __device__ __forceinline__ void lds_inc(uint32_t byte_addr) {
                            __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// d-space bounds of the reference's d for a key in bin b (header comment above), in f32:
-// E_b (1 -+ 2^-20) rounds by <= u, sqrtf adds u, the final product u: <= 3u < 2^-19, so the
-// (1 -+ 2^-19) factors keep the bounds outward.  Bin 0 also holds every s below E_1.
+// The bias: s' = fma(dz, dz, fma(dy, dy, fma(dx, dx, E0g))) with E0g = the lower edge of the
+// bin kGuard bins (4 binades) below bin 0: every key is >= base - kGuard, so the histogram
+// address needs no clamp -- keys in the kGuard guard bins below bin 0 (distances below the
+// range) are added to bin 0 by the epilogue.  The bias shifts s by E0g = E_0 / 16, i.e. by
+// 2^-(4 + binades above the floor) relative: negligible in the bins that hold the window's ranks.
+constexpr int kGuard = 64;
+__device__ __forceinline__ float bounds_bias(int elo) {
+    return bin_edge_s(elo > 4 ? elo - 4 : 1, 0);
+}
+// d-space bounds of the reference's d for a biased key in bin b (header comment above), in f32:
+// s' in [E_b, E_b+1) puts S in [E_b (1 - 3.0001u) - E0g, E_b+1 (1 + 3.0001u) - E0g] and the
+// reference's d within (1 +- 2u) of sqrt(S) (E0g <= E_b / 16: no cancellation); E_b (1 -+ 2^-20)
+// - E0g, sqrtf and the final product round by <= u each, so the (1 -+ 2^-19) factors keep the
+// bounds outward.  Bin 0 also holds every s below E_1 (the guard bins).
 __device__ __forceinline__ float bin_lower_d(int elo, int b) {
     if (b == 0) return 0.f;
-    return __builtin_sqrtf(bin_edge_s(elo, b) * (1.0f - 0x1p-20f)) * (1.0f - 0x1p-19f);
+    const float v = bin_edge_s(elo, b) * (1.0f - 0x1p-20f) - bounds_bias(elo);
+    return __builtin_sqrtf(fmaxf(v, 0.f)) * (1.0f - 0x1p-19f);
 }
 __device__ __forceinline__ float bin_upper_d(int elo, int b) {
     if (b == kNB - 1) return kInf;
@@ -1543,9 +1556,11 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     constexpr int NS = 256 / R;        // epilogue slices per row
     constexpr int per = kNB / NS;      // bins per slice
     static_assert(kNB % NS == 0, "slices");
-    __shared__ __align__(16) uint32_t hist[kNB * R];  // [bin][row]
-    __shared__ int part[NS][R];                       // per-slice counts
-    __shared__ float partL[NS][R], partU[NS][R];
+    __shared__ __align__(16) uint32_t hist[(kGuard + kNB) * R];  // [guard + bin][row]
+    // epilogue partials alias the histogram (read into registers first)
+    int (*part)[R] = reinterpret_cast<int (*)[R]>(hist);
+    float (*partL)[R] = reinterpret_cast<float (*)[R]>(hist + NS * R);
+    float (*partU)[R] = reinterpret_cast<float (*)[R]>(hist + 2 * NS * R);
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
     const int r0 = blockIdx.x * R;
@@ -1566,12 +1581,13 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
         xi[t >> 1][t & 1] = X[row];
         yi[t >> 1][t & 1] = Y[row];
         zi[t >> 1][t & 1] = Z[row];
-        hoff[t] = hist_addr + 4u * (uint32_t)r - 64u * (uint32_t)base;
+        hoff[t] = hist_addr + 4u * (uint32_t)r - 64u * (uint32_t)(base - kGuard);
     }
-    for (int k = tid; k < kNB * R / 4; k += 256)
+    for (int k = tid; k < (kGuard + kNB) * R / 4; k += 256)
         reinterpret_cast<uint4*>(hist)[k] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
-    const uint32_t ubase = (uint32_t)base;  // keys below the first bin go to bin 0
+    const float e0 = bounds_bias(elo);
+    const f32x2 bias = {e0, e0};
     // columns in batches of 4 per lane (j0 + 256 c + tid, c < 4: every load coalesced), the next
     // batch loaded while this one is binned (4 x 32 distances of VALU work hide the L2 latency)
     constexpr int CB = 4;
@@ -1598,13 +1614,11 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
 #pragma unroll
                 for (int t = 0; t < kPairs; t++) {
                     const f32x2 dx = xi[t] - xj, dy = yi[t] - yj, dz = zi[t] - zj;
-                    f32x2 s = dx * dx;
+                    f32x2 s = __builtin_elementwise_fma(dx, dx, bias);
                     s = __builtin_elementwise_fma(dy, dy, s);
                     s = __builtin_elementwise_fma(dz, dz, s);
-                    const uint32_t k0 = max(__float_as_uint(s[0]) >> kBinShift, ubase);
-                    const uint32_t k1 = max(__float_as_uint(s[1]) >> kBinShift, ubase);
-                    lds_inc(lshl6_add(k0, hoff[2 * t]));
-                    lds_inc(lshl6_add(k1, hoff[2 * t + 1]));
+                    lds_inc(lshl6_add(__float_as_uint(s[0]) >> kBinShift, hoff[2 * t]));
+                    lds_inc(lshl6_add(__float_as_uint(s[1]) >> kBinShift, hoff[2 * t + 1]));
                 }
             }
         }
@@ -1630,9 +1644,13 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     for (int q = 0; q < per; q++) {
         el[q] = ed[q];
         eu[q] = ed[kNB + q];
-        n[q] = (int)hist[(sl * per + q) * R + r];
-        c += n[q];
+        n[q] = (int)hist[(kGuard + sl * per + q) * R + r];
     }
+    if (sl == 0)  // distances below the range (guard bins) count as bin 0
+        for (int g = 0; g < kGuard; g++) n[0] += (int)hist[g * R + r];
+#pragma unroll
+    for (int q = 0; q < per; q++) c += n[q];
+    __syncthreads();  // every count is in registers: the partials may overwrite the histogram
     part[sl][r] = c;
     __syncthreads();
     int cum = 0;
