@@ -1592,20 +1592,26 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     // batch loaded while this one is binned (4 x 32 distances of VALU work hide the L2 latency)
     constexpr int CB = 4;
     float cx[CB], cy[CB], cz[CB], nx[CB], ny[CB], nz[CB];
+    // (unsigned 32-bit offsets from uniform bases: global_load with an SGPR base, no 64-bit
+    // address arithmetic per load)
+    const uint32_t kmax4 = 4u * (uint32_t)(K - 1);  // byte offsets (K < 2^30)
+    auto ld = [](const float* base, uint32_t off) {
+        return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + off);
+    };
 #pragma unroll
     for (int c = 0; c < CB; c++) {
-        const int j = min(c * 256 + tid, K - 1);
-        cx[c] = X[j];
-        cy[c] = Y[j];
-        cz[c] = Z[j];
+        const uint32_t o = min(4u * (uint32_t)(c * 256 + tid), kmax4);
+        cx[c] = ld(X, o);
+        cy[c] = ld(Y, o);
+        cz[c] = ld(Z, o);
     }
     for (int j0 = 0; j0 < K; j0 += CB * 256) {
 #pragma unroll
         for (int c = 0; c < CB; c++) {
-            const int j = min(j0 + CB * 256 + c * 256 + tid, K - 1);
-            nx[c] = X[j];
-            ny[c] = Y[j];
-            nz[c] = Z[j];
+            const uint32_t o = min(4u * (uint32_t)(j0 + CB * 256 + c * 256 + tid), kmax4);
+            nx[c] = ld(X, o);
+            ny[c] = ld(Y, o);
+            nz[c] = ld(Z, o);
         }
 #pragma unroll
         for (int c = 0; c < CB; c++) {
