@@ -765,10 +765,12 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
         const uint32_t bit = 1u << (j & 31);
         const bool isB = MODE == 1 || (MODE == 2 && ii < s);
         if (MODE == 0) {
-            const bool valid = j < (uint32_t)s;
-            const uint32_t orm = valid ? bit : 0u;
-            olds[u] = atomicOr(&bm[(valid ? (j >> 5) : 0u) * 64 + lane], orm);
-            sel[u] = orm;
+            // j >= s is clamped to the sentinel position s, whose bit is always set: the OR is
+            // harmless and the step is never selected (no validity select per step)
+            const uint32_t jc = min(j, (uint32_t)s);
+            const uint32_t bc = 1u << (jc & 31);
+            olds[u] = atomicOr(&bm[(jc >> 5) * 64 + lane], bc);
+            sel[u] = bc;
         } else {
             const uint32_t cw = ((ii >> 5) == wA) ? curA : curB;
             const uint32_t bi = (cw >> (ii & 31)) & 1u;
@@ -785,10 +787,10 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
             sel[u] = (validA || validB) ? bit : 0u;
         }
     }
+    // selected iff the step's bit was not yet set: sel & ~old != 0 (sel is 0 or one bit)
     uint32_t word = 0;
 #pragma unroll
-    for (int u = 0; u < 31; u++)
-        word |= (sel[u] != 0u && (olds[u] & sel[u]) == 0u) ? (1u << u) : 0u;
+    for (int u = 0; u < 31; u++) word |= min(sel[u] & ~olds[u], 1u) << u;
     return word;
 }
 
@@ -803,8 +805,8 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;
-    const int nwords = (s + 31) >> 5;
-    for (int k = 0; k < nwords; k++) bm[k * 64 + lane] = 0u;
+    const int nwords = (s >> 5) + 1;  // positions 0..s (s: the always-set sentinel)
+    for (int k = 0; k < nwords; k++) bm[k * 64 + lane] = (k == (s >> 5)) ? (1u << (s & 31)) : 0u;
     uint32_t ring[31];
     {
         const uint32_t* wi = wins + ((size_t)p * nwaves + w) * 31 * 64 + lane;
@@ -2410,7 +2412,7 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         hipLaunchKernelGGL(sampler_window_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts,
                            polyR, polyQ, w0, nwaves, sample_frac, wins);
     } else {
-        const int nwords = (sh.max_s + 31) / 32;
+        const int nwords = sh.max_s / 32 + 1;  // + the sentinel position max_s
         const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
         hipLaunchKernelGGL(sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
                            wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags);
