@@ -35,6 +35,7 @@ namespace {
 constexpr float kInf = __builtin_huge_valf();
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // x^(31+d) mod (x^31 - x^28 - 1), d = 0..29: reduction of a 61-coefficient product
 __constant__ uint32_t c_red[30][31];
@@ -738,9 +739,19 @@ __device__ __forceinline__ uint32_t mod_rup_i24(uint32_t x, double r, int d) {
 // reverse-step set T of the header comment is the complement.)  The atomics' old values are
 // consumed after the block, so the LDS traffic streams without waits; MODE 1/2 read bm[i] from
 // registers mirroring the (at most two) words holding i0-30..i0.
+// atomic OR into the lane's bitmap word of position j (bm_lane = LDS byte address of the lane's
+// word 0; words are 256 B apart): the address is one v_lshl_add_u32 of j >> 5
+__device__ __forceinline__ uint32_t atomicOr_lds_word(uint32_t bm_lane, uint32_t j, uint32_t bits) {
+    uint32_t a;
+    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(a) : "v"(j >> 5), "v"(bm_lane));
+    return __hip_atomic_fetch_or((lds_u32*)(size_t)a, bits, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 template <int MODE, bool I24>
 __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t* bm, int lane,
                                                  int i0, int s, const double* __restrict__ rtab) {
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
     double rt[31];  // 1/(i+1) of the block's steps: scalar loads (uniform index)
 #pragma unroll
     for (int u = 0; u < 31; u++) rt[u] = rtab[max(i0 - u, 1) + 1];
@@ -769,8 +780,8 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
             // harmless and the step is never selected (no validity select per step)
             const uint32_t jc = min(j, (uint32_t)s);
             const uint32_t bc = 1u << (jc & 31);
-            olds[u] = atomicOr(&bm[(jc >> 5) * 64 + lane], bc);
-            sel[u] = bc;
+            olds[u] = atomicOr_lds_word(bm_lane, jc, bc);
+            sel[u] = jc;  // (MODE 0: the bit position)
         } else {
             const uint32_t cw = ((ii >> 5) == wA) ? curA : curB;
             const uint32_t bi = (cw >> (ii & 31)) & 1u;
@@ -787,10 +798,19 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
             sel[u] = (validA || validB) ? bit : 0u;
         }
     }
-    // selected iff the step's bit was not yet set: sel & ~old != 0 (sel is 0 or one bit)
     uint32_t word = 0;
+    if (MODE == 0) {
+        // selected iff bit sel of the old word was clear: collect the SET bits (one bfe and one
+        // lshl_or per step), complement once
+        uint32_t nw = 0;
 #pragma unroll
-    for (int u = 0; u < 31; u++) word |= min(sel[u] & ~olds[u], 1u) << u;
+        for (int u = 0; u < 31; u++) nw |= __builtin_amdgcn_ubfe(olds[u], sel[u], 1) << u;
+        word = ~nw & 0x7fffffffu;
+    } else {
+        // selected iff the step's bit was not yet set: sel & ~old != 0 (sel is 0 or one bit)
+#pragma unroll
+        for (int u = 0; u < 31; u++) word |= min(sel[u] & ~olds[u], 1u) << u;
+    }
     return word;
 }
 
@@ -1487,7 +1507,6 @@ __device__ __forceinline__ float bin_edge_s(int elo, int e) {
     return __uint_as_float((uint32_t)((elo << kMantBits) + e) << kBinShift);
 }
 
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
 // (key << 2) + base as ONE v_lshl_add_u32 (the compiler otherwise rewrites (x >> 19) << 2 as
 // (x >> 17) & ~3 and adds: three instructions in the K^2 loop)
