@@ -878,7 +878,6 @@ __global__ __launch_bounds__(64) void sampler_kernel(
 constexpr int kGramLimbs = 6;
 constexpr int kGramTiles = 7;                 // 32-column MFMA tiles
 constexpr int kGramN = kGramTiles * 32;
-constexpr int kGramLdsCol = 48;               // LDS bytes per staged column (conflict-free b128)
 constexpr double kGramScale = 0x1p44;
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -888,7 +887,14 @@ __device__ __forceinline__ int gram_col(int limb, int c) {
     return c < 32 ? limb * 32 + c : 192 + limb * 4 + (c - 32);
 }
 
-// limbs[p][b][n][32 bytes]: byte u of column n = gram_col(limb, c) = digit of row M-1-31b-u
+// Byte u of column n in a word's 7 KB limb image: 32 B per column, the two 16-B halves swapped
+// on columns with bit 3 set, so the ds_read_b128 of 16 consecutive columns (half hh) covers all
+// 64 banks once.  The image is copied into LDS unchanged (lane-linear LDS-DMA).
+__device__ __forceinline__ int gram_swz(int n, int u) {
+    return n * 32 + ((((u >> 4) ^ (n >> 3)) & 1) << 4) + (u & 15);
+}
+
+// limbs[p][b][7 KB image]: byte u of column n = gram_col(limb, c) = digit of row M-1-31b-u
 __global__ __launch_bounds__(256) void gram_limbs_kernel(const int32_t* __restrict__ counts,
                                                          const double* __restrict__ pts,
                                                          int max_nq, int nbw,
@@ -915,7 +921,7 @@ __global__ __launch_bounds__(256) void gram_limbs_kernel(const int32_t* __restri
 #pragma unroll
         for (int k = 0; k < kGramLimbs; k++) {
             const int d = (int)(int8_t)(q & 0xff);
-            tile[gram_col(k, c) * 32 + u] = (int8_t)d;
+            tile[gram_swz(gram_col(k, c), u)] = (int8_t)d;
             q = (q - d) >> 8;
         }
     }
@@ -925,21 +931,30 @@ __global__ __launch_bounds__(256) void gram_limbs_kernel(const int32_t* __restri
 }
 
 // Block = 4 waves x 32 iterations (one MFMA row tile each); K loop over the pair's selection
-// words, two words (64 rows, 14 MFMAs per wave) per step.  The next step's limb tiles (2 x 7 KB)
-// are loaded into registers while the current step's feed the MFMAs, and written to the other
-// LDS buffer after them (one barrier per step).  gram[p][36][iters] (SoA, the eigen layout).
-constexpr int kGramWords = 2;                                 // selection words per K step
-constexpr int kGramStepPieces = kGramWords * kGramN * 2;      // 16-B pieces per step (896)
-constexpr int kGramPiecesPerThread = (kGramStepPieces + 255) / 256;
-constexpr int kGramLdsWord = kGramN * kGramLdsCol;            // LDS bytes per staged word
+// words, two words (64 rows, 14 MFMAs per wave) per step.  Operands reach LDS only by LDS-DMA
+// (global_load_lds: the 14 KB limb images of the step's two words and the block's 2 x 128
+// selection words) into a ring of kGramRing slots, issued kGramRing - 1 steps ahead: the
+// selection words stream from HBM once, and their latency is covered by the ring, not by
+// occupancy.  One raw barrier per step after a counted vmcnt (never 0 in the loop); all LDS in
+// one __shared__ array.  All 14 B fragments of a step are read before the first MFMA.
+// gram[p][36][iters] (SoA, the eigen layout).
+constexpr int kGramWords = 2;                                   // selection words per K step
+constexpr int kGramWordBytes = kGramN * 32;                     // one word's limb image (7 KB)
+constexpr int kGramSelOff = kGramWords * kGramWordBytes;        // selection words in a slot
+constexpr int kGramSlotBytes = kGramSelOff + kGramWords * 128 * 4;
+constexpr int kGramRing = 3;
+static_assert(kGramSelOff == 14 * 1024, "14 limb pieces of 1 KB per step");
 
-__global__ __launch_bounds__(256, 2) void gram_mfma_kernel(const int32_t* __restrict__ counts,
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef const __attribute__((address_space(1))) void* glb_vptr;
+
+__global__ __launch_bounds__(256, 3) void gram_mfma_kernel(const int32_t* __restrict__ counts,
                                                            const int8_t* __restrict__ limbs,
                                                            const uint32_t* __restrict__ selw,
                                                            int iters, int nwaves, int nbw,
                                                            double sample_frac,
                                                            double* __restrict__ gram) {
-    __shared__ __align__(16) int8_t bs[2][kGramWords * kGramLdsWord];
+    __shared__ __align__(16) int8_t lds[kGramRing * kGramSlotBytes];
     const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
@@ -947,79 +962,71 @@ __global__ __launch_bounds__(256, 2) void gram_mfma_kernel(const int32_t* __rest
     const int hb = blockIdx.x * 128;
     if (hb >= iters) return;  // uniform over the block
     const int nb = (M - 1) / 31 + 1;
-    const int nsteps = (nb + kGramWords - 1) / kGramWords;
+    const int nsteps = (nb + kGramWords - 1) / kGramWords;  // words read: <= 2 nsteps - 1 <= nb < nbw
     const int h0 = hb + wv * 32;
     const int r = lane & 31, hh = lane >> 5;
-    const int h = h0 + r;
-    const bool hv = h < iters;
-    const uint32_t* sp = selw + ((size_t)p * nwaves + (hv ? h >> 6 : 0)) * (size_t)nbw * 64 + (h & 63);
-    const uint4* lg = reinterpret_cast<const uint4*>(limbs + (size_t)p * nbw * kGramN * 32);
-    // staging piece q of a step: word q / (2 kGramN), column (q >> 1) % kGramN, half q & 1
-    uint4 stg[kGramPiecesPerThread];
-    auto stage_load = [&](int step) {
+    const int8_t* lg = limbs + (size_t)p * nbw * kGramWordBytes + lane * 16;
+    // waves 0, 1 move limb pieces 4 wv .. 4 wv + 3 and selection word wv; waves 2, 3 move limb
+    // pieces 8 + 3 (wv - 2) .. + 2 and selection word wv (word (wv >> 1), 64-iteration chunk
+    // (wv & 1); chunks past the last iteration are clamped: their rows are never stored)
+    const int lp0 = wv < 2 ? 4 * wv : 8 + 3 * (wv - 2);
+    const int chunk = min((hb >> 6) + (wv & 1), nwaves - 1);
+    const uint32_t* sg = selw + ((size_t)p * nwaves + chunk) * (size_t)nbw * 64 + lane;
+    const int soff = kGramSelOff + wv * 256;
+    auto issue = [&](int step) {
+        const int sx = min(step, nsteps - 1);  // past the end: a harmless reload, never read
+        int8_t* slot = lds + (step % kGramRing) * kGramSlotBytes;
+        const int8_t* src = lg + (size_t)sx * kGramSelOff;
 #pragma unroll
-        for (int i = 0; i < kGramPiecesPerThread; i++) {
-            const int q = tid + 256 * i;
-            const int w = step * kGramWords + q / (2 * kGramN);
-            stg[i] = (q < kGramStepPieces && w < nb)
-                         ? lg[(size_t)step * kGramStepPieces + q]
-                         : make_uint4(0u, 0u, 0u, 0u);
-        }
-    };
-    auto stage_store = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < kGramPiecesPerThread; i++) {
-            const int q = tid + 256 * i;
-            if (q < kGramStepPieces) {
-                const int w = q / (2 * kGramN), col = (q >> 1) % kGramN;
-                *reinterpret_cast<uint4*>(
-                    &bs[buf][w * kGramLdsWord + col * kGramLdsCol + (q & 1) * 16]) = stg[i];
-            }
-        }
-    };
-    auto sel_load = [&](int step, uint32_t (&w)[kGramWords]) {
-#pragma unroll
-        for (int i = 0; i < kGramWords; i++) {
-            const int b = step * kGramWords + i;
-            w[i] = (hv && b < nb) ? sp[(size_t)b * 64] : 0u;
-        }
+        for (int k = 0; k < 3; k++)
+            __builtin_amdgcn_global_load_lds((glb_vptr)(src + (lp0 + k) * 1024),
+                                             (lds_vptr)(slot + (lp0 + k) * 1024), 16, 0, 0);
+        if (wv < 2)
+            __builtin_amdgcn_global_load_lds((glb_vptr)(src + (lp0 + 3) * 1024),
+                                             (lds_vptr)(slot + (lp0 + 3) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(
+            (glb_vptr)(sg + (size_t)(sx * kGramWords + (wv >> 1)) * 64), (lds_vptr)(slot + soff),
+            4, 0, 0);
     };
     i32x16 acc[kGramTiles];
 #pragma unroll
     for (int t = 0; t < kGramTiles; t++)
 #pragma unroll
         for (int k = 0; k < 16; k++) acc[t][k] = 0;
-    uint32_t wcur[kGramWords], wnext[kGramWords];
-    stage_load(0);
-    stage_store(0);
-    sel_load(0, wcur);
-    if (nsteps > 1) stage_load(1);
-    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kGramRing - 1; k++) issue(k);
+    const int boff = r * 32 + (((hh ^ (r >> 3)) & 1) << 4);
     for (int st = 0; st < nsteps; st++) {
-        const int buf = st & 1;
-        if (st + 1 < nsteps) sel_load(st + 1, wnext);
+        // step st's DMAs retired: the kGramRing - 2 later steps (5 or 4 per step) may fly
+        static_assert(kGramRing == 3, "vmcnt counts");
+        if (wv < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        issue(st + kGramRing - 1);  // into the slot every wave finished reading in step st - 1
+        const int8_t* slot = lds + (st % kGramRing) * kGramSlotBytes;
+        uint32_t wsel[kGramWords];
+#pragma unroll
+        for (int i = 0; i < kGramWords; i++)
+            wsel[i] = reinterpret_cast<const uint32_t*>(slot + kGramSelOff)[i * 128 + wv * 32 + r];
 #pragma unroll
         for (int i = 0; i < kGramWords; i++) {
-            const uint32_t bits = (wcur[i] >> (16 * hh)) & 0xffffu;
+            i32x4 bf[kGramTiles];
+#pragma unroll
+            for (int t = 0; t < kGramTiles; t++)
+                bf[t] = *reinterpret_cast<const i32x4*>(slot + i * kGramWordBytes + t * 32 * 32 +
+                                                        boff);
+            const uint32_t wm = (st * kGramWords + i < nb) ? 0xffffu : 0u;  // words past nb
+            const uint32_t bits = (wsel[i] >> (16 * hh)) & wm;
             i32x4 a;
 #pragma unroll
             for (int v = 0; v < 4; v++)
                 a[v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
-            const int8_t* bt = &bs[buf][i * kGramLdsWord + r * kGramLdsCol + hh * 16];
 #pragma unroll
-            for (int t = 0; t < kGramTiles; t++) {
-                const i32x4 bf = *reinterpret_cast<const i32x4*>(bt + t * 32 * kGramLdsCol);
-                acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf, acc[t], 0, 0, 0);
-            }
+            for (int t = 0; t < kGramTiles; t++)
+                acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf[t], acc[t], 0, 0, 0);
         }
-        if (st + 1 < nsteps) {
-            stage_store(buf ^ 1);                   // tile st+1 (loaded during step st-1)
-            if (st + 2 < nsteps) stage_load(st + 2);
-#pragma unroll
-            for (int i = 0; i < kGramWords; i++) wcur[i] = wnext[i];
-        }
-        __syncthreads();
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's tail DMAs
     // recombine: row = (k & 3) + 8 (k >> 2) + 4 hh; entry r from tiles 0..5 of this lane,
     // entries 32..35 from tile 6 (lane 4 limb + e)
     double* go = gram + (size_t)p * 36 * iters;
