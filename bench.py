@@ -49,7 +49,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=20200423)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--profile-tag", default="r01d")
+    ap.add_argument("--profile-tag", default="r01e")
     return ap.parse_args()
 
 
