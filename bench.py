@@ -50,6 +50,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--profile-tag", default="r01e")
+    ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
+                    help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
+    ap.add_argument("--workload", choices=["pairs", "dense"], default="pairs",
+                    help="pairs: configs[1] (the metric); dense: configs[3], one N x N match "
+                         "(--kpts, default 16384) on both matcher methods, compared")
     return ap.parse_args()
 
 
@@ -82,6 +87,9 @@ def stage_work(stage, B, kpts, iters, res):
     if stage in ("knn2_filter", "knn2_candidates"):
         flops = 2.0 * kpts * kpts * 64 * B  # one bf16 product qh.th per (query, train) pair
         return flops, "TFLOP/s", PEAK_BF16_MFMA, "mfma", "2*N*T*64 bf16 MFMA flops per pair"
+    if stage == "knn2_exact":
+        ops = 3.0 * kpts * kpts * 64 * B  # sub, mul, add per element, flann::L2 order
+        return ops, "Top/s", PEAK_FP32_VALU_UNFUSED, "valu", "3*N*T*64 fp32 ops per pair"
     if stage == "gram":
         nb = np.floor((M - 1) / 31) + 1  # selection words (31 rows + 1 pad each)
         ops = float(np.sum(2.0 * iters * 32 * nb * 216))  # 6 int8 limbs x 36 Gram entries
@@ -127,9 +135,67 @@ def load_pmc(tag, stage):
     return None
 
 
+def run_dense(args):
+    """configs[3]: one dense N x N exact k=2 + ratio match on one GPU with both methods (bf16
+    MFMA filter + exact rescoring vs the LDS-tiled packed-FP32 sweep), HIP-event stage times,
+    each against its own roof; the two match lists must be identical."""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, capi, feature_matcher, synth
+    n = args.kpts if args.kpts != 4096 else 16384
+    dev = torch.device("cuda:0")
+    p = synth.make_pair(args.seed, n_kpts=n)
+    q = torch.from_numpy(p["desc_l"]).to(dev)
+    t = torch.from_numpy(p["desc_r"]).to(dev)
+    methods = {}
+    outs = {}
+    for name, m in (("mfma", capi.MATCHER_MFMA_FILTER), ("valu", capi.MATCHER_VALU_EXACT)):
+        ctx = Context(0)
+        fm = feature_matcher(ctx=ctx, method=m)
+        for _ in range(args.warmup):
+            out = fm._match_device(q, t, 0.3)
+        torch.cuda.synchronize()
+        ctx.set_profiling(True)
+        ctx.stage_times()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = fm._match_device(q, t, 0.3)  # (reads the match count: one sync per call)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / args.steps
+        st = {k: v[0] / args.steps for k, v in ctx.stage_times().items() if v[1] > 0}
+        ctx.set_profiling(False)
+        outs[name] = out.cpu().numpy()
+        if name == "mfma":
+            kern = st.get("knn2_filter", 0) + st.get("knn2_candidates", 0)
+            work = 2 * 2.0 * n * n * 64  # two bf16 MFMA passes, 2 N T 64 flops each
+            roof = {"bound": "mfma", "kernels": "knn2_filter + knn2_candidates", "peak": PEAK_BF16_MFMA,
+                    "unit": "TFLOP/s", "achieved": work / (kern / 1e3) / 1e12}
+        else:
+            kern = st.get("knn2_exact", 0)
+            work = 3.0 * n * n * 64  # sub, mul, add per element (flann::L2 order, no FMA)
+            roof = {"bound": "valu", "kernels": "knn2_exact", "peak": PEAK_FP32_VALU_UNFUSED,
+                    "unit": "Top/s", "achieved": work / (kern / 1e3) / 1e12}
+        roof["frac"] = roof["achieved"] / roof["peak"]
+        methods[name] = {"ms_per_match": el * 1e3, "stages_ms": st, "roofline": roof,
+                         "M": int(outs[name].shape[0])}
+    same = outs["mfma"].shape == outs["valu"].shape and np.array_equal(outs["mfma"], outs["valu"])
+    best = min(methods, key=lambda k: methods[k]["ms_per_match"])
+    line = {"metric": f"dense {n}x{n} exact k=2 + ratio match (configs[3]); match-set bit-exact",
+            "value": 1e3 / methods[best]["ms_per_match"], "unit": "matches/s",
+            "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": methods[best]["ms_per_match"], "higher_is_better": True,
+            "scaling": "none", "vs_baseline": None, "dtype": "f32 (bf16 MFMA filter)",
+            "data": "synthetic (seeded SURF-like descriptors, synth.make_pair)",
+            "config": {"workload": f"configs[3]: one pair, {n} x {n} 64-D descriptors",
+                       "kpts": n, "faster": best},
+            "methods": methods, "check": {"identical_matches": bool(same)}}
+    print(json.dumps(line))
+
+
 def main():
     args = parse()
     import torch
+    if args.workload == "dense":
+        return run_dense(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -149,6 +215,7 @@ def main():
     for part in parts:  # one context (scratch) and one HIP stream per sub-batch
         b = to_device(part, dev)
         ctx = Context(local)
+        ctx.set_matcher(0 if args.matcher == "mfma" else 1)
         runner = PairBatchRunner(ctx=ctx, iters=args.iters)
         runner.reserve(len(part), b["max_nq"], b["max_nt"])
         subs.append(dict(b=b, ctx=ctx, runner=runner, stream=torch.cuda.Stream(dev),
@@ -242,7 +309,7 @@ def main():
         "config": {"workload": "configs[1] shape: 4096x4096 kpts/pair, 10k initial_guess iters, "
                                f"batch of {args.pairs} independent pairs per step per GPU",
                    "kpts": args.kpts, "iters": args.iters, "pairs_per_step_per_gpu": args.pairs,
-                   "streams": S,
+                   "streams": S, "matcher": args.matcher,
                    "parallelism": f"pair-sharded x{world}", "sampler": "glibc replay (seed 1)"},
         "roofline": roof,
         "roofline_stages": stage_roofs,

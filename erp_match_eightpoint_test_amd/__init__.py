@@ -37,8 +37,10 @@ class feature_matcher:  # noqa: N801  (reference class name)
     (queryIdx, trainIdx, imgIdx, distance), ascending queryIdx, kept when d0 < 0.3 * d1.
     """
 
-    def __init__(self, device: int = 0, ctx: Context | None = None):
+    def __init__(self, device: int = 0, ctx: Context | None = None, method: int | None = None):
         self.ctx = ctx or Context(device)
+        if method is not None:  # capi.MATCHER_MFMA_FILTER (default) / capi.MATCHER_VALU_EXACT
+            self.ctx.set_matcher(method)
 
     def match_two_image(self, descriptor1, descriptor2, ratio: float = 0.3):
         try:

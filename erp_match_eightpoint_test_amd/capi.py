@@ -85,11 +85,13 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_eight_point_find_dev", "erp_eight_point_find", "erp_initial_guess",
             "erp_eight_point_estimation", "erp_pair_batch_run", "erp_ctx_set_profiling",
             "erp_stage_name", "erp_ctx_stage_times", "erp_eight_point_hypotheses_dev",
-            "erp_consensus_dev"]
+            "erp_consensus_dev", "erp_ctx_set_matcher"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
-          "consensus_refine"]
+          "consensus_refine", "knn2_exact"]
+MATCHER_MFMA_FILTER = 0  # erp_matcher_method
+MATCHER_VALU_EXACT = 1
 
 
 class ErpError(RuntimeError):
@@ -140,6 +142,7 @@ def load(build_if_missing: bool = False):
                                                  C.POINTER(RansacCfg), P, P]
     L.erp_consensus_dev.argtypes = [P, P, P, C.c_int32, C.c_double, C.c_double, P, P]
     L.erp_ctx_set_profiling.argtypes = [P, C.c_int32]
+    L.erp_ctx_set_matcher.argtypes = [P, C.c_int32]
     L.erp_stage_name.argtypes = [C.c_int32]
     L.erp_stage_name.restype = C.c_char_p
     L.erp_ctx_stage_times.argtypes = [P, P, P]
@@ -171,6 +174,10 @@ class Context:
 
     def set_profiling(self, enable: bool = True):
         check(self.L.erp_ctx_set_profiling(self.h, 1 if enable else 0), "set_profiling")
+
+    def set_matcher(self, method: int):
+        """erp_ctx_set_matcher: MATCHER_MFMA_FILTER (default) or MATCHER_VALU_EXACT."""
+        check(self.L.erp_ctx_set_matcher(self.h, int(method)), "set_matcher")
 
     def stage_times(self) -> dict:
         """{stage: (total_ms, launches)} since the last call (syncs on the recorded events)."""

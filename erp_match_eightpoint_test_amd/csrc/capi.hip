@@ -65,10 +65,11 @@ struct erp_ctx {
     std::mutex mu;
     // stage timing
     bool profiling = false;
+    int32_t matcher = ERP_MATCHER_MFMA_FILTER;
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
-    DevBuf part, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
+    DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
         rtab, limbs, tsplit, ovf;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
@@ -159,7 +160,7 @@ erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
 erp_status erp_ctx_destroy(erp_ctx* ctx) {
     if (!ctx) return ERP_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    DevBuf* all[] = {&ctx->part, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->edges, &ctx->gfin,
+    DevBuf* all[] = {&ctx->part, &ctx->part1, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->edges, &ctx->gfin,
                      &ctx->matches,
                      &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
                      &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
@@ -192,6 +193,11 @@ erp::BatchShape make_shape(int n_pairs, int max_nq, int max_nt, int iters, doubl
     chunk_len = (chunk_len + 31) / 32 * 32;
     sh.fchunk_len = chunk_len;
     sh.fchunks = (sh.max_nt + chunk_len - 1) / chunk_len;
+    // exact VALU sweep: 128 queries x one chunk (multiple of 128 train rows) per block
+    int xch = (2048 + qblocks * n_pairs - 1) / (qblocks * n_pairs);
+    xch = std::max(1, std::min(xch, (sh.max_nt + 127) / 128));
+    sh.xchunk_len = ((sh.max_nt + xch - 1) / xch + 127) / 128 * 128;
+    sh.xchunks = (sh.max_nt + sh.xchunk_len - 1) / sh.xchunk_len;
     sh.iters = std::max(iters, 1);
     sh.max_s = std::max((int)(sh.max_nq * frac), 1);
     sh.idx_stride = sh.max_s;
@@ -201,17 +207,47 @@ erp::BatchShape make_shape(int n_pairs, int max_nq, int max_nt, int iters, doubl
 
 bool ensure_matcher(erp_ctx* c, const erp::BatchShape& sh) {
     const size_t PQ = (size_t)sh.n_pairs * sh.max_nq;
-    return ensure(c->part, PQ * sizeof(erp::Top2)) &&
+    const size_t fold = PQ * sizeof(erp::Top2);
+    if (c->matcher == ERP_MATCHER_VALU_EXACT)
+        return ensure(c->part, PQ * sh.xchunks * sizeof(erp::Top2)) && ensure(c->part1, fold);
+    return ensure(c->part, PQ * sh.fchunks * sizeof(erp::Top2)) && ensure(c->part1, fold) &&
            ensure(c->pu, PQ * sh.fchunks * sizeof(float2)) &&
            ensure(c->ccount, PQ * sh.fchunks * 2 * 4) &&
            ensure(c->cand, PQ * sh.fchunks * 2 * erp::kCandSub * 4) &&
-           ensure(c->tsplit, erp::knn2_split_bytes(sh)) && ensure(c->ovf, 4 + 8 * PQ);
+           ensure(c->tsplit, erp::knn2_split_bytes(sh)) &&
+           ensure(c->ovf, 4 + 12 * PQ * sh.fchunks);
 }
 
-// exact k=2 + ratio test: MFMA filter (upper bounds), candidates, exact rescoring, merge
+// per-chunk partials -> (fold when there are several chunks) -> ratio test + compaction
+erp_status fold_and_merge(erp_ctx* ctx, const int64_t* oq, const int64_t* ot,
+                          const erp::BatchShape& sh, int chunk_len, int chunks, float ratio,
+                          erp_dmatch* matches, int32_t* counts, int32_t* flags, hipStream_t st) {
+    StageTimer _t(ctx, ERP_STAGE_KNN2_MERGE, st);
+    const erp::Top2* part = (const erp::Top2*)ctx->part.p;
+    if (chunks > 1) {
+        ERP_CK(erp::launch_knn2_fold(part, oq, ot, sh, chunk_len, chunks, (erp::Top2*)ctx->part1.p,
+                                     st));
+        part = (const erp::Top2*)ctx->part1.p;
+    }
+    // a single chunk spanning the whole train set
+    ERP_CK(erp::launch_knn2_merge(part, oq, ot, sh, sh.max_nt, 1, ratio, matches, counts, flags,
+                                  st));
+    return ERP_OK;
+}
+
+// exact k=2 + ratio test: MFMA filter (upper bounds), candidates, exact rescoring, merge -- or
+// the exact packed-FP32 sweep, merge
 erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int64_t* oq,
                        const int64_t* ot, const erp::BatchShape& sh, float ratio,
                        erp_dmatch* matches, int32_t* counts, int32_t* flags, hipStream_t st) {
+    if (ctx->matcher == ERP_MATCHER_VALU_EXACT) {
+        {
+            StageTimer _t(ctx, ERP_STAGE_KNN2_EXACT, st);
+            ERP_CK(erp::launch_knn2_exact(dq, dt, oq, ot, sh, (erp::Top2*)ctx->part.p, st));
+        }
+        return fold_and_merge(ctx, oq, ot, sh, sh.xchunk_len, sh.xchunks, ratio, matches, counts,
+                              flags, st);
+    }
     auto* pu = (float2*)ctx->pu.p;
     auto* cc = (int32_t*)ctx->ccount.p;
     auto* cand = (int32_t*)ctx->cand.p;
@@ -228,12 +264,8 @@ erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int
         ERP_CK(erp::launch_knn2_rescore(dq, dt, oq, ot, sh, cc, cand, (erp::Top2*)ctx->part.p,
                                         (int32_t*)ctx->ovf.p, st));
     }
-    {
-        StageTimer _t(ctx, ERP_STAGE_KNN2_MERGE, st);
-        ERP_CK(erp::launch_knn2_merge((erp::Top2*)ctx->part.p, oq, ot, sh, ratio, matches, counts,
-                                      flags, st));
-    }
-    return ERP_OK;
+    return fold_and_merge(ctx, oq, ot, sh, sh.fchunk_len, sh.fchunks, ratio, matches, counts,
+                          flags, st);
 }
 
 erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_batch_outputs* out) {
@@ -408,12 +440,21 @@ erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable) {
     return ERP_OK;
 }
 
+erp_status erp_ctx_set_matcher(erp_ctx* ctx, int32_t method) {
+    if (!ctx) return ERP_INVALID_ARG;
+    if (method != ERP_MATCHER_MFMA_FILTER && method != ERP_MATCHER_VALU_EXACT)
+        return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ctx->matcher = method;
+    return ERP_OK;
+}
+
 const char* erp_stage_name(int32_t stage) {
     static const char* names[ERP_STAGE_COUNT] = {
         "knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler",
         "eigen", "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
         "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
-        "consensus_refine"};
+        "consensus_refine", "knn2_exact"};
     return (stage >= 0 && stage < ERP_STAGE_COUNT) ? names[stage] : "unknown";
 }
 

@@ -43,6 +43,7 @@ struct BatchShape {
     int n_pairs;
     int max_nq, max_nt;
     int fchunks, fchunk_len;      // train chunks of the matcher's filter passes
+    int xchunks, xchunk_len;      // train chunks of the exact VALU sweep (multiples of 128)
     int iters;
     int max_s;                    // (int)(max_nq * sample_frac)
     int idx_stride;               // entries of one hypothesis in the debug samples output
@@ -63,13 +64,26 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
                               const int64_t* off_t, const BatchShape& sh, void* split,
                               float2* pu, int32_t* ccount, int32_t* cand, int pass,
                               hipStream_t st);
-// ovf = scratch of 4 + 8 * n_pairs * max_nq bytes: overflow list for the exact sweep
+// rescore -> per-chunk exact partials part[pairs][fchunks][max_nq]; ovf = scratch of
+// 4 + 12 * n_pairs * max_nq * fchunks bytes: overflowed (pair, query, chunk) for the exact sweep
 hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
                                const int64_t* off_t, const BatchShape& sh, const int32_t* ccount,
                                const int32_t* cand, Top2* part, int32_t* ovf, hipStream_t st);
+// exact sweep on packed FP32 VALU (no MFMA filter): per-(chunk, query) exact k=2 into
+// xpart[pairs][xchunks][max_nq]
+hipError_t launch_knn2_exact(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                             const int64_t* off_t, const BatchShape& sh, Top2* xpart,
+                             hipStream_t st);
+// per-chunk partials part[pairs][chunks][max_nq] -> one Top2 per query out[pairs][max_nq]
+hipError_t launch_knn2_fold(const Top2* part, const int64_t* off_q, const int64_t* off_t,
+                            const BatchShape& sh, int chunk_len, int chunks, Top2* out,
+                            hipStream_t st);
+// fold of per-chunk partials part[pairs][chunks][max_nq] (chunk c = train rows
+// [c*chunk_len, (c+1)*chunk_len)), ratio test, compaction
 hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
-                             const BatchShape& sh, float ratio, erp_dmatch* matches,
-                             int32_t* counts, int32_t* flags, hipStream_t st);
+                             const BatchShape& sh, int chunk_len, int chunks, float ratio,
+                             erp_dmatch* matches, int32_t* counts, int32_t* flags,
+                             hipStream_t st);
 hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t* counts,
                                         const erp_point2f* kp_l, const erp_point2f* kp_r,
                                         const int64_t* off_l, const int64_t* off_r,

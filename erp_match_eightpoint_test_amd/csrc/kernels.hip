@@ -333,8 +333,10 @@ __device__ __forceinline__ void top2_consider(float acc, int j, float& b0, int& 
     }
 }
 
-// one lane per query: exact distances of its candidates (~2 on SURF-like data); a query whose
-// candidate list overflowed goes to the overflow list (exact sweep, knn2_sweep_kernel)
+// one lane per (query, train chunk): exact distances of its candidates (~2 per query on
+// SURF-like data) -> the chunk's exact k=2 in part[pair][chunk][query]; a (query, chunk) whose
+// candidate list overflowed goes to the overflow list (exact sweep of that chunk,
+// knn2_sweep_kernel).  Chunks with no candidates write an empty Top2.
 __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restrict__ dq,
                                                            const float* __restrict__ dt,
                                                            const int64_t* __restrict__ off_q,
@@ -344,62 +346,66 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                                                            const int32_t* __restrict__ cand,
                                                            Top2* __restrict__ part,
                                                            int32_t* __restrict__ ovf) {
-    const int p = blockIdx.y;
+    const int p = blockIdx.z, c = blockIdx.y;
     const int q = blockIdx.x * 256 + threadIdx.x;
     const int64_t qbase = off_q[p];
     const int nq = (int)(off_q[p + 1] - qbase);
     const int64_t tbase = off_t[p];
-    if (q >= nq) return;
     const int nt = (int)(off_t[p + 1] - tbase);
-    const int nl = 2 * ((nt + chunk_len - 1) / chunk_len);  // lists of this query
-    const size_t l0 = ((size_t)p * max_nq + q) * chunks * 2;
-    bool over = false;
-    for (int l = 0; l < nl; l++) over = over || ccount[l0 + l] > kCandSub;
-    if (over) {
+    if (q >= nq || c * chunk_len >= nt) return;
+    const size_t l0 = (((size_t)p * max_nq + q) * chunks + c) * 2;
+    const int n0 = ccount[l0], n1 = ccount[l0 + 1];
+    Top2* out = part + ((size_t)p * chunks + c) * max_nq + q;
+    if (n0 > kCandSub || n1 > kCandSub) {
         const int slot = atomicAdd(&ovf[0], 1);
-        ovf[1 + 2 * slot] = p;
-        ovf[2 + 2 * slot] = q;
+        ovf[1 + 3 * slot] = p;
+        ovf[2 + 3 * slot] = q;
+        ovf[3 + 3 * slot] = c;
         return;
     }
-    float4 qr[16];
-    const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
-#pragma unroll
-    for (int c = 0; c < 16; c++) qr[c] = qp[c];
     float b0 = kInf, b1 = kInf;
     int j0 = 0x7fffffff;
-    for (int l = 0; l < nl; l++) {
-        const int n = ccount[l0 + l];
-        const int32_t* cl = cand + (l0 + l) * kCandSub;
-        for (int k = 0; k < n; k++) {
-            const int j = cl[k];
-            top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim)), j,
-                          b0, j0, b1);
+    if (n0 + n1 > 0) {
+        float4 qr[16];
+        const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
+#pragma unroll
+        for (int k = 0; k < 16; k++) qr[k] = qp[k];
+        for (int h = 0; h < 2; h++) {
+            const int n = h ? n1 : n0;
+            const int32_t* cl = cand + (l0 + h) * kCandSub;
+            for (int k = 0; k < n; k++) {
+                const int j = cl[k];
+                top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim)),
+                              j, b0, j0, b1);
+            }
         }
     }
-    part[(size_t)p * max_nq + q] = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
+    *out = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
 }
 
-// exact sweep over every train row for the overflow queries: one wave per query, a fixed grid
-// striding over the list
+// exact sweep over the train rows of one chunk for the overflowed (query, chunk) entries: one
+// wave per entry, a fixed grid striding over the list
 __global__ __launch_bounds__(256) void knn2_sweep_kernel(const float* __restrict__ dq,
                                                          const float* __restrict__ dt,
                                                          const int64_t* __restrict__ off_q,
                                                          const int64_t* __restrict__ off_t,
-                                                         int max_nq, const int32_t* __restrict__ ovf,
+                                                         int max_nq, int chunk_len, int chunks,
+                                                         const int32_t* __restrict__ ovf,
                                                          Top2* __restrict__ part) {
     const int lane = wave_lane();
     const int nov = ovf[0];
     for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < nov; w += gridDim.x * 4) {
-        const int p = ovf[1 + 2 * w], q = ovf[2 + 2 * w];
+        const int p = ovf[1 + 3 * w], q = ovf[2 + 3 * w], c = ovf[3 + 3 * w];
         const int64_t qbase = off_q[p], tbase = off_t[p];
         const int nt = (int)(off_t[p + 1] - tbase);
+        const int ja = c * chunk_len, jb = min(nt, ja + chunk_len);
         float4 qr[16];
         const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
 #pragma unroll
-        for (int c = 0; c < 16; c++) qr[c] = qp[c];
+        for (int k = 0; k < 16; k++) qr[k] = qp[k];
         float b0 = kInf, b1 = kInf;
         int j0 = 0x7fffffff;
-        for (int j = lane; j < nt; j += 64)
+        for (int j = ja + lane; j < jb; j += 64)
             top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim)), j,
                           b0, j0, b1);
 #pragma unroll
@@ -414,8 +420,197 @@ __global__ __launch_bounds__(256) void knn2_sweep_kernel(const float* __restrict
                 b1 = fminf(b1, ob0);
             }
         }
-        if (lane == 0) part[(size_t)p * max_nq + q] = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
+        if (lane == 0)
+            part[((size_t)p * chunks + c) * max_nq + q] = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
     }
+}
+
+// ---- LDS-tiled exact sweep on packed FP32 VALU (the non-MFMA matcher, configs[3]) ----------
+// Every (query, train) distance in the flann::L2<float> order, no filter: per group of 4 dims
+// acc += ((d0*d0 + d1*d1) + d2*d2) + d3*d3, each operation rounded (no FMA).  Two train rows
+// share every instruction (v_pk_add_f32 / v_pk_mul_f32 with the query value broadcast), so an
+// element costs 1.5 VALU instructions: sub, mul, add.
+// Block = 256 threads = 16 (tq) x 16 (tt); tile = 128 queries (resident in LDS for the whole
+// chunk) x 128 train rows per step.  Thread (tq, tt) owns queries tq + 16 k (k < 8) and the
+// train row pairs tt + 16 k (k < 4): 64 accumulators.  Train rows sit in LDS as row pairs,
+// dims interleaved ([pair][dim][2]), so one ds_read_b128 yields 2 dims x 2 rows = two packed
+// operands; query rows are [row][68] (the 16 rows a wave reads per instruction fall on 64
+// distinct banks).  The next tile is prefetched into registers during the current one.
+// Output: per (pair, chunk, query) the chunk's exact k=2 (Top2, lowest index among ties);
+// knn2_merge folds chunks in train order.
+constexpr int kXQ = 128, kXT = 128;
+constexpr int kXQRow = 68;             // floats per query row in LDS
+constexpr int kXPair = 2 * kDim + 4;   // floats per train row pair in LDS
+
+struct ExactLds {
+    float q[kXQ * kXQRow];
+    float t[kXT / 2 * kXPair];
+    Top2 red[4][kXQ];                  // cross-wave fold of the k=2 partials
+};
+
+__global__ __launch_bounds__(256) void knn2_exact_kernel(const float* __restrict__ dq,
+                                                         const float* __restrict__ dt,
+                                                         const int64_t* __restrict__ off_q,
+                                                         const int64_t* __restrict__ off_t,
+                                                         int chunk_len, int chunks, int max_nq,
+                                                         Top2* __restrict__ xpart) {
+    __shared__ ExactLds sm;
+    const int p = blockIdx.z;
+    const int64_t qbase = off_q[p], tbase = off_t[p];
+    const int nq = (int)(off_q[p + 1] - qbase);
+    const int nt = (int)(off_t[p + 1] - tbase);
+    const int q0 = blockIdx.x * kXQ;
+    const int t0 = blockIdx.y * chunk_len;
+    if (q0 >= nq || t0 >= nt) return;  // uniform over the block
+    const int t1 = min(t0 + chunk_len, nt);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tq = lane & 15, tt = (lane >> 4) + 4 * wid;
+    // query tile: 128 rows x 16 float4, 8 float4 per thread (rows beyond nq read as 0)
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const int e = tid + 256 * u, row = e >> 4, c = e & 15;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (q0 + row < nq) v = reinterpret_cast<const float4*>(dq + (qbase + q0 + row) * kDim)[c];
+        *reinterpret_cast<float4*>(&sm.q[row * kXQRow + 4 * c]) = v;
+    }
+    // train staging: thread -> row pair (tid >> 2) of the tile, dims 16 (tid & 3) .. +15
+    const int spair = tid >> 2, sdim = 16 * (tid & 3);
+    float4 ga[4], gb[4];
+    auto gload = [&](int tile0) {
+        const int ra = tile0 + 2 * spair, rb = ra + 1;
+        const float4* pa = reinterpret_cast<const float4*>(dt + (tbase + min(ra, t1 - 1)) * kDim + sdim);
+        const float4* pb = reinterpret_cast<const float4*>(dt + (tbase + min(rb, t1 - 1)) * kDim + sdim);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            ga[c] = pa[c];
+            gb[c] = pb[c];
+        }
+    };
+    float b0[8], b1[8];
+    int j0[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        b0[k] = kInf;
+        b1[k] = kInf;
+        j0[k] = 0x7fffffff;
+    }
+    const int ntiles = (t1 - t0 + kXT - 1) / kXT;
+    gload(t0);
+    for (int s = 0; s < ntiles; s++) {
+        const int tile0 = t0 + s * kXT;
+        __syncthreads();  // previous tile's reads are done
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            float* w = &sm.t[spair * kXPair + 2 * (sdim + 4 * c)];
+            *reinterpret_cast<float4*>(w) = make_float4(ga[c].x, gb[c].x, ga[c].y, gb[c].y);
+            *reinterpret_cast<float4*>(w + 4) = make_float4(ga[c].z, gb[c].z, ga[c].w, gb[c].w);
+        }
+        __syncthreads();
+        if (s + 1 < ntiles) gload(tile0 + kXT);
+        f32x2 acc[8][4];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) acc[k][kk] = f32x2{0.f, 0.f};
+#pragma unroll 2
+        for (int g = 0; g < 16; g++) {
+            float4 tv[4][2];
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const float* tp = &sm.t[(tt + 16 * kk) * kXPair + 8 * g];
+                tv[kk][0] = *reinterpret_cast<const float4*>(tp);
+                tv[kk][1] = *reinterpret_cast<const float4*>(tp + 4);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const float4 qv = *reinterpret_cast<const float4*>(&sm.q[(tq + 16 * k) * kXQRow + 4 * g]);
+                const f32x2 qx = {qv.x, qv.x}, qy = {qv.y, qv.y}, qz = {qv.z, qv.z},
+                            qw = {qv.w, qv.w};
+#pragma unroll
+                for (int kk = 0; kk < 4; kk++) {
+                    const f32x2 e0 = qx - f32x2{tv[kk][0].x, tv[kk][0].y};
+                    const f32x2 e1 = qy - f32x2{tv[kk][0].z, tv[kk][0].w};
+                    const f32x2 e2 = qz - f32x2{tv[kk][1].x, tv[kk][1].y};
+                    const f32x2 e3 = qw - f32x2{tv[kk][1].z, tv[kk][1].w};
+                    acc[k][kk] = acc[k][kk] + (((e0 * e0 + e1 * e1) + e2 * e2) + e3 * e3);
+                }
+            }
+        }
+        // k=2 update, branch-free: a thread sees its rows in increasing train index, so a later
+        // row never wins a tie (strict <); second = med3(b0, b1, d).  Rows >= t1 count as +inf.
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+            const int ja = tile0 + 2 * (tt + 16 * kk);
+            const bool va = ja < t1, vb = ja + 1 < t1;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const float d = (h ? vb : va) ? acc[k][kk][h] : kInf;
+                    b1[k] = __builtin_amdgcn_fmed3f(b0[k], b1[k], d);
+                    j0[k] = d < b0[k] ? ja + h : j0[k];
+                    b0[k] = fminf(b0[k], d);
+                }
+            }
+        }
+    }
+    // fold the 16 threads of a query: lanes tq + 16 m of a wave (xor 16, 32), then 4 waves
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+#pragma unroll
+        for (int o = 16; o < 64; o <<= 1) {
+            const float ob0 = __shfl_xor(b0[k], o, 64), ob1 = __shfl_xor(b1[k], o, 64);
+            const int oj = __shfl_xor(j0[k], o, 64);
+            if (ob0 < b0[k] || (ob0 == b0[k] && oj < j0[k])) {
+                b1[k] = fminf(b0[k], ob1);
+                b0[k] = ob0;
+                j0[k] = oj;
+            } else {
+                b1[k] = fminf(b1[k], ob0);
+            }
+        }
+        if (lane < 16) sm.red[wid][tq + 16 * k] = Top2{b0[k], j0[k], b1[k]};
+    }
+    __syncthreads();
+    if (tid < kXQ && q0 + tid < nq) {
+        Top2 r = sm.red[0][tid];
+#pragma unroll
+        for (int w = 1; w < 4; w++) {
+            const Top2 o = sm.red[w][tid];
+            if (o.d0 < r.d0 || (o.d0 == r.d0 && o.j0 < r.j0)) {
+                r.d1 = fminf(r.d0, o.d1);
+                r.d0 = o.d0;
+                r.j0 = o.j0;
+            } else {
+                r.d1 = fminf(r.d1, o.d0);
+            }
+        }
+        if (r.j0 == 0x7fffffff) r.j0 = -1;
+        xpart[((size_t)p * chunks + blockIdx.y) * max_nq + q0 + tid] = r;
+    }
+}
+
+// Fold of per-chunk partials part[pair][chunk][query] into one exact k=2 per query
+// (out[pair][query]), chunks in train order (an earlier chunk wins ties): one lane per query,
+// so a single large pair uses the whole chip (the merge below is one block per pair).
+__device__ __forceinline__ void merge_query(const Top2* part, size_t stride, int nch, int q,
+                                            float& B0, int& J, float& B1);
+
+__global__ __launch_bounds__(256) void knn2_fold_kernel(const Top2* __restrict__ part,
+                                                        const int64_t* __restrict__ off_q,
+                                                        const int64_t* __restrict__ off_t,
+                                                        int chunk_len, int chunks, int max_nq,
+                                                        Top2* __restrict__ out) {
+    const int p = blockIdx.y;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    const int nq = (int)(off_q[p + 1] - off_q[p]);
+    const int nt = (int)(off_t[p + 1] - off_t[p]);
+    if (q >= nq) return;
+    float B0, B1;
+    int J;
+    merge_query(part + (size_t)p * chunks * max_nq, (size_t)max_nq,
+                max(1, (nt + chunk_len - 1) / chunk_len), q, B0, J, B1);
+    out[(size_t)p * max_nq + q] = Top2{B0, J, B1};
 }
 
 // Fold chunk partials in train order (lowest index wins ties), apply the ratio test
@@ -2377,20 +2572,37 @@ hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const i
                                const int64_t* off_t, const BatchShape& sh, const int32_t* ccount,
                                const int32_t* cand, Top2* part, int32_t* ovf, hipStream_t st) {
     hipLaunchKernelGGL(set_i32_kernel, dim3(1), dim3(1), 0, st, ovf, 0);
-    dim3 grid((sh.max_nq + 255) / 256, sh.n_pairs);
+    dim3 grid((sh.max_nq + 255) / 256, sh.fchunks, sh.n_pairs);
     hipLaunchKernelGGL(knn2_rescore_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
                        sh.max_nq, sh.fchunk_len, sh.fchunks, ccount, cand, part, ovf);
     hipLaunchKernelGGL(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
-                       sh.max_nq, ovf, part);
+                       sh.max_nq, sh.fchunk_len, sh.fchunks, ovf, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn2_exact(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                             const int64_t* off_t, const BatchShape& sh, Top2* xpart,
+                             hipStream_t st) {
+    dim3 grid((sh.max_nq + kXQ - 1) / kXQ, sh.xchunks, sh.n_pairs);
+    hipLaunchKernelGGL(knn2_exact_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
+                       sh.xchunk_len, sh.xchunks, sh.max_nq, xpart);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn2_fold(const Top2* part, const int64_t* off_q, const int64_t* off_t,
+                            const BatchShape& sh, int chunk_len, int chunks, Top2* out,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(knn2_fold_kernel, dim3((sh.max_nq + 255) / 256, sh.n_pairs), dim3(256), 0,
+                       st, part, off_q, off_t, chunk_len, chunks, sh.max_nq, out);
     return hipGetLastError();
 }
 
 hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
-                             const BatchShape& sh, float ratio, erp_dmatch* matches,
-                             int32_t* counts, int32_t* flags, hipStream_t st) {
-    // the rescored Top2 are one "chunk" spanning the whole train set
+                             const BatchShape& sh, int chunk_len, int chunks, float ratio,
+                             erp_dmatch* matches, int32_t* counts, int32_t* flags,
+                             hipStream_t st) {
     hipLaunchKernelGGL(knn2_merge_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, part, off_q, off_t,
-                       max(sh.max_nt, 1), 1, sh.max_nq, ratio, matches, counts, flags);
+                       chunk_len, chunks, sh.max_nq, ratio, matches, counts, flags);
     return hipGetLastError();
 }
 

@@ -175,7 +175,8 @@ typedef enum erp_stage {
     ERP_STAGE_KNN2_CANDIDATES = 13, /* MFMA pass 2: candidate train rows per query */
     ERP_STAGE_KNN2_RESCORE = 14,    /* exact flann::L2 distances of the candidates */
     ERP_STAGE_CONSENSUS_REFINE = 15, /* tighter bounds for the survivors (sub-bins) */
-    ERP_STAGE_COUNT = 16
+    ERP_STAGE_KNN2_EXACT = 16,      /* exact sweep on packed FP32 VALU (ERP_MATCHER_VALU_EXACT) */
+    ERP_STAGE_COUNT = 17
 } erp_stage;
 erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable);
 const char* erp_stage_name(int32_t stage);
@@ -184,6 +185,15 @@ const char* erp_stage_name(int32_t stage);
 erp_status erp_ctx_stage_times(erp_ctx* ctx, double* total_ms, int64_t* launches);
 
 /* ---- matcher (feature_matcher::match_two_image) ---- */
+/* How the exact k=2 is computed (both give the same bit-exact matches):
+   MFMA_FILTER: bf16 MFMA upper/lower bounds -> candidates -> exact flann::L2 rescoring (default);
+   VALU_EXACT:  every distance exactly, LDS-tiled packed FP32 sweep (configs[3]'s scalar path). */
+typedef enum erp_matcher_method {
+    ERP_MATCHER_MFMA_FILTER = 0,
+    ERP_MATCHER_VALU_EXACT = 1
+} erp_matcher_method;
+erp_status erp_ctx_set_matcher(erp_ctx* ctx, int32_t method);
+
 /* device pointers; writes up to nq matches in ascending queryIdx order and *d_count. */
 erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,
                                 const float* d_train, int32_t nt, int32_t dim, float ratio,

@@ -32,10 +32,20 @@ def _npz(name):
 
 
 # ------------------------------------------------------------------------------ matcher
-def test_match_golden_fixture(ctx):
+# every matcher test runs on both exact-k=2 methods: the bf16-MFMA filter + exact rescoring
+# (default) and the LDS-tiled packed-FP32 sweep (configs[3]'s scalar path)
+@pytest.fixture(scope="module", params=["mfma_filter", "valu_exact"])
+def mctx(gpu_lib, request):
+    from erp_match_eightpoint_test_amd import Context, capi
+    c = Context(0)
+    c.set_matcher(capi.MATCHER_MFMA_FILTER if request.param == "mfma_filter"
+                  else capi.MATCHER_VALU_EXACT)
+    return c
+
+def test_match_golden_fixture(mctx):
     from erp_match_eightpoint_test_amd import feature_matcher
     g = _npz("match_384.npz")
-    fm = feature_matcher(ctx=ctx)
+    fm = feature_matcher(ctx=mctx)
     mt = fm.match_two_image(g["desc_l"], g["desc_r"])
     assert np.array_equal(mt["queryIdx"], g["query"])
     assert np.array_equal(mt["trainIdx"], g["train"])
@@ -45,16 +55,16 @@ def test_match_golden_fixture(ctx):
 
 @pytest.mark.parametrize("nq,nt", [(1, 2), (2, 2), (63, 65), (300, 4097), (2048, 2048),
                                    (4096, 4096), (5000, 1000)])
-def test_match_vs_oracle_sizes(ctx, oracle, nq, nt):
+def test_match_vs_oracle_sizes(mctx, oracle, nq, nt):
     from erp_match_eightpoint_test_amd import feature_matcher
     p = synth.make_pair(nq * 7 + nt, n_kpts=nq, n_train=nt)
     ref, _, _, _ = oracle.match_two_image(p["desc_l"], p["desc_r"])
-    mt = feature_matcher(ctx=ctx).match_two_image(p["desc_l"], p["desc_r"])
+    mt = feature_matcher(ctx=mctx).match_two_image(p["desc_l"], p["desc_r"])
     assert len(mt) == len(ref)
     assert np.array_equal(mt.view(np.uint32), ref.view(np.uint32))
 
 
-def test_match_ties_and_ratio_boundary(ctx, oracle):
+def test_match_ties_and_ratio_boundary(mctx, oracle):
     from erp_match_eightpoint_test_amd import feature_matcher
     rng = np.random.default_rng(5)
     t = synth.random_descriptors(rng, 700)
@@ -62,16 +72,16 @@ def test_match_ties_and_ratio_boundary(ctx, oracle):
     q = np.concatenate([t[5:40], synth.random_descriptors(rng, 60)])
     q[40] = q[41]
     ref, _, _, _ = oracle.match_two_image(q, t)
-    mt = feature_matcher(ctx=ctx).match_two_image(q, t)
+    mt = feature_matcher(ctx=mctx).match_two_image(q, t)
     assert np.array_equal(mt.view(np.uint32), ref.view(np.uint32))
 
 
-def _all_queries_vs_oracle(ctx, oracle, q, t):
+def _all_queries_vs_oracle(mctx, oracle, q, t):
     """every query's exact k=2 through the matcher: ratio 1e30 keeps every query (checks
     trainIdx = j0 and distance = sqrtf(d0) bit-exactly), ratio 1.0 drops exactly the queries
     whose two nearest distances tie (checks d1 == d0 detection), ratio 0.3 = the reference."""
     from erp_match_eightpoint_test_amd import feature_matcher
-    fm = feature_matcher(ctx=ctx)
+    fm = feature_matcher(ctx=mctx)
     for ratio in (1e30, 1.0, 0.3):
         ref, _, _, _ = oracle.match_two_image(q, t, ratio=ratio)
         mt = fm.match_two_image(q, t, ratio=ratio)
@@ -79,7 +89,7 @@ def _all_queries_vs_oracle(ctx, oracle, q, t):
         assert np.array_equal(mt.view(np.uint32), ref.view(np.uint32)), ratio
 
 
-def test_match_filter_candidate_overflow(ctx, oracle):
+def test_match_filter_candidate_overflow(mctx, oracle):
     """>32 train rows inside the filter's error window of one query (near-duplicates differing
     in the last bits): the candidate list overflows and the exact sweep path must decide."""
     rng = np.random.default_rng(11)
@@ -90,10 +100,10 @@ def test_match_filter_candidate_overflow(ctx, oracle):
         v[k % 64] = np.nextafter(v[k % 64], np.float32(2.0) if k % 2 else np.float32(-2.0))
         t[100 + k] = v
     q = np.concatenate([base[None, :], t[50:90], synth.random_descriptors(rng, 100)])
-    _all_queries_vs_oracle(ctx, oracle, q, t)
+    _all_queries_vs_oracle(mctx, oracle, q, t)
 
 
-def test_match_filter_near_ties_unnormalised(ctx, oracle):
+def test_match_filter_near_ties_unnormalised(mctx, oracle):
     """distances equal up to rounding, unnormalised magnitudes (1e-3 .. 1e2) and zero rows: the
     filter's error bound scales with |q|^2 + |t|^2 and must never drop a true neighbour."""
     rng = np.random.default_rng(12)
@@ -109,31 +119,31 @@ def test_match_filter_near_ties_unnormalised(ctx, oracle):
     d = rng.normal(0, 1e-3, 64).astype(np.float32)
     t[11] = t[10] + d
     t[12] = t[10] - d
-    _all_queries_vs_oracle(ctx, oracle, q.astype(np.float32), t)
+    _all_queries_vs_oracle(mctx, oracle, q.astype(np.float32), t)
 
 
 @pytest.mark.parametrize("nq,nt", [(300, 4097), (4096, 4096)])
-def test_match_all_queries_vs_oracle(ctx, oracle, nq, nt):
+def test_match_all_queries_vs_oracle(mctx, oracle, nq, nt):
     p = synth.make_pair(nq * 3 + nt, n_kpts=nq, n_train=nt)
-    _all_queries_vs_oracle(ctx, oracle, p["desc_l"], p["desc_r"])
+    _all_queries_vs_oracle(mctx, oracle, p["desc_l"], p["desc_r"])
 
 
-def test_match_edge_counts(ctx):
+def test_match_edge_counts(mctx):
     from erp_match_eightpoint_test_amd import ErpError, feature_matcher
-    fm = feature_matcher(ctx=ctx)
+    fm = feature_matcher(ctx=mctx)
     assert len(fm.match_two_image(np.zeros((0, 64), np.float32), np.zeros((5, 64), np.float32))) == 0
     with pytest.raises(ErpError):
         fm.match_two_image(np.ones((3, 64), np.float32), np.ones((1, 64), np.float32))
 
 
-def test_match_device_path(ctx, oracle):
+def test_match_device_path(mctx, oracle):
     import torch
     from erp_match_eightpoint_test_amd import feature_matcher
     p = synth.make_pair(99, n_kpts=1500)
     ref, _, _, _ = oracle.match_two_image(p["desc_l"], p["desc_r"])
     q = torch.from_numpy(p["desc_l"]).cuda()
     t = torch.from_numpy(p["desc_r"]).cuda()
-    out = feature_matcher(ctx=ctx).match_two_image(q, t).cpu().numpy()
+    out = feature_matcher(ctx=mctx).match_two_image(q, t).cpu().numpy()
     assert np.array_equal(out.view(np.uint32).reshape(-1), ref.view(np.uint32).reshape(-1))
 
 
@@ -284,6 +294,39 @@ def test_batch_pipeline_vs_oracle(ctx, oracle):
         live = np.isfinite(d)
         assert live.sum() >= 1 and np.all(dref[~live] >= dref.min())
         assert np.allclose(d[live], dref[live], rtol=1e-12, atol=0)
+
+
+def test_batch_pipeline_valu_matcher_equals_mfma(gpu_lib):
+    """the whole batch pipeline with the packed-FP32 exact sweep as the matcher: matches and
+    results identical to the MFMA-filter pipeline (ragged pair sizes, several train chunks)"""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner, capi, results_to_numpy
+    sizes = [(700, 650), (1300, 1290), (257, 1031), (2048, 2048)]
+    pairs = [synth.make_pair(400 + i, n_kpts=nq, n_train=nt) for i, (nq, nt) in enumerate(sizes)]
+    dev = torch.device("cuda:0")
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    ol = np.concatenate([[0], np.cumsum([len(p["desc_l"]) for p in pairs])]).astype(np.int64)
+    orr = np.concatenate([[0], np.cumsum([len(p["desc_r"]) for p in pairs])]).astype(np.int64)
+    args = (t(np.concatenate([p["desc_l"] for p in pairs])),
+            t(np.concatenate([p["desc_r"] for p in pairs])),
+            t(np.concatenate([p["kp_l"] for p in pairs])),
+            t(np.concatenate([p["kp_r"] for p in pairs])), t(ol), t(orr),
+            t(np.array([p["W"] for p in pairs], np.int32)),
+            t(np.array([p["H"] for p in pairs], np.int32)),
+            int(np.diff(ol).max()), int(np.diff(orr).max()))
+    outs = {}
+    for name, method in (("mfma", capi.MATCHER_MFMA_FILTER), ("valu", capi.MATCHER_VALU_EXACT)):
+        c = Context(0)
+        c.set_matcher(method)
+        o = PairBatchRunner(ctx=c, iters=300).run(*args, want=("matches",))
+        torch.cuda.synchronize()
+        outs[name] = (results_to_numpy(o["results"]), o["matches"].cpu().numpy())
+    ra, ma = outs["mfma"]
+    rb, mb = outs["valu"]
+    assert np.array_equal(ra.view(np.uint8), rb.view(np.uint8))
+    for i in range(len(pairs)):
+        M = int(ra[i]["M"])
+        assert M > 0 and np.array_equal(ma[i, :M], mb[i, :M])
 
 
 def test_batch_full_size_properties(ctx, oracle):
