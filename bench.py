@@ -52,9 +52,12 @@ def parse():
     ap.add_argument("--profile-tag", default="r01e")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
-    ap.add_argument("--workload", choices=["pairs", "dense"], default="pairs",
-                    help="pairs: configs[1] (the metric); dense: configs[3], one N x N match "
-                         "(--kpts, default 16384) on both matcher methods, compared")
+    ap.add_argument("--workload", choices=["pairs", "dense", "manual"], default="pairs",
+                    help="pairs: configs[1] (the metric; configs[2] with --kpts 2048); dense: "
+                         "configs[3], one N x N match (--kpts, default 16384) on both matcher "
+                         "methods; manual: configs[4], one find() of --iters (default 100k) on "
+                         "100 manual-pickup correspondences (60%% outliers), hypothesis blocks "
+                         "sharded over the ranks")
     return ap.parse_args()
 
 
@@ -191,11 +194,85 @@ def run_dense(args):
     print(json.dumps(line))
 
 
+def run_manual(args):
+    """configs[4]: ONE find() with I = 100k initial_guess iterations on the manual-pickup regime
+    (100 integer-pixel correspondences on 2048 x 1024, 60 % outliers), its iterations split into
+    contiguous hypothesis blocks over the ranks (glibc jump-ahead per block), records
+    all-gathered over RCCL, consensus on the merged list (strong scaling: the work is fixed)."""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, dist as D, results_to_numpy, synth
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    iters = args.iters if args.iters != 10000 else 100000
+    c = synth.make_correspondences(args.seed, m=100, outlier_frac=0.6)
+    kl = torch.from_numpy(c["kp_l"]).to(dev)
+    kr = torch.from_numpy(c["kp_r"]).to(dev)
+    ctx = Context(local)
+
+    def step():
+        return D.find_hypothesis_sharded_dev(ctx, c["W"], c["H"], kl, kr, 100, iters)[0]
+
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    ctx.set_profiling(True)
+    ctx.stage_times()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = {k: v[0] / args.steps for k, v in ctx.stage_times().items() if v[1] > 0}
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    r = results_to_numpy(res.view(1, -1))[0]
+    if rank == 0:
+        # the unsharded find() on this GPU must give the same winner (outside the timed region)
+        from erp_match_eightpoint_test_amd import eight_point
+        ep = eight_point(ctx=Context(local), iters=iters)
+        R1, T1 = ep.find(c["W"], c["H"], c["kp_l"], c["kp_r"])
+        line = {"metric": f"find() calls/sec, {iters // 1000}k-iteration RANSAC on 100 manual-pickup "
+                          "correspondences (60% outliers), hypothesis blocks sharded (configs[4])",
+                "value": args.steps / elapsed, "unit": "finds/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+                "scaling": "strong", "vs_baseline": None, "dtype": "f64+f32",
+                "data": "synthetic (synth.make_correspondences, seeded)",
+                "config": {"workload": "configs[4]", "iters": iters, "m": 100,
+                           "parallelism": f"hypothesis blocks x{world}",
+                           "iterations_per_s": iters * args.steps / elapsed},
+                "stages_ms_rank0": st,
+                "check": {"status": int(r["status"]), "K": int(r["K"]),
+                          "min_idx": int(r["min_idx"]), "survivors": int(r["survivors"]),
+                          "same_as_unsharded": bool(np.array_equal(r["R"], R1) and
+                                                    np.array_equal(r["T"], T1))}}
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     import torch
     if args.workload == "dense":
         return run_dense(args)
+    if args.workload == "manual":
+        return run_manual(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

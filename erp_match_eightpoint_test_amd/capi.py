@@ -85,7 +85,7 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_eight_point_find_dev", "erp_eight_point_find", "erp_initial_guess",
             "erp_eight_point_estimation", "erp_pair_batch_run", "erp_ctx_set_profiling",
             "erp_stage_name", "erp_ctx_stage_times", "erp_eight_point_hypotheses_dev",
-            "erp_consensus_dev", "erp_ctx_set_matcher"]
+            "erp_consensus_dev", "erp_ctx_set_matcher", "erp_consensus_hyps_dev"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
@@ -143,6 +143,7 @@ def load(build_if_missing: bool = False):
     L.erp_consensus_dev.argtypes = [P, P, P, C.c_int32, C.c_double, C.c_double, P, P]
     L.erp_ctx_set_profiling.argtypes = [P, C.c_int32]
     L.erp_ctx_set_matcher.argtypes = [P, C.c_int32]
+    L.erp_consensus_hyps_dev.argtypes = [P, C.c_int32, P, C.c_int32, C.POINTER(RansacCfg), P, P]
     L.erp_stage_name.argtypes = [C.c_int32]
     L.erp_stage_name.restype = C.c_char_p
     L.erp_ctx_stage_times.argtypes = [P, P, P]

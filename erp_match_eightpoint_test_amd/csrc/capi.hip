@@ -656,6 +656,25 @@ erp_status erp_consensus_dev(erp_ctx* ctx, const float* d_rvec, const float* d_t
     return run_consensus(ctx, sh, &cfg, nullptr, d_result, st, false);
 }
 
+erp_status erp_consensus_hyps_dev(erp_ctx* ctx, int32_t m, const erp_hypothesis* d_hyps,
+                                  int32_t n_hyps, const erp_ransac_cfg* cfg,
+                                  erp_pair_result* d_result, void* stream) {
+    if (!ctx || m < 0 || m > 65535 || n_hyps < 1 || !d_hyps || !d_result || !cfg_ok(cfg))
+        return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    const erp::BatchShape sh = make_shape(1, std::max(m, 1), std::max(m, 1), n_hyps,
+                                          cfg->sample_frac);
+    erp_batch_outputs out{};
+    out.hyps = const_cast<erp_hypothesis*>(d_hyps);  // read only by the consensus stages
+    erp_status es = ensure_estimator(ctx, sh, &out);
+    if (es != ERP_OK) return es;
+    ERP_CK(hipMemsetAsync(ctx->flags.p, 0, 4, st));
+    ERP_CK(erp::launch_set_i32((int32_t*)ctx->counts.p, m, st));
+    return run_consensus(ctx, sh, cfg, &out, d_result, st, true);
+}
+
 erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* h_kl,
                                 const erp_point2f* h_kr, int32_t m, const erp_ransac_cfg* cfg,
                                 float R_out[3], float T_out[3], erp_pair_result* h_result) {

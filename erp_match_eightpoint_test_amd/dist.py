@@ -71,6 +71,52 @@ def find_hypothesis_sharded(hyp_fn, consensus_fn, m: int, iters: int, offset: in
     return consensus_fn(rvec, tvec), merged
 
 
+def padded_block(iters: int, world: int, rank: int) -> tuple[int, int, int]:
+    """block size B = ceil(iters / world) and this rank's iterations [a, b) = [rank B, ..)."""
+    blk = max(1, -(-iters // world))
+    a = min(iters, rank * blk)
+    return blk, a, min(iters, a + blk)
+
+
+def find_hypothesis_sharded_dev(ctx, W: int, H: int, d_kl, d_kr, m: int, iters: int,
+                                cfg_kwargs: dict | None = None, group=None, stream=None):
+    """configs[4] on GPUs, device-resident end to end: rank r computes iterations
+    [r B, (r+1) B) (B = ceil(iters / world)) into a zero-padded block of B records
+    (erp_eight_point_hypotheses_dev at glibc offset base + r B (m-1)), the blocks are
+    all-gathered over RCCL in rank order (= iteration order; zero records push nothing), and
+    every rank runs the valid-list compaction + consensus on the merged records
+    (erp_consensus_hyps_dev).  Returns (result record tensor [64] uint8, merged records)."""
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+
+    from .capi import HYP_DTYPE, RESULT_DTYPE, check, default_cfg
+    cfg_kwargs = dict(cfg_kwargs or {})
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    blk, a, b = padded_block(iters, world, rank)
+    dev = d_kl.device
+    st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    local = torch.zeros((blk, HYP_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    base = int(cfg_kwargs.pop("offset", 0))
+    if b > a:
+        cfg = default_cfg(**dict(cfg_kwargs, iters=b - a, offset=base + a * (m - 1)))
+        check(ctx.L.erp_eight_point_hypotheses_dev(ctx.h, W, H, d_kl.data_ptr(), d_kr.data_ptr(),
+                                                   m, C.byref(cfg), local.data_ptr(), st),
+              "erp_eight_point_hypotheses_dev")
+    if world > 1:
+        merged = torch.empty((world * blk, HYP_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        dist.all_gather_into_tensor(merged, local, group=group)
+    else:
+        merged = local
+    res = torch.zeros(RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    cfg = default_cfg(**dict(cfg_kwargs, iters=iters))
+    check(ctx.L.erp_consensus_hyps_dev(ctx.h, m, merged.data_ptr(), merged.shape[0], C.byref(cfg),
+                                       res.data_ptr(), st), "erp_consensus_hyps_dev")
+    return res, merged
+
+
 def shard_pairs(n_pairs: int, group=None) -> range:
     import torch.distributed as dist
     a, b = block_range(n_pairs, dist.get_world_size(group), dist.get_rank(group))

@@ -222,6 +222,13 @@ erp_status erp_eight_point_hypotheses_dev(erp_ctx* ctx, int32_t W, int32_t H,
 erp_status erp_consensus_dev(erp_ctx* ctx, const float* d_rvec, const float* d_tvec, int32_t K,
                              double trim_lo, double trim_hi, erp_pair_result* d_result,
                              void* stream);
+/* device pointers: valid-list compaction (R1 then R2 per record, src/eight_point.cpp:113-126)
+   + the consensus over n_hyps initial_guess records d_hyps (e.g. the rank-ordered all-gather of
+   hypothesis blocks; records with both flags 0 push nothing, so blocks may be zero-padded);
+   m = match_size (only reported in the result). */
+erp_status erp_consensus_hyps_dev(erp_ctx* ctx, int32_t m, const erp_hypothesis* d_hyps,
+                                  int32_t n_hyps, const erp_ransac_cfg* cfg,
+                                  erp_pair_result* d_result, void* stream);
 /* host pointers, synchronous: the drop-in for eight_point::find. */
 erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* h_kl,
                                 const erp_point2f* h_kr, int32_t m, const erp_ransac_cfg* cfg,

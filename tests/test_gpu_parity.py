@@ -381,6 +381,51 @@ def test_hypothesis_blocks_by_offset_match_full_run(ctx, oracle):
     assert np.abs(res["R"] - g["R"]).max() <= 2e-6 and np.abs(res["T"] - g["T"]).max() <= 2e-6
 
 
+@pytest.mark.parametrize("world", [1, 3, 8])
+def test_hypothesis_sharded_dev_padded_blocks(ctx, world):
+    """the device-resident configs[4] partition: zero-padded blocks of B = ceil(I / world)
+    records per rank (emulated in one process, concatenated in rank order as the RCCL
+    all-gather would) -> erp_consensus_hyps_dev gives the unsharded find's result; world 1 goes
+    through dist.find_hypothesis_sharded_dev itself."""
+    import ctypes as C
+
+    import torch
+    from erp_match_eightpoint_test_amd import HYP_DTYPE, capi, eight_point, results_to_numpy
+    from erp_match_eightpoint_test_amd import dist as D
+    g = _npz("find_manual_100_it500.npz")
+    W, H = int(g["W"]), int(g["H"])
+    kl = torch.from_numpy(np.ascontiguousarray(g["kl"])).cuda()
+    kr = torch.from_numpy(np.ascontiguousarray(g["kr"])).cuda()
+    m, iters = kl.shape[0], 500
+    if world == 1:
+        res, _ = D.find_hypothesis_sharded_dev(ctx, W, H, kl, kr, m, iters)
+    else:
+        blocks = []
+        for r in range(world):
+            blk, a, b = D.padded_block(iters, world, r)
+            loc = torch.zeros((blk, HYP_DTYPE.itemsize), dtype=torch.uint8, device="cuda")
+            if b > a:
+                cfg = capi.default_cfg(iters=b - a, offset=a * (m - 1))
+                capi.check(ctx.L.erp_eight_point_hypotheses_dev(
+                    ctx.h, W, H, kl.data_ptr(), kr.data_ptr(), m, C.byref(cfg), loc.data_ptr(),
+                    torch.cuda.current_stream().cuda_stream), "hypotheses")
+            blocks.append(loc)
+        merged = torch.cat(blocks)
+        res = torch.zeros(64, dtype=torch.uint8, device="cuda")
+        cfg = capi.default_cfg(iters=iters)
+        capi.check(ctx.L.erp_consensus_hyps_dev(ctx.h, m, merged.data_ptr(), merged.shape[0],
+                                                C.byref(cfg), res.data_ptr(),
+                                                torch.cuda.current_stream().cuda_stream),
+                   "consensus_hyps")
+    torch.cuda.synchronize()
+    r = results_to_numpy(res.view(1, -1))[0]
+    ep = eight_point(ctx=ctx, iters=iters)
+    R, T = ep.find(W, H, g["kl"], g["kr"])
+    assert r["status"] == 0 and r["K"] == int(g["K"]) == ep.last_result["K"]
+    assert r["min_idx"] == ep.last_result["min_idx"]
+    assert np.array_equal(r["R"], R) and np.array_equal(r["T"], T)
+
+
 @pytest.mark.parametrize("K", [1, 2, 3, 5, 40, 1000])
 def test_consensus_dev_vs_oracle(ctx, oracle, K):
     from erp_match_eightpoint_test_amd import dist as D
