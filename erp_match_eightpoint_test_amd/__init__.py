@@ -4,6 +4,8 @@ Host-side mirror of the reference's hot-path classes (Kitsunetic/ERP_match_eight
 
 * ``feature_matcher.match_two_image``  -- src/feature_matcher.cpp:42-59
 * ``eight_point.find / initial_guess / eight_point_estimation`` -- src/eight_point.cpp:16-192
+* ``erp_rotation`` / ``spherical_surf`` -- the ERP remaps either side of the path
+  (src/erp_rotation.cpp:14-122, src/spherical_surf.cpp:16-133, src/automatic.cpp:50-79,148-152)
 * ``PairBatchRunner`` -- the batched hot path: match -> gather -> find for many ERP pairs,
   i.e. what src/automatic.cpp:117-126 runs per pair, as one sequence of gfx950 kernels.
 
@@ -21,7 +23,7 @@ from . import capi, synth
 from .capi import (DMATCH_DTYPE, HYP_DTYPE, RESULT_DTYPE, Context, ErpError, check,
                    default_cfg)
 
-__all__ = ["feature_matcher", "eight_point", "PairBatchRunner", "Context", "ErpError",
+__all__ = ["feature_matcher", "eight_point", "erp_rotation", "spherical_surf", "PairBatchRunner", "Context", "ErpError",
            "default_cfg", "DMATCH_DTYPE", "HYP_DTYPE", "RESULT_DTYPE", "results_to_numpy",
            "hyps_to_numpy", "synth", "capi"]
 
@@ -138,6 +140,151 @@ class eight_point:  # noqa: N801  (reference class name)
         r = np.frombuffer(bytes(h), HYP_DTYPE)[0]
         return (r["R1"].copy(), r["R2"].copy(), r["T"].copy(), bool(r["R1_valid"]),
                 bool(r["R2_valid"]), r["E"].copy())
+
+
+def _m9(a) -> np.ndarray:
+    return np.ascontiguousarray(a, np.float64).reshape(9)
+
+
+def _img_dev(im):
+    import torch
+    if not (isinstance(im, torch.Tensor) and im.is_cuda and im.dtype == torch.uint8
+            and im.dim() == 3 and im.shape[2] == 3 and im.is_contiguous()):
+        raise ValueError("images are contiguous CUDA uint8 tensors [H, W, 3] (CV_8UC3)")
+    return im
+
+
+class erp_rotation:  # noqa: N801  (reference class name)
+    """erp_rotation (src/erp_rotation.hpp:9-19).  Matrices are host numpy (3, 3) float64;
+    images are CUDA uint8 tensors [H, W, 3].  Output pixels whose source falls outside the
+    image are not written (uninitialised in the reference): ``fill`` pre-fills them."""
+
+    def __init__(self, device: int = 0, ctx: Context | None = None):
+        self.ctx = ctx or Context(device)
+        self.L = self.ctx.L
+
+    def eular2rot(self, theta) -> np.ndarray:
+        th = np.ascontiguousarray(theta, np.float64).reshape(3)
+        R = np.zeros(9, np.float64)
+        self.L.erp_eular2rot(_np_ptr(th), _np_ptr(R))
+        return R.reshape(3, 3)
+
+    def rot2eular(self, R) -> np.ndarray:
+        m = _m9(R)
+        e = np.zeros(3, np.float64)
+        self.L.erp_rot2eular(_np_ptr(m), _np_ptr(e))
+        return e
+
+    def rotate_image(self, im, rot_mat, fill: int = 0):
+        import torch
+        im = _img_dev(im)
+        H, W = im.shape[:2]
+        out = torch.full_like(im, fill)
+        m = _m9(rot_mat)
+        check(self.L.erp_rotate_image_dev(self.ctx.h, im.data_ptr(), W, H, _np_ptr(m),
+                                          out.data_ptr(), torch.cuda.current_stream().cuda_stream),
+              "rotate_image")
+        return out
+
+    def rot_from_vec(self, v1, v2) -> np.ndarray:
+        a = np.ascontiguousarray(v1, np.float64).reshape(3)
+        b = np.ascontiguousarray(v2, np.float64).reshape(3)
+        R = np.zeros(9, np.float64)
+        self.L.erp_rot_from_vec(_np_ptr(a), _np_ptr(b), _np_ptr(R))
+        return R.reshape(3, 3)
+
+    def inv(self, m) -> np.ndarray:
+        """cv::Mat::inv() of a 3x3 double matrix"""
+        a = _m9(m)
+        o = np.zeros(9, np.float64)
+        if not self.L.erp_inv3(_np_ptr(a), _np_ptr(o)):
+            raise ErpError(capi.ERP_INVALID_ARG, "inv: singular")
+        return o.reshape(3, 3)
+
+    def rectify(self, im_left, im_right, rot_vec, t_vec, fill: int = 0):
+        """rectify (src/automatic.cpp:66-79) -> (left_rectified, right_rectified)"""
+        import torch
+        im_left, im_right = _img_dev(im_left), _img_dev(im_right)
+        H, W = im_left.shape[:2]
+        lo, ro = torch.full_like(im_left, fill), torch.full_like(im_right, fill)
+        rv = np.ascontiguousarray(rot_vec, np.float64).reshape(3)
+        tv = np.ascontiguousarray(t_vec, np.float64).reshape(3)
+        check(self.L.erp_rectify_dev(self.ctx.h, im_left.data_ptr(), im_right.data_ptr(), W, H,
+                                     _np_ptr(rv), _np_ptr(tv), lo.data_ptr(), ro.data_ptr(),
+                                     torch.cuda.current_stream().cuda_stream), "rectify")
+        return lo, ro
+
+    def vertical_rotate(self, im, fill: int = 0):
+        """src/automatic.cpp:148-151: rotate_image by eular2rot(RAD(89.999),0,0).inv(), then
+        cv::rotate(ROTATE_90_CLOCKWISE) -> [W, H, 3]"""
+        import torch
+        im = _img_dev(im)
+        H, W = im.shape[:2]
+        out = torch.full((W, H, 3), fill, dtype=torch.uint8, device=im.device)
+        check(self.L.erp_vertical_rotate_dev(self.ctx.h, im.data_ptr(), W, H, out.data_ptr(),
+                                             torch.cuda.current_stream().cuda_stream),
+              "vertical_rotate")
+        return out
+
+
+class spherical_surf:  # noqa: N801  (reference class name)
+    """spherical_surf (src/spherical_surf.hpp:11-29), the remap half: the four de-distorted bands
+    of an ERP image and the keypoint un-rotation back to ERP pixels.  (SURF detection itself is
+    out of scope: descriptors + band keypoints come from the caller.)"""
+
+    PITCH = (45.0, 0.0, -45.0, -90.0)  # bands n0..n3 (src/spherical_surf.cpp:77-83)
+
+    def __init__(self, device: int = 0, ctx: Context | None = None):
+        self.ctx = ctx or Context(device)
+        self.L = self.ctx.L
+
+    def crop_rotated_image(self, pitch_rot: float, im, fill: int = 0):
+        import torch
+        im = _img_dev(im)
+        H, W = im.shape[:2]
+        out = torch.full((H // 4, W, 3), fill, dtype=torch.uint8, device=im.device)
+        check(self.L.erp_crop_rotated_image_dev(self.ctx.h, im.data_ptr(), W, H, pitch_rot,
+                                                out.data_ptr(),
+                                                torch.cuda.current_stream().cuda_stream),
+              "crop_rotated_image")
+        return out
+
+    def bands(self, ims, fill: int = 0):
+        """ims: CUDA uint8 [n, H, W, 3] (or [H, W, 3]) -> [n, 4, H/4, W, 3]"""
+        import torch
+        single = ims.dim() == 3
+        if single:
+            ims = ims.unsqueeze(0)
+        if not (ims.is_cuda and ims.dtype == torch.uint8 and ims.is_contiguous()
+                and ims.dim() == 4 and ims.shape[3] == 3):
+            raise ValueError("images are contiguous CUDA uint8 tensors [n, H, W, 3]")
+        n, H, W = ims.shape[:3]
+        out = torch.full((n, 4, H // 4, W, 3), fill, dtype=torch.uint8, device=ims.device)
+        check(self.L.erp_spherical_bands_dev(self.ctx.h, ims.data_ptr(), n, W, H, out.data_ptr(),
+                                             torch.cuda.current_stream().cuda_stream), "bands")
+        return out[0] if single else out
+
+    def rotate_keypoint(self, pitch_rot_inv: float, key, width: int, height: int):
+        """in place on a CUDA float32 tensor [n, 2] of (pt.x, pt.y)"""
+        import torch
+        check(self.L.erp_rotate_keypoints_dev(self.ctx.h, key.data_ptr(), key.shape[0],
+                                              pitch_rot_inv, width, height,
+                                              torch.cuda.current_stream().cuda_stream),
+              "rotate_keypoint")
+        return key
+
+    def unrotate_band_keypoints(self, key, counts, width: int, height: int):
+        """do_all's keypoint step (src/spherical_surf.cpp:120-144), in place on the band
+        keypoints concatenated n0, n1, n2, n3 (CUDA float32 [n, 2]); counts = 4 band sizes"""
+        import torch
+        c = np.ascontiguousarray(counts, np.int32).reshape(4)
+        if int(c.sum()) != key.shape[0]:
+            raise ValueError("counts do not sum to the keypoint count")
+        check(self.L.erp_unrotate_band_keypoints_dev(self.ctx.h, key.data_ptr(), _np_ptr(c),
+                                                     width, height,
+                                                     torch.cuda.current_stream().cuda_stream),
+              "unrotate_band_keypoints")
+        return key
 
 
 class PairBatchRunner:

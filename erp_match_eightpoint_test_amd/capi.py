@@ -85,7 +85,11 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_eight_point_find_dev", "erp_eight_point_find", "erp_initial_guess",
             "erp_eight_point_estimation", "erp_pair_batch_run", "erp_ctx_set_profiling",
             "erp_stage_name", "erp_ctx_stage_times", "erp_eight_point_hypotheses_dev",
-            "erp_consensus_dev", "erp_ctx_set_matcher", "erp_consensus_hyps_dev"]
+            "erp_consensus_dev", "erp_ctx_set_matcher", "erp_consensus_hyps_dev",
+            "erp_crop_rotated_image_dev", "erp_spherical_bands_dev", "erp_rotate_keypoints_dev",
+            "erp_unrotate_band_keypoints_dev", "erp_rotate_image_dev", "erp_rectify_dev",
+            "erp_vertical_rotate_dev", "erp_eular2rot", "erp_rot2eular", "erp_rot_from_vec",
+            "erp_inv3", "erp_rectify_matrices"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
@@ -143,6 +147,22 @@ def load(build_if_missing: bool = False):
     L.erp_consensus_dev.argtypes = [P, P, P, C.c_int32, C.c_double, C.c_double, P, P]
     L.erp_ctx_set_profiling.argtypes = [P, C.c_int32]
     L.erp_ctx_set_matcher.argtypes = [P, C.c_int32]
+    L.erp_crop_rotated_image_dev.argtypes = [P, P, C.c_int32, C.c_int32, C.c_float, P, P]
+    L.erp_spherical_bands_dev.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P]
+    L.erp_rotate_keypoints_dev.argtypes = [P, P, C.c_int32, C.c_float, C.c_int32, C.c_int32, P]
+    L.erp_unrotate_band_keypoints_dev.argtypes = [P, P, P, C.c_int32, C.c_int32, P]
+    L.erp_rotate_image_dev.argtypes = [P, P, C.c_int32, C.c_int32, P, P, P]
+    L.erp_rectify_dev.argtypes = [P, P, P, C.c_int32, C.c_int32, P, P, P, P, P]
+    L.erp_vertical_rotate_dev.argtypes = [P, P, C.c_int32, C.c_int32, P, P]
+    L.erp_eular2rot.argtypes = [P, P]
+    L.erp_eular2rot.restype = None
+    L.erp_rot2eular.argtypes = [P, P]
+    L.erp_rot2eular.restype = None
+    L.erp_rot_from_vec.argtypes = [P, P, P]
+    L.erp_rot_from_vec.restype = None
+    L.erp_inv3.argtypes = [P, P]
+    L.erp_inv3.restype = C.c_int32
+    L.erp_rectify_matrices.argtypes = [P, P, P, P]
     L.erp_consensus_hyps_dev.argtypes = [P, C.c_int32, P, C.c_int32, C.POINTER(RansacCfg), P, P]
     L.erp_stage_name.argtypes = [C.c_int32]
     L.erp_stage_name.restype = C.c_char_p

@@ -115,6 +115,12 @@ extern "C" {
 
 int32_t erp_abi_version(void) { return ERP_MATCH_ABI_VERSION; }
 
+}  // extern "C"
+
+int32_t erp_ctx_device_internal(erp_ctx* ctx) { return ctx->device; }  // remap_api.hip
+
+extern "C" {
+
 const char* erp_status_string(erp_status s) {
     switch (s) {
         case ERP_OK: return "ok";

@@ -14,6 +14,7 @@
 //   rot2eular         src/erp_rotation.cpp:43-63
 //   pixel_to_bearing  src/eight_point.cpp:163-186
 //   estimate_from_e   src/eight_point.cpp:42-84 (rank-2 fix, decompose, Euler, validity)
+//   rotate_pixel      src/erp_rotation.cpp:66-92 (band remap, keypoint un-rotation, rectification)
 #pragma once
 
 #include <stdint.h>
@@ -249,6 +250,69 @@ ERP_HD ERP_INLINE void pixel_to_bearing(int32_t W, int32_t H, float px, float py
     b[0] = -sl * cos(lon);
     b[1] = sl * sin(lon);
     b[2] = cos(lat);
+}
+
+// ---- ERP remapping (section 8f: band remap and rectification) ---------------------------
+// double -> int32 as x86-64's cvttsd2si (the reference's implicit conversions compile to it):
+// truncation toward zero, and the "integer indefinite" INT32_MIN for NaN or out-of-range values
+// (C leaves those undefined; the GPU's v_cvt_i32_f64 would clamp / give 0 instead).
+ERP_HD ERP_INLINE int32_t trunc_i32_x86(double x) {
+    if (!(x > -2147483649.0 && x < 2147483648.0)) return INT32_MIN;
+    return (int32_t)x;
+}
+ERP_HD ERP_INLINE int32_t trunc_i32_x86f(float x) {  // cvttss2si
+    if (!(x >= -2147483648.0f && x < 2147483648.0f)) return INT32_MIN;
+    return (int32_t)x;
+}
+
+// atan2 / acos as glibc's (correctly rounded in practice) where the device library is not:
+// the results that decide a truncated pixel index at the ERP seams are pi - tiny and
+// pi/2 - tiny (e.g. column W/2, where sin(2*M_PI*col/W) = 1.2e-16 makes atan2(tiny, x<0));
+// the device atan2 returns atan(|y/x|) subtracted from pi without pi's low part and can land
+// one ulp below glibc, flipping (int)(W*v/(2*M_PI)) from W/2 to W/2-1.  In those regimes the
+// value is rebuilt from pi = PI_HI + PI_LO: pi - z = PI_HI + (PI_LO - z) (one rounding), with
+// atan(z) = z (1 - z^2/3 + ...) = z to far below an ulp for z <= 2^-30.
+ERP_HD ERP_INLINE double atan2_ref(double y, double x) {
+    constexpr double kPiHi = 3.141592653589793116, kPiLo = 1.2246467991473532e-16;
+    if (x < 0 && fabs(y) <= 0x1p-30 * -x) {
+        const double z = fabs(y) / -x;
+        return copysign(kPiHi + (kPiLo - z), y);
+    }
+    return atan2(y, x);
+}
+ERP_HD ERP_INLINE double acos_ref(double r) {
+    constexpr double kPio2Hi = 1.5707963267948966, kPio2Lo = 6.123233995736766e-17;
+    if (fabs(r) <= 0x1p-30) return kPio2Hi + (kPio2Lo - r);  // acos r = pi/2 - r - r^3/6 ...
+    return acos(r);
+}
+
+// erp_rotation::rotate_pixel (src/erp_rotation.cpp:66-92): pixel (row, col) -> sphere (OMAF
+// axes) -> m * v -> pixel, each conversion truncating.  The polar / azimuth angles of the input
+// come from their sines and cosines (sa = sin(M_PI*row/height), ca = cos(...), sb, cb of
+// 2*M_PI*col/width), so callers can tabulate them per row / per column.
+ERP_HD ERP_INLINE void rotate_pixel_sc(double sa, double ca, double sb, double cb,
+                                       const double* m, int32_t W, int32_t H, int32_t* out_row,
+                                       int32_t* out_col) {
+    const double c0 = -sa * cb;
+    const double c1 = sa * sb;
+    const double c2 = ca;
+    const double r0 = m[0] * c0 + m[1] * c1 + m[2] * c2;
+    const double r1 = m[3] * c0 + m[4] * c1 + m[5] * c2;
+    const double r2 = m[6] * c0 + m[7] * c1 + m[8] * c2;
+    const double v0 = acos_ref(r2);
+    double v1 = atan2_ref(r1, -r0);
+    if (v1 < 0) v1 += kPi * 2;
+    *out_row = trunc_i32_x86((double)H * v0 / kPi);
+    *out_col = trunc_i32_x86((double)W * v1 / (2 * kPi));
+}
+ERP_HD ERP_INLINE double erp_polar(int32_t row, int32_t H) { return kPi * (double)row / (double)H; }
+ERP_HD ERP_INLINE double erp_azimuth(int32_t col, int32_t W) {
+    return 2 * kPi * (double)col / (double)W;
+}
+ERP_HD ERP_INLINE void rotate_pixel(int32_t row, int32_t col, const double* m, int32_t W,
+                                    int32_t H, int32_t* out_row, int32_t* out_col) {
+    const double a = erp_polar(row, H), b = erp_azimuth(col, W);
+    rotate_pixel_sc(sin(a), cos(a), sin(b), cos(b), m, W, H, out_row, out_col);
 }
 
 ERP_HD ERP_INLINE double max_vec(const float* v) {

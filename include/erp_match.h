@@ -247,6 +247,50 @@ erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* batch, float r
                               const erp_ransac_cfg* cfg, const erp_batch_outputs* out,
                               void* stream);
 
+/* ---- ERP remaps around the hot path ----
+   Images are 8-bit 3-channel (CV_8UC3, BGR) H x W x 3, row-major, device pointers.  Output
+   pixels whose inverse-warped source falls outside the image are NOT written (the reference
+   leaves them uninitialised): pre-fill the outputs. */
+/* spherical_surf::crop_rotated_image(pitch, im) (src/spherical_surf.cpp:16-48): the central
+   H/4 rows of the image rotated by pitch degrees about Y -> d_out (H/4) x W x 3. */
+erp_status erp_crop_rotated_image_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W, int32_t H,
+                                      float pitch_deg, uint8_t* d_out, void* stream);
+/* the four bands of spherical_surf::do_all (src/spherical_surf.cpp:77-93) for n_images images
+   (contiguous, each H x W x 3): d_bands [n][4][H/4][W][3] = crop(45), rows [3H/8, 3H/8 + H/4),
+   crop(-45), crop(-90). */
+erp_status erp_spherical_bands_dev(erp_ctx* ctx, const uint8_t* d_ims, int32_t n_images,
+                                   int32_t W, int32_t H, uint8_t* d_bands, void* stream);
+/* spherical_surf::rotate_keypoint(pitch, key, width, height) (src/spherical_surf.cpp:50-63),
+   in place on n keypoints (pt.x, pt.y). */
+erp_status erp_rotate_keypoints_dev(erp_ctx* ctx, erp_point2f* d_kp, int32_t n, float pitch_deg,
+                                    int32_t W, int32_t H, void* stream);
+/* do_all's keypoint un-rotation (src/spherical_surf.cpp:120-133) on the band keypoints
+   concatenated in band order n0, n1, n2, n3 (counts[4]), in place: the result is the
+   left_key_tmp / right_key_tmp index space of the matcher (:136-144). */
+erp_status erp_unrotate_band_keypoints_dev(erp_ctx* ctx, erp_point2f* d_kp,
+                                           const int32_t counts[4], int32_t W, int32_t H,
+                                           void* stream);
+/* erp_rotation::rotate_image(im, rot_mat) (src/erp_rotation.cpp:94-122). */
+erp_status erp_rotate_image_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W, int32_t H,
+                                const double rot_mat[9], uint8_t* d_out, void* stream);
+/* rectify(im_left, im_right, R_vec, T_vec) (src/automatic.cpp:66-79): both rotate_image calls
+   in one launch. */
+erp_status erp_rectify_dev(erp_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right, int32_t W,
+                           int32_t H, const double rot_vec[3], const double t_vec[3],
+                           uint8_t* d_left_out, uint8_t* d_right_out, void* stream);
+/* the vertical view of src/automatic.cpp:148-151: rotate_image by eular2rot(RAD(89.999), 0, 0)
+   .inv(), then cv::rotate(ROTATE_90_CLOCKWISE), fused -> d_out W x H x 3 (W rows). */
+erp_status erp_vertical_rotate_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W, int32_t H,
+                                   uint8_t* d_out, void* stream);
+/* host 3x3 geometry (row-major doubles) */
+void erp_eular2rot(const double theta[3], double R[9]);         /* erp_rotation.cpp:14-40 */
+void erp_rot2eular(const double R[9], double e[3]);             /* erp_rotation.cpp:43-63 */
+void erp_rot_from_vec(const double v1[3], const double v2[3], double R[9]); /* automatic.cpp:50-64 */
+int32_t erp_inv3(const double m[9], double out[9]);            /* cv::Mat::inv() on 3x3 */
+/* the two matrices rotate_pixel applies in rectify's rotate_image calls */
+erp_status erp_rectify_matrices(const double rot_vec[3], const double t_vec[3], double m_left[9],
+                                double m_right[9]);
+
 #ifdef __cplusplus
 }
 #endif

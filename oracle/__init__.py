@@ -94,6 +94,20 @@ def lib():
         L.erpo_find.argtypes = [C.c_int32, C.c_int32, P, P, C.c_int32, C.POINTER(Cfg), P, P,
                                 C.POINTER(Diag), P, P, P, P, P]
         L.erpo_find.restype = C.c_int
+        L.erpo_rotate_pixel.argtypes = [C.c_int32, C.c_int32, P, C.c_int32, C.c_int32, P]
+        L.erpo_rotate_pixel_prefix.argtypes = [P, P, C.c_int32, P, C.c_int32, C.c_int32, P]
+        L.erpo_inv3.argtypes = [P, P]
+        L.erpo_inv3.restype = C.c_int32
+        L.erpo_rot_from_vec.argtypes = [P, P, P]
+        L.erpo_crop_rotated_image.argtypes = [P, C.c_int32, C.c_int32, C.c_float, P]
+        L.erpo_rotate_keypoint.argtypes = [P, C.c_int32, C.c_float, C.c_int32, C.c_int32]
+        L.erpo_unrotate_band_keypoints.argtypes = [P, P, C.c_int32, C.c_int32]
+        L.erpo_rotate_image.argtypes = [P, C.c_int32, C.c_int32, P, P]
+        L.erpo_rotate_image.restype = C.c_int32
+        L.erpo_rectify.argtypes = [P, P, C.c_int32, C.c_int32, P, P, P, P]
+        L.erpo_rectify.restype = C.c_int32
+        L.erpo_vertical_rotate.argtypes = [P, C.c_int32, C.c_int32, P]
+        L.erpo_vertical_rotate.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -248,3 +262,109 @@ def find(W: int, H: int, kl, kr, cfg: Cfg | None = None, detail: bool = False):
     kr = np.ascontiguousarray(kr, np.float32).reshape(-1, 2)
     m = kl.shape[0]
     return _run_guess(lib().erpo_find, (W, H, _p(kl), _p(kr), m), m, cfg, detail)
+
+
+# ------------------------------------------------------------------ ERP remaps (section 8f)
+def _img(im):
+    im = np.ascontiguousarray(im, np.uint8)
+    assert im.ndim == 3 and im.shape[2] == 3
+    return im
+
+
+def rotate_pixel(row: int, col: int, m, W: int, H: int) -> tuple[int, int]:
+    m = np.ascontiguousarray(m, np.float64).reshape(9)
+    o = np.zeros(2, np.int32)
+    lib().erpo_rotate_pixel(int(row), int(col), _p(m), W, H, _p(o))
+    return int(o[0]), int(o[1])
+
+
+def inv3(m) -> np.ndarray:
+    m = np.ascontiguousarray(m, np.float64).reshape(9)
+    o = np.zeros(9, np.float64)
+    if not lib().erpo_inv3(_p(m), _p(o)):
+        raise ValueError("singular")
+    return o.reshape(3, 3)
+
+
+def rot_from_vec(v1, v2) -> np.ndarray:
+    a = np.ascontiguousarray(v1, np.float64)
+    b = np.ascontiguousarray(v2, np.float64)
+    R = np.zeros(9, np.float64)
+    lib().erpo_rot_from_vec(_p(a), _p(b), _p(R))
+    return R.reshape(3, 3)
+
+
+def crop_rotated_image(im, pitch_deg: float, fill: int = 0) -> np.ndarray:
+    im = _img(im)
+    H, W = im.shape[:2]
+    out = np.full((H // 4, W, 3), fill, np.uint8)
+    lib().erpo_crop_rotated_image(_p(im), W, H, pitch_deg, _p(out))
+    return out
+
+
+def spherical_bands(im, fill: int = 0) -> np.ndarray:
+    """do_all's four bands (src/spherical_surf.cpp:77-83): [4, H/4, W, 3]"""
+    im = _img(im)
+    H = im.shape[0]
+    n1 = im[H * 3 // 8: H * 3 // 8 + H // 4]
+    return np.stack([crop_rotated_image(im, 45.0, fill), n1, crop_rotated_image(im, -45.0, fill),
+                     crop_rotated_image(im, -90.0, fill)])
+
+
+def rotate_keypoint(kp, pitch_deg: float, W: int, H: int) -> np.ndarray:
+    kp = np.array(kp, np.float32).reshape(-1, 2)
+    lib().erpo_rotate_keypoint(_p(kp), kp.shape[0], pitch_deg, W, H)
+    return kp
+
+
+def unrotate_band_keypoints(kp, counts, W: int, H: int) -> np.ndarray:
+    kp = np.array(kp, np.float32).reshape(-1, 2)
+    c = np.ascontiguousarray(counts, np.int32)
+    assert c.sum() == kp.shape[0]
+    lib().erpo_unrotate_band_keypoints(_p(kp), _p(c), W, H)
+    return kp
+
+
+def rotate_image(im, rot_mat, fill: int = 0) -> np.ndarray:
+    im = _img(im)
+    H, W = im.shape[:2]
+    m = np.ascontiguousarray(rot_mat, np.float64).reshape(9)
+    out = np.full_like(im, fill)
+    if not lib().erpo_rotate_image(_p(im), W, H, _p(m), _p(out)):
+        raise ValueError("singular rot_mat")
+    return out
+
+
+def rectify(left, right, rot_vec, t_vec, fill: int = 0):
+    left, right = _img(left), _img(right)
+    H, W = left.shape[:2]
+    rv = np.ascontiguousarray(rot_vec, np.float64)
+    tv = np.ascontiguousarray(t_vec, np.float64)
+    lo, ro = np.full_like(left, fill), np.full_like(right, fill)
+    if not lib().erpo_rectify(_p(left), _p(right), W, H, _p(rv), _p(tv), _p(lo), _p(ro)):
+        raise ValueError("singular rectification matrix")
+    return lo, ro
+
+
+def vertical_rotate(im, fill: int = 0) -> np.ndarray:
+    im = _img(im)
+    H, W = im.shape[:2]
+    out = np.full((W, H, 3), fill, np.uint8)
+    if not lib().erpo_vertical_rotate(_p(im), W, H, _p(out)):
+        raise ValueError("singular")
+    return out
+
+
+def pitch_matrix(deg: float) -> np.ndarray:
+    """eular2rot(Vec3f(0, RAD(deg), 0)) (src/spherical_surf.cpp:26)"""
+    return eular2rot([0.0, float(np.float32(np.pi * np.float64(np.float32(deg)) / 180.0)), 0.0])
+
+
+def rotate_pixel_prefix(rows, cols, m, W: int, H: int) -> np.ndarray:
+    """[n, 2] values rotate_pixel truncates (row value, column value)"""
+    r = np.ascontiguousarray(rows, np.int32)
+    c = np.ascontiguousarray(cols, np.int32)
+    m = np.ascontiguousarray(m, np.float64).reshape(9)
+    out = np.zeros((len(r), 2), np.float64)
+    lib().erpo_rotate_pixel_prefix(_p(r), _p(c), len(r), _p(m), W, H, _p(out))
+    return out

@@ -652,3 +652,205 @@ int erpo_find(int32_t W, int32_t H, const float* kl, const float* kr, int32_t m,
     free(br);
     return rc;
 }
+
+/* ======================================================================================
+ * ERP remaps: src/erp_rotation.cpp:66-122, src/spherical_surf.cpp:16-63,
+ * 77-133, src/automatic.cpp:50-79,148-152.
+ * ==================================================================================== */
+/* x86-64 cvttsd2si / cvttss2si: truncation, INT32_MIN ("integer indefinite") for NaN and
+ * out-of-range values -- what the reference's implicit double/float -> int conversions do */
+static int32_t cvt_x86_d(double x) {
+    if (!(x > -2147483649.0 && x < 2147483648.0)) return INT32_MIN;
+    return (int32_t)x;
+}
+static int32_t cvt_x86_f(float x) {
+    if (!(x >= -2147483648.0f && x < 2147483648.0f)) return INT32_MIN;
+    return (int32_t)x;
+}
+
+/* erp_rotation::rotate_pixel, src/erp_rotation.cpp:66-92 (in_vec = (row, col)) */
+void erpo_rotate_pixel(int32_t row, int32_t col, const double m[9], int32_t W, int32_t H,
+                       int32_t out[2]) {
+    const double a = M_PI * row / H;                 /* :68 */
+    const double b = 2 * M_PI * col / W;
+    const double c0 = -sin(a) * cos(b);              /* :71-73 */
+    const double c1 = sin(a) * sin(b);
+    const double c2 = cos(a);
+    const double r0 = m[0] * c0 + m[1] * c1 + m[2] * c2;  /* :77-79 */
+    const double r1 = m[3] * c0 + m[4] * c1 + m[5] * c2;
+    const double r2 = m[6] * c0 + m[7] * c1 + m[8] * c2;
+    const double v0 = acos(r2);                      /* :82-85 */
+    double v1 = atan2(r1, -r0);
+    if (v1 < 0) v1 += M_PI * 2;
+    out[0] = cvt_x86_d(H * v0 / M_PI);               /* :88-89 */
+    out[1] = cvt_x86_d(W * v1 / (2 * M_PI));
+}
+
+/* rotate_pixel's two values BEFORE the truncating conversion (H*acos/M_PI, W*atan2'/(2*M_PI))
+ * for n pixels: the test diagnostic that tells a last-ulp libm decision (value within ~1e-12
+ * of an integer) from a real remap error */
+void erpo_rotate_pixel_prefix(const int32_t* rows, const int32_t* cols, int32_t n, const double m[9],
+                              int32_t W, int32_t H, double* out) {
+    int32_t k;
+    for (k = 0; k < n; k++) {
+        const double a = M_PI * rows[k] / H;
+        const double b = 2 * M_PI * cols[k] / W;
+        const double c0 = -sin(a) * cos(b);
+        const double c1 = sin(a) * sin(b);
+        const double c2 = cos(a);
+        const double r0 = m[0] * c0 + m[1] * c1 + m[2] * c2;
+        const double r1 = m[3] * c0 + m[4] * c1 + m[5] * c2;
+        const double r2 = m[6] * c0 + m[7] * c1 + m[8] * c2;
+        double v1 = atan2(r1, -r0);
+        if (v1 < 0) v1 += M_PI * 2;
+        out[2 * k] = H * acos(r2) / M_PI;
+        out[2 * k + 1] = W * v1 / (2 * M_PI);
+    }
+}
+
+/* Mat::inv() (DECOMP_LU) on a 3x3 double matrix: adjugate / determinant [OpenCV, recalled] */
+int32_t erpo_inv3(const double m[9], double out[9]) {
+    double d = m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
+               m[2] * (m[3] * m[7] - m[4] * m[6]);
+    double t[9];
+    if (d == 0.0) return 0;
+    d = 1. / d;
+    t[0] = (m[4] * m[8] - m[5] * m[7]) * d;
+    t[1] = (m[2] * m[7] - m[1] * m[8]) * d;
+    t[2] = (m[1] * m[5] - m[2] * m[4]) * d;
+    t[3] = (m[5] * m[6] - m[3] * m[8]) * d;
+    t[4] = (m[0] * m[8] - m[2] * m[6]) * d;
+    t[5] = (m[2] * m[3] - m[0] * m[5]) * d;
+    t[6] = (m[3] * m[7] - m[4] * m[6]) * d;
+    t[7] = (m[1] * m[6] - m[0] * m[7]) * d;
+    t[8] = (m[0] * m[4] - m[1] * m[3]) * d;
+    memcpy(out, t, sizeof(t));
+    return 1;
+}
+
+/* rot_from_vec, src/automatic.cpp:50-64: I + [v]x + [v]x*[v]x*(1/1+c), 1/1 = 1 (int) */
+void erpo_rot_from_vec(const double v1[3], const double v2[3], double R[9]) {
+    const double v[3] = {v1[1] * v2[2] - v1[2] * v2[1], v1[2] * v2[0] - v1[0] * v2[2],
+                         v1[0] * v2[1] - v1[1] * v2[0]};
+    const double c = v1[0] * v2[0] + v1[1] * v2[1] + v1[2] * v2[2];
+    const double vx[9] = {0, -v[2], v[1], v[2], 0, -v[0], -v[1], v[0], 0};
+    double sq[9];
+    int k;
+    gemm33(vx, vx, sq);
+    for (k = 0; k < 9; k++) R[k] = ((k % 4 == 0 ? 1.0 : 0.0) + vx[k]) + sq[k] * (1 / 1 + c);
+}
+
+/* eular2rot(Vec3f(0, RAD(pitch), 0)): RAD in double, stored into a float Vec3f */
+static void pitch_rot(float deg, double R[9]) {
+    const double e[3] = {0.0, (double)(float)(M_PI * deg / 180.0), 0.0};
+    erpo_eular2rot(e, R);
+}
+
+static void copy_px(const uint8_t* s, uint8_t* d) { d[0] = s[0]; d[1] = s[1]; d[2] = s[2]; }
+
+/* crop_rotated_image, src/spherical_surf.cpp:16-48 */
+void erpo_crop_rotated_image(const uint8_t* im, int32_t W, int32_t H, float pitch_deg,
+                             uint8_t* out) {
+    double R[9];
+    int i;
+    pitch_rot(pitch_deg, R);
+#pragma omp parallel for schedule(static)
+    for (i = 0; i < H / 4; i++) {
+        int j;
+        for (j = 0; j < W; j++) {
+            int32_t o[2];
+            erpo_rotate_pixel(i + H * 3 / 8, j, R, W, H, o);
+            if (o[0] >= 0 && o[1] >= 0 && o[0] < H && o[1] < W)
+                copy_px(im + ((size_t)o[0] * W + o[1]) * 3, out + ((size_t)i * W + j) * 3);
+        }
+    }
+}
+
+/* rotate_keypoint, src/spherical_surf.cpp:50-63 (kp_xy = n x (pt.x, pt.y) floats) */
+void erpo_rotate_keypoint(float* kp_xy, int32_t n, float pitch_deg, int32_t W, int32_t H) {
+    double R[9];
+    int32_t i;
+    pitch_rot(pitch_deg, R);
+    for (i = 0; i < n; i++) {
+        const int32_t offset_i = cvt_x86_f(kp_xy[2 * i + 1] + (float)(H * 3 / 8));
+        int32_t o[2];
+        erpo_rotate_pixel(offset_i, cvt_x86_f(kp_xy[2 * i]), R, W, H, o);
+        kp_xy[2 * i] = (float)o[1];
+        kp_xy[2 * i + 1] = (float)o[0];
+    }
+}
+
+/* do_all's keypoint step, src/spherical_surf.cpp:120-126 (bands n0, n1, n2, n3 in order) */
+void erpo_unrotate_band_keypoints(float* kp_xy, const int32_t counts[4], int32_t W, int32_t H) {
+    float* p = kp_xy;
+    int32_t i;
+    erpo_rotate_keypoint(p, counts[0], 45.f, W, H);
+    p += 2 * (size_t)counts[0];
+    for (i = 0; i < counts[1]; i++) p[2 * i + 1] = p[2 * i + 1] + (float)(H * 3 / 8);
+    p += 2 * (size_t)counts[1];
+    erpo_rotate_keypoint(p, counts[2], -45.f, W, H);
+    p += 2 * (size_t)counts[2];
+    erpo_rotate_keypoint(p, counts[3], -90.f, W, H);
+}
+
+/* rotate_image, src/erp_rotation.cpp:94-122 (rot_mat inverted inside, :103) */
+int32_t erpo_rotate_image(const uint8_t* im, int32_t W, int32_t H, const double rot_mat[9],
+                          uint8_t* out) {
+    double Ri[9];
+    int i;
+    if (!erpo_inv3(rot_mat, Ri)) return 0;
+#pragma omp parallel for schedule(static)
+    for (i = 0; i < H; i++) {
+        int j;
+        for (j = 0; j < W; j++) {
+            int32_t o[2];
+            erpo_rotate_pixel(i, j, Ri, W, H, o);
+            if (o[0] >= 0 && o[1] >= 0 && o[0] < H && o[1] < W)
+                copy_px(im + ((size_t)o[0] * W + o[1]) * 3, out + ((size_t)i * W + j) * 3);
+        }
+    }
+    return 1;
+}
+
+/* rectify, src/automatic.cpp:66-79 */
+int32_t erpo_rectify(const uint8_t* left, const uint8_t* right, int32_t W, int32_t H,
+                     const double rot_vec[3], const double t_vec[3], uint8_t* left_out,
+                     uint8_t* right_out) {
+    const double down[3] = {0, -1, 0};
+    double Rl[9], Rl_inv[9], E[9], E_inv[9], Rr[9], Rr_inv[9];
+    erpo_rot_from_vec(down, t_vec, Rl);
+    if (!erpo_inv3(Rl, Rl_inv)) return 0;
+    erpo_eular2rot(rot_vec, E);
+    if (!erpo_inv3(E, E_inv)) return 0;
+    gemm33(Rl, E_inv, Rr);
+    if (!erpo_inv3(Rr, Rr_inv)) return 0;
+    return erpo_rotate_image(left, W, H, Rl_inv, left_out) &&
+           erpo_rotate_image(right, W, H, Rr_inv, right_out);
+}
+
+/* src/automatic.cpp:148-151: rotate_image by eular2rot(RAD(89.999),0,0).inv(), then
+ * cv::rotate(ROTATE_90_CLOCKWISE): out (W rows x H cols), out[r][c] = tmp[H-1-c][r].  The
+ * intermediate starts as a copy of `out`'s prior content transposed back, so unwritten pixels
+ * keep it (the kernel writes only mapped pixels). */
+int32_t erpo_vertical_rotate(const uint8_t* im, int32_t W, int32_t H, uint8_t* out) {
+    const double e[3] = {M_PI * (89.999) / 180.0, 0, 0};
+    double R[9], Ri[9];
+    uint8_t* tmp = (uint8_t*)malloc((size_t)W * H * 3);
+    int i;
+    if (!tmp) return 0;
+    erpo_eular2rot(e, R);
+    if (!erpo_inv3(R, Ri)) { free(tmp); return 0; }
+    for (i = 0; i < H; i++) {
+        int j;
+        for (j = 0; j < W; j++)  /* tmp[i][j] <- out[j][H-1-i] (prior content) */
+            copy_px(out + ((size_t)j * H + (H - 1 - i)) * 3, tmp + ((size_t)i * W + j) * 3);
+    }
+    if (!erpo_rotate_image(im, W, H, Ri, tmp)) { free(tmp); return 0; }
+    for (i = 0; i < W; i++) {
+        int c;
+        for (c = 0; c < H; c++)
+            copy_px(tmp + ((size_t)(H - 1 - c) * W + i) * 3, out + ((size_t)i * H + c) * 3);
+    }
+    free(tmp);
+    return 1;
+}

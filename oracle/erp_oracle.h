@@ -16,11 +16,16 @@
  *   - eight_point::eight_point_estimation   /root/reference/src/eight_point.cpp:16-85
  *   - random_array (iota + random_shuffle)  /root/reference/src/eight_point.hpp:30-59
  *   - erp_rotation::eular2rot / rot2eular   /root/reference/src/erp_rotation.cpp:14-63
+ *   - erp_rotation::rotate_pixel / rotate_image  /root/reference/src/erp_rotation.cpp:66-122
+ *   - spherical_surf::crop_rotated_image / rotate_keypoint + do_all's band steps
+ *                                           /root/reference/src/spherical_surf.cpp:16-63,77-133
+ *   - rot_from_vec / rectify / vertical view /root/reference/src/automatic.cpp:50-79,148-152
  * plus the third-party arithmetic those call, restated from the published algorithms:
  *   - glibc rand() (TYPE_3 additive feedback generator, srand never called => seed 1)
  *   - libstdc++ (GCC 11) std::random_shuffle
  *   - OpenCV 3.4 cv::SVDecomp (JacobiSVDImpl_, flags=0, thin/full selection of _SVDcompute)
- *   - OpenCV 3.4 cv::decomposeEssentialMat, cv::determinant (3x3), small-matrix gemm
+ *   - OpenCV 3.4 cv::decomposeEssentialMat, cv::determinant (3x3), small-matrix gemm,
+ *     Mat::inv() on 3x3 doubles (adjugate / determinant), cv::rotate(ROTATE_90_CLOCKWISE)
  *
  * Pinning status (see DESIGN.md "Oracle"):
  *   - glibc rand() and std::random_shuffle: PINNED against the real libc / libstdc++ of this
@@ -78,6 +83,25 @@ void erpo_eular2rot(const double e[3], double R[9]);
 void erpo_rot2eular(const double R[9], double e[3]);
 /* eight_point::find pixel -> bearing (src/eight_point.cpp:163-186) */
 void erpo_pixel_to_bearing(int32_t W, int32_t H, float px, float py, double b[3]);
+
+/* ---- ERP remaps.  Images: H x W x 3 bytes.  Unwritten pixels (source
+   outside the image) keep the output's prior content, as in the reference. ---- */
+void erpo_rotate_pixel(int32_t row, int32_t col, const double m[9], int32_t W, int32_t H,
+                       int32_t out[2]);
+int32_t erpo_inv3(const double m[9], double out[9]);
+void erpo_rotate_pixel_prefix(const int32_t* rows, const int32_t* cols, int32_t n, const double m[9],
+                              int32_t W, int32_t H, double* out);
+void erpo_rot_from_vec(const double v1[3], const double v2[3], double R[9]);
+void erpo_crop_rotated_image(const uint8_t* im, int32_t W, int32_t H, float pitch_deg,
+                             uint8_t* out);
+void erpo_rotate_keypoint(float* kp_xy, int32_t n, float pitch_deg, int32_t W, int32_t H);
+void erpo_unrotate_band_keypoints(float* kp_xy, const int32_t counts[4], int32_t W, int32_t H);
+int32_t erpo_rotate_image(const uint8_t* im, int32_t W, int32_t H, const double rot_mat[9],
+                          uint8_t* out);
+int32_t erpo_rectify(const uint8_t* left, const uint8_t* right, int32_t W, int32_t H,
+                     const double rot_vec[3], const double t_vec[3], uint8_t* left_out,
+                     uint8_t* right_out);
+int32_t erpo_vertical_rotate(const uint8_t* im, int32_t W, int32_t H, uint8_t* out);
 
 /* OpenCV 3.4 SVDecomp(src m x n, flags=0) restated.  w: min(m,n); u: m x min(m,n) row-major;
  * vt: min(m,n) x n row-major.  Returns 0 on success. */

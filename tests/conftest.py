@@ -41,6 +41,7 @@ def harness():
     L.erph_gram36.argtypes = [P, P, C.c_int32, P]
     L.erph_svd3.argtypes = [P, P, P, P]
     L.erph_pixel_to_bearing.argtypes = [C.c_int32, C.c_int32, C.c_float, C.c_float, P]
+    L.erph_rotate_pixel.argtypes = [C.c_int32, C.c_int32, P, C.c_int32, C.c_int32, P]
     return L
 
 

@@ -42,5 +42,10 @@ void erph_pixel_to_bearing(int32_t W, int32_t H, float px, float py, double* b) 
     erp::pixel_to_bearing(W, H, px, py, b);
 }
 
+void erph_rotate_pixel(int32_t row, int32_t col, const double* m, int32_t W, int32_t H,
+                       int32_t* out) {
+    erp::rotate_pixel(row, col, m, W, H, &out[0], &out[1]);
+}
+
 int32_t erph_sizeof_hyp() { return (int32_t)sizeof(erp::Hyp); }
 }

@@ -124,3 +124,23 @@ def test_min_eigvec_unstructured_grams(harness, s):
         err = min(np.abs(e - ref).max(), np.abs(e + ref).max())
         worst = max(worst, err * (w[1] - w[0]) / w[-1])  # scale by the conditioning
     assert worst < 1e-12, worst
+
+
+def test_rotate_pixel_bit_exact(oracle, harness):
+    """erp_device.hpp rotate_pixel (the remap kernels' formula, host build) against the oracle's
+    restatement of src/erp_rotation.cpp:66-92 on the band-remap and rectification matrices,
+    including the poles, the seams and non-finite matrices (x86 INT32_MIN conversion)."""
+    rng = np.random.default_rng(3)
+    W, H = 5376, 2688
+    mats = [oracle.eular2rot([0.0, float(np.float32(np.pi * d / 180.0)), 0.0])
+            for d in (45.0, -45.0, -90.0)]
+    mats += [oracle.eular2rot(rng.uniform(-0.3, 0.3, 3)) for _ in range(3)]
+    mats.append(np.full((3, 3), np.nan))
+    rows = np.concatenate([[0, 1, H // 2, H - 1, H], rng.integers(0, H, 300)])
+    cols = np.concatenate([[0, 1, W // 4, W // 2, 3 * W // 4, W - 1], rng.integers(0, W, 300)])
+    o = np.zeros(2, np.int32)
+    for m in mats:
+        m = np.ascontiguousarray(m, np.float64).reshape(9)
+        for r, c in zip(rows, cols[: len(rows)]):
+            harness.erph_rotate_pixel(int(r), int(c), _p(m), W, H, _p(o))
+            assert (int(o[0]), int(o[1])) == oracle.rotate_pixel(r, c, m, W, H), (r, c)
