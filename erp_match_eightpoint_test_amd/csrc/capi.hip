@@ -71,7 +71,7 @@ struct erp_ctx {
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
     DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
-        rtab, limbs, tsplit, ovf;
+        rtab, limbs, tsplit, ovf, remap_scr;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -118,6 +118,11 @@ int32_t erp_abi_version(void) { return ERP_MATCH_ABI_VERSION; }
 }  // extern "C"
 
 int32_t erp_ctx_device_internal(erp_ctx* ctx) { return ctx->device; }  // remap_api.hip
+void* erp_ctx_scratch_internal(erp_ctx* ctx, int which, size_t bytes) {  // remap_api.hip
+    (void)which;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    return ensure(ctx->remap_scr, bytes) ? ctx->remap_scr.p : nullptr;
+}
 
 extern "C" {
 
@@ -173,7 +178,7 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
                      &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
                      &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins,
-                     &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf};
+                     &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf, &ctx->remap_scr};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);

@@ -286,24 +286,156 @@ ERP_HD ERP_INLINE double acos_ref(double r) {
     return acos(r);
 }
 
+// ---- correctly rounded sin / cos / acos / atan2 (double-double), the boundary slow path ----
+// rotate_pixel truncates H*acos(.)/M_PI and W*atan2(.)/(2*M_PI); when such a value lies within
+// ~1e-8 of an integer the index depends on the LAST ulp of the four transcendentals.  glibc
+// (the reference's libm) rounds them correctly but for rare hard cases (<= ~0.52 ulp), the
+// device library does not (1-2 ulp), so near a boundary the pixel is recomputed with these
+// correctly rounded versions: reduction by pi/2 in three parts, Taylor series in double-double
+// (|r| <= pi/4: 14 terms, truncation < 1e-30), and one Newton step in double-double for
+// acos / atan2 from the fast value.
+struct DD {
+    double h, l;
+};
+ERP_HD ERP_INLINE DD dd_two_sum(double a, double b) {
+    const double s = a + b, t = s - a;
+    return DD{s, (a - (s - t)) + (b - t)};
+}
+ERP_HD ERP_INLINE DD dd_quick(double a, double b) {
+    const double s = a + b;
+    return DD{s, b - (s - a)};
+}
+ERP_HD ERP_INLINE DD dd_add(DD x, DD y) {
+    DD s = dd_two_sum(x.h, y.h);
+    const DD t = dd_two_sum(x.l, y.l);
+    s.l += t.h;
+    s = dd_quick(s.h, s.l);
+    s.l += t.l;
+    return dd_quick(s.h, s.l);
+}
+ERP_HD ERP_INLINE DD dd_mul(DD x, DD y) {
+    const double p = x.h * y.h;
+    double e = fma(x.h, y.h, -p);
+    e += x.h * y.l + x.l * y.h;
+    return dd_quick(p, e);
+}
+ERP_HD ERP_INLINE DD dd_mul_d(DD x, double d) {
+    const double p = x.h * d;
+    double e = fma(x.h, d, -p);
+    e += x.l * d;
+    return dd_quick(p, e);
+}
+// 1/n!, n = 2..27, as double-double
+ERP_HD ERP_INLINE DD dd_inv_fact(int n) {
+    const double t[26][2] = {
+        {0.5, 0.0}, {0.16666666666666666, 9.25185853854297e-18},
+        {0.041666666666666664, 2.3129646346357427e-18}, {0.008333333333333333, 1.1564823173178714e-19},
+        {0.001388888888888889, -5.300543954373577e-20}, {0.0001984126984126984, 1.7209558293420705e-22},
+        {2.48015873015873e-05, 2.1511947866775882e-23}, {2.7557319223985893e-06, -1.858393274046472e-22},
+        {2.755731922398589e-07, 2.3767714622250297e-23}, {2.505210838544172e-08, -1.448814070935912e-24},
+        {2.08767569878681e-09, -1.20734505911326e-25}, {1.6059043836821613e-10, 1.2585294588752098e-26},
+        {1.1470745597729725e-11, 2.0655512752830745e-28}, {7.647163731819816e-13, 7.03872877733453e-30},
+        {4.779477332387385e-14, 4.399205485834081e-31}, {2.8114572543455206e-15, 1.6508842730861433e-31},
+        {1.5619206968586225e-16, 1.1910679660273754e-32}, {8.22063524662433e-18, 2.2141894119604265e-34},
+        {4.110317623312165e-19, 1.4412973378659527e-36}, {1.9572941063391263e-20, -1.3643503830087908e-36},
+        {8.896791392450574e-22, -7.911402614872376e-38}, {3.868170170630684e-23, -8.843177655482344e-40},
+        {1.6117375710961184e-24, -3.6846573564509766e-41}, {6.446950284384474e-26, -1.9330404233703465e-42},
+        {2.4795962632247976e-27, -1.2953730964765229e-43}, {9.183689863795546e-29, 1.4303150396787322e-45}};
+    return DD{t[n - 2][0], t[n - 2][1]};
+}
+// sin and cos of a double x (|x| < 16) in double-double
+ERP_HD ERP_INLINE void dd_sincos(double x, DD* sn, DD* cs) {
+    constexpr double P1 = 1.5707963267948966, P2 = 6.123233995736766e-17,
+                     P3 = -1.4973849048591698e-33;
+    const double k = rint(x * 0.63661977236758138);
+    const double p = k * P1, pe = fma(k, P1, -p);  // k * P1 = p + pe exactly
+    DD r = dd_two_sum(x - p, -pe);                  // x - p exact (Sterbenz, or k = 0)
+    const double q2 = k * P2;
+    r = dd_add(r, DD{-q2, -fma(k, P2, -q2)});
+    r = dd_add(r, DD{-k * P3, 0.0});
+    const DD z = dd_mul(r, r);
+    DD s = dd_inv_fact(27), c = dd_inv_fact(26);
+#pragma unroll
+    for (int n = 25; n >= 3; n -= 2) {  // (unrolled: the table folds into constants)  // S(z) = 1/1! - z/3! + ..., C(z) = 1 - z/2! + ...
+        s = dd_add(dd_inv_fact(n), dd_mul_d(dd_mul(s, z), -1.0));
+        c = dd_add(dd_inv_fact(n - 1), dd_mul_d(dd_mul(c, z), -1.0));
+    }
+    s = dd_add(DD{1.0, 0.0}, dd_mul_d(dd_mul(s, z), -1.0));
+    c = dd_add(DD{1.0, 0.0}, dd_mul_d(dd_mul(c, z), -1.0));
+    s = dd_mul(s, r);
+    const int q = ((int)fmod(k, 4.0) + 4) & 3;
+    const DD ns{-s.h, -s.l}, nc{-c.h, -c.l};
+    *sn = q == 0 ? s : q == 1 ? c : q == 2 ? ns : nc;
+    *cs = q == 0 ? c : q == 1 ? ns : q == 2 ? nc : s;
+}
+ERP_HD ERP_INLINE void sincos_cr(double x, double* sn, double* cs) {
+    if (!(fabs(x) < 16.0)) {
+        *sn = sin(x);
+        *cs = cos(x);
+        return;
+    }
+    DD s, c;
+    dd_sincos(x, &s, &c);
+    *sn = s.h;
+    *cs = c.h;
+}
+ERP_HD ERP_INLINE double acos_cr(double x) {
+    const double y0 = acos_ref(x);
+    if (!(fabs(x) < 1.0) || y0 == 0.0) return y0;
+    DD s, c;
+    dd_sincos(y0, &s, &c);
+    const DD num = dd_add(c, DD{-x, 0.0});  // cos(y0) - x;  acos' = -1/sin
+    return y0 + num.h / s.h;
+}
+ERP_HD ERP_INLINE double atan2_cr(double y, double x) {
+    const double t0 = atan2_ref(y, x);
+    if (!(fabs(t0) < 4.0) || (x == 0.0 && y == 0.0) || !(fabs(x) < 1e300 && fabs(y) < 1e300))
+        return t0;
+    DD s, c;
+    dd_sincos(t0, &s, &c);
+    const DD num = dd_add(dd_mul_d(c, y), dd_mul_d(s, -x));  // y cos t - x sin t
+    const double den = x * c.h + y * s.h;                     // x cos t + y sin t (= rho)
+    if (!(den > 0.0)) return t0;
+    return t0 + num.h / den;
+}
+
 // erp_rotation::rotate_pixel (src/erp_rotation.cpp:66-92): pixel (row, col) -> sphere (OMAF
 // axes) -> m * v -> pixel, each conversion truncating.  The polar / azimuth angles of the input
 // come from their sines and cosines (sa = sin(M_PI*row/height), ca = cos(...), sb, cb of
-// 2*M_PI*col/width), so callers can tabulate them per row / per column.
-ERP_HD ERP_INLINE void rotate_pixel_sc(double sa, double ca, double sb, double cb,
-                                       const double* m, int32_t W, int32_t H, int32_t* out_row,
-                                       int32_t* out_col) {
+// 2*M_PI*col/width), so callers can tabulate them per row / per column.  Returns true when a
+// truncated value lies within 1e-8 of an integer: the caller then redoes the pixel with
+// rotate_pixel_cr (correctly rounded transcendentals, see above).
+ERP_HD ERP_INLINE bool near_boundary(double X) { return fabs(X - rint(X)) < 1e-8; }
+template <bool CR>
+ERP_HD ERP_INLINE bool rotate_pixel_core(double sa, double ca, double sb, double cb,
+                                         const double* m, int32_t W, int32_t H, int32_t* out_row,
+                                         int32_t* out_col) {
     const double c0 = -sa * cb;
     const double c1 = sa * sb;
     const double c2 = ca;
     const double r0 = m[0] * c0 + m[1] * c1 + m[2] * c2;
     const double r1 = m[3] * c0 + m[4] * c1 + m[5] * c2;
     const double r2 = m[6] * c0 + m[7] * c1 + m[8] * c2;
-    const double v0 = acos_ref(r2);
-    double v1 = atan2_ref(r1, -r0);
+    const double v0 = CR ? acos_cr(r2) : acos_ref(r2);
+    double v1 = CR ? atan2_cr(r1, -r0) : atan2_ref(r1, -r0);
     if (v1 < 0) v1 += kPi * 2;
-    *out_row = trunc_i32_x86((double)H * v0 / kPi);
-    *out_col = trunc_i32_x86((double)W * v1 / (2 * kPi));
+    const double X0 = (double)H * v0 / kPi, X1 = (double)W * v1 / (2 * kPi);
+    *out_row = trunc_i32_x86(X0);
+    *out_col = trunc_i32_x86(X1);
+    return near_boundary(X0) || near_boundary(X1);
+}
+ERP_HD ERP_INLINE bool rotate_pixel_sc(double sa, double ca, double sb, double cb,
+                                       const double* m, int32_t W, int32_t H, int32_t* out_row,
+                                       int32_t* out_col) {
+    return rotate_pixel_core<false>(sa, ca, sb, cb, m, W, H, out_row, out_col);
+}
+// the boundary slow path: every transcendental correctly rounded (a = polar, b = azimuth)
+ERP_HD ERP_INLINE void rotate_pixel_cr(double a, double b, const double* m, int32_t W, int32_t H,
+                                       int32_t* out_row, int32_t* out_col) {
+    double sa, ca, sb, cb;
+    sincos_cr(a, &sa, &ca);
+    sincos_cr(b, &sb, &cb);
+    (void)rotate_pixel_core<true>(sa, ca, sb, cb, m, W, H, out_row, out_col);
 }
 ERP_HD ERP_INLINE double erp_polar(int32_t row, int32_t H) { return kPi * (double)row / (double)H; }
 ERP_HD ERP_INLINE double erp_azimuth(int32_t col, int32_t W) {
@@ -312,7 +444,8 @@ ERP_HD ERP_INLINE double erp_azimuth(int32_t col, int32_t W) {
 ERP_HD ERP_INLINE void rotate_pixel(int32_t row, int32_t col, const double* m, int32_t W,
                                     int32_t H, int32_t* out_row, int32_t* out_col) {
     const double a = erp_polar(row, H), b = erp_azimuth(col, W);
-    rotate_pixel_sc(sin(a), cos(a), sin(b), cos(b), m, W, H, out_row, out_col);
+    if (rotate_pixel_sc(sin(a), cos(a), sin(b), cos(b), m, W, H, out_row, out_col))
+        rotate_pixel_cr(a, b, m, W, H, out_row, out_col);
 }
 
 ERP_HD ERP_INLINE double max_vec(const float* v) {

@@ -31,9 +31,18 @@ struct RemapJobs {
     RemapJob j[kMaxRemapJobs];
 };
 
-// up to kMaxRemapJobs independent remaps of images sharing W x H, one launch
+// pixels whose truncated values fall within 1e-8 of an integer are deferred to a fix-up kernel
+// (correctly rounded transcendentals, erp_device.hpp rotate_pixel_cr): list of
+// (job << 32 | output pixel index), sized for every output pixel of the launch
+struct RemapScratch {
+    uint32_t* count;        // device counter (zeroed by launch_remap)
+    uint64_t* list;         // [n_jobs * out_rows * out_cols]
+};
+
+// up to kMaxRemapJobs independent remaps of images sharing W x H: the remap launch + the
+// boundary fix-up launch
 hipError_t launch_remap(const RemapJobs& jobs, int n_jobs, int max_out_rows, int max_out_cols,
-                        int W, int H, hipStream_t st);
+                        int W, int H, const RemapScratch& scr, hipStream_t st);
 
 struct BandKeypointArgs {
     double m[4][9];     // per band: rotate_keypoint's matrix (unused for shift_band)

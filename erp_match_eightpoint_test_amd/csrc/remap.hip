@@ -36,7 +36,20 @@ __device__ __forceinline__ void copy_px(const uint8_t* __restrict__ s, uint8_t* 
     d[2] = s[2];
 }
 
-__global__ __launch_bounds__(256) void remap_kernel(const RemapJobs jobs, int W, int H) {
+// the boundary slow path of one output pixel
+__device__ __forceinline__ void remap_pixel_cr(const RemapJob& jb, int r, int c, int W, int H,
+                                            int out_cols, const double* m) {
+    int32_t oi, oj;
+    if (jb.mode == kRemapRot90)
+        rotate_pixel_cr(erp_polar(H - 1 - c, H), erp_azimuth(r, W), m, W, H, &oi, &oj);
+    else
+        rotate_pixel_cr(erp_polar(jb.row0 + r, H), erp_azimuth(c, W), m, W, H, &oi, &oj);
+    if (oi >= 0 && oj >= 0 && oi < H && oj < W)
+        copy_px(jb.src + ((size_t)oi * W + oj) * 3, jb.dst + ((size_t)r * out_cols + c) * 3);
+}
+
+__global__ __launch_bounds__(256) void remap_kernel(const RemapJobs jobs, int W, int H,
+                                                    RemapScratch scr) {
     __shared__ double rs[kRmRows], rc[kRmRows];
     const RemapJob& jb = jobs.j[blockIdx.z];
     const int mode = jb.mode;
@@ -89,12 +102,34 @@ __global__ __launch_bounds__(256) void remap_kernel(const RemapJobs jobs, int W,
     const int r1 = min(r0 + kRmRows, out_rows);
     for (int r = r0; r < r1; r++) {
         int32_t oi, oj;
+        bool slow;
         if (mode == kRemapRot90)
-            rotate_pixel_sc(sa_t, ca_t, rs[r - r0], rc[r - r0], m, W, H, &oi, &oj);
+            slow = rotate_pixel_sc(sa_t, ca_t, rs[r - r0], rc[r - r0], m, W, H, &oi, &oj);
         else
-            rotate_pixel_sc(rs[r - r0], rc[r - r0], sb_t, cb_t, m, W, H, &oi, &oj);
+            slow = rotate_pixel_sc(rs[r - r0], rc[r - r0], sb_t, cb_t, m, W, H, &oi, &oj);
+        if (slow) {  // near a truncation boundary: deferred to the fix-up kernel
+            const uint32_t k = atomicAdd(scr.count, 1u);  // (cap = every pixel of the launch)
+            scr.list[k] = ((uint64_t)blockIdx.z << 32) | ((uint64_t)r * out_cols + c);
+            continue;
+        }
         if (oi >= 0 && oj >= 0 && oi < H && oj < W)
             copy_px(src + ((size_t)oi * W + oj) * 3, dst + ((size_t)r * out_cols + c) * 3);
+    }
+}
+
+// the deferred boundary pixels: correctly rounded transcendentals (grid-stride over the list)
+__global__ __launch_bounds__(256) void remap_fixup_kernel(const RemapJobs jobs, int W, int H,
+                                                          RemapScratch scr) {
+    const uint32_t n = *scr.count;
+    for (uint32_t k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+        const uint64_t e = scr.list[k];
+        const RemapJob& jb = jobs.j[e >> 32];
+        const int out_cols = jb.mode == kRemapRot90 ? H : W;
+        const uint32_t pix = (uint32_t)e;
+        double m[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) m[q] = jb.m[q];
+        remap_pixel_cr(jb, (int)(pix / out_cols), (int)(pix % out_cols), W, H, out_cols, m);
     }
 }
 
@@ -124,10 +159,13 @@ __global__ __launch_bounds__(256) void band_keypoints_kernel(erp_point2f* __rest
 }  // namespace
 
 hipError_t launch_remap(const RemapJobs& jobs, int n_jobs, int max_out_rows, int max_out_cols,
-                        int W, int H, hipStream_t st) {
+                        int W, int H, const RemapScratch& scr, hipStream_t st) {
+    hipError_t e = hipMemsetAsync(scr.count, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
     dim3 grid((max_out_cols + kRmCols - 1) / kRmCols, (max_out_rows + kRmRows - 1) / kRmRows,
               n_jobs);
-    hipLaunchKernelGGL(remap_kernel, grid, dim3(256), 0, st, jobs, W, H);
+    hipLaunchKernelGGL(remap_kernel, grid, dim3(256), 0, st, jobs, W, H, scr);
+    hipLaunchKernelGGL(remap_fixup_kernel, dim3(256), dim3(256), 0, st, jobs, W, H, scr);
     return hipGetLastError();
 }
 

@@ -14,6 +14,7 @@
 #include "erp_remap.hpp"
 
 int32_t erp_ctx_device_internal(erp_ctx* ctx);  // capi.hip
+void* erp_ctx_scratch_internal(erp_ctx* ctx, int which, size_t bytes);  // capi.hip (grow-only)
 
 namespace {
 
@@ -39,6 +40,15 @@ void pitch_matrix(float deg, double m[9]) {
 erp_status set_dev(erp_ctx* ctx) {
     if (!ctx) return ERP_INVALID_ARG;
     return hipSetDevice(erp_ctx_device_internal(ctx)) == hipSuccess ? ERP_OK : ERP_HIP_ERROR;
+}
+
+// the boundary list of a launch of up to kMaxRemapJobs jobs of `pixels` output pixels each
+bool scratch(erp_ctx* ctx, size_t pixels, erp::RemapScratch* scr) {
+    void* p = erp_ctx_scratch_internal(ctx, 0, 16 + pixels * erp::kMaxRemapJobs * 8);
+    if (!p) return false;
+    scr->count = (uint32_t*)p;
+    scr->list = (uint64_t*)((char*)p + 16);
+    return true;
 }
 
 bool dims_ok(int32_t W, int32_t H) {
@@ -128,6 +138,8 @@ erp_status erp_crop_rotated_image_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t
     if (!d_im || !d_out || !dims_ok(W, H) || H < 4) return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    erp::RemapScratch scr;
+    if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     erp::RemapJobs jobs{};
     erp::RemapJob& j = jobs.j[0];
     j.src = d_im;
@@ -136,7 +148,7 @@ erp_status erp_crop_rotated_image_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t
     j.row0 = H * 3 / 8;
     j.rows = H / 4;
     j.mode = erp::kRemapCrop;
-    return erp::launch_remap(jobs, 1, H / 4, W, W, H, (hipStream_t)stream) == hipSuccess
+    return erp::launch_remap(jobs, 1, H / 4, W, W, H, scr, (hipStream_t)stream) == hipSuccess
                ? ERP_OK : ERP_HIP_ERROR;
 }
 
@@ -146,6 +158,8 @@ erp_status erp_spherical_bands_dev(erp_ctx* ctx, const uint8_t* d_ims, int32_t n
         return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    erp::RemapScratch scr;
+    if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     static const float pitch[4] = {45.f, 0.f, -45.f, -90.f};  // do_all :77-83 (n1 unrotated)
     double pm[4][9];
     for (int b = 0; b < 4; b++)
@@ -165,7 +179,7 @@ erp_status erp_spherical_bands_dev(erp_ctx* ctx, const uint8_t* d_ims, int32_t n
                 j.rows = H / 4;
                 j.mode = b == 1 ? erp::kRemapCopy : erp::kRemapCrop;
             }
-        if (erp::launch_remap(jobs, n, H / 4, W, W, H, (hipStream_t)stream) != hipSuccess)
+        if (erp::launch_remap(jobs, n, H / 4, W, W, H, scr, (hipStream_t)stream) != hipSuccess)
             return ERP_HIP_ERROR;
     }
     return ERP_OK;
@@ -220,6 +234,8 @@ erp_status erp_rotate_image_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W, in
     if (!d_im || !d_out || !rot_mat || !dims_ok(W, H)) return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    erp::RemapScratch scr;
+    if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     erp::RemapJobs jobs{};
     erp::RemapJob& j = jobs.j[0];
     if (!erp_inv3(rot_mat, j.m)) return ERP_INVALID_ARG;  // rot_mat.inv(), erp_rotation.cpp:103
@@ -228,7 +244,7 @@ erp_status erp_rotate_image_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W, in
     j.row0 = 0;
     j.rows = H;
     j.mode = erp::kRemapFull;
-    return erp::launch_remap(jobs, 1, H, W, W, H, (hipStream_t)stream) == hipSuccess
+    return erp::launch_remap(jobs, 1, H, W, W, H, scr, (hipStream_t)stream) == hipSuccess
                ? ERP_OK : ERP_HIP_ERROR;
 }
 
@@ -239,6 +255,8 @@ erp_status erp_rectify_dev(erp_ctx* ctx, const uint8_t* d_left, const uint8_t* d
         return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    erp::RemapScratch scr;
+    if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     erp::RemapJobs jobs{};
     s = erp_rectify_matrices(rot_vec, t_vec, jobs.j[0].m, jobs.j[1].m);
     if (s != ERP_OK) return s;
@@ -250,7 +268,7 @@ erp_status erp_rectify_dev(erp_ctx* ctx, const uint8_t* d_left, const uint8_t* d
         j.rows = H;
         j.mode = erp::kRemapFull;
     }
-    return erp::launch_remap(jobs, 2, H, W, W, H, (hipStream_t)stream) == hipSuccess
+    return erp::launch_remap(jobs, 2, H, W, W, H, scr, (hipStream_t)stream) == hipSuccess
                ? ERP_OK : ERP_HIP_ERROR;
 }
 
@@ -259,6 +277,8 @@ erp_status erp_vertical_rotate_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W,
     if (!d_im || !d_out || !dims_ok(W, H)) return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    erp::RemapScratch scr;
+    if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     // rot_mat_90deg = eular2rot(Vec3d(RAD(89.999), 0, 0)).inv(); rotate_image inverts it again
     const double th[3] = {erp::kPi * (89.999) / 180.0, 0, 0};
     double R[9], Ri[9];
@@ -271,7 +291,7 @@ erp_status erp_vertical_rotate_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W,
     j.row0 = 0;
     j.rows = H;
     j.mode = erp::kRemapRot90;
-    return erp::launch_remap(jobs, 1, W, H, W, H, (hipStream_t)stream) == hipSuccess
+    return erp::launch_remap(jobs, 1, W, H, W, H, scr, (hipStream_t)stream) == hipSuccess
                ? ERP_OK : ERP_HIP_ERROR;
 }
 

