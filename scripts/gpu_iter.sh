@@ -12,6 +12,6 @@ python - <<'PY'
 import json
 d = json.loads(open("gpurun_out/bench_iter.log").read().strip().splitlines()[-1])
 print("value", round(d["value"], 1), "ms/step", round(d["ms_per_step"], 3), "roof", d["roofline"] and {k: d["roofline"][k] for k in ("kernel", "frac")})
-print({k: round(v, 3) for k, v in sorted(d["stages_ms_per_step"].items(), key=lambda kv: -kv[1])})
+print({k: round(v, 3) for k, v in sorted(d["stages_ms_serial_step"].items(), key=lambda kv: -kv[1])})
 c = d["check"]; print("ok", c["all_status_ok"], "err", c["mean_abs_euler_err_deg_max"], "surv max", max(c["consensus_survivors"]))
 PY
