@@ -460,6 +460,26 @@ def main():
         stage_roofs[k] = {"bound": bound, "achieved": amount / avg_s / 1e12, "peak": peak,
                           "unit": unit, "frac": amount / avg_s / 1e12 / peak,
                           "avg_launch_ms": avg_s * 1e3}
+    # latency of ONE pair alone through the same pipeline (the reference's per-pair use,
+    # src/automatic.cpp:117-126): a batch of 1, median of 20 synchronous runs (not `value`)
+    lat = None
+    if args.steps > 0:
+        b1 = to_device(pairs[:1], dev)
+        ctx1 = Context(local)
+        ctx1.set_matcher(0 if args.matcher == "mfma" else 1)
+        run1 = PairBatchRunner(ctx=ctx1, iters=args.iters)
+        run1.reserve(1, b1["max_nq"], b1["max_nt"])
+        ts = []
+        for k in range(23):
+            torch.cuda.synchronize()
+            ta = time.perf_counter()
+            run1.run(b1["desc_l"], b1["desc_r"], b1["kp_l"], b1["kp_r"], b1["off_l"], b1["off_r"],
+                     b1["width"], b1["height"], b1["max_nq"], b1["max_nt"])
+            torch.cuda.synchronize()
+            if k >= 3:
+                ts.append(time.perf_counter() - ta)
+        lat = {"single_pair_ms": float(np.median(ts)) * 1e3,
+               "note": "one 4096x4096 pair, 10k iterations, batch of 1, host-timed, median of 20"}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(pairs, args.iters, args.cpu_seconds)
@@ -477,6 +497,7 @@ def main():
         "roofline": roof,
         "roofline_stages": stage_roofs,
         "cpu_baseline": cpu,
+        "latency": lat,
         "stages_ms_serial_step": {k: v[0] for k, v in stages.items()},
         "check": {"all_status_ok": ok, "mean_abs_euler_err_deg_max": max(err_deg),
                   "M_mean": float(res["M"].mean()), "K_mean": float(res["K"].mean()),

@@ -71,7 +71,7 @@ struct erp_ctx {
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
     DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
-        rtab, limbs, tsplit, ovf, remap_scr;
+        rtab, limbs, tsplit, ovf, remap_scr, vchunk;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -178,7 +178,7 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
                      &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
                      &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins,
-                     &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf, &ctx->remap_scr};
+                     &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf, &ctx->remap_scr, &ctx->vchunk};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
@@ -294,7 +294,7 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->dscale, P * 4) && ensure(c->lb, P * 2 * sh.iters * 8) &&
               ensure(c->ub, P * 2 * sh.iters * 8) && ensure(c->surv, P * 2 * sh.iters * 4) &&
               ensure(c->bsel, P * 2 * sh.iters * 8) && ensure(c->edges, erp::consensus_edges_bytes((int)P)) &&
-              ensure(c->nsurv, P * 4);
+              ensure(c->nsurv, P * 4) && ensure(c->vchunk, erp::valid_chunk_bytes(sh));
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
     if (ok && !(out && out->dist)) ok = ensure(c->tmean, P * 2 * sh.iters * 8);
@@ -382,7 +382,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     auto* tmean = (out && out->dist) ? out->dist : (double*)c->tmean.p;
     if (from_hyps) {
         StageTimer _t(ctx, ERP_STAGE_VALID_COMPACT, st);
-        ERP_CK(erp::launch_valid_compact(counts, hyps, sh, cfg->sample_frac, (float*)c->rv.p, tv,
+        ERP_CK(erp::launch_valid_compact(counts, hyps, sh, cfg->sample_frac,
+                                         (int32_t*)c->vchunk.p, (float*)c->rv.p, tv,
                                          (int32_t*)c->kcount.p, out ? out->rvec : nullptr,
                                          (float*)c->dscale.p, st));
     }

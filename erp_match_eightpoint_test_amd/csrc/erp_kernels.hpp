@@ -115,9 +115,13 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
 hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
                         double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
                         hipStream_t st);
+// R_vec_arr / T_vec_arr in push order + K + bounding-box scale; vchunk = scratch of
+// valid_chunk_bytes(sh) (per 1024-iteration chunk: count and bounding box)
+size_t valid_chunk_bytes(const BatchShape& sh);
 hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyps,
-                                const BatchShape& sh, double sample_frac, float* rv, float* tv,
-                                int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st);
+                                const BatchShape& sh, double sample_frac, int32_t* vchunk,
+                                float* rv, float* tv, int32_t* kcount, float* rv_aos,
+                                float* dscale, hipStream_t st);
 hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream_t st);
 hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, int stride, float* rv,
                                   float* tv, int32_t* kcount, float* dscale, int32_t* flags,

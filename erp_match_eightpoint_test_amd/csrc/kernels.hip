@@ -1362,85 +1362,134 @@ __global__ __launch_bounds__(64) void estimate_kernel(const int32_t* __restrict_
 }
 
 // push R1 (if valid) then R2 (if valid) per iteration, in iteration order
-__global__ __launch_bounds__(1024) void valid_compact_kernel(const int32_t* __restrict__ counts,
-                                                             const erp_hypothesis* __restrict__ hyps,
-                                                             int iters, double sample_frac,
-                                                             float* __restrict__ rv,
-                                                             float* __restrict__ tv,
-                                                             int32_t* __restrict__ kcount,
-                                                             float* __restrict__ rv_aos,
-                                                             float* __restrict__ dscale) {
+// Two launches over (chunk of 1024 iterations, pair): valid_count_kernel writes each chunk's
+// number of valid rotations and its bounding box; valid_scatter_kernel adds the totals of the
+// chunks before it (at most ~200 values) and block-scans its chunk, keeping the reference's
+// push order (iteration, then R1, R2).  Chunk 0 also writes K and the bounding-box diagonal
+// of the valid R set (>= every pairwise distance: the scale of the consensus histograms).
+// vchunk[p][c] = {count, min x, min y, min z, max x, max y, max z, pad}
+__device__ __forceinline__ int hyp_valid_count(const erp_hypothesis& hy) {
+    return (hy.R1_valid != 0) + (hy.R2_valid != 0);
+}
+
+__global__ __launch_bounds__(1024) void valid_count_kernel(const int32_t* __restrict__ counts,
+                                                           const erp_hypothesis* __restrict__ hyps,
+                                                           int iters, double sample_frac,
+                                                           int32_t* __restrict__ vchunk) {
     __shared__ int ws[16];
     __shared__ float red6[6][16];
-    const int p = blockIdx.x, tid = threadIdx.x;
+    const int p = blockIdx.y, c = blockIdx.x, tid = threadIdx.x;
     const int M = counts[p];
-    if ((int)(M * sample_frac) < 1) {
-        if (tid == 0) kcount[p] = 0;
-        return;
-    }
-    const erp_hypothesis* H = hyps + (size_t)p * iters;
-    const int stride = 2 * iters;
-    float* X = rv + (size_t)p * 3 * stride;
-    float* T = tv + (size_t)p * 3 * stride;
-    float* A = rv_aos ? rv_aos + (size_t)p * 3 * stride : nullptr;
+    if ((int)(M * sample_frac) < 1) return;
+    const int h = c * 1024 + tid;
+    erp_hypothesis hy;
+    hy.R1_valid = 0;
+    hy.R2_valid = 0;
+    if (h < iters) hy = hyps[(size_t)p * iters + h];
     float mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
-    int base = 0;
-    // chunks of 1024 consecutive iterations (one per thread, coalesced record reads); the
-    // block scan of each chunk keeps the reference's push order (iteration, then R1, R2)
-    for (int h0 = 0; h0 < iters; h0 += 1024) {
-        const int h = h0 + tid;
-        erp_hypothesis hy;
-        hy.R1_valid = 0;
-        hy.R2_valid = 0;
-        if (h < iters) hy = H[h];
-        const int cnt = (hy.R1_valid != 0) + (hy.R2_valid != 0);
-        int total;
-        int pos = base + block_exclusive_scan<1024>(cnt, ws, &total);
 #pragma unroll
-        for (int which = 0; which < 2; which++) {
-            if (!(which ? hy.R2_valid : hy.R1_valid)) continue;
-            const float* R = which ? hy.R2 : hy.R1;
+    for (int which = 0; which < 2; which++) {
+        if (!(which ? hy.R2_valid : hy.R1_valid)) continue;
+        const float* R = which ? hy.R2 : hy.R1;
 #pragma unroll
-            for (int c = 0; c < 3; c++) {
-                X[c * stride + pos] = R[c];
-                mn[c] = fminf(mn[c], R[c]);
-                mx[c] = fmaxf(mx[c], R[c]);
-                T[3 * pos + c] = hy.T[c];
-                if (A) A[3 * pos + c] = R[c];
-            }
-            pos++;
+        for (int k = 0; k < 3; k++) {
+            mn[k] = fminf(mn[k], R[k]);
+            mx[k] = fmaxf(mx[k], R[k]);
         }
-        base += total;
     }
-    if (tid == 0) kcount[p] = base;
-    // bounding-box diagonal of the valid R set (>= every pairwise distance): the scale of
-    // the consensus bounds histogram
+    int total;
+    (void)block_exclusive_scan<1024>(hyp_valid_count(hy), ws, &total);
 #pragma unroll
-    for (int c = 0; c < 3; c++) {
-        float a = mn[c], b = mx[c];
+    for (int k = 0; k < 3; k++) {
+        float a = mn[k], b = mx[k];
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
             a = fminf(a, __shfl_xor(a, o, 64));
             b = fmaxf(b, __shfl_xor(b, o, 64));
         }
         if ((tid & 63) == 0) {
-            red6[c][tid >> 6] = a;
-            red6[3 + c][tid >> 6] = b;
+            red6[k][tid >> 6] = a;
+            red6[3 + k][tid >> 6] = b;
         }
     }
     __syncthreads();
-    if (tid == 0) {
-        double d2 = 0;
-        for (int c = 0; c < 3; c++) {
-            float a = kInf, b = -kInf;
-            for (int w = 0; w < 16; w++) {
-                a = fminf(a, red6[c][w]);
-                b = fmaxf(b, red6[3 + c][w]);
+    int32_t* o = vchunk + ((size_t)p * gridDim.x + c) * 8;
+    if (tid == 0) o[0] = total;
+    if (tid >= 1 && tid <= 6) {
+        const int k = tid - 1;
+        float v = k < 3 ? kInf : -kInf;
+        for (int w = 0; w < 16; w++) v = k < 3 ? fminf(v, red6[k][w]) : fmaxf(v, red6[k][w]);
+        o[tid] = __float_as_int(v);
+    }
+}
+
+__global__ __launch_bounds__(1024) void valid_scatter_kernel(const int32_t* __restrict__ counts,
+                                                             const erp_hypothesis* __restrict__ hyps,
+                                                             int iters, double sample_frac,
+                                                             const int32_t* __restrict__ vchunk,
+                                                             float* __restrict__ rv,
+                                                             float* __restrict__ tv,
+                                                             int32_t* __restrict__ kcount,
+                                                             float* __restrict__ rv_aos,
+                                                             float* __restrict__ dscale) {
+    __shared__ int ws[16];
+    __shared__ int sbase[16];
+    const int p = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, nch = gridDim.x;
+    const int M = counts[p];
+    if ((int)(M * sample_frac) < 1) {
+        if (c == 0 && tid == 0) kcount[p] = 0;
+        return;
+    }
+    const int32_t* vc = vchunk + (size_t)p * nch * 8;
+    // chunks before this one (and, for chunk 0, all of them: K and the bounding box)
+    const int upto = c == 0 ? nch : c;
+    int part = 0;
+    for (int q = tid; q < upto; q += 1024) part += vc[q * 8];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if ((tid & 63) == 0) sbase[tid >> 6] = part;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < 16; w++) base += sbase[w];
+    if (c == 0) {
+        if (tid == 0) {
+            kcount[p] = base;
+            double d2 = 0;
+            for (int k = 0; k < 3; k++) {
+                float a = kInf, b = -kInf;
+                for (int q = 0; q < nch; q++) {
+                    a = fminf(a, __int_as_float(vc[q * 8 + 1 + k]));
+                    b = fmaxf(b, __int_as_float(vc[q * 8 + 4 + k]));
+                }
+                const double e = base > 0 ? (double)b - (double)a : 0.0;
+                d2 += e * e;
             }
-            const double e = base > 0 ? (double)b - (double)a : 0.0;
-            d2 += e * e;
+            dscale[p] = (float)(sqrt(d2) * (1.0 + 1e-6));
         }
-        dscale[p] = (float)(sqrt(d2) * (1.0 + 1e-6));
+        base = 0;
+    }
+    const int h = c * 1024 + tid;
+    erp_hypothesis hy;
+    hy.R1_valid = 0;
+    hy.R2_valid = 0;
+    if (h < iters) hy = hyps[(size_t)p * iters + h];
+    int total;
+    int pos = base + block_exclusive_scan<1024>(hyp_valid_count(hy), ws, &total);
+    const int stride = 2 * iters;
+    float* X = rv + (size_t)p * 3 * stride;
+    float* T = tv + (size_t)p * 3 * stride;
+    float* A = rv_aos ? rv_aos + (size_t)p * 3 * stride : nullptr;
+#pragma unroll
+    for (int which = 0; which < 2; which++) {
+        if (!(which ? hy.R2_valid : hy.R1_valid)) continue;
+        const float* R = which ? hy.R2 : hy.R1;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            X[k * stride + pos] = R[k];
+            T[3 * pos + k] = hy.T[k];
+            if (A) A[3 * pos + k] = R[k];
+        }
+        pos++;
     }
 }
 
@@ -2319,17 +2368,25 @@ __global__ __launch_bounds__(1024) void consensus_select_kernel(const int32_t* _
     __syncthreads();
     double minub = sm[0];
     for (int w = 1; w < 16; w++) minub = fmin(minub, sm[w]);
-    const int per = (K + 1023) / 1024;
-    const int ka = min(K, tid * per), kb = min(K, ka + per);
-    int cnt = 0;
-    for (int k = ka; k < kb; k++) cnt += L[k] <= minub;
-    int total;
-    int pos = block_exclusive_scan<1024>(cnt, ws, &total);
-    for (int k = ka; k < kb; k++) {
-        if (L[k] <= minub) S[pos++] = k;
-        else Tm[k] = __builtin_huge_val();
+    // compaction in any order (the survivors' means are written per row and the final pass
+    // scans rows in index order): coalesced strided reads, one LDS atomic per wave
+    if (tid == 0) ws[0] = 0;
+    __syncthreads();
+    const int lane = tid & 63;
+    for (int k0 = 0; k0 < K; k0 += 1024) {
+        const int k = k0 + tid;
+        const bool keep = k < K && L[k] <= minub;
+        if (k < K && !keep) Tm[k] = __builtin_huge_val();
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
+        if (bal) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&ws[0], __builtin_popcountll(bal));
+            base = __shfl(base, 0, 64);
+            if (keep) S[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = k;
+        }
     }
-    if (tid == 0) nsurv[p] = total;
+    __syncthreads();
+    if (tid == 0) nsurv[p] = ws[0];
 }
 
 // exact sorted-sequential trimmed mean of one row (std::sort + std::accumulate semantics)
@@ -2700,11 +2757,19 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
     return hipGetLastError();
 }
 
+size_t valid_chunk_bytes(const BatchShape& sh) {
+    return (size_t)sh.n_pairs * ((sh.iters + 1023) / 1024) * 8 * sizeof(int32_t);
+}
+
 hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyps,
-                                const BatchShape& sh, double sample_frac, float* rv, float* tv,
-                                int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st) {
-    hipLaunchKernelGGL(valid_compact_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, hyps,
-                       sh.iters, sample_frac, rv, tv, kcount, rv_aos, dscale);
+                                const BatchShape& sh, double sample_frac, int32_t* vchunk,
+                                float* rv, float* tv, int32_t* kcount, float* rv_aos,
+                                float* dscale, hipStream_t st) {
+    dim3 grid((sh.iters + 1023) / 1024, sh.n_pairs);
+    hipLaunchKernelGGL(valid_count_kernel, grid, dim3(1024), 0, st, counts, hyps, sh.iters,
+                       sample_frac, vchunk);
+    hipLaunchKernelGGL(valid_scatter_kernel, grid, dim3(1024), 0, st, counts, hyps, sh.iters,
+                       sample_frac, vchunk, rv, tv, kcount, rv_aos, dscale);
     return hipGetLastError();
 }
 
