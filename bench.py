@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--profile-tag", default="r01g")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
+    ap.add_argument("--no-shard-consensus", action="store_true",
+                    help="manual workload: replicate the consensus on every rank")
     ap.add_argument("--workload", choices=["pairs", "dense", "manual", "remap"], default="pairs",
                     help="pairs: configs[1] (the metric; configs[2] with --kpts 2048); dense: "
                          "configs[3], one N x N match (--kpts, default 16384) on both matcher "
@@ -221,7 +223,8 @@ def run_manual(args):
     ctx = Context(local)
 
     def step():
-        return D.find_hypothesis_sharded_dev(ctx, c["W"], c["H"], kl, kr, 100, iters)[0]
+        return D.find_hypothesis_sharded_dev(ctx, c["W"], c["H"], kl, kr, 100, iters,
+                                             shard_consensus=not args.no_shard_consensus)[0]
 
     for _ in range(args.warmup):
         res = step()

@@ -89,7 +89,8 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_crop_rotated_image_dev", "erp_spherical_bands_dev", "erp_rotate_keypoints_dev",
             "erp_unrotate_band_keypoints_dev", "erp_rotate_image_dev", "erp_rectify_dev",
             "erp_vertical_rotate_dev", "erp_eular2rot", "erp_rot2eular", "erp_rot_from_vec",
-            "erp_inv3", "erp_rectify_matrices"]
+            "erp_inv3", "erp_rectify_matrices", "erp_consensus_hyps_shard_dev",
+            "erp_consensus_hyps_finish_dev"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
@@ -163,6 +164,10 @@ def load(build_if_missing: bool = False):
     L.erp_inv3.argtypes = [P, P]
     L.erp_inv3.restype = C.c_int32
     L.erp_rectify_matrices.argtypes = [P, P, P, P]
+    L.erp_consensus_hyps_shard_dev.argtypes = [P, C.c_int32, P, C.c_int32, C.POINTER(RansacCfg),
+                                               C.c_int32, C.c_int32, P, P, P, P]
+    L.erp_consensus_hyps_finish_dev.argtypes = [P, C.c_int32, P, C.c_int32, C.POINTER(RansacCfg),
+                                                P, P, P, P, P]
     L.erp_consensus_hyps_dev.argtypes = [P, C.c_int32, P, C.c_int32, C.POINTER(RansacCfg), P, P]
     L.erp_stage_name.argtypes = [C.c_int32]
     L.erp_stage_name.restype = C.c_char_p

@@ -371,34 +371,41 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
 
 // consensus stages after the hypothesis records are in place (counts may be null when the
 // valid list is given directly: erp_consensus_dev)
+// phase: 0 = everything; 1 = compaction + bounds of rows shard / nshards only (into lb_/ub_/
+// bsel_); 2 = the rest (select onward) after a phase-1 call on this context, with the bounds
+// of every row in lb_/ub_/bsel_ (combined over the shards by the caller)
 erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
                          const erp_batch_outputs* out, erp_pair_result* results, hipStream_t st,
-                         bool from_hyps) {
+                         bool from_hyps, int phase = 0, int shard = 0, int nshards = 1,
+                         double* lb_ = nullptr, double* ub_ = nullptr, int32_t* bsel_ = nullptr) {
     erp_ctx* ctx = c;
+    double* lbp = lb_ ? lb_ : (double*)c->lb.p;
+    double* ubp = ub_ ? ub_ : (double*)c->ub.p;
+    int32_t* bselp = bsel_ ? bsel_ : (int32_t*)c->bsel.p;
     auto* counts = from_hyps ? (int32_t*)c->counts.p : nullptr;
     auto* flags = (int32_t*)c->flags.p;  // consensus-only: set by consensus_input (non-finite)
     auto* hyps = (out && out->hyps) ? out->hyps : (erp_hypothesis*)c->hyps.p;
     auto* tv = (out && out->tvec) ? out->tvec : (float*)c->tv.p;
     auto* tmean = (out && out->dist) ? out->dist : (double*)c->tmean.p;
-    if (from_hyps) {
+    if (from_hyps && phase != 2) {
         StageTimer _t(ctx, ERP_STAGE_VALID_COMPACT, st);
         ERP_CK(erp::launch_valid_compact(counts, hyps, sh, cfg->sample_frac,
                                          (int32_t*)c->vchunk.p, (float*)c->rv.p, tv,
                                          (int32_t*)c->kcount.p, out ? out->rvec : nullptr,
                                          (float*)c->dscale.p, st));
     }
-    {
+    if (phase != 2) {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
         ERP_CK(erp::launch_consensus_bounds((int32_t*)c->kcount.p, (float*)c->rv.p,
                                             (float*)c->dscale.p, (float*)c->edges.p, sh,
-                                            cfg->trim_lo, cfg->trim_hi,
-                                            (double*)c->lb.p, (double*)c->ub.p,
-                                            (int32_t*)c->bsel.p, st));
+                                            cfg->trim_lo, cfg->trim_hi, lbp, ubp, bselp, shard,
+                                            nshards, st));
     }
+    if (phase == 1) return ERP_OK;
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
-        ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, (double*)c->lb.p,
-                                            (double*)c->ub.p, sh, cfg->trim_lo, cfg->trim_hi,
+        ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, lbp,
+                                            ubp, sh, cfg->trim_lo, cfg->trim_hi,
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, 0,
                                             st));
     }
@@ -407,13 +414,13 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         ERP_CK(erp::launch_consensus_refine((int32_t*)c->kcount.p, (float*)c->rv.p,
                                             (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
-                                            (int32_t*)c->bsel.p, (double*)c->lb.p,
-                                            (double*)c->ub.p, st));
+                                            bselp, lbp,
+                                            ubp, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
-        ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, (double*)c->lb.p,
-                                            (double*)c->ub.p, sh, cfg->trim_lo, cfg->trim_hi,
+        ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, lbp,
+                                            ubp, sh, cfg->trim_lo, cfg->trim_hi,
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, 1,
                                             st));
     }
@@ -422,7 +429,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         ERP_CK(erp::launch_consensus_rows((int32_t*)c->kcount.p, (float*)c->rv.p,
                                           (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
                                           (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
-                                          (int32_t*)c->bsel.p, tmean, st));
+                                          bselp, tmean, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_FINAL, st);
@@ -685,6 +692,51 @@ erp_status erp_consensus_hyps_dev(erp_ctx* ctx, int32_t m, const erp_hypothesis*
     ERP_CK(hipMemsetAsync(ctx->flags.p, 0, 4, st));
     ERP_CK(erp::launch_set_i32((int32_t*)ctx->counts.p, m, st));
     return run_consensus(ctx, sh, cfg, &out, d_result, st, true);
+}
+
+erp_status erp_consensus_hyps_shard_dev(erp_ctx* ctx, int32_t m, const erp_hypothesis* d_hyps,
+                                        int32_t n_hyps, const erp_ransac_cfg* cfg, int32_t shard,
+                                        int32_t nshards, double* d_lb, double* d_ub,
+                                        int32_t* d_bsel, void* stream) {
+    if (!ctx || m < 0 || m > 65535 || n_hyps < 1 || !d_hyps || !cfg_ok(cfg) || nshards < 1 ||
+        shard < 0 || shard >= nshards || !d_lb || !d_ub || !d_bsel)
+        return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    const erp::BatchShape sh = make_shape(1, std::max(m, 1), std::max(m, 1), n_hyps,
+                                          cfg->sample_frac);
+    erp_batch_outputs out{};
+    out.hyps = const_cast<erp_hypothesis*>(d_hyps);
+    erp_status es = ensure_estimator(ctx, sh, &out);
+    if (es != ERP_OK) return es;
+    const size_t rows = 2 * (size_t)n_hyps;
+    ERP_CK(hipMemsetAsync(d_lb, 0, rows * 8, st));
+    ERP_CK(hipMemsetAsync(d_ub, 0, rows * 8, st));
+    ERP_CK(hipMemsetAsync(d_bsel, 0, rows * 8, st));
+    ERP_CK(hipMemsetAsync(ctx->flags.p, 0, 4, st));
+    ERP_CK(erp::launch_set_i32((int32_t*)ctx->counts.p, m, st));
+    return run_consensus(ctx, sh, cfg, &out, nullptr, st, true, 1, shard, nshards, d_lb, d_ub,
+                         d_bsel);
+}
+
+erp_status erp_consensus_hyps_finish_dev(erp_ctx* ctx, int32_t m, const erp_hypothesis* d_hyps,
+                                         int32_t n_hyps, const erp_ransac_cfg* cfg, double* d_lb,
+                                         double* d_ub, int32_t* d_bsel, erp_pair_result* d_result,
+                                         void* stream) {
+    if (!ctx || m < 0 || m > 65535 || n_hyps < 1 || !d_hyps || !cfg_ok(cfg) || !d_lb || !d_ub ||
+        !d_bsel || !d_result)
+        return ERP_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    hipStream_t st = (hipStream_t)stream;
+    const erp::BatchShape sh = make_shape(1, std::max(m, 1), std::max(m, 1), n_hyps,
+                                          cfg->sample_frac);
+    erp_batch_outputs out{};
+    out.hyps = const_cast<erp_hypothesis*>(d_hyps);
+    erp_status es = ensure_estimator(ctx, sh, &out);
+    if (es != ERP_OK) return es;
+    return run_consensus(ctx, sh, cfg, &out, d_result, st, true, 2, 0, 1, d_lb, d_ub, d_bsel);
 }
 
 erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* h_kl,

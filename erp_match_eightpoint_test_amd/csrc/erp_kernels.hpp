@@ -131,7 +131,7 @@ size_t consensus_edges_bytes(int n_pairs);
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
-                                   hipStream_t st);
+                                   int shard, int nshards, hipStream_t st);
 // survivors = rows with LB <= min UB (again = 1: only pairs the refine pass touched)
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
                                    const BatchShape& sh, double trim_lo, double trim_hi,

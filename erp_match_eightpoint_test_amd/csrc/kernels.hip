@@ -1823,7 +1823,8 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
                                                                double trim_hi,
                                                                double* __restrict__ lb,
                                                                double* __restrict__ ub,
-                                                               int32_t* __restrict__ bsel) {
+                                                               int32_t* __restrict__ bsel,
+                                                               int shard, int nshards) {
     constexpr int R = kBoundRows;
     constexpr int NS = 256 / R;        // epilogue slices per row
     constexpr int per = kNB / NS;      // bins per slice
@@ -1835,8 +1836,12 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     float (*partU)[R] = reinterpret_cast<float (*)[R]>(hist + 2 * NS * R);
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
-    const int r0 = blockIdx.x * R;
-    if (r0 >= K) return;
+    // rows [ra, rb) of this shard (hypothesis-block sharding of one find over ranks; 0 / 1
+    // otherwise); every column
+    const int ra = (int)((int64_t)K * shard / nshards);
+    const int rb = (int)((int64_t)K * (shard + 1) / nshards);
+    const int r0 = ra + blockIdx.x * R;
+    if (r0 >= rb) return;
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
@@ -1951,14 +1956,14 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
             c0 = c1;
         }
     }
-    if (row < K) {
+    if (row < rb) {
         if (sel_a >= 0) bsel[((size_t)p * stride + row) * 2] = sel_a;
         if (sel_b >= 0) bsel[((size_t)p * stride + row) * 2 + 1] = sel_b;
     }
     partL[sl][r] = L;
     partU[sl][r] = U;
     __syncthreads();
-    if (sl == 0 && row < K) {
+    if (sl == 0 && row < rb) {
         for (int q = 1; q < NS; q++) {
             L += partL[q][r];
             U += partU[q][r];
@@ -2786,11 +2791,12 @@ size_t consensus_edges_bytes(int n_pairs) { return (size_t)n_pairs * 2 * kNB * s
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
-                                   hipStream_t st) {
+                                   int shard, int nshards, hipStream_t st) {
     hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
-    dim3 grid((2 * sh.iters + kBoundRows - 1) / kBoundRows, sh.n_pairs);
+    const int rows = (2 * sh.iters + nshards - 1) / nshards + 1;  // >= any shard's rows
+    dim3 grid((rows + kBoundRows - 1) / kBoundRows, sh.n_pairs);
     hipLaunchKernelGGL(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale, edges,
-                       2 * sh.iters, trim_lo, trim_hi, lb, ub, bsel);
+                       2 * sh.iters, trim_lo, trim_hi, lb, ub, bsel, shard, nshards);
     return hipGetLastError();
 }
 

@@ -79,13 +79,19 @@ def padded_block(iters: int, world: int, rank: int) -> tuple[int, int, int]:
 
 
 def find_hypothesis_sharded_dev(ctx, W: int, H: int, d_kl, d_kr, m: int, iters: int,
-                                cfg_kwargs: dict | None = None, group=None, stream=None):
+                                cfg_kwargs: dict | None = None, group=None, stream=None,
+                                shard_consensus: bool = True, emulate_world: int = 0):
     """configs[4] on GPUs, device-resident end to end: rank r computes iterations
     [r B, (r+1) B) (B = ceil(iters / world)) into a zero-padded block of B records
     (erp_eight_point_hypotheses_dev at glibc offset base + r B (m-1)), the blocks are
     all-gathered over RCCL in rank order (= iteration order; zero records push nothing), and
-    every rank runs the valid-list compaction + consensus on the merged records
-    (erp_consensus_hyps_dev).  Returns (result record tensor [64] uint8, merged records)."""
+    every rank runs the valid-list compaction + consensus on the merged records.  With
+    shard_consensus the consensus's K^2 bounds pass is split too: rank r bounds the rows
+    [K r / world, K (r+1) / world) (erp_consensus_hyps_shard_dev), one RCCL all_reduce(SUM)
+    combines the per-row [LB, UB] and boundary bins, and every rank finishes the selection
+    (erp_consensus_hyps_finish_dev) -- the same result as erp_consensus_hyps_dev.
+    emulate_world > 1 (tests, one process): run every shard of the consensus locally in turn and
+    sum them, as the all_reduce would.  Returns (result record tensor [64] uint8, merged)."""
     import ctypes as C
 
     import torch
@@ -112,8 +118,34 @@ def find_hypothesis_sharded_dev(ctx, W: int, H: int, d_kl, d_kr, m: int, iters: 
         merged = local
     res = torch.zeros(RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
     cfg = default_cfg(**dict(cfg_kwargs, iters=iters))
-    check(ctx.L.erp_consensus_hyps_dev(ctx.h, m, merged.data_ptr(), merged.shape[0], C.byref(cfg),
-                                       res.data_ptr(), st), "erp_consensus_hyps_dev")
+    n = merged.shape[0]
+    nsh = world if world > 1 else max(emulate_world, 1)
+    if not shard_consensus or nsh == 1:
+        check(ctx.L.erp_consensus_hyps_dev(ctx.h, m, merged.data_ptr(), n, C.byref(cfg),
+                                           res.data_ptr(), st), "erp_consensus_hyps_dev")
+        return res, merged
+    bounds = torch.zeros((3, 2 * n), dtype=torch.float64, device=dev)  # lb, ub, bsel (2 x i32)
+    shards = [rank] if world > 1 else list(range(nsh))
+    part = torch.empty_like(bounds)
+    for sh in shards:
+        check(ctx.L.erp_consensus_hyps_shard_dev(ctx.h, m, merged.data_ptr(), n, C.byref(cfg), sh,
+                                                 nsh, part[0].data_ptr(), part[1].data_ptr(),
+                                                 part[2].data_ptr(), st),
+              "erp_consensus_hyps_shard_dev")
+        if world > 1:
+            bounds = part
+        else:  # emulation: integer bsel halves summed as int64 words (disjoint rows, no carry)
+            bounds[:2] += part[:2]
+            bounds[2].view(torch.int64).add_(part[2].view(torch.int64))
+    if world > 1:
+        # lb / ub as doubles; bsel's int32 pairs as int64 words (one rank writes each row, the
+        # others hold 0: the sums are exact)
+        dist.all_reduce(bounds[:2], group=group)
+        dist.all_reduce(bounds[2].view(torch.int64), group=group)
+    check(ctx.L.erp_consensus_hyps_finish_dev(ctx.h, m, merged.data_ptr(), n, C.byref(cfg),
+                                              bounds[0].data_ptr(), bounds[1].data_ptr(),
+                                              bounds[2].data_ptr(), res.data_ptr(), st),
+          "erp_consensus_hyps_finish_dev")
     return res, merged
 
 

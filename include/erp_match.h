@@ -229,6 +229,20 @@ erp_status erp_consensus_dev(erp_ctx* ctx, const float* d_rvec, const float* d_t
 erp_status erp_consensus_hyps_dev(erp_ctx* ctx, int32_t m, const erp_hypothesis* d_hyps,
                                   int32_t n_hyps, const erp_ransac_cfg* cfg,
                                   erp_pair_result* d_result, void* stream);
+/* The same consensus with its K^2 bounds pass split over nshards ranks (configs[4] strong
+   scaling): on every rank, with the same merged d_hyps, call _shard_dev (valid-list compaction
+   + the bounds of rows [K*shard/nshards, K*(shard+1)/nshards) into d_lb / d_ub / d_bsel, each
+   2*n_hyps entries of 8 bytes, zero elsewhere), SUM the three arrays over the ranks (e.g. one
+   RCCL all_reduce), then call _finish_dev on the SAME context (select, refine, exact means,
+   first-argmin).  The result equals erp_consensus_hyps_dev's. */
+erp_status erp_consensus_hyps_shard_dev(erp_ctx* ctx, int32_t m, const erp_hypothesis* d_hyps,
+                                        int32_t n_hyps, const erp_ransac_cfg* cfg, int32_t shard,
+                                        int32_t nshards, double* d_lb, double* d_ub,
+                                        int32_t* d_bsel, void* stream);
+erp_status erp_consensus_hyps_finish_dev(erp_ctx* ctx, int32_t m, const erp_hypothesis* d_hyps,
+                                         int32_t n_hyps, const erp_ransac_cfg* cfg, double* d_lb,
+                                         double* d_ub, int32_t* d_bsel, erp_pair_result* d_result,
+                                         void* stream);
 /* host pointers, synchronous: the drop-in for eight_point::find. */
 erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_point2f* h_kl,
                                 const erp_point2f* h_kr, int32_t m, const erp_ransac_cfg* cfg,

@@ -426,6 +426,31 @@ def test_hypothesis_sharded_dev_padded_blocks(ctx, world):
     assert np.array_equal(r["R"], R) and np.array_equal(r["T"], T)
 
 
+@pytest.mark.parametrize("world,iters", [(2, 500), (3, 500), (8, 500), (5, 4000)])
+def test_consensus_row_shards_equal_unsharded(ctx, world, iters):
+    """configs[4]'s sharded consensus: the K^2 bounds pass split into `world` row shards
+    (erp_consensus_hyps_shard_dev per shard, summed as the RCCL all_reduce would) then
+    erp_consensus_hyps_finish_dev gives the unsharded find's result, field for field."""
+    import torch
+    from erp_match_eightpoint_test_amd import eight_point, results_to_numpy
+    from erp_match_eightpoint_test_amd import dist as D
+    g = _npz("find_manual_100_it500.npz")
+    W, H = int(g["W"]), int(g["H"])
+    kl = torch.from_numpy(np.ascontiguousarray(g["kl"])).cuda()
+    kr = torch.from_numpy(np.ascontiguousarray(g["kr"])).cuda()
+    m = kl.shape[0]
+    res, _ = D.find_hypothesis_sharded_dev(ctx, W, H, kl, kr, m, iters, emulate_world=world)
+    torch.cuda.synchronize()
+    r = results_to_numpy(res.view(1, -1))[0]
+    ep = eight_point(ctx=ctx, iters=iters)
+    R, T = ep.find(W, H, g["kl"], g["kr"])
+    ref = ep.last_result
+    for f in ("status", "K", "min_idx", "survivors", "near_ties"):
+        assert r[f] == ref[f], (f, r[f], ref[f])
+    assert np.array_equal(r["R"], R) and np.array_equal(r["T"], T)
+    assert r["min_dist"] == ref["min_dist"]
+
+
 @pytest.mark.parametrize("K", [1, 2, 3, 5, 40, 1000])
 def test_consensus_dev_vs_oracle(ctx, oracle, K):
     from erp_match_eightpoint_test_amd import dist as D
