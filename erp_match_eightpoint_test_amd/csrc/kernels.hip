@@ -110,9 +110,10 @@ constexpr int kFRow = 72;           // bf16 per LDS row: 64 + 8 pad (conflict-fr
 constexpr float kFEps = 0x1.08p-7f;
 constexpr float kFTiny = 0x1p-100f; // absolute floor (flushed denormals)
 
+constexpr int kFST = 4;             // 32-row tiles per LDS stage (one barrier per stage)
 struct FilterLds {
-    bf16x8 hi[2][kFT * kFRow / 8];
-    float tb[2][kFT];               // tu (pass 1) or tl (pass 2) of the tile's rows
+    bf16x8 hi[2][kFST * kFT * kFRow / 8];
+    float tb[2][kFST * kFT];        // tu (pass 1) or tl (pass 2) of the stage's rows
 };
 
 __device__ __forceinline__ bf16x8 round8(const float4 a, const float4 b) {
@@ -210,49 +211,44 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     const size_t cl = (((size_t)p * max_nq + (qv ? q : 0)) * chunks + blockIdx.y) * 2 + h;
     int32_t* clist = cand + cl * kCandSub;
     int ncand = 0;
-    // staging: thread -> train row tid >> 3 of the tile, 16 bytes (tid & 7) of it
+    // staging: thread -> train rows (tid >> 3) + 32 u of the stage (u < kFST), 16 bytes
+    // (tid & 7) of each; the next stage is loaded into registers while this one is computed
+    // (kFST tiles of MFMA work cover an L2 miss), one barrier per stage
     const int srow = tid >> 3, spart = tid & 7;
     const bf16x8* thp = thi + (size_t)p * max_nt * 8;
     const float* tnp = tn + (size_t)p * max_nt;
     const bf16x8 z8 = {};
-    // two tiles in flight: tile k+2 is loaded while tile k is computed (one tile of work is
-    // shorter than an L2 round trip)
-    bf16x8 gh[2] = {z8, z8};
-    float gn[2] = {kInf, kInf};
-    auto gload = [&](int tile0, int slot) {
-        const int j = tile0 + srow;
-        if (j < t1) {
-            gh[slot] = thp[(size_t)j * 8 + spart];
-            if (spart == 0) gn[slot] = tnp[j];
-        } else {
-            gh[slot] = z8;
-            gn[slot] = kInf;
+    bf16x8 gh[kFST];
+    float gn[kFST];
+    auto gload = [&](int st) {
+#pragma unroll
+        for (int u = 0; u < kFST; u++) {
+            const int j = t0 + (st * kFST + u) * kFT + srow;
+            if (j < t1) {
+                gh[u] = thp[(size_t)j * 8 + spart];
+                gn[u] = spart == 0 ? tnp[j] : kInf;
+            } else {
+                gh[u] = z8;
+                gn[u] = kInf;
+            }
         }
     };
     const int ntiles = (t1 - t0 + kFT - 1) / kFT;
-    gload(t0, 0);
-    if (ntiles > 1) gload(t0 + kFT, 1);
+    const int nstages = (ntiles + kFST - 1) / kFST;
+    gload(0);
     const int r = lane & 31;
-    auto tile_step = [&](int k, auto slot_c) {
-        constexpr int buf = decltype(slot_c)::value;
+    auto tile_step = [&](int k, int buf, int u) {
         const int tile0 = t0 + k * kFT;
-        sm.hi[buf][(srow * kFRow) / 8 + spart] = gh[buf];
-        if (spart == 0)
-            sm.tb[buf][srow] = gn[buf] == kInf
-                                   ? kInf
-                                   : __builtin_fmaf(gn[buf], PASS == 1 ? kFEps : -kFEps, gn[buf]);
-        __syncthreads();
-        if (k + 2 < ntiles) gload(tile0 + 2 * kFT, buf);
         f32x16 acc = {};
 #pragma unroll
         for (int c = 0; c < 4; c++) {
-            const bf16x8 ah = sm.hi[buf][(r * kFRow + 16 * c + 8 * h) / 8];
+            const bf16x8 ah = sm.hi[buf][((u * kFT + r) * kFRow + 16 * c + 8 * h) / 8];
             acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, qh[c], acc, 0, 0, 0);
         }
         f32x2 b2[8];
 #pragma unroll
         for (int g = 0; g < 4; g++) {
-            const float4 t4 = *reinterpret_cast<const float4*>(&sm.tb[buf][8 * g + 4 * h]);
+            const float4 t4 = *reinterpret_cast<const float4*>(&sm.tb[buf][u * kFT + 8 * g + 4 * h]);
             const f32x2 ta = {t4.x, t4.y}, tb = {t4.z, t4.w};
             const f32x2 a0 = {acc[4 * g], acc[4 * g + 1]}, a1 = {acc[4 * g + 2], acc[4 * g + 3]};
             b2[2 * g] = __builtin_elementwise_fma(m2x, a0, qb2 + ta);
@@ -290,9 +286,20 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
             }
         }
     };
-    for (int k = 0; k < ntiles; k += 2) {
-        tile_step(k, std::integral_constant<int, 0>{});
-        if (k + 1 < ntiles) tile_step(k + 1, std::integral_constant<int, 1>{});
+    for (int st = 0; st < nstages; st++) {
+        const int buf = st & 1;
+#pragma unroll
+        for (int u = 0; u < kFST; u++) {
+            sm.hi[buf][((u * kFT + srow) * kFRow) / 8 + spart] = gh[u];
+            if (spart == 0)
+                sm.tb[buf][u * kFT + srow] =
+                    gn[u] == kInf ? kInf : __builtin_fmaf(gn[u], PASS == 1 ? kFEps : -kFEps, gn[u]);
+        }
+        __syncthreads();
+        if (st + 1 < nstages) gload(st + 1);
+#pragma unroll
+        for (int u = 0; u < kFST; u++)
+            if (st * kFST + u < ntiles) tile_step(st * kFST + u, buf, u);
     }
     if (PASS == 1) {
         // top-2 of the query's four group minima (this lane's two and the other half's two)
