@@ -51,13 +51,22 @@ class Diag(C.Structure):
                 ("status", C.c_int32), ("min_dist", C.c_double)]
 
 
+class SurfParams(C.Structure):
+    _fields_ = [("hessian_threshold", C.c_double), ("n_octaves", C.c_int32),
+                ("n_octave_layers", C.c_int32)]
+
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+
 _lib = None
 
 
 def build(force: bool = False) -> str:
     """Compile the oracle with its Makefile (gcc only; no reference sources involved)."""
     if force or not os.path.exists(LIB_PATH) or (
-            os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "erp_oracle.c"))):
+            os.path.getmtime(LIB_PATH) < max(os.path.getmtime(os.path.join(HERE, f))
+                                             for f in ("erp_oracle.c", "erp_surf.c", "erp_oracle.h"))):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
@@ -96,6 +105,14 @@ def lib():
         L.erpo_find.restype = C.c_int
         L.erpo_rotate_pixel.argtypes = [C.c_int32, C.c_int32, P, C.c_int32, C.c_int32, P]
         L.erpo_rotate_pixel_prefix.argtypes = [P, P, C.c_int32, P, C.c_int32, C.c_int32, P]
+        L.erpo_surf.argtypes = [P, C.c_int32, C.c_int32, C.c_int32, C.POINTER(SurfParams), P, P,
+                                C.c_int32]
+        L.erpo_surf.restype = C.c_int32
+        L.erpo_fast_atan2.argtypes = [C.c_float, C.c_float]
+        L.erpo_fast_atan2.restype = C.c_float
+        L.erpo_gray_bgr.argtypes = [P, C.c_int32, C.c_int32, P]
+        L.erpo_integral.argtypes = [P, C.c_int32, C.c_int32, P]
+        L.erpo_resize_area.argtypes = [P, C.c_int, P, C.c_int]
         L.erpo_inv3.argtypes = [P, P]
         L.erpo_inv3.restype = C.c_int32
         L.erpo_rot_from_vec.argtypes = [P, P, P]
@@ -367,4 +384,29 @@ def rotate_pixel_prefix(rows, cols, m, W: int, H: int) -> np.ndarray:
     m = np.ascontiguousarray(m, np.float64).reshape(9)
     out = np.zeros((len(r), 2), np.float64)
     lib().erpo_rotate_pixel_prefix(_p(r), _p(c), len(r), _p(m), W, H, _p(out))
+    return out
+
+
+# ------------------------------------------------------------------ SURF (section 8f-2)
+def surf(img, hessian_threshold=100.0, n_octaves=4, n_octave_layers=3, max_kp=1 << 16):
+    """SURF::detect + compute (OpenCV defaults restated; parity with OpenCV unpinned):
+    img uint8 [H, W] or [H, W, 3] (BGR) -> (keypoints KEYPOINT_DTYPE, descriptors [n, 64])"""
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape[:2]
+    ch = 1 if img.ndim == 2 else img.shape[2]
+    prm = SurfParams(hessian_threshold, n_octaves, n_octave_layers)
+    while True:
+        kps = np.zeros(max_kp, KEYPOINT_DTYPE)
+        desc = np.zeros((max_kp, 64), np.float32)
+        n = lib().erpo_surf(_p(img), W, H, ch, C.byref(prm), _p(kps), _p(desc), max_kp)
+        if n >= 0:
+            return kps[:n].copy(), desc[:n].copy()
+        max_kp = -n
+
+
+def gray_bgr(img):
+    img = np.ascontiguousarray(img, np.uint8)
+    H, W = img.shape[:2]
+    out = np.zeros((H, W), np.uint8)
+    lib().erpo_gray_bgr(_p(img), W, H, _p(out))
     return out

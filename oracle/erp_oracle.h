@@ -103,6 +103,29 @@ int32_t erpo_rectify(const uint8_t* left, const uint8_t* right, int32_t W, int32
                      uint8_t* right_out);
 int32_t erpo_vertical_rotate(const uint8_t* im, int32_t W, int32_t H, uint8_t* out);
 
+/* ---- SURF (erp_surf.c): xfeatures2d::SURF::create() defaults as
+   called by src/feature_matcher.cpp:13-15,26-40.  Parity with OpenCV UNPINNED. ---- */
+typedef struct erpo_keypoint {  /* cv::KeyPoint layout */
+    float x, y, size, angle, response;
+    int32_t octave, class_id;
+} erpo_keypoint;
+typedef struct erpo_surf_params {
+    double hessian_threshold;  /* 100 */
+    int32_t n_octaves;         /* 4 */
+    int32_t n_octave_layers;   /* 3 */
+} erpo_surf_params;
+void erpo_gray_bgr(const uint8_t* bgr, int32_t W, int32_t H, uint8_t* gray);
+void erpo_integral(const uint8_t* img, int32_t W, int32_t H, int32_t* sum);
+float erpo_fast_atan2(float y, float x);
+int32_t erpo_surf_layer_size(int octave, int layer);
+int32_t erpo_surf_detect(const int32_t* sum, int32_t W, int32_t H, const erpo_surf_params* prm,
+                         erpo_keypoint* kps, int32_t max_kp);
+void erpo_resize_area(const uint8_t* src, int ss, uint8_t* dst, int ds);
+void erpo_surf_describe(const uint8_t* img, const int32_t* sum, int32_t W, int32_t H,
+                        erpo_keypoint* kp, float* vec);
+int32_t erpo_surf(const uint8_t* img, int32_t W, int32_t H, int32_t channels,
+                  const erpo_surf_params* prm, erpo_keypoint* kps, float* desc, int32_t max_kp);
+
 /* OpenCV 3.4 SVDecomp(src m x n, flags=0) restated.  w: min(m,n); u: m x min(m,n) row-major;
  * vt: min(m,n) x n row-major.  Returns 0 on success. */
 int erpo_svdecomp(const double* src, int32_t m, int32_t n, double* w, double* u, double* vt);
