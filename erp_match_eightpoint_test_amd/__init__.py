@@ -67,6 +67,41 @@ class feature_matcher:  # noqa: N801  (reference class name)
               "match_two_image")
         return out[:n.value].copy()
 
+    # ---- SURF (src/feature_matcher.cpp:26-40, xfeatures2d::SURF::create() defaults) ----
+    def surf(self, images, max_kp: int = 16384, **params):
+        """detect_key_point + comput_descriptor on CUDA uint8 images [n, H, W] (gray) or
+        [n, H, W, 3] (BGR); a single [H, W] / [H, W, 3] image is one image -> (keypoints list
+        of KEYPOINT_DTYPE arrays, descriptor list of [k, 64] float32), per image, in OpenCV's
+        KeypointGreater order.  Parity with OpenCV is unpinned (oracle/erp_surf.c)."""
+        import torch
+        if images.dim() == 2 or (images.dim() == 3 and images.shape[-1] == 3):
+            images = images.unsqueeze(0)  # one gray [H, W] or one BGR [H, W, 3] image
+        if not (images.is_cuda and images.dtype == torch.uint8 and images.is_contiguous()):
+            raise ValueError("images must be contiguous CUDA uint8 tensors")
+        ch = 3 if images.dim() == 4 else 1
+        n, H, W = images.shape[:3]
+        prm = capi.SurfParams()
+        self.ctx.L.erp_surf_params_default(C.byref(prm))
+        for k, v in params.items():
+            setattr(prm, k, v)
+        st = torch.cuda.current_stream(images.device).cuda_stream
+        while True:
+            kp = torch.empty((n, max_kp, 28), dtype=torch.uint8, device=images.device)
+            desc = torch.empty((n, max_kp, 64), dtype=torch.float32, device=images.device)
+            cnt = torch.zeros(n, dtype=torch.int32, device=images.device)
+            check(self.ctx.L.erp_surf_detect_compute_dev(self.ctx.h, images.data_ptr(), n, W, H, ch,
+                                                         C.byref(prm), max_kp, kp.data_ptr(),
+                                                         desc.data_ptr(), cnt.data_ptr(), st),
+                  "erp_surf_detect_compute_dev")
+            counts = cnt.cpu().numpy()
+            if (counts >= 0).all():
+                break
+            max_kp = int(-counts.min()) + 16
+        kps = kp.cpu().numpy()
+        ds = desc.cpu().numpy()
+        return ([kps[i, :counts[i]].reshape(-1).view(capi.KEYPOINT_DTYPE).copy() for i in range(n)],
+                [ds[i, :counts[i]].copy() for i in range(n)])
+
     def _to_device(self, a):
         import torch
         return torch.from_numpy(a).to(f"cuda:{self.ctx.device}")

@@ -90,13 +90,24 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_unrotate_band_keypoints_dev", "erp_rotate_image_dev", "erp_rectify_dev",
             "erp_vertical_rotate_dev", "erp_eular2rot", "erp_rot2eular", "erp_rot_from_vec",
             "erp_inv3", "erp_rectify_matrices", "erp_consensus_hyps_shard_dev",
-            "erp_consensus_hyps_finish_dev"]
+            "erp_consensus_hyps_finish_dev", "erp_surf_params_default",
+            "erp_surf_detect_compute_dev"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
           "consensus_refine", "knn2_exact"]
 MATCHER_MFMA_FILTER = 0  # erp_matcher_method
 MATCHER_VALU_EXACT = 1
+
+
+class SurfParams(C.Structure):
+    _fields_ = [("hessian_threshold", C.c_double), ("n_octaves", C.c_int32),
+                ("n_octave_layers", C.c_int32), ("extended", C.c_int32), ("upright", C.c_int32)]
+
+
+KEYPOINT_DTYPE = np.dtype([("x", "<f4"), ("y", "<f4"), ("size", "<f4"), ("angle", "<f4"),
+                           ("response", "<f4"), ("octave", "<i4"), ("class_id", "<i4")])
+assert KEYPOINT_DTYPE.itemsize == 28
 
 
 class ErpError(RuntimeError):
@@ -168,6 +179,10 @@ def load(build_if_missing: bool = False):
                                                C.c_int32, C.c_int32, P, P, P, P]
     L.erp_consensus_hyps_finish_dev.argtypes = [P, C.c_int32, P, C.c_int32, C.POINTER(RansacCfg),
                                                 P, P, P, P, P]
+    L.erp_surf_params_default.argtypes = [C.POINTER(SurfParams)]
+    L.erp_surf_params_default.restype = None
+    L.erp_surf_detect_compute_dev.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                              C.POINTER(SurfParams), C.c_int32, P, P, P, P]
     L.erp_consensus_hyps_dev.argtypes = [P, C.c_int32, P, C.c_int32, C.POINTER(RansacCfg), P, P]
     L.erp_stage_name.argtypes = [C.c_int32]
     L.erp_stage_name.restype = C.c_char_p

@@ -72,6 +72,8 @@ struct erp_ctx {
     DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
         rtab, limbs, tsplit, ovf, remap_scr, vchunk;
+    DevBuf extra[12];         // erp_ctx_scratch_internal slots (SURF)
+    uint64_t surf_key = 0;    // (W, H, params) of the SURF layer table in extra[1]
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -118,10 +120,15 @@ int32_t erp_abi_version(void) { return ERP_MATCH_ABI_VERSION; }
 }  // extern "C"
 
 int32_t erp_ctx_device_internal(erp_ctx* ctx) { return ctx->device; }  // remap_api.hip
-void* erp_ctx_scratch_internal(erp_ctx* ctx, int which, size_t bytes) {  // remap_api.hip
-    (void)which;
+uint64_t* erp_ctx_surf_key_internal(erp_ctx* ctx) { return &ctx->surf_key; }  // surf_api.hip
+
+// grow-only scratch slots for remap_api.hip / surf_api.hip (slot 0: remap boundary list;
+// 1..: SURF buffers)
+void* erp_ctx_scratch_internal(erp_ctx* ctx, int which, size_t bytes) {
     std::lock_guard<std::mutex> lk(ctx->mu);
-    return ensure(ctx->remap_scr, bytes) ? ctx->remap_scr.p : nullptr;
+    if (which < 0 || which >= (int)(sizeof(ctx->extra) / sizeof(ctx->extra[0]))) return nullptr;
+    DevBuf& b = which == 0 ? ctx->remap_scr : ctx->extra[which];
+    return ensure(b, bytes) ? b.p : nullptr;
 }
 
 extern "C" {
@@ -181,6 +188,8 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf, &ctx->remap_scr, &ctx->vchunk};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
+    for (DevBuf& b : ctx->extra)
+        if (b.p) (void)hipFree(b.p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     delete ctx;
     return ERP_OK;

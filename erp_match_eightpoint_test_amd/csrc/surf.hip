@@ -1,0 +1,574 @@
+// surf.hip -- SURF detector + 64-D descriptor on gfx950: what the reference
+// runs on every band image before the matcher (src/feature_matcher.cpp:13-15,26-40:
+// xfeatures2d::SURF::create() defaults, detect() then compute(); 8 calls per pair from
+// src/spherical_surf.cpp:96-118).  The algorithm follows OpenCV 3.4's surf.cpp as restated in
+// oracle/erp_surf.c (OpenCV itself is absent: parity with it is unpinned); the kernels repeat
+// the restatement operation for operation, so detection is bit-exact with the oracle and the
+// descriptor differs only where the device sin/cos of the orientation differ in the last ulp.
+//
+//   surf_gray_kernel        cvtColor(BGR2GRAY), 14-bit fixed point
+//   surf_integral_*         integral(CV_32S): row scans, then column scans
+//   surf_hessian_kernel     calcLayerDetAndTrace for every (octave, layer): box filters on the
+//                           integral image, det = dx dy - 0.81 dxy^2 (fp64 box accumulation)
+//   surf_extrema_kernel     findMaximaInLayer: 3x3x3 strict maxima above the threshold,
+//                           interpolateKeypoint (Cramer), appended per image
+//   surf_sort_kernel        KeypointGreater order by rank counting (deterministic)
+//   surf_describe_kernel    one wave per keypoint: orientation (Haar responses on the radius-6s
+//                           disc, fastAtan2, 72 sliding 60-degree windows), the rotated 20s window
+//                           (bilinear), INTER_AREA to 21 x 21, gradients, 4 x 4 x 4 sums, norm
+//   surf_compact_kernel     drop the keypoints marked for deletion, keep the order
+#include <hip/hip_runtime.h>
+
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "erp_surf.hpp"
+
+namespace erp {
+
+namespace {
+
+__device__ __forceinline__ int cv_roundf(float v) { return (int)__builtin_rintf(v); }
+__device__ __forceinline__ int cv_roundd(double v) { return (int)__builtin_rint(v); }
+
+__global__ __launch_bounds__(256) void surf_gray_kernel(const uint8_t* __restrict__ src, int ch,
+                                                        size_t npix, uint8_t* __restrict__ gray) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < npix; i += (size_t)gridDim.x * 256) {
+        if (ch == 3) {
+            const uint32_t b = src[3 * i], g = src[3 * i + 1], r = src[3 * i + 2];
+            gray[i] = (uint8_t)((b * 1868u + g * 9617u + r * 4899u + (1u << 13)) >> 14);
+        } else {
+            gray[i] = src[i];
+        }
+    }
+}
+
+// row prefix sums: sum[img][y+1][x+1] = sum over x' <= x of gray[y][x'] (row 0 / column 0 = 0)
+__global__ __launch_bounds__(256) void surf_integral_rows_kernel(const uint8_t* __restrict__ gray,
+                                                                 int W, int H,
+                                                                 int32_t* __restrict__ sum) {
+    __shared__ int32_t ws[4];
+    const int y = blockIdx.x, img = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+    const uint8_t* g = gray + ((size_t)img * H + y) * W;
+    int32_t* out = sum + ((size_t)img * (H + 1) + y + 1) * (W + 1);
+    if (tid == 0) out[0] = 0;
+    int32_t carry = 0;
+    for (int x0 = 0; x0 < W; x0 += 256) {
+        const int x = x0 + tid;
+        int32_t v = x < W ? (int32_t)g[x] : 0;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t t = __shfl_up(v, o, 64);
+            if (lane >= o) v += t;
+        }
+        if (lane == 63) ws[tid >> 6] = v;
+        __syncthreads();
+        int32_t pre = carry;
+        for (int w = 0; w < (tid >> 6); w++) pre += ws[w];
+        if (x < W) out[x + 1] = pre + v;
+        carry += ws[0] + ws[1] + ws[2] + ws[3];
+        __syncthreads();
+    }
+}
+
+// column prefix sums over the row sums (one thread per column, rows in order); row 0 = 0
+__global__ __launch_bounds__(256) void surf_integral_cols_kernel(int W, int H,
+                                                                 int32_t* __restrict__ sum) {
+    const int x = blockIdx.x * 256 + threadIdx.x, img = blockIdx.y;
+    if (x > W) return;
+    int32_t* s = sum + (size_t)img * (H + 1) * (W + 1) + x;
+    s[0] = 0;
+    int32_t acc = 0;
+    for (int y = 1; y <= H; y++) {
+        acc += s[(size_t)y * (W + 1)];
+        s[(size_t)y * (W + 1)] = acc;
+    }
+}
+
+// calcHaarPattern: (int box sum) * float weight in float, accumulated in double
+__device__ __forceinline__ float haar(const int32_t* __restrict__ o, const SurfHF* f, int n) {
+    double d = 0;
+    for (int k = 0; k < n; k++) d += (float)(o[f[k].p0] + o[f[k].p3] - o[f[k].p1] - o[f[k].p2]) * f[k].w;
+    return (float)d;
+}
+
+__global__ __launch_bounds__(256) void surf_hessian_kernel(const int32_t* __restrict__ sum, int W,
+                                                           int H, const SurfLayer* __restrict__ layers,
+                                                           size_t det_per_img,
+                                                           float* __restrict__ det) {
+    const SurfLayer L = layers[blockIdx.y];
+    const int img = blockIdx.z;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (L.samples_i <= 0 || idx >= L.samples_i * L.samples_j) return;
+    const int i = idx / L.samples_j, j = idx % L.samples_j;
+    const int32_t* o = sum + (size_t)img * (H + 1) * (W + 1) + (size_t)i * L.step * (W + 1) +
+                       (size_t)j * L.step;
+    const float dx = haar(o, L.dx, 3);
+    const float dy = haar(o, L.dy, 3);
+    const float dxy = haar(o, L.dxy, 4);
+    det[(size_t)img * det_per_img + L.off + (size_t)(i + L.margin) * L.cols + j + L.margin] =
+        dx * dy - 0.81f * dxy * dxy;
+}
+
+// interpolateKeypoint (restated in oracle/erp_surf.c)
+__device__ bool surf_interpolate(const float (&N9)[3][9], int dx, int dy, int ds, erp_keypoint& kp) {
+    const float b0 = -(N9[1][5] - N9[1][3]) / 2, b1 = -(N9[1][7] - N9[1][1]) / 2,
+                b2 = -(N9[2][4] - N9[0][4]) / 2;
+    const float a00 = N9[1][3] - 2 * N9[1][4] + N9[1][5];
+    const float a01 = (N9[1][8] - N9[1][6] - N9[1][2] + N9[1][0]) / 4;
+    const float a02 = (N9[2][5] - N9[2][3] - N9[0][5] + N9[0][3]) / 4;
+    const float a11 = N9[1][1] - 2 * N9[1][4] + N9[1][7];
+    const float a12 = (N9[2][7] - N9[2][1] - N9[0][7] + N9[0][1]) / 4;
+    const float a22 = N9[0][4] - 2 * N9[1][4] + N9[2][4];
+    const float a10 = a01, a20 = a02, a21 = a12;
+    const double dd = (double)a00 * ((double)a11 * a22 - (double)a12 * a21) -
+                      (double)a01 * ((double)a10 * a22 - (double)a12 * a20) +
+                      (double)a02 * ((double)a10 * a21 - (double)a11 * a20);
+    float d = (float)dd;
+    if (d == 0) return false;
+    d = 1 / d;
+    const float x0 = d * (b0 * (a11 * a22 - a12 * a21) - a01 * (b1 * a22 - a12 * b2) +
+                          a02 * (b1 * a21 - a11 * b2));
+    const float x1 = d * (a00 * (b1 * a22 - a12 * b2) - b0 * (a10 * a22 - a12 * a20) +
+                          a02 * (a10 * b2 - b1 * a20));
+    const float x2 = d * (a00 * (a11 * b2 - b1 * a21) - a01 * (a10 * b2 - b1 * a20) +
+                          b0 * (a10 * a21 - a11 * a20));
+    if (!((x0 != 0 || x1 != 0 || x2 != 0) && fabsf(x0) <= 1 && fabsf(x1) <= 1 && fabsf(x2) <= 1))
+        return false;
+    kp.x += x0 * dx;
+    kp.y += x1 * dy;
+    kp.size = (float)cv_roundf(kp.size + x2 * ds);
+    return true;
+}
+
+// findMaximaInLayer over every middle layer (blockIdx.y indexes the middle layers)
+__global__ __launch_bounds__(256) void surf_extrema_kernel(
+    const int32_t* __restrict__ sum, int W, int H, const SurfLayer* __restrict__ layers,
+    const int* __restrict__ mid, size_t det_per_img, const float* __restrict__ det, float thr,
+    int max_kp, erp_keypoint* __restrict__ raw, int32_t* __restrict__ counts) {
+    const int li = mid[blockIdx.y], img = blockIdx.z;
+    const SurfLayer L = layers[li];
+    const SurfLayer& Lu = layers[li + 1];
+    const int size = L.size, step = L.step, lr = L.rows, lc = L.cols;
+    const int margin = (Lu.size / 2) / step + 1;
+    if (Lu.size > H || Lu.size > W) return;
+    const int nr = lr - 2 * margin, ncol = lc - 2 * margin;
+    if (nr <= 0 || ncol <= 0) return;
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= nr * ncol) return;
+    const int i = margin + idx / ncol, j = margin + idx % ncol;
+    const float* base = det + (size_t)img * det_per_img;
+    const size_t c = (size_t)i * lc + j;
+    const float v = base[L.off + c];
+    if (!(v > thr)) return;
+    float N9[3][9];
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int u = 0; u < 9; u++)
+            N9[a][u] = base[layers[li - 1 + a].off + c + (size_t)((u / 3 - 1) * lc) + (u % 3 - 1)];
+    bool ok = true;
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int u = 0; u < 9; u++)
+            if (!(a == 1 && u == 4)) ok = ok && (v > N9[a][u]);
+    if (!ok) return;
+    const int sum_i = step * (i - (size / 2) / step);
+    const int sum_j = step * (j - (size / 2) / step);
+    erp_keypoint kp;
+    kp.x = sum_j + (size - 1) * 0.5f;
+    kp.y = sum_i + (size - 1) * 0.5f;
+    kp.size = (float)size;
+    kp.angle = -1;
+    kp.response = v;
+    kp.octave = L.octave;
+    {  // trace = dx + dy at the maximum (the layer's sign; recomputed, not stored)
+        const int32_t* o = sum + (size_t)img * (H + 1) * (W + 1) + (size_t)(i - L.margin) * step * (W + 1) +
+                           (size_t)(j - L.margin) * step;
+        const float tr = haar(o, L.dx, 3) + haar(o, L.dy, 3);
+        kp.class_id = (tr > 0) - (tr < 0);
+    }
+    if (!surf_interpolate(N9, step, step, size - layers[li - 1].size, kp)) return;
+    const int slot = atomicAdd(&counts[img], 1);
+    if (slot < max_kp) raw[(size_t)img * max_kp + slot] = kp;
+}
+
+__device__ __forceinline__ bool kp_greater(const erp_keypoint& a, const erp_keypoint& b) {
+    if (a.response > b.response) return true;
+    if (a.response < b.response) return false;
+    if (a.size > b.size) return true;
+    if (a.size < b.size) return false;
+    if (a.octave > b.octave) return true;
+    if (a.octave < b.octave) return false;
+    if (a.y < b.y) return false;
+    if (a.y > b.y) return true;
+    return a.x < b.x;
+}
+
+// rank = #keypoints greater + #equal keys earlier in the raw list (those are identical
+// keypoints: their relative order changes nothing)
+__global__ __launch_bounds__(256) void surf_sort_kernel(const erp_keypoint* __restrict__ raw,
+                                                        const int32_t* __restrict__ counts,
+                                                        int max_kp, erp_keypoint* __restrict__ out) {
+    __shared__ erp_keypoint tile[256];
+    const int img = blockIdx.y, k = blockIdx.x * 256 + threadIdx.x;
+    const int n = min(counts[img], max_kp);
+    if (blockIdx.x * 256 >= n) return;
+    const erp_keypoint* R = raw + (size_t)img * max_kp;
+    erp_keypoint me{};
+    if (k < n) me = R[k];
+    int rank = 0;
+    for (int t0 = 0; t0 < n; t0 += 256) {
+        __syncthreads();
+        if (t0 + threadIdx.x < n) tile[threadIdx.x] = R[t0 + threadIdx.x];
+        __syncthreads();
+        const int m = min(256, n - t0);
+        for (int u = 0; u < m; u++) {
+            const erp_keypoint& o = tile[u];
+            rank += kp_greater(o, me) || (!kp_greater(me, o) && t0 + u < k);
+        }
+    }
+    if (k < n) out[(size_t)img * max_kp + rank] = me;
+}
+
+// ---- descriptor ---------------------------------------------------------------------------
+constexpr int kPatch = 20, kNOri = kSurfNOri;  // lattice points of the radius-6 disc
+constexpr int kWinLds = 160;                              // windows up to 160^2 bytes in LDS
+
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float s = (float)(180 / M_PI);
+    const float p1 = 0.9997878412794807f * s, p3 = -0.3258083974640975f * s;
+    const float p5 = 0.1555786518463281f * s, p7 = -0.04432655554792128f * s;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + (float)DBL_EPSILON);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+__device__ __forceinline__ void resize_haar4(const int (&src)[2][5], SurfHF* dst, int newSize,
+                                             int widthStep) {
+    const float ratio = (float)newSize / 4;
+    for (int k = 0; k < 2; k++) {
+        const int dx1 = cv_roundf(ratio * src[k][0]), dy1 = cv_roundf(ratio * src[k][1]);
+        const int dx2 = cv_roundf(ratio * src[k][2]), dy2 = cv_roundf(ratio * src[k][3]);
+        dst[k].p0 = dy1 * widthStep + dx1;
+        dst[k].p1 = dy2 * widthStep + dx1;
+        dst[k].p2 = dy1 * widthStep + dx2;
+        dst[k].p3 = dy2 * widthStep + dx2;
+        dst[k].w = src[k][4] / ((float)(dx2 - dx1) * (dy2 - dy1));
+    }
+}
+
+// one area-resize table entry range for output index d (computeResizeAreaTab): up to two
+// fractional ends and the whole cells between
+struct AreaSpan {
+    int first, last;        // whole cells [first, last)
+    int lo_i, hi_i;         // fractional cells (-1: none)
+    float lo_a, hi_a, mid_a;
+};
+__device__ __forceinline__ AreaSpan area_span(int d, double scale, int ss) {
+    const double f1 = d * scale, f2 = f1 + scale;
+    const double cw = fmin(scale, ss - f1);
+    int s1 = (int)ceil(f1), s2 = (int)floor(f2);
+    s2 = min(s2, ss - 1);
+    s1 = min(s1, s2);
+    AreaSpan a;
+    a.lo_i = (s1 - f1 > 1e-3) ? s1 - 1 : -1;
+    a.lo_a = (float)((s1 - f1) / cw);
+    a.first = s1;
+    a.last = s2;
+    a.mid_a = (float)(1.0 / cw);
+    a.hi_i = (f2 - s2 > 1e-3) ? s2 : -1;
+    a.hi_a = (float)(fmin(fmin(f2 - s2, 1.), cw) / cw);
+    return a;
+}
+
+// one wave (64 threads) per keypoint: orientation + descriptor, grid-stride over the keypoints
+// of all images; windows larger than kWinLds^2 use the block's global scratch slot
+__global__ __launch_bounds__(64) void surf_describe_kernel(
+    const uint8_t* __restrict__ gray, const int32_t* __restrict__ sum, int W, int H,
+    int n_images, int max_kp, const int32_t* __restrict__ counts, erp_keypoint* __restrict__ kps,
+    float* __restrict__ desc, SurfConsts K, uint8_t* __restrict__ big, size_t big_slot) {
+    __shared__ float sX[kNOri], sY[kNOri], sA[kNOri];
+    __shared__ float sBest[2];
+    __shared__ float sMod[72], sSx[72], sSy[72];
+    __shared__ uint8_t swin[kWinLds * kWinLds];
+    __shared__ uint8_t patch[kPatch + 1][kPatch + 1];
+    __shared__ float DX[kPatch][kPatch], DY[kPatch][kPatch];
+    __shared__ float vecs[64];
+    const int lane = threadIdx.x;
+    const int ws = W + 1;
+    for (int g = blockIdx.x; g < n_images * max_kp; g += gridDim.x) {
+        const int img = g / max_kp, k = g % max_kp;
+        const int n = min(counts[img], max_kp);
+        if (k >= n) continue;  // uniform over the block
+        erp_keypoint kp = kps[(size_t)img * max_kp + k];
+        const uint8_t* I = gray + (size_t)img * W * H;
+        const int32_t* S = sum + (size_t)img * (H + 1) * ws;
+        const float s = kp.size * 1.2f / 9.0f;
+        const int grad = 2 * cv_roundf(2 * s);
+        if (H + 1 < grad || W + 1 < grad) {
+            if (lane == 0) kps[(size_t)img * max_kp + k].size = -1;
+            continue;
+        }
+        const int dx_s[2][5] = {{0, 0, 2, 4, -1}, {2, 0, 4, 4, 1}};
+        const int dy_s[2][5] = {{0, 0, 4, 2, 1}, {0, 2, 4, 4, -1}};
+        SurfHF dxt[2], dyt[2];
+        resize_haar4(dx_s, dxt, grad, ws);
+        resize_haar4(dy_s, dyt, grad, ws);
+        // orientation samples in disc order, compacted (order kept) into sX / sY
+        int nangle = 0;
+        for (int k0 = 0; k0 < kNOri; k0 += 64) {
+            const int kk = k0 + lane;
+            bool valid = false;
+            float vx = 0, vy = 0;
+            if (kk < kNOri) {
+                const int x = cv_roundf(kp.x + K.aptx[kk] * s - (float)(grad - 1) / 2);
+                const int y = cv_roundf(kp.y + K.apty[kk] * s - (float)(grad - 1) / 2);
+                valid = !(y < 0 || y >= H + 1 - grad || x < 0 || x >= W + 1 - grad);
+                if (valid) {
+                    const int32_t* ptr = S + (size_t)y * ws + x;
+                    vx = haar(ptr, dxt, 2) * K.aptw[kk];
+                    vy = haar(ptr, dyt, 2) * K.aptw[kk];
+                }
+            }
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(valid);
+            if (valid) {
+                const int pos = nangle + __builtin_popcountll(bal & ((1ull << lane) - 1ull));
+                sX[pos] = vx;
+                sY[pos] = vy;
+                sA[pos] = fast_atan2(vy, vx);
+            }
+            nangle += __builtin_popcountll(bal);
+        }
+        if (nangle == 0) {
+            if (lane == 0) kps[(size_t)img * max_kp + k].size = -1;
+            continue;
+        }
+        __syncthreads();
+        // 72 windows of 60 degrees, 5 apart; each summed sequentially over the samples
+        for (int w = lane; w < 72; w += 64) {
+            const int i = 5 * w;
+            float sx = 0, sy = 0;
+            for (int j = 0; j < nangle; j++) {
+                const int d = abs(cv_roundf(sA[j]) - i);
+                if (d < 30 || d > 330) {
+                    sx += sX[j];
+                    sy += sY[j];
+                }
+            }
+            sMod[w] = sx * sx + sy * sy;
+            sSx[w] = sx;
+            sSy[w] = sy;
+        }
+        __syncthreads();
+        if (lane == 0) {  // the first window with a strictly larger modulus wins
+            float best = 0, bx = 0, by = 0;
+            for (int w = 0; w < 72; w++)
+                if (sMod[w] > best) {
+                    best = sMod[w];
+                    bx = sSx[w];
+                    by = sSy[w];
+                }
+            sBest[0] = bx;
+            sBest[1] = by;
+        }
+        __syncthreads();
+        const float dir_deg = fast_atan2(-sBest[1], sBest[0]);
+        if (lane == 0) kps[(size_t)img * max_kp + k].angle = dir_deg;
+        // the rotated window (bilinear), row i by lane i (its own sequential column recurrence)
+        const int win = (int)((kPatch + 1) * s);
+        uint8_t* wbuf = win <= kWinLds ? swin : big + (size_t)blockIdx.x * big_slot;
+        const float dir = dir_deg * (float)(M_PI / 180);
+        const float sin_dir = -(float)sin((double)dir), cos_dir = (float)cos((double)dir);
+        const float woff = -(float)(win - 1) / 2;
+        const float sx0 = kp.x + woff * cos_dir + woff * sin_dir;
+        const float sy0 = kp.y - woff * sin_dir + woff * cos_dir;
+        const int nc1 = W - 1, nr1 = H - 1;
+        {
+            float stx = sx0, sty = sy0;
+            for (int i = 0; i < win; i++, stx += sin_dir, sty += cos_dir) {
+                if ((i & 63) != lane) continue;
+                double px = stx, py = sty;
+                for (int j = 0; j < win; j++, px += cos_dir, py -= sin_dir) {
+                    const int ix = (int)floor(px), iy = (int)floor(py);
+                    uint8_t v;
+                    if ((unsigned)ix < (unsigned)nc1 && (unsigned)iy < (unsigned)nr1) {
+                        const float a = (float)(px - ix), b = (float)(py - iy);
+                        const uint8_t* p = I + (size_t)iy * W + ix;
+                        v = (uint8_t)cv_roundf(p[0] * (1.f - a) * (1.f - b) + p[1] * a * (1.f - b) +
+                                               p[W] * (1.f - a) * b + p[W + 1] * a * b);
+                    } else {
+                        int x = cv_roundd(px), y = cv_roundd(py);
+                        x = x < 0 ? 0 : x > nc1 ? nc1 : x;
+                        y = y < 0 ? 0 : y > nr1 ? nr1 : y;
+                        v = I[(size_t)y * W + x];
+                    }
+                    wbuf[(size_t)i * win + j] = v;
+                }
+            }
+        }
+        __threadfence_block();
+        __syncthreads();
+        // INTER_AREA to 21 x 21: lane dx < 21 owns output column dx
+        const double scale = (double)win / (kPatch + 1);
+        const int iscale = (int)(scale + 0.5);
+        if (lane < kPatch + 1) {
+            const int dx = lane;
+            if (fabs(scale - iscale) < DBL_EPSILON && iscale >= 1) {
+                const int area = iscale * iscale;
+                for (int dy = 0; dy < kPatch + 1; dy++) {
+                    int sacc = 0;
+                    for (int a = 0; a < iscale; a++)
+                        for (int b = 0; b < iscale; b++)
+                            sacc += wbuf[(size_t)(dy * iscale + a) * win + dx * iscale + b];
+                    patch[dy][dx] = (uint8_t)((sacc + area / 2) / area);
+                }
+            } else {
+                const AreaSpan xs = area_span(dx, scale, win);
+                auto rowbuf = [&](int sy) {
+                    const uint8_t* Sr = wbuf + (size_t)sy * win;
+                    float b = 0;
+                    if (xs.lo_i >= 0) b += Sr[xs.lo_i] * xs.lo_a;
+                    for (int sx = xs.first; sx < xs.last; sx++) b += Sr[sx] * xs.mid_a;
+                    if (xs.hi_i >= 0) b += Sr[xs.hi_i] * xs.hi_a;
+                    return b;
+                };
+                for (int dy = 0; dy < kPatch + 1; dy++) {
+                    const AreaSpan ys = area_span(dy, scale, win);
+                    float acc = 0;
+                    if (ys.lo_i >= 0) acc += ys.lo_a * rowbuf(ys.lo_i);
+                    for (int sy = ys.first; sy < ys.last; sy++) acc += ys.mid_a * rowbuf(sy);
+                    if (ys.hi_i >= 0) acc += ys.hi_a * rowbuf(ys.hi_i);
+                    const int v = cv_roundf(acc);
+                    patch[dy][dx] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
+                }
+            }
+        }
+        __syncthreads();
+        for (int c = lane; c < kPatch * kPatch; c += 64) {
+            const int i = c / kPatch, j = c % kPatch;
+            const float dw = K.gdesc[i] * K.gdesc[j];
+            DX[i][j] = (patch[i][j + 1] - patch[i][j] + patch[i + 1][j + 1] - patch[i + 1][j]) * dw;
+            DY[i][j] = (patch[i + 1][j] - patch[i][j] + patch[i + 1][j + 1] - patch[i][j + 1]) * dw;
+        }
+        __syncthreads();
+        if (lane < 16) {
+            const int i = lane >> 2, j = lane & 3;
+            float v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+            for (int y = i * 5; y < i * 5 + 5; y++)
+                for (int x = j * 5; x < j * 5 + 5; x++) {
+                    const float tx = DX[y][x], ty = DY[y][x];
+                    v0 += tx;
+                    v1 += ty;
+                    v2 += fabsf(tx);
+                    v3 += fabsf(ty);
+                }
+            vecs[4 * lane] = v0;
+            vecs[4 * lane + 1] = v1;
+            vecs[4 * lane + 2] = v2;
+            vecs[4 * lane + 3] = v3;
+        }
+        __syncthreads();
+        if (lane == 0) {
+            double sq = 0;
+            for (int q = 0; q < 64; q++) sq += vecs[q] * vecs[q];
+            sBest[0] = (float)(1. / (sqrt(sq) + FLT_EPSILON));
+        }
+        __syncthreads();
+        desc[((size_t)img * max_kp + k) * 64 + lane] = vecs[lane] * sBest[0];
+        __syncthreads();
+    }
+}
+
+// remove the keypoints marked for deletion (size <= 0), order kept; counts -> final counts
+// (or -needed when the raw list overflowed max_kp)
+__global__ __launch_bounds__(1024) void surf_compact_kernel(const erp_keypoint* __restrict__ kin,
+                                                            const float* __restrict__ din,
+                                                            int max_kp, int32_t* __restrict__ counts,
+                                                            erp_keypoint* __restrict__ kout,
+                                                            float* __restrict__ dout) {
+    __shared__ int ws[16];
+    const int img = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nraw = counts[img];
+    if (nraw > max_kp) {
+        __syncthreads();
+        if (tid == 0) counts[img] = -nraw;
+        return;
+    }
+    int base = 0;
+    for (int k0 = 0; k0 < nraw; k0 += 1024) {
+        const int k = k0 + tid;
+        const bool keep = k < nraw && kin[(size_t)img * max_kp + k].size > 0;
+        int x = keep;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws[wid] = x;
+        __syncthreads();
+        int pre = base, tot = 0;
+        for (int w = 0; w < 16; w++) {
+            if (w < wid) pre += ws[w];
+            tot += ws[w];
+        }
+        if (keep) {
+            const int pos = pre + x - 1;
+            kout[(size_t)img * max_kp + pos] = kin[(size_t)img * max_kp + k];
+            for (int q = 0; q < 64; q++)
+                dout[((size_t)img * max_kp + pos) * 64 + q] = din[((size_t)img * max_kp + k) * 64 + q];
+        }
+        base += tot;
+        __syncthreads();
+    }
+    if (tid == 0) counts[img] = base;
+}
+
+}  // namespace
+
+hipError_t launch_surf(const uint8_t* images, int n_images, int W, int H, int channels,
+                       const SurfPlan& plan, const SurfScratch& scr, int max_kp,
+                       erp_keypoint* kp_out, float* desc_out, int32_t* counts, hipStream_t st) {
+    const size_t npix = (size_t)n_images * W * H;
+    const uint8_t* gray = images;
+    if (channels == 3) {
+        hipLaunchKernelGGL(surf_gray_kernel, dim3(2048), dim3(256), 0, st, images, 3, npix, scr.gray);
+        gray = scr.gray;
+    }
+    hipLaunchKernelGGL(surf_integral_rows_kernel, dim3(H, n_images), dim3(256), 0, st, gray, W, H, scr.sum);
+    hipLaunchKernelGGL(surf_integral_cols_kernel, dim3((W + 1 + 255) / 256, n_images), dim3(256), 0, st,
+                       W, H, scr.sum);
+    hipError_t e = hipMemsetAsync(scr.det, 0, plan.det_per_img * n_images * sizeof(float), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(surf_hessian_kernel, dim3((plan.max_samples + 255) / 256, plan.n_layers, n_images),
+                       dim3(256), 0, st, scr.sum, W, H, plan.d_layers, plan.det_per_img, scr.det);
+    e = hipMemsetAsync(counts, 0, sizeof(int32_t) * n_images, st);
+    if (e != hipSuccess) return e;
+    if (plan.n_mid > 0)
+        hipLaunchKernelGGL(surf_extrema_kernel, dim3((plan.max_mid_cells + 255) / 256, plan.n_mid, n_images),
+                           dim3(256), 0, st, scr.sum, W, H, plan.d_layers, plan.d_mid, plan.det_per_img,
+                           scr.det, plan.threshold, max_kp, scr.raw, counts);
+    hipLaunchKernelGGL(surf_sort_kernel, dim3((max_kp + 255) / 256, n_images), dim3(256), 0, st, scr.raw,
+                       counts, max_kp, scr.sorted);
+    hipLaunchKernelGGL(surf_describe_kernel, dim3(kSurfDescBlocks), dim3(64), 0, st,
+                       channels == 3 ? (const uint8_t*)scr.gray : images, scr.sum, W, H, n_images,
+                       max_kp, counts, scr.sorted, scr.desc, plan.consts, scr.big, scr.big_slot);
+    hipLaunchKernelGGL(surf_compact_kernel, dim3(n_images), dim3(1024), 0, st, scr.sorted, scr.desc,
+                       max_kp, counts, kp_out, desc_out);
+    return hipGetLastError();
+}
+
+}  // namespace erp

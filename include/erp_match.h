@@ -296,6 +296,31 @@ erp_status erp_rectify_dev(erp_ctx* ctx, const uint8_t* d_left, const uint8_t* d
    .inv(), then cv::rotate(ROTATE_90_CLOCKWISE), fused -> d_out W x H x 3 (W rows). */
 erp_status erp_vertical_rotate_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W, int32_t H,
                                    uint8_t* d_out, void* stream);
+/* ---- SURF: feature_matcher::detect_key_point + comput_descriptor
+   (src/feature_matcher.cpp:26-40) with xfeatures2d::SURF::create() defaults ---- */
+typedef struct erp_keypoint {   /* cv::KeyPoint layout */
+    float x, y;                 /* pt */
+    float size, angle, response;
+    int32_t octave, class_id;
+} erp_keypoint;
+typedef struct erp_surf_params {
+    double hessian_threshold;   /* 100 */
+    int32_t n_octaves;          /* 4 */
+    int32_t n_octave_layers;    /* 3 */
+    int32_t extended;           /* 0 (64-D; 1 is not supported) */
+    int32_t upright;            /* 0 (1 is not supported) */
+} erp_surf_params;
+void erp_surf_params_default(erp_surf_params* p);
+/* n_images images of H x W (channels 1 = gray, 3 = BGR), contiguous, device pointers ->
+   per image up to max_kp keypoints [n][max_kp] in OpenCV's KeypointGreater order (descending
+   response) and their unit 64-D descriptors [n][max_kp][64]; d_count[n] = keypoints found, or
+   -(needed) when max_kp was too small (rerun larger).  Asynchronous on `stream`. */
+erp_status erp_surf_detect_compute_dev(erp_ctx* ctx, const uint8_t* d_images, int32_t n_images,
+                                       int32_t W, int32_t H, int32_t channels,
+                                       const erp_surf_params* params, int32_t max_kp,
+                                       erp_keypoint* d_kp, float* d_desc, int32_t* d_count,
+                                       void* stream);
+
 /* host 3x3 geometry (row-major doubles) */
 void erp_eular2rot(const double theta[3], double R[9]);         /* erp_rotation.cpp:14-40 */
 void erp_rot2eular(const double R[9], double e[3]);             /* erp_rotation.cpp:43-63 */
