@@ -263,9 +263,9 @@ class erp_rotation:  # noqa: N801  (reference class name)
 
 
 class spherical_surf:  # noqa: N801  (reference class name)
-    """spherical_surf (src/spherical_surf.hpp:11-29), the remap half: the four de-distorted bands
-    of an ERP image and the keypoint un-rotation back to ERP pixels.  (SURF detection itself is
-    out of scope: descriptors + band keypoints come from the caller.)"""
+    """spherical_surf (src/spherical_surf.hpp:11-29): the four de-distorted bands of an ERP
+    image, SURF on every band, the keypoint un-rotation back to ERP pixels, the band
+    concatenation, the match and the gather of the matched keypoints (do_all)."""
 
     PITCH = (45.0, 0.0, -45.0, -90.0)  # bands n0..n3 (src/spherical_surf.cpp:77-83)
 
@@ -307,6 +307,33 @@ class spherical_surf:  # noqa: N801  (reference class name)
                                               torch.cuda.current_stream().cuda_stream),
               "rotate_keypoint")
         return key
+
+    def do_all(self, im_left, im_right, max_kp: int = 16384, fill: int = 0):
+        """spherical_surf::do_all (src/spherical_surf.cpp:65-180) on two CUDA uint8 BGR ERP
+        images [H, W, 3]: bands (:77-93) -> SURF on the 8 bands (:96-118) -> keypoint
+        un-rotation + concatenation n0..n3 (:120-150) -> match_two_image (:153) -> gather
+        (:155-162).  Returns (left_key [M, 2], right_key [M, 2]) CUDA float32 tensors of the
+        matched ERP pixels, match_size and total_key_num (the left keypoints, :179)."""
+        import torch
+        H, W = im_left.shape[:2]
+        ims = torch.stack([_img_dev(im_left), _img_dev(im_right)]).contiguous()
+        bands = self.bands(ims, fill=fill)                      # [2, 4, H/4, W, 3]
+        fm = feature_matcher(ctx=self.ctx)
+        kps, descs = fm.surf(bands.reshape(8, H // 4, W, 3), max_kp=max_kp)
+        dev = ims.device
+        keys, dcat = [], []
+        for side in range(2):
+            k4 = kps[4 * side: 4 * side + 4]
+            pts = np.concatenate([np.stack([k["x"], k["y"]], 1) for k in k4]).astype(np.float32)
+            key = torch.from_numpy(pts.reshape(-1, 2)).to(dev)
+            if key.shape[0]:
+                self.unrotate_band_keypoints(key, [len(k) for k in k4], W, H)
+            keys.append(key)
+            dcat.append(torch.from_numpy(np.concatenate(descs[4 * side: 4 * side + 4])
+                                         .reshape(-1, 64)).to(dev))
+        m = fm._match_device(dcat[0], dcat[1], 0.3)            # [M, 4] int32 DMatch rows
+        q, t = m[:, 0].long(), m[:, 1].long()
+        return keys[0][q], keys[1][t], int(m.shape[0]), int(keys[0].shape[0])
 
     def unrotate_band_keypoints(self, key, counts, width: int, height: int):
         """do_all's keypoint step (src/spherical_surf.cpp:120-144), in place on the band
