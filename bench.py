@@ -56,13 +56,15 @@ def parse():
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
     ap.add_argument("--no-shard-consensus", action="store_true",
                     help="manual workload: replicate the consensus on every rank")
-    ap.add_argument("--workload", choices=["pairs", "dense", "manual", "remap"], default="pairs",
+    ap.add_argument("--workload", choices=["pairs", "dense", "manual", "remap", "e2e"],
+                    default="pairs",
                     help="pairs: configs[1] (the metric; configs[2] with --kpts 2048); dense: "
                          "configs[3], one N x N match (--kpts, default 16384) on both matcher "
                          "methods; manual: configs[4], one find() of --iters (default 100k) on "
                          "100 manual-pickup correspondences (60%% outliers), hypothesis blocks "
                          "sharded over the ranks; remap: section 8f, the spherical band remap "
-                         "and rectification of 5376 x 2688 ERP images")
+                         "and rectification of 5376 x 2688 ERP images; e2e: the whole reference "
+                         "pipeline per pair from 5376 x 2688 images (do_all + find)")
     return ap.parse_args()
 
 
@@ -331,6 +333,74 @@ def run_remap(args):
     print(json.dumps(line))
 
 
+def run_e2e(args):
+    """automatic.cpp:117-126 per pair from the images: spherical_surf::do_all (4 bands per
+    image, SURF on the 8 bands, un-rotation, concat, match, gather) then eight_point::find with
+    --iters iterations, on synthetic 5376 x 2688 BGR ERP pairs (a blob texture rendered on the
+    sphere; the right image = rotate_image of the left by a known small rotation).  Stage
+    times from HIP events around each stage (torch's stream)."""
+    import torch
+    from erp_match_eightpoint_test_amd import (Context, eight_point, erp_rotation, feature_matcher,
+                                                spherical_surf, synth)
+    dev = torch.device("cuda:0")
+    H, W, B = 2688, 5376, 4
+    rng = np.random.default_rng(args.seed)
+    ctx = Context(0)
+    ss, er, fm = spherical_surf(ctx=ctx), erp_rotation(ctx=ctx), feature_matcher(ctx=ctx)
+    ep = eight_point(ctx=ctx, iters=args.iters)
+    lefts, rights = [], []
+    for b in range(B):
+        lo = synth.sphere_texture(args.seed + b, H // 4, W // 4)
+        t = torch.from_numpy(lo).to(dev).permute(2, 0, 1)[None].float()
+        up = torch.nn.functional.interpolate(t, size=(H, W), mode="bilinear", align_corners=False)
+        up = (up + torch.randn(up.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(b)) * 3)
+        left = up.clamp(0, 255).round().to(torch.uint8)[0].permute(1, 2, 0).contiguous()
+        R = er.eular2rot(np.radians(rng.uniform(0, 15, 3)))
+        lefts.append(left)
+        rights.append(er.rotate_image(left, er.inv(R)))
+    torch.cuda.synchronize()
+
+    def one(b):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record()
+        kl, kr, M, total = ss.do_all(lefts[b], rights[b])
+        ev[1].record()
+        R, T = ep.find(W, H, kl.cpu().numpy(), kr.cpu().numpy())
+        ev[2].record()
+        return ev, M, total
+
+    for b in range(min(args.warmup, B)):
+        one(b)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    recs = []
+    for s_ in range(args.steps):
+        recs.append(one(s_ % B))
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) / args.steps
+    do_ms = float(np.mean([e[0].elapsed_time(e[1]) for e, _, _ in recs]))
+    find_ms = float(np.mean([e[1].elapsed_time(e[2]) for e, _, _ in recs]))
+    # SURF alone on the 8 bands of one pair (device time)
+    bands = ss.bands(torch.stack([lefts[0], rights[0]])).reshape(8, H // 4, W, 3)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fm.surf(bands)
+    e0.record()
+    for _ in range(3):
+        fm.surf(bands)
+    e1.record()
+    torch.cuda.synchronize()
+    line = {"metric": "ERP image pairs/sec through the whole reference pipeline (do_all + find), "
+                      "5376x2688 images", "value": 1.0 / el, "unit": "pairs/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": el * 1e3,
+            "higher_is_better": True, "scaling": "none", "vs_baseline": None, "dtype": "u8+f32+f64",
+            "data": "synthetic ERP images (sphere blob texture, known rotation)",
+            "config": {"workload": "e2e, one pair per step", "iters": args.iters},
+            "stages_ms": {"do_all (bands + SURF x 8 + concat + match + gather)": do_ms,
+                          "find": find_ms, "surf_8_bands_device": e0.elapsed_time(e1) / 3},
+            "check": {"M": [int(r[1]) for r in recs], "total_key_num": [int(r[2]) for r in recs]}}
+    print(json.dumps(line))
+
+
 def main():
     args = parse()
     import torch
@@ -340,6 +410,8 @@ def main():
         return run_manual(args)
     if args.workload == "remap":
         return run_remap(args)
+    if args.workload == "e2e":
+        return run_e2e(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -50,7 +50,7 @@ struct SurfScratch {
     erp_keypoint* raw;      // [n][max_kp]
     erp_keypoint* sorted;   // [n][max_kp]
     float* desc;            // [n][max_kp][64]
-    uint8_t* big;           // [kSurfDescBlocks][big_slot]: windows too large for LDS
+    uint8_t* big;           // [kSurfDescBlocks][big_slot]: the horizontal area pass tmp[21][win]
     size_t big_slot;
 };
 

@@ -235,7 +235,6 @@ __global__ __launch_bounds__(256) void surf_sort_kernel(const erp_keypoint* __re
 
 // ---- descriptor ---------------------------------------------------------------------------
 constexpr int kPatch = 20, kNOri = kSurfNOri;  // lattice points of the radius-6 disc
-constexpr int kWinLds = 160;                              // windows up to 160^2 bytes in LDS
 
 __device__ __forceinline__ float fast_atan2(float y, float x) {
     const float s = (float)(180 / M_PI);
@@ -295,72 +294,93 @@ __device__ __forceinline__ AreaSpan area_span(int d, double scale, int ss) {
     return a;
 }
 
-// one wave (64 threads) per keypoint: orientation + descriptor, grid-stride over the keypoints
-// of all images; windows larger than kWinLds^2 use the block's global scratch slot
-__global__ __launch_bounds__(64) void surf_describe_kernel(
+// The rotated window's sample positions: the reference walks each row with
+// px += cos_dir, py -= sin_dir in DOUBLE from a float row start.  When the row starts and
+// |cos_dir|, |sin_dir| are 0 or >= 2^-16 and every |coordinate| stays below 2^14, every partial
+// sum start + j*c is a multiple of min(ulp(start), ulp(c)) >= 2^-39 below 2^14, i.e. exactly
+// representable: the walk never rounds and fma(j, c, start) gives the same double.  Keypoints
+// outside that range walk sequentially (rare).
+__device__ __forceinline__ bool exact_walk(float v) {
+    return v == 0.f || (fabsf(v) >= 0x1p-16f && fabsf(v) < 0x1p13f);
+}
+
+// one block (256 threads) per keypoint, grid-stride over the keypoints of all images:
+// orientation, the rotated window generated on the fly inside a separable INTER_AREA
+// (horizontal pass into the block's global scratch tmp[dx][sy], then vertical), gradients,
+// descriptor, norm
+constexpr int kDescThreads = 256;
+__global__ __launch_bounds__(kDescThreads) void surf_describe_kernel(
     const uint8_t* __restrict__ gray, const int32_t* __restrict__ sum, int W, int H,
     int n_images, int max_kp, const int32_t* __restrict__ counts, erp_keypoint* __restrict__ kps,
     float* __restrict__ desc, SurfConsts K, uint8_t* __restrict__ big, size_t big_slot) {
     __shared__ float sX[kNOri], sY[kNOri], sA[kNOri];
+    __shared__ int sN;
     __shared__ float sBest[2];
     __shared__ float sMod[72], sSx[72], sSy[72];
-    __shared__ uint8_t swin[kWinLds * kWinLds];
+    __shared__ float stx[kSurfBigWin], sty[kSurfBigWin];
+    __shared__ int sExact;
     __shared__ uint8_t patch[kPatch + 1][kPatch + 1];
     __shared__ float DX[kPatch][kPatch], DY[kPatch][kPatch];
     __shared__ float vecs[64];
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int ws = W + 1;
+    float* tmp = reinterpret_cast<float*>(big + (size_t)blockIdx.x * big_slot);
     for (int g = blockIdx.x; g < n_images * max_kp; g += gridDim.x) {
         const int img = g / max_kp, k = g % max_kp;
         const int n = min(counts[img], max_kp);
         if (k >= n) continue;  // uniform over the block
-        erp_keypoint kp = kps[(size_t)img * max_kp + k];
+        const erp_keypoint kp = kps[(size_t)img * max_kp + k];
         const uint8_t* I = gray + (size_t)img * W * H;
         const int32_t* S = sum + (size_t)img * (H + 1) * ws;
         const float s = kp.size * 1.2f / 9.0f;
         const int grad = 2 * cv_roundf(2 * s);
         if (H + 1 < grad || W + 1 < grad) {
-            if (lane == 0) kps[(size_t)img * max_kp + k].size = -1;
+            if (tid == 0) kps[(size_t)img * max_kp + k].size = -1;
             continue;
         }
-        const int dx_s[2][5] = {{0, 0, 2, 4, -1}, {2, 0, 4, 4, 1}};
-        const int dy_s[2][5] = {{0, 0, 4, 2, 1}, {0, 2, 4, 4, -1}};
-        SurfHF dxt[2], dyt[2];
-        resize_haar4(dx_s, dxt, grad, ws);
-        resize_haar4(dy_s, dyt, grad, ws);
-        // orientation samples in disc order, compacted (order kept) into sX / sY
-        int nangle = 0;
-        for (int k0 = 0; k0 < kNOri; k0 += 64) {
-            const int kk = k0 + lane;
-            bool valid = false;
-            float vx = 0, vy = 0;
-            if (kk < kNOri) {
-                const int x = cv_roundf(kp.x + K.aptx[kk] * s - (float)(grad - 1) / 2);
-                const int y = cv_roundf(kp.y + K.apty[kk] * s - (float)(grad - 1) / 2);
-                valid = !(y < 0 || y >= H + 1 - grad || x < 0 || x >= W + 1 - grad);
-                if (valid) {
-                    const int32_t* ptr = S + (size_t)y * ws + x;
-                    vx = haar(ptr, dxt, 2) * K.aptw[kk];
-                    vy = haar(ptr, dyt, 2) * K.aptw[kk];
+        // orientation samples in disc order, compacted (order kept) by wave 0
+        if (wid == 0) {
+            const int dx_s[2][5] = {{0, 0, 2, 4, -1}, {2, 0, 4, 4, 1}};
+            const int dy_s[2][5] = {{0, 0, 4, 2, 1}, {0, 2, 4, 4, -1}};
+            SurfHF dxt[2], dyt[2];
+            resize_haar4(dx_s, dxt, grad, ws);
+            resize_haar4(dy_s, dyt, grad, ws);
+            int nangle = 0;
+            for (int k0 = 0; k0 < kNOri; k0 += 64) {
+                const int kk = k0 + lane;
+                bool valid = false;
+                float vx = 0, vy = 0;
+                if (kk < kNOri) {
+                    const int x = cv_roundf(kp.x + K.aptx[kk] * s - (float)(grad - 1) / 2);
+                    const int y = cv_roundf(kp.y + K.apty[kk] * s - (float)(grad - 1) / 2);
+                    valid = !(y < 0 || y >= H + 1 - grad || x < 0 || x >= W + 1 - grad);
+                    if (valid) {
+                        const int32_t* ptr = S + (size_t)y * ws + x;
+                        vx = haar(ptr, dxt, 2) * K.aptw[kk];
+                        vy = haar(ptr, dyt, 2) * K.aptw[kk];
+                    }
                 }
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(valid);
+                if (valid) {
+                    const int pos = nangle + __builtin_popcountll(bal & ((1ull << lane) - 1ull));
+                    sX[pos] = vx;
+                    sY[pos] = vy;
+                    sA[pos] = fast_atan2(vy, vx);
+                }
+                nangle += __builtin_popcountll(bal);
             }
-            const uint64_t bal = __builtin_amdgcn_ballot_w64(valid);
-            if (valid) {
-                const int pos = nangle + __builtin_popcountll(bal & ((1ull << lane) - 1ull));
-                sX[pos] = vx;
-                sY[pos] = vy;
-                sA[pos] = fast_atan2(vy, vx);
-            }
-            nangle += __builtin_popcountll(bal);
-        }
-        if (nangle == 0) {
-            if (lane == 0) kps[(size_t)img * max_kp + k].size = -1;
-            continue;
+            if (lane == 0) sN = nangle;
         }
         __syncthreads();
+        const int nangle = sN;
+        if (nangle == 0) {
+            if (tid == 0) kps[(size_t)img * max_kp + k].size = -1;
+            __syncthreads();
+            continue;
+        }
         // 72 windows of 60 degrees, 5 apart; each summed sequentially over the samples
-        for (int w = lane; w < 72; w += 64) {
-            const int i = 5 * w;
+        if (tid < 72) {
+            const int i = 5 * tid;
             float sx = 0, sy = 0;
             for (int j = 0; j < nangle; j++) {
                 const int d = abs(cv_roundf(sA[j]) - i);
@@ -369,12 +389,13 @@ __global__ __launch_bounds__(64) void surf_describe_kernel(
                     sy += sY[j];
                 }
             }
-            sMod[w] = sx * sx + sy * sy;
-            sSx[w] = sx;
-            sSy[w] = sy;
+            sMod[tid] = sx * sx + sy * sy;
+            sSx[tid] = sx;
+            sSy[tid] = sy;
         }
         __syncthreads();
-        if (lane == 0) {  // the first window with a strictly larger modulus wins
+        const int win = (int)((kPatch + 1) * s);
+        if (tid == 0) {  // the first window with a strictly larger modulus wins
             float best = 0, bx = 0, by = 0;
             for (int w = 0; w < 72; w++)
                 if (sMod[w] > best) {
@@ -387,86 +408,99 @@ __global__ __launch_bounds__(64) void surf_describe_kernel(
         }
         __syncthreads();
         const float dir_deg = fast_atan2(-sBest[1], sBest[0]);
-        if (lane == 0) kps[(size_t)img * max_kp + k].angle = dir_deg;
-        // the rotated window (bilinear), row i by lane i (its own sequential column recurrence)
-        const int win = (int)((kPatch + 1) * s);
-        uint8_t* wbuf = win <= kWinLds ? swin : big + (size_t)blockIdx.x * big_slot;
         const float dir = dir_deg * (float)(M_PI / 180);
         const float sin_dir = -(float)sin((double)dir), cos_dir = (float)cos((double)dir);
-        const float woff = -(float)(win - 1) / 2;
-        const float sx0 = kp.x + woff * cos_dir + woff * sin_dir;
-        const float sy0 = kp.y - woff * sin_dir + woff * cos_dir;
+        if (tid == 0) {
+            kps[(size_t)img * max_kp + k].angle = dir_deg;
+            // row starts: the reference's float recurrence, sequentially
+            const float woff = -(float)(win - 1) / 2;
+            float a = kp.x + woff * cos_dir + woff * sin_dir;
+            float b = kp.y - woff * sin_dir + woff * cos_dir;
+            bool ex = exact_walk(cos_dir) && exact_walk(sin_dir) && win <= kSurfBigWin;
+            for (int i = 0; i < win; i++, a += sin_dir, b += cos_dir) {
+                stx[i] = a;
+                sty[i] = b;
+                ex = ex && exact_walk(a) && exact_walk(b) &&
+                     fabsf(a) + win * fabsf(cos_dir) < 0x1p13f &&
+                     fabsf(b) + win * fabsf(sin_dir) < 0x1p13f;
+            }
+            sExact = ex;
+        }
+        __syncthreads();
+        const bool exact = sExact != 0;
         const int nc1 = W - 1, nr1 = H - 1;
-        {
-            float stx = sx0, sty = sy0;
-            for (int i = 0; i < win; i++, stx += sin_dir, sty += cos_dir) {
-                if ((i & 63) != lane) continue;
-                double px = stx, py = sty;
-                for (int j = 0; j < win; j++, px += cos_dir, py -= sin_dir) {
-                    const int ix = (int)floor(px), iy = (int)floor(py);
-                    uint8_t v;
-                    if ((unsigned)ix < (unsigned)nc1 && (unsigned)iy < (unsigned)nr1) {
-                        const float a = (float)(px - ix), b = (float)(py - iy);
-                        const uint8_t* p = I + (size_t)iy * W + ix;
-                        v = (uint8_t)cv_roundf(p[0] * (1.f - a) * (1.f - b) + p[1] * a * (1.f - b) +
-                                               p[W] * (1.f - a) * b + p[W + 1] * a * b);
-                    } else {
-                        int x = cv_roundd(px), y = cv_roundd(py);
-                        x = x < 0 ? 0 : x > nc1 ? nc1 : x;
-                        y = y < 0 ? 0 : y > nr1 ? nr1 : y;
-                        v = I[(size_t)y * W + x];
-                    }
-                    wbuf[(size_t)i * win + j] = v;
+        auto pixel = [&](int i, int j) -> float {  // window pixel (row i, column j)
+            double px, py;
+            if (exact) {
+                px = __builtin_fma((double)j, (double)cos_dir, (double)stx[i]);
+                py = __builtin_fma(-(double)j, (double)sin_dir, (double)sty[i]);
+            } else {
+                px = stx[i];
+                py = sty[i];
+                for (int q = 0; q < j; q++) {
+                    px += cos_dir;
+                    py -= sin_dir;
                 }
             }
-        }
-        __threadfence_block();
-        __syncthreads();
-        // INTER_AREA to 21 x 21: lane dx < 21 owns output column dx
+            const int ix = (int)floor(px), iy = (int)floor(py);
+            if ((unsigned)ix < (unsigned)nc1 && (unsigned)iy < (unsigned)nr1) {
+                const float a = (float)(px - ix), b = (float)(py - iy);
+                const uint8_t* p = I + (size_t)iy * W + ix;
+                return (float)(uint8_t)cv_roundf(p[0] * (1.f - a) * (1.f - b) + p[1] * a * (1.f - b) +
+                                                 p[W] * (1.f - a) * b + p[W + 1] * a * b);
+            }
+            int x = cv_roundd(px), y = cv_roundd(py);
+            x = x < 0 ? 0 : x > nc1 ? nc1 : x;
+            y = y < 0 ? 0 : y > nr1 ? nr1 : y;
+            return (float)I[(size_t)y * W + x];
+        };
+        // INTER_AREA to 21 x 21
         const double scale = (double)win / (kPatch + 1);
         const int iscale = (int)(scale + 0.5);
-        if (lane < kPatch + 1) {
-            const int dx = lane;
-            if (fabs(scale - iscale) < DBL_EPSILON && iscale >= 1) {
-                const int area = iscale * iscale;
-                for (int dy = 0; dy < kPatch + 1; dy++) {
-                    int sacc = 0;
-                    for (int a = 0; a < iscale; a++)
-                        for (int b = 0; b < iscale; b++)
-                            sacc += wbuf[(size_t)(dy * iscale + a) * win + dx * iscale + b];
-                    patch[dy][dx] = (uint8_t)((sacc + area / 2) / area);
-                }
-            } else {
+        if (fabs(scale - iscale) < DBL_EPSILON && iscale >= 1) {
+            const int area = iscale * iscale;
+            for (int o = tid; o < (kPatch + 1) * (kPatch + 1); o += kDescThreads) {
+                const int dy = o / (kPatch + 1), dx = o % (kPatch + 1);
+                int sacc = 0;
+                for (int a = 0; a < iscale; a++)
+                    for (int b = 0; b < iscale; b++) sacc += (int)pixel(dy * iscale + a, dx * iscale + b);
+                patch[dy][dx] = (uint8_t)((sacc + area / 2) / area);
+            }
+        } else {
+            // horizontal: tmp[dx][sy] = sum over the dx span of win(sy, sx) * alpha (in order)
+            for (int o = tid; o < win * (kPatch + 1); o += kDescThreads) {
+                const int sy = o % win, dx = o / win;
                 const AreaSpan xs = area_span(dx, scale, win);
-                auto rowbuf = [&](int sy) {
-                    const uint8_t* Sr = wbuf + (size_t)sy * win;
-                    float b = 0;
-                    if (xs.lo_i >= 0) b += Sr[xs.lo_i] * xs.lo_a;
-                    for (int sx = xs.first; sx < xs.last; sx++) b += Sr[sx] * xs.mid_a;
-                    if (xs.hi_i >= 0) b += Sr[xs.hi_i] * xs.hi_a;
-                    return b;
-                };
-                for (int dy = 0; dy < kPatch + 1; dy++) {
-                    const AreaSpan ys = area_span(dy, scale, win);
-                    float acc = 0;
-                    if (ys.lo_i >= 0) acc += ys.lo_a * rowbuf(ys.lo_i);
-                    for (int sy = ys.first; sy < ys.last; sy++) acc += ys.mid_a * rowbuf(sy);
-                    if (ys.hi_i >= 0) acc += ys.hi_a * rowbuf(ys.hi_i);
-                    const int v = cv_roundf(acc);
-                    patch[dy][dx] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
-                }
+                float bsum = 0;
+                if (xs.lo_i >= 0) bsum += pixel(sy, xs.lo_i) * xs.lo_a;
+                for (int sx = xs.first; sx < xs.last; sx++) bsum += pixel(sy, sx) * xs.mid_a;
+                if (xs.hi_i >= 0) bsum += pixel(sy, xs.hi_i) * xs.hi_a;
+                tmp[(size_t)dx * win + sy] = bsum;
+            }
+            __threadfence_block();
+            __syncthreads();
+            for (int o = tid; o < (kPatch + 1) * (kPatch + 1); o += kDescThreads) {
+                const int dy = o / (kPatch + 1), dx = o % (kPatch + 1);
+                const AreaSpan ys = area_span(dy, scale, win);
+                const float* T = tmp + (size_t)dx * win;
+                float acc = 0;
+                if (ys.lo_i >= 0) acc += ys.lo_a * T[ys.lo_i];
+                for (int sy = ys.first; sy < ys.last; sy++) acc += ys.mid_a * T[sy];
+                if (ys.hi_i >= 0) acc += ys.hi_a * T[ys.hi_i];
+                const int v = cv_roundf(acc);
+                patch[dy][dx] = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
             }
         }
         __syncthreads();
-        for (int c = lane; c < kPatch * kPatch; c += 64) {
+        for (int c = tid; c < kPatch * kPatch; c += kDescThreads) {
             const int i = c / kPatch, j = c % kPatch;
             const float dw = K.gdesc[i] * K.gdesc[j];
             DX[i][j] = (patch[i][j + 1] - patch[i][j] + patch[i + 1][j + 1] - patch[i + 1][j]) * dw;
             DY[i][j] = (patch[i + 1][j] - patch[i][j] + patch[i + 1][j + 1] - patch[i][j + 1]) * dw;
         }
         __syncthreads();
-        if (lane < 16) {
-            const int i = lane >> 2, j = lane & 3;
+        if (tid < 16) {
+            const int i = tid >> 2, j = tid & 3;
             float v0 = 0, v1 = 0, v2 = 0, v3 = 0;
             for (int y = i * 5; y < i * 5 + 5; y++)
                 for (int x = j * 5; x < j * 5 + 5; x++) {
@@ -476,19 +510,19 @@ __global__ __launch_bounds__(64) void surf_describe_kernel(
                     v2 += fabsf(tx);
                     v3 += fabsf(ty);
                 }
-            vecs[4 * lane] = v0;
-            vecs[4 * lane + 1] = v1;
-            vecs[4 * lane + 2] = v2;
-            vecs[4 * lane + 3] = v3;
+            vecs[4 * tid] = v0;
+            vecs[4 * tid + 1] = v1;
+            vecs[4 * tid + 2] = v2;
+            vecs[4 * tid + 3] = v3;
         }
         __syncthreads();
-        if (lane == 0) {
+        if (tid == 0) {
             double sq = 0;
             for (int q = 0; q < 64; q++) sq += vecs[q] * vecs[q];
             sBest[0] = (float)(1. / (sqrt(sq) + FLT_EPSILON));
         }
         __syncthreads();
-        desc[((size_t)img * max_kp + k) * 64 + lane] = vecs[lane] * sBest[0];
+        if (tid < 64) desc[((size_t)img * max_kp + k) * 64 + tid] = vecs[tid] * sBest[0];
         __syncthreads();
     }
 }
@@ -563,7 +597,7 @@ hipError_t launch_surf(const uint8_t* images, int n_images, int W, int H, int ch
                            scr.det, plan.threshold, max_kp, scr.raw, counts);
     hipLaunchKernelGGL(surf_sort_kernel, dim3((max_kp + 255) / 256, n_images), dim3(256), 0, st, scr.raw,
                        counts, max_kp, scr.sorted);
-    hipLaunchKernelGGL(surf_describe_kernel, dim3(kSurfDescBlocks), dim3(64), 0, st,
+    hipLaunchKernelGGL(surf_describe_kernel, dim3(kSurfDescBlocks), dim3(kDescThreads), 0, st,
                        channels == 3 ? (const uint8_t*)scr.gray : images, scr.sum, W, H, n_images,
                        max_kp, counts, scr.sorted, scr.desc, plan.consts, scr.big, scr.big_slot);
     hipLaunchKernelGGL(surf_compact_kernel, dim3(n_images), dim3(1024), 0, st, scr.sorted, scr.desc,

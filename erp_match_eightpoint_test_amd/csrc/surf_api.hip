@@ -154,7 +154,7 @@ erp_status erp_surf_detect_compute_dev(erp_ctx* ctx, const uint8_t* d_images, in
     // scratch
     erp::SurfScratch scr{};
     const size_t n = (size_t)n_images, K = (size_t)max_kp;
-    scr.big_slot = (size_t)erp::kSurfBigWin * erp::kSurfBigWin;
+    scr.big_slot = (size_t)erp::kSurfBigWin * 21 * sizeof(float);  // tmp[21][win] per block
     scr.gray = (uint8_t*)erp_ctx_scratch_internal(ctx, 2, channels == 3 ? n * W * H : 16);
     scr.sum = (int32_t*)erp_ctx_scratch_internal(ctx, 3, n * (W + 1) * (H + 1) * 4);
     scr.det = (float*)erp_ctx_scratch_internal(ctx, 4, n * plan.det_per_img * 4);

@@ -120,3 +120,23 @@ def make_correspondences(seed: int, m: int = 100, outlier_frac: float = 0.6, W: 
         kl, kr = np.floor(kl), np.floor(kr)
     return {"kp_l": kl.astype(np.float32), "kp_r": kr.astype(np.float32), "W": W, "H": H,
             "euler_gt": euler, "t_gt": t}
+
+
+def sphere_texture(seed: int, H: int, W: int, n_blobs: int = 500) -> np.ndarray:
+    """an H x W x 3 (BGR) ERP image of random Gaussian blobs on the unit sphere (OMAF axes):
+    synthetic input for the band remap / SURF / end-to-end pipeline (the reference's images
+    are missing blobs)"""
+    rng = np.random.default_rng(seed)
+    y, x = np.mgrid[0:H, 0:W].astype(np.float64)
+    lat, lon = np.pi * (y + 0.5) / H, 2 * np.pi * (x + 0.5) / W
+    b = np.stack([-np.sin(lat) * np.cos(lon), np.sin(lat) * np.sin(lon), np.cos(lat)], -1)
+    c = rng.standard_normal((n_blobs, 3))
+    c /= np.linalg.norm(c, axis=1, keepdims=True)
+    sig = rng.uniform(0.01, 0.06, n_blobs)
+    amp = rng.uniform(-120, 120, (n_blobs, 3))
+    img = np.full((H, W, 3), 128.0)
+    for k in range(n_blobs):
+        d2 = ((b - c[k]) ** 2).sum(-1)
+        m = d2 < (4 * sig[k]) ** 2
+        img[m] += amp[k] * np.exp(-d2[m] / (2 * sig[k] ** 2))[:, None]
+    return np.clip(img, 0, 255).astype(np.uint8)
