@@ -40,8 +40,12 @@ struct SurfPlan {
     SurfConsts consts;
 };
 
-constexpr int kSurfDescBlocks = 2048;  // describe grid (one wave each, grid-stride)
-constexpr int kSurfBigWin = 900;       // largest rotated window (s < 43 -> 21 s < 900)
+constexpr int kSurfPatch = 20;  // the descriptor's 20 x 20 gradient patch (21 x 21 resampled)
+
+struct SurfJob {        // a keypoint's rotated window (surf_orient_kernel)
+    float cos_dir, sin_dir;
+    int win, exact;     // win = 0: deleted keypoint
+};
 
 struct SurfScratch {
     uint8_t* gray;          // [n][H][W] (BGR input only)
@@ -50,12 +54,30 @@ struct SurfScratch {
     erp_keypoint* raw;      // [n][max_kp]
     erp_keypoint* sorted;   // [n][max_kp]
     float* desc;            // [n][max_kp][64]
-    uint8_t* big;           // [kSurfDescBlocks][big_slot]: the horizontal area pass tmp[21][win]
-    size_t big_slot;
+    // descriptor pass over a chunk of keypoints (surf.hip): per keypoint slot tmp[21][win],
+    // stx[win], sty[win] (slot = 23 * max_win floats), a job record, band work items
+    float* pool;
+    size_t slot;
+    int max_win;
+    SurfJob* jobs;
+    int2* items;
+    int32_t* nitems;
 };
 
-hipError_t launch_surf(const uint8_t* images, int n_images, int W, int H, int channels,
-                       const SurfPlan& plan, const SurfScratch& scr, int max_kp,
-                       erp_keypoint* kp_out, float* desc_out, int32_t* counts, hipStream_t st);
+size_t surf_job_bytes();
+int surf_band_rows();
+// detection: gray, integral, Fast-Hessian layers, maxima + interpolation, KeypointGreater order
+// (raw counts in counts[]; -needed when max_kp overflowed)
+hipError_t launch_surf_detect(const uint8_t* images, int n_images, int W, int H, int channels,
+                              const SurfPlan& plan, const SurfScratch& scr, int max_kp,
+                              int32_t* counts, hipStream_t st);
+// orientation + descriptor of keypoints g0 .. g0 + ng - 1 (numbered over the images by the
+// device prefix d_kpre[n_images])
+hipError_t launch_surf_describe(const uint8_t* images, int n_images, int W, int H, int channels,
+                                const SurfPlan& plan, const SurfScratch& scr, int max_kp,
+                                const int32_t* d_kpre, int g0, int ng, hipStream_t st);
+// drop the deleted keypoints (order kept) into the outputs; final counts
+hipError_t launch_surf_compact(int n_images, const SurfScratch& scr, int max_kp, erp_keypoint* kp_out,
+                               float* desc_out, int32_t* counts, hipStream_t st);
 
 }  // namespace erp

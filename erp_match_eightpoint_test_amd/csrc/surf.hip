@@ -13,9 +13,11 @@
 //   surf_extrema_kernel     findMaximaInLayer: 3x3x3 strict maxima above the threshold,
 //                           interpolateKeypoint (Cramer), appended per image
 //   surf_sort_kernel        KeypointGreater order by rank counting (deterministic)
-//   surf_describe_kernel    one wave per keypoint: orientation (Haar responses on the radius-6s
-//                           disc, fastAtan2, 72 sliding 60-degree windows), the rotated 20s window
-//                           (bilinear), INTER_AREA to 21 x 21, gradients, 4 x 4 x 4 sums, norm
+//   surf_orient_kernel      one wave per keypoint: orientation (Haar responses on the radius-6s
+//                           disc, fastAtan2, 72 sliding 60-degree windows), window row starts
+//   surf_window_kernel      per 16-row band of a keypoint's rotated 20s window: pixels generated
+//                           on the fly (bilinear), horizontal INTER_AREA pass
+//   surf_descriptor_kernel  vertical INTER_AREA pass -> 21 x 21, gradients, 4 x 4 x 4 sums, norm
 //   surf_compact_kernel     drop the keypoints marked for deletion, keep the order
 #include <hip/hip_runtime.h>
 
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(256) void surf_sort_kernel(const erp_keypoint* __re
 }
 
 // ---- descriptor ---------------------------------------------------------------------------
-constexpr int kPatch = 20, kNOri = kSurfNOri;  // lattice points of the radius-6 disc
+constexpr int kPatch = kSurfPatch, kNOri = kSurfNOri;  // lattice points of the radius-6 disc
 
 __device__ __forceinline__ float fast_atan2(float y, float x) {
     const float s = (float)(180 / M_PI);
@@ -304,83 +306,134 @@ __device__ __forceinline__ bool exact_walk(float v) {
     return v == 0.f || (fabsf(v) >= 0x1p-16f && fabsf(v) < 0x1p13f);
 }
 
-// one block (256 threads) per keypoint, grid-stride over the keypoints of all images:
-// orientation, the rotated window generated on the fly inside a separable INTER_AREA
-// (horizontal pass into the block's global scratch tmp[dx][sy], then vertical), gradients,
-// descriptor, norm
-constexpr int kDescThreads = 256;
-__global__ __launch_bounds__(kDescThreads) void surf_describe_kernel(
-    const uint8_t* __restrict__ gray, const int32_t* __restrict__ sum, int W, int H,
-    int n_images, int max_kp, const int32_t* __restrict__ counts, erp_keypoint* __restrict__ kps,
-    float* __restrict__ desc, SurfConsts K, uint8_t* __restrict__ big, size_t big_slot) {
+// The descriptor in three launches, so that a few large keypoints (window up to ~740^2 pixels)
+// do not serialise the whole pass behind one block:
+//   surf_orient_kernel   one wave per keypoint: orientation, the window's row starts and its
+//                        exact-walk flag into the keypoint's slot, band items (16 window rows)
+//                        appended to the work list
+//   surf_window_kernel   one block per band item: the horizontal INTER_AREA pass
+//                        tmp[dx][sy] = sum over the dx span of win(sy, sx) * alpha, each window
+//                        pixel generated on the fly (bilinear, the reference's walk)
+//   surf_descriptor_kernel  one block per keypoint: the vertical pass -> the 21 x 21 patch,
+//                        gradients, 4 x 4 x 4 sums, norm
+// Keypoints are numbered g = 0 .. total-1 over the images (kpre[img] = first g of img); a
+// chunk [g0, g0 + n) is described per launch triple; slot g - g0 holds tmp[21][win] then
+// stx[win], sty[win] (slot stride = 23 * max_win floats).
+constexpr int kBandRows = 16;
+
+__device__ __forceinline__ void kp_of(int g, const int32_t* __restrict__ kpre, int n_images,
+                                      int* img, int* k) {
+    int i = 0;
+    while (i + 1 < n_images && g >= kpre[i + 1]) i++;
+    *img = i;
+    *k = g - kpre[i];
+}
+
+// window pixel (row i, column j): bilinear inside, nearest clamped outside (the reference's
+// rotated-window loop); the exact walk = fma(j, c, start) when it never rounds (header above)
+__device__ __forceinline__ float win_pixel(const uint8_t* __restrict__ I, int W, int H, float stx,
+                                           float sty, int j, float cos_dir, float sin_dir,
+                                           bool exact) {
+    double px, py;
+    if (exact) {
+        px = __builtin_fma((double)j, (double)cos_dir, (double)stx);
+        py = __builtin_fma(-(double)j, (double)sin_dir, (double)sty);
+    } else {
+        px = stx;
+        py = sty;
+        for (int q = 0; q < j; q++) {
+            px += cos_dir;
+            py -= sin_dir;
+        }
+    }
+    const int nc1 = W - 1, nr1 = H - 1;
+    const int ix = (int)floor(px), iy = (int)floor(py);
+    if ((unsigned)ix < (unsigned)nc1 && (unsigned)iy < (unsigned)nr1) {
+        const float a = (float)(px - ix), b = (float)(py - iy);
+        const uint8_t* p = I + (size_t)iy * W + ix;
+        return (float)(uint8_t)cv_roundf(p[0] * (1.f - a) * (1.f - b) + p[1] * a * (1.f - b) +
+                                         p[W] * (1.f - a) * b + p[W + 1] * a * b);
+    }
+    int x = cv_roundd(px), y = cv_roundd(py);
+    x = x < 0 ? 0 : x > nc1 ? nc1 : x;
+    y = y < 0 ? 0 : y > nr1 ? nr1 : y;
+    return (float)I[(size_t)y * W + x];
+}
+
+__device__ __forceinline__ bool integer_scale(int win, double* scale, int* iscale) {
+    *scale = (double)win / (kPatch + 1);
+    *iscale = (int)(*scale + 0.5);
+    return fabs(*scale - *iscale) < DBL_EPSILON && *iscale >= 1;
+}
+
+__global__ __launch_bounds__(64) void surf_orient_kernel(
+    const int32_t* __restrict__ sum, int W, int H, int n_images, int max_kp,
+    const int32_t* __restrict__ kpre, int g0, int ng, erp_keypoint* __restrict__ kps, SurfConsts K,
+    float* __restrict__ pool, size_t slot, int max_win, SurfJob* __restrict__ jobs,
+    int2* __restrict__ items, int32_t* __restrict__ nitems) {
     __shared__ float sX[kNOri], sY[kNOri], sA[kNOri];
-    __shared__ int sN;
-    __shared__ float sBest[2];
     __shared__ float sMod[72], sSx[72], sSy[72];
-    __shared__ float stx[kSurfBigWin], sty[kSurfBigWin];
-    __shared__ int sExact;
-    __shared__ uint8_t patch[kPatch + 1][kPatch + 1];
-    __shared__ float DX[kPatch][kPatch], DY[kPatch][kPatch];
-    __shared__ float vecs[64];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int lane = threadIdx.x;
     const int ws = W + 1;
-    float* tmp = reinterpret_cast<float*>(big + (size_t)blockIdx.x * big_slot);
-    for (int g = blockIdx.x; g < n_images * max_kp; g += gridDim.x) {
-        const int img = g / max_kp, k = g % max_kp;
-        const int n = min(counts[img], max_kp);
-        if (k >= n) continue;  // uniform over the block
-        const erp_keypoint kp = kps[(size_t)img * max_kp + k];
-        const uint8_t* I = gray + (size_t)img * W * H;
+    for (int c = blockIdx.x; c < ng; c += gridDim.x) {
+        int img, k;
+        kp_of(g0 + c, kpre, n_images, &img, &k);
+        erp_keypoint* kpp = kps + (size_t)img * max_kp + k;
+        const erp_keypoint kp = *kpp;
         const int32_t* S = sum + (size_t)img * (H + 1) * ws;
         const float s = kp.size * 1.2f / 9.0f;
         const int grad = 2 * cv_roundf(2 * s);
-        if (H + 1 < grad || W + 1 < grad) {
-            if (tid == 0) kps[(size_t)img * max_kp + k].size = -1;
+        const int win = (int)((kPatch + 1) * s);
+        SurfJob job{0.f, 0.f, 0, 0};
+        if (H + 1 < grad || W + 1 < grad || win > max_win) {  // (win > max_win cannot happen)
+            if (lane == 0) {
+                kpp->size = -1;
+                jobs[c] = job;
+            }
             continue;
         }
-        // orientation samples in disc order, compacted (order kept) by wave 0
-        if (wid == 0) {
-            const int dx_s[2][5] = {{0, 0, 2, 4, -1}, {2, 0, 4, 4, 1}};
-            const int dy_s[2][5] = {{0, 0, 4, 2, 1}, {0, 2, 4, 4, -1}};
-            SurfHF dxt[2], dyt[2];
-            resize_haar4(dx_s, dxt, grad, ws);
-            resize_haar4(dy_s, dyt, grad, ws);
-            int nangle = 0;
-            for (int k0 = 0; k0 < kNOri; k0 += 64) {
-                const int kk = k0 + lane;
-                bool valid = false;
-                float vx = 0, vy = 0;
-                if (kk < kNOri) {
-                    const int x = cv_roundf(kp.x + K.aptx[kk] * s - (float)(grad - 1) / 2);
-                    const int y = cv_roundf(kp.y + K.apty[kk] * s - (float)(grad - 1) / 2);
-                    valid = !(y < 0 || y >= H + 1 - grad || x < 0 || x >= W + 1 - grad);
-                    if (valid) {
-                        const int32_t* ptr = S + (size_t)y * ws + x;
-                        vx = haar(ptr, dxt, 2) * K.aptw[kk];
-                        vy = haar(ptr, dyt, 2) * K.aptw[kk];
-                    }
-                }
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(valid);
+        // orientation samples in disc order, compacted (order kept)
+        const int dx_s[2][5] = {{0, 0, 2, 4, -1}, {2, 0, 4, 4, 1}};
+        const int dy_s[2][5] = {{0, 0, 4, 2, 1}, {0, 2, 4, 4, -1}};
+        SurfHF dxt[2], dyt[2];
+        resize_haar4(dx_s, dxt, grad, ws);
+        resize_haar4(dy_s, dyt, grad, ws);
+        int nangle = 0;
+        for (int k0 = 0; k0 < kNOri; k0 += 64) {
+            const int kk = k0 + lane;
+            bool valid = false;
+            float vx = 0, vy = 0;
+            if (kk < kNOri) {
+                const int x = cv_roundf(kp.x + K.aptx[kk] * s - (float)(grad - 1) / 2);
+                const int y = cv_roundf(kp.y + K.apty[kk] * s - (float)(grad - 1) / 2);
+                valid = !(y < 0 || y >= H + 1 - grad || x < 0 || x >= W + 1 - grad);
                 if (valid) {
-                    const int pos = nangle + __builtin_popcountll(bal & ((1ull << lane) - 1ull));
-                    sX[pos] = vx;
-                    sY[pos] = vy;
-                    sA[pos] = fast_atan2(vy, vx);
+                    const int32_t* ptr = S + (size_t)y * ws + x;
+                    vx = haar(ptr, dxt, 2) * K.aptw[kk];
+                    vy = haar(ptr, dyt, 2) * K.aptw[kk];
                 }
-                nangle += __builtin_popcountll(bal);
             }
-            if (lane == 0) sN = nangle;
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(valid);
+            if (valid) {
+                const int pos = nangle + __builtin_popcountll(bal & ((1ull << lane) - 1ull));
+                sX[pos] = vx;
+                sY[pos] = vy;
+                sA[pos] = fast_atan2(vy, vx);
+            }
+            nangle += __builtin_popcountll(bal);
         }
         __syncthreads();
-        const int nangle = sN;
         if (nangle == 0) {
-            if (tid == 0) kps[(size_t)img * max_kp + k].size = -1;
+            if (lane == 0) {
+                kpp->size = -1;
+                jobs[c] = job;
+            }
             __syncthreads();
             continue;
         }
         // 72 windows of 60 degrees, 5 apart; each summed sequentially over the samples
-        if (tid < 72) {
-            const int i = 5 * tid;
+        for (int w = lane; w < 72; w += 64) {
+            const int i = 5 * w;
             float sx = 0, sy = 0;
             for (int j = 0; j < nangle; j++) {
                 const int d = abs(cv_roundf(sA[j]) - i);
@@ -389,34 +442,30 @@ __global__ __launch_bounds__(kDescThreads) void surf_describe_kernel(
                     sy += sY[j];
                 }
             }
-            sMod[tid] = sx * sx + sy * sy;
-            sSx[tid] = sx;
-            sSy[tid] = sy;
+            sMod[w] = sx * sx + sy * sy;
+            sSx[w] = sx;
+            sSy[w] = sy;
         }
         __syncthreads();
-        const int win = (int)((kPatch + 1) * s);
-        if (tid == 0) {  // the first window with a strictly larger modulus wins
-            float best = 0, bx = 0, by = 0;
+        if (lane == 0) {
+            float best = 0, bx = 0, by = 0;  // the first window with a strictly larger modulus
             for (int w = 0; w < 72; w++)
                 if (sMod[w] > best) {
                     best = sMod[w];
                     bx = sSx[w];
                     by = sSy[w];
                 }
-            sBest[0] = bx;
-            sBest[1] = by;
-        }
-        __syncthreads();
-        const float dir_deg = fast_atan2(-sBest[1], sBest[0]);
-        const float dir = dir_deg * (float)(M_PI / 180);
-        const float sin_dir = -(float)sin((double)dir), cos_dir = (float)cos((double)dir);
-        if (tid == 0) {
-            kps[(size_t)img * max_kp + k].angle = dir_deg;
+            const float dir_deg = fast_atan2(-by, bx);
+            const float dir = dir_deg * (float)(M_PI / 180);
+            const float sin_dir = -(float)sin((double)dir), cos_dir = (float)cos((double)dir);
+            kpp->angle = dir_deg;
             // row starts: the reference's float recurrence, sequentially
+            float* stx = pool + (size_t)c * slot + (size_t)(kPatch + 1) * win;
+            float* sty = stx + win;
             const float woff = -(float)(win - 1) / 2;
             float a = kp.x + woff * cos_dir + woff * sin_dir;
             float b = kp.y - woff * sin_dir + woff * cos_dir;
-            bool ex = exact_walk(cos_dir) && exact_walk(sin_dir) && win <= kSurfBigWin;
+            bool ex = exact_walk(cos_dir) && exact_walk(sin_dir);
             for (int i = 0; i < win; i++, a += sin_dir, b += cos_dir) {
                 stx[i] = a;
                 sty[i] = b;
@@ -424,65 +473,96 @@ __global__ __launch_bounds__(kDescThreads) void surf_describe_kernel(
                      fabsf(a) + win * fabsf(cos_dir) < 0x1p13f &&
                      fabsf(b) + win * fabsf(sin_dir) < 0x1p13f;
             }
-            sExact = ex;
+            job.cos_dir = cos_dir;
+            job.sin_dir = sin_dir;
+            job.win = win;
+            job.exact = ex;
+            jobs[c] = job;
+            const int nb = (win + kBandRows - 1) / kBandRows;
+            const int base = atomicAdd(nitems, nb);
+            for (int q = 0; q < nb; q++) items[base + q] = make_int2(c, q);
         }
         __syncthreads();
-        const bool exact = sExact != 0;
-        const int nc1 = W - 1, nr1 = H - 1;
-        auto pixel = [&](int i, int j) -> float {  // window pixel (row i, column j)
-            double px, py;
-            if (exact) {
-                px = __builtin_fma((double)j, (double)cos_dir, (double)stx[i]);
-                py = __builtin_fma(-(double)j, (double)sin_dir, (double)sty[i]);
-            } else {
-                px = stx[i];
-                py = sty[i];
-                for (int q = 0; q < j; q++) {
-                    px += cos_dir;
-                    py -= sin_dir;
-                }
-            }
-            const int ix = (int)floor(px), iy = (int)floor(py);
-            if ((unsigned)ix < (unsigned)nc1 && (unsigned)iy < (unsigned)nr1) {
-                const float a = (float)(px - ix), b = (float)(py - iy);
-                const uint8_t* p = I + (size_t)iy * W + ix;
-                return (float)(uint8_t)cv_roundf(p[0] * (1.f - a) * (1.f - b) + p[1] * a * (1.f - b) +
-                                                 p[W] * (1.f - a) * b + p[W + 1] * a * b);
-            }
-            int x = cv_roundd(px), y = cv_roundd(py);
-            x = x < 0 ? 0 : x > nc1 ? nc1 : x;
-            y = y < 0 ? 0 : y > nr1 ? nr1 : y;
-            return (float)I[(size_t)y * W + x];
-        };
-        // INTER_AREA to 21 x 21
-        const double scale = (double)win / (kPatch + 1);
-        const int iscale = (int)(scale + 0.5);
-        if (fabs(scale - iscale) < DBL_EPSILON && iscale >= 1) {
-            const int area = iscale * iscale;
-            for (int o = tid; o < (kPatch + 1) * (kPatch + 1); o += kDescThreads) {
-                const int dy = o / (kPatch + 1), dx = o % (kPatch + 1);
+    }
+}
+
+__global__ __launch_bounds__(256) void surf_window_kernel(
+    const uint8_t* __restrict__ gray, int W, int H, int n_images, const int32_t* __restrict__ kpre,
+    int g0, const float* __restrict__ pool_in, float* __restrict__ pool, size_t slot,
+    const SurfJob* __restrict__ jobs, const int2* __restrict__ items,
+    const int32_t* __restrict__ nitems) {
+    const int tid = threadIdx.x;
+    const int n = *nitems;
+    for (int it = blockIdx.x; it < n; it += gridDim.x) {
+        const int2 item = items[it];
+        const int c = item.x, r0 = item.y * kBandRows;
+        const SurfJob job = jobs[c];
+        const int win = job.win;
+        const int rows = min(kBandRows, win - r0);
+        int img, k;
+        kp_of(g0 + c, kpre, n_images, &img, &k);
+        const uint8_t* I = gray + (size_t)img * W * H;
+        float* tmp = pool + (size_t)c * slot;
+        const float* stx = pool_in + (size_t)c * slot + (size_t)(kPatch + 1) * win;
+        const float* sty = stx + win;
+        double scale;
+        int iscale;
+        const bool integ = integer_scale(win, &scale, &iscale);
+        for (int o = tid; o < rows * (kPatch + 1); o += 256) {
+            const int sy = r0 + o % rows, dx = o / rows;
+            const float ax = stx[sy], ay = sty[sy];
+            float bsum = 0;
+            if (integ) {  // integer sums (exact in float)
                 int sacc = 0;
-                for (int a = 0; a < iscale; a++)
-                    for (int b = 0; b < iscale; b++) sacc += (int)pixel(dy * iscale + a, dx * iscale + b);
-                patch[dy][dx] = (uint8_t)((sacc + area / 2) / area);
-            }
-        } else {
-            // horizontal: tmp[dx][sy] = sum over the dx span of win(sy, sx) * alpha (in order)
-            for (int o = tid; o < win * (kPatch + 1); o += kDescThreads) {
-                const int sy = o % win, dx = o / win;
+                for (int b = 0; b < iscale; b++)
+                    sacc += (int)win_pixel(I, W, H, ax, ay, dx * iscale + b, job.cos_dir, job.sin_dir,
+                                           job.exact);
+                bsum = (float)sacc;
+            } else {
                 const AreaSpan xs = area_span(dx, scale, win);
-                float bsum = 0;
-                if (xs.lo_i >= 0) bsum += pixel(sy, xs.lo_i) * xs.lo_a;
-                for (int sx = xs.first; sx < xs.last; sx++) bsum += pixel(sy, sx) * xs.mid_a;
-                if (xs.hi_i >= 0) bsum += pixel(sy, xs.hi_i) * xs.hi_a;
-                tmp[(size_t)dx * win + sy] = bsum;
+                if (xs.lo_i >= 0)
+                    bsum += win_pixel(I, W, H, ax, ay, xs.lo_i, job.cos_dir, job.sin_dir, job.exact) *
+                            xs.lo_a;
+                for (int sx = xs.first; sx < xs.last; sx++)
+                    bsum += win_pixel(I, W, H, ax, ay, sx, job.cos_dir, job.sin_dir, job.exact) *
+                            xs.mid_a;
+                if (xs.hi_i >= 0)
+                    bsum += win_pixel(I, W, H, ax, ay, xs.hi_i, job.cos_dir, job.sin_dir, job.exact) *
+                            xs.hi_a;
             }
-            __threadfence_block();
-            __syncthreads();
-            for (int o = tid; o < (kPatch + 1) * (kPatch + 1); o += kDescThreads) {
-                const int dy = o / (kPatch + 1), dx = o % (kPatch + 1);
+            tmp[(size_t)dx * win + sy] = bsum;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void surf_descriptor_kernel(
+    int n_images, int max_kp, const int32_t* __restrict__ kpre, int g0, int ng,
+    const float* __restrict__ pool, size_t slot, const SurfJob* __restrict__ jobs,
+    float* __restrict__ desc, SurfConsts K) {
+    __shared__ uint8_t patch[kPatch + 1][kPatch + 1];
+    __shared__ float DX[kPatch][kPatch], DY[kPatch][kPatch];
+    __shared__ float vecs[64];
+    __shared__ float sNorm;
+    const int tid = threadIdx.x;
+    for (int c = blockIdx.x; c < ng; c += gridDim.x) {
+        const int win = jobs[c].win;
+        if (win == 0) continue;  // deleted keypoint (uniform over the block)
+        int img, k;
+        kp_of(g0 + c, kpre, n_images, &img, &k);
+        const float* tmp = pool + (size_t)c * slot;
+        double scale;
+        int iscale;
+        const bool integ = integer_scale(win, &scale, &iscale);
+        for (int o = tid; o < (kPatch + 1) * (kPatch + 1); o += 256) {
+            const int dy = o / (kPatch + 1), dx = o % (kPatch + 1);
+            const float* T = tmp + (size_t)dx * win;
+            if (integ) {
+                const int area = iscale * iscale;
+                int sacc = 0;
+                for (int a = 0; a < iscale; a++) sacc += (int)T[dy * iscale + a];
+                patch[dy][dx] = (uint8_t)((sacc + area / 2) / area);
+            } else {
                 const AreaSpan ys = area_span(dy, scale, win);
-                const float* T = tmp + (size_t)dx * win;
                 float acc = 0;
                 if (ys.lo_i >= 0) acc += ys.lo_a * T[ys.lo_i];
                 for (int sy = ys.first; sy < ys.last; sy++) acc += ys.mid_a * T[sy];
@@ -492,8 +572,8 @@ __global__ __launch_bounds__(kDescThreads) void surf_describe_kernel(
             }
         }
         __syncthreads();
-        for (int c = tid; c < kPatch * kPatch; c += kDescThreads) {
-            const int i = c / kPatch, j = c % kPatch;
+        for (int q = tid; q < kPatch * kPatch; q += 256) {
+            const int i = q / kPatch, j = q % kPatch;
             const float dw = K.gdesc[i] * K.gdesc[j];
             DX[i][j] = (patch[i][j + 1] - patch[i][j] + patch[i + 1][j + 1] - patch[i + 1][j]) * dw;
             DY[i][j] = (patch[i + 1][j] - patch[i][j] + patch[i + 1][j + 1] - patch[i][j + 1]) * dw;
@@ -519,10 +599,10 @@ __global__ __launch_bounds__(kDescThreads) void surf_describe_kernel(
         if (tid == 0) {
             double sq = 0;
             for (int q = 0; q < 64; q++) sq += vecs[q] * vecs[q];
-            sBest[0] = (float)(1. / (sqrt(sq) + FLT_EPSILON));
+            sNorm = (float)(1. / (sqrt(sq) + FLT_EPSILON));
         }
         __syncthreads();
-        if (tid < 64) desc[((size_t)img * max_kp + k) * 64 + tid] = vecs[tid] * sBest[0];
+        if (tid < 64) desc[((size_t)img * max_kp + k) * 64 + tid] = vecs[tid] * sNorm;
         __syncthreads();
     }
 }
@@ -573,9 +653,9 @@ __global__ __launch_bounds__(1024) void surf_compact_kernel(const erp_keypoint* 
 
 }  // namespace
 
-hipError_t launch_surf(const uint8_t* images, int n_images, int W, int H, int channels,
-                       const SurfPlan& plan, const SurfScratch& scr, int max_kp,
-                       erp_keypoint* kp_out, float* desc_out, int32_t* counts, hipStream_t st) {
+hipError_t launch_surf_detect(const uint8_t* images, int n_images, int W, int H, int channels,
+                              const SurfPlan& plan, const SurfScratch& scr, int max_kp,
+                              int32_t* counts, hipStream_t st) {
     const size_t npix = (size_t)n_images * W * H;
     const uint8_t* gray = images;
     if (channels == 3) {
@@ -597,12 +677,36 @@ hipError_t launch_surf(const uint8_t* images, int n_images, int W, int H, int ch
                            scr.det, plan.threshold, max_kp, scr.raw, counts);
     hipLaunchKernelGGL(surf_sort_kernel, dim3((max_kp + 255) / 256, n_images), dim3(256), 0, st, scr.raw,
                        counts, max_kp, scr.sorted);
-    hipLaunchKernelGGL(surf_describe_kernel, dim3(kSurfDescBlocks), dim3(kDescThreads), 0, st,
-                       channels == 3 ? (const uint8_t*)scr.gray : images, scr.sum, W, H, n_images,
-                       max_kp, counts, scr.sorted, scr.desc, plan.consts, scr.big, scr.big_slot);
+    return hipGetLastError();
+}
+
+hipError_t launch_surf_describe(const uint8_t* images, int n_images, int W, int H, int channels,
+                                const SurfPlan& plan, const SurfScratch& scr, int max_kp,
+                                const int32_t* d_kpre, int g0, int ng, hipStream_t st) {
+    if (ng <= 0) return hipSuccess;
+    const uint8_t* gray = channels == 3 ? (const uint8_t*)scr.gray : images;
+    hipError_t e = hipMemsetAsync(scr.nitems, 0, sizeof(int32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(surf_orient_kernel, dim3(min(ng, 8192)), dim3(64), 0, st, scr.sum, W, H,
+                       n_images, max_kp, d_kpre, g0, ng, scr.sorted, plan.consts, scr.pool, scr.slot,
+                       scr.max_win, scr.jobs, scr.items, scr.nitems);
+    hipLaunchKernelGGL(surf_window_kernel, dim3(8192), dim3(256), 0, st, gray, W, H, n_images, d_kpre,
+                       g0, (const float*)scr.pool, scr.pool, scr.slot, (const SurfJob*)scr.jobs,
+                       (const int2*)scr.items, (const int32_t*)scr.nitems);
+    hipLaunchKernelGGL(surf_descriptor_kernel, dim3(min(ng, 4096)), dim3(256), 0, st, n_images, max_kp,
+                       d_kpre, g0, ng, (const float*)scr.pool, scr.slot, (const SurfJob*)scr.jobs,
+                       scr.desc, plan.consts);
+    return hipGetLastError();
+}
+
+hipError_t launch_surf_compact(int n_images, const SurfScratch& scr, int max_kp, erp_keypoint* kp_out,
+                               float* desc_out, int32_t* counts, hipStream_t st) {
     hipLaunchKernelGGL(surf_compact_kernel, dim3(n_images), dim3(1024), 0, st, scr.sorted, scr.desc,
                        max_kp, counts, kp_out, desc_out);
     return hipGetLastError();
 }
+
+size_t surf_job_bytes() { return sizeof(SurfJob); }
+int surf_band_rows() { return kBandRows; }
 
 }  // namespace erp

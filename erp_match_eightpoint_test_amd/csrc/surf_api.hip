@@ -111,6 +111,15 @@ erp_status erp_surf_detect_compute_dev(erp_ctx* ctx, const uint8_t* d_images, in
                 max_mid = std::max(max_mid, L.rows * L.cols);
             }
         }
+    // largest rotated window: keypoint sizes of a fitting middle layer grow by < one layer
+    // step (6 << o) in interpolateKeypoint; win = (int)(21 * size * 1.2 / 9)
+    int max_win = 1;
+    for (int li : mid) {
+        const erp::SurfLayer& L = layers[li];
+        if (L.size > H || L.size > W) continue;
+        const float sz = (float)(L.size + (6 << L.octave) + 1);
+        max_win = std::max(max_win, (int)(21.0f * (sz * 1.2f / 9.0f)) + 1);
+    }
     plan.det_per_img = std::max<size_t>(off, 1);
     plan.n_layers = nT;
     plan.n_mid = (int)mid.size();
@@ -154,18 +163,50 @@ erp_status erp_surf_detect_compute_dev(erp_ctx* ctx, const uint8_t* d_images, in
     // scratch
     erp::SurfScratch scr{};
     const size_t n = (size_t)n_images, K = (size_t)max_kp;
-    scr.big_slot = (size_t)erp::kSurfBigWin * 21 * sizeof(float);  // tmp[21][win] per block
     scr.gray = (uint8_t*)erp_ctx_scratch_internal(ctx, 2, channels == 3 ? n * W * H : 16);
     scr.sum = (int32_t*)erp_ctx_scratch_internal(ctx, 3, n * (W + 1) * (H + 1) * 4);
     scr.det = (float*)erp_ctx_scratch_internal(ctx, 4, n * plan.det_per_img * 4);
     scr.raw = (erp_keypoint*)erp_ctx_scratch_internal(ctx, 5, n * K * sizeof(erp_keypoint));
     scr.sorted = (erp_keypoint*)erp_ctx_scratch_internal(ctx, 6, n * K * sizeof(erp_keypoint));
     scr.desc = (float*)erp_ctx_scratch_internal(ctx, 7, n * K * 64 * 4);
-    scr.big = (uint8_t*)erp_ctx_scratch_internal(ctx, 8, erp::kSurfDescBlocks * scr.big_slot);
-    if (!scr.gray || !scr.sum || !scr.det || !scr.raw || !scr.sorted || !scr.desc || !scr.big)
+    if (!scr.gray || !scr.sum || !scr.det || !scr.raw || !scr.sorted || !scr.desc)
         return ERP_OUT_OF_MEMORY;
-    return erp::launch_surf(d_images, n_images, W, H, channels, plan, scr, max_kp, d_kp, d_desc,
-                            d_count, st) == hipSuccess ? ERP_OK : ERP_HIP_ERROR;
+    if (erp::launch_surf_detect(d_images, n_images, W, H, channels, plan, scr, max_kp, d_count, st) !=
+        hipSuccess)
+        return ERP_HIP_ERROR;
+    // the raw counts on the host (the descriptor pass is sized by them): one stream sync
+    std::vector<int32_t> cnt(n_images);
+    if (hipMemcpyAsync(cnt.data(), d_count, sizeof(int32_t) * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return ERP_HIP_ERROR;
+    std::vector<int32_t> kpre(n_images + 1, 0);
+    for (int i = 0; i < n_images; i++)  // an overflowed image (count < 0) is not described
+        kpre[i + 1] = kpre[i] + std::min(std::max(cnt[i], 0), max_kp);
+    const int total = kpre[n_images];
+    // chunks of keypoints whose slots fit in 1 GiB
+    scr.max_win = max_win;
+    scr.slot = (size_t)(erp::kSurfPatch + 3) * max_win;
+    const int chunk = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(total, 1),
+                                                                 ((size_t)1 << 30) / (scr.slot * 4)));
+    const int nbands = (max_win + erp::surf_band_rows() - 1) / erp::surf_band_rows();
+    scr.pool = (float*)erp_ctx_scratch_internal(ctx, 8, (size_t)chunk * scr.slot * 4);
+    scr.jobs = (erp::SurfJob*)erp_ctx_scratch_internal(ctx, 9, (size_t)chunk * erp::surf_job_bytes());
+    scr.items = (int2*)erp_ctx_scratch_internal(ctx, 10, (size_t)chunk * nbands * sizeof(int2));
+    int32_t* dk = (int32_t*)erp_ctx_scratch_internal(ctx, 11, (n + 1 + 16) * sizeof(int32_t));
+    if (!scr.pool || !scr.jobs || !scr.items || !dk) return ERP_OUT_OF_MEMORY;
+    scr.nitems = dk + n + 1;
+    if (total > 0) {
+        if (hipMemcpyAsync(dk, kpre.data(), sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice, st) !=
+            hipSuccess)
+            return ERP_HIP_ERROR;
+        for (int g0 = 0; g0 < total; g0 += chunk)
+            if (erp::launch_surf_describe(d_images, n_images, W, H, channels, plan, scr, max_kp, dk, g0,
+                                          std::min(chunk, total - g0), st) != hipSuccess)
+                return ERP_HIP_ERROR;
+    }
+    return erp::launch_surf_compact(n_images, scr, max_kp, d_kp, d_desc, d_count, st) == hipSuccess
+               ? ERP_OK
+               : ERP_HIP_ERROR;
 }
 
 }  // extern "C"
