@@ -383,10 +383,10 @@ def run_e2e(args):
     # SURF alone on the 8 bands of one pair (device time)
     bands = ss.bands(torch.stack([lefts[0], rights[0]])).reshape(8, H // 4, W, 3)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fm.surf(bands)
+    fm.surf_dev(bands)
     e0.record()
     for _ in range(3):
-        fm.surf(bands)
+        fm.surf_dev(bands)
     e1.record()
     torch.cuda.synchronize()
     line = {"metric": "ERP image pairs/sec through the whole reference pipeline (do_all + find), "

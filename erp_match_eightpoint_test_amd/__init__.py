@@ -73,6 +73,19 @@ class feature_matcher:  # noqa: N801  (reference class name)
         [n, H, W, 3] (BGR); a single [H, W] / [H, W, 3] image is one image -> (keypoints list
         of KEYPOINT_DTYPE arrays, descriptor list of [k, 64] float32), per image, in OpenCV's
         KeypointGreater order.  Parity with OpenCV is unpinned (oracle/erp_surf.c)."""
+        kp, desc, counts = self.surf_dev(images, max_kp, **params)
+        c = int(counts.max()) if len(counts) else 0
+        kps = kp[:, :c].cpu().numpy()
+        ds = desc[:, :c].cpu().numpy()
+        return ([kps[i, :counts[i]].reshape(-1).view(capi.KEYPOINT_DTYPE).copy()
+                 for i in range(len(counts))],
+                [ds[i, :counts[i]].copy() for i in range(len(counts))])
+
+    def surf_dev(self, images, max_kp: int = 16384, **params):
+        """surf() without leaving the device -> (keypoints uint8 [n, max_kp', 28] (view as
+        float32 [.., 7]: x, y, size, angle, response, octave, class_id), descriptors float32
+        [n, max_kp', 64], counts numpy int32 [n]); rows [0, counts[i]) of image i are valid.
+        max_kp' >= max_kp grows when an image overflows (the call is repeated)."""
         import torch
         if images.dim() == 2 or (images.dim() == 3 and images.shape[-1] == 3):
             images = images.unsqueeze(0)  # one gray [H, W] or one BGR [H, W, 3] image
@@ -95,12 +108,8 @@ class feature_matcher:  # noqa: N801  (reference class name)
                   "erp_surf_detect_compute_dev")
             counts = cnt.cpu().numpy()
             if (counts >= 0).all():
-                break
+                return kp, desc, counts
             max_kp = int(-counts.min()) + 16
-        kps = kp.cpu().numpy()
-        ds = desc.cpu().numpy()
-        return ([kps[i, :counts[i]].reshape(-1).view(capi.KEYPOINT_DTYPE).copy() for i in range(n)],
-                [ds[i, :counts[i]].copy() for i in range(n)])
 
     def _to_device(self, a):
         import torch
@@ -319,18 +328,16 @@ class spherical_surf:  # noqa: N801  (reference class name)
         ims = torch.stack([_img_dev(im_left), _img_dev(im_right)]).contiguous()
         bands = self.bands(ims, fill=fill)                      # [2, 4, H/4, W, 3]
         fm = feature_matcher(ctx=self.ctx)
-        kps, descs = fm.surf(bands.reshape(8, H // 4, W, 3), max_kp=max_kp)
-        dev = ims.device
+        kp, desc, counts = fm.surf_dev(bands.reshape(8, H // 4, W, 3), max_kp=max_kp)
+        kxy = kp.view(torch.float32)[..., :2]                   # pt.x, pt.y of every row
         keys, dcat = [], []
         for side in range(2):
-            k4 = kps[4 * side: 4 * side + 4]
-            pts = np.concatenate([np.stack([k["x"], k["y"]], 1) for k in k4]).astype(np.float32)
-            key = torch.from_numpy(pts.reshape(-1, 2)).to(dev)
+            c4 = [int(c) for c in counts[4 * side: 4 * side + 4]]
+            key = torch.cat([kxy[4 * side + b, :c4[b]] for b in range(4)]).contiguous()
             if key.shape[0]:
-                self.unrotate_band_keypoints(key, [len(k) for k in k4], W, H)
+                self.unrotate_band_keypoints(key, c4, W, H)
             keys.append(key)
-            dcat.append(torch.from_numpy(np.concatenate(descs[4 * side: 4 * side + 4])
-                                         .reshape(-1, 64)).to(dev))
+            dcat.append(torch.cat([desc[4 * side + b, :c4[b]] for b in range(4)]).contiguous())
         m = fm._match_device(dcat[0], dcat[1], 0.3)            # [M, 4] int32 DMatch rows
         q, t = m[:, 0].long(), m[:, 1].long()
         return keys[0][q], keys[1][t], int(m.shape[0]), int(keys[0].shape[0])

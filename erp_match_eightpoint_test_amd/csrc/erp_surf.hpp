@@ -21,6 +21,10 @@ struct SurfLayer {      // one (octave, layer) of the Fast-Hessian pyramid
     int octave;
     size_t off;         // float offset of the layer in the image's det buffer
     SurfHF dx[3], dy[3], dxy[4];
+    int box[10][4];     // the same 10 boxes as (x1, y1, x2, y2) (the LDS-tiled octave-0 pass)
+    int sample_pre;     // first block of this layer (the Hessian pass of octaves >= n_tiled)
+    int cell_pre;       // first block of this layer's extrema cells (middle layers)
+    int cells, cell_margin, cell_cols;
 };
 
 constexpr int kSurfNOri = 113;
@@ -35,6 +39,11 @@ struct SurfPlan {
     const int* d_mid;   // indices of the middle layers
     int n_layers, n_mid;
     int max_samples, max_mid_cells;
+    int n_layers0;      // layers per octave (nL + 2)
+    int n_tiled;        // octaves of the LDS-tiled Hessian pass (1 or 2), the rest flattened
+    int max_size0;      // largest filter of octave 0
+    int samples_hi;     // blocks of the Hessian pass of octaves >= n_tiled
+    int mid_cells;      // blocks of the extrema pass
     size_t det_per_img;
     float threshold;
     SurfConsts consts;

@@ -95,15 +95,99 @@ __device__ __forceinline__ float haar(const int32_t* __restrict__ o, const SurfH
     return (float)d;
 }
 
-__global__ __launch_bounds__(256) void surf_hessian_kernel(const int32_t* __restrict__ sum, int W,
-                                                           int H, const SurfLayer* __restrict__ layers,
-                                                           size_t det_per_img,
-                                                           float* __restrict__ det) {
-    const SurfLayer L = layers[blockIdx.y];
-    const int img = blockIdx.z;
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (L.samples_i <= 0 || idx >= L.samples_i * L.samples_j) return;
-    const int i = idx / L.samples_j, j = idx % L.samples_j;
+// octave 0 (step 1, ~80 % of the samples; SurfPlan.n_tiled octaves): one block per
+// 64 x (16 / STEP) samples stages the integral image tile they and all nL + 2 filters of the
+// octave touch ((16 + max_size) x (64 STEP + max_size) int32, <= 40 KB at step 1) in LDS
+// once, one wave per tile row (coalesced).  The tile is stored as STEP x STEP parity planes
+// (row % STEP, column % STEP), so the lanes of a wave (consecutive samples) read consecutive
+// words of one plane for every box corner: conflict-free at any step.  Same integer / float /
+// double operations as calcHaarPattern (surf_hessian_hi_kernel, the oracle).
+constexpr int kHTJ = 64;
+// A 1-D grid is dealt round-robin over the 8 XCDs; renumber so that XCD x owns the x-th
+// contiguous run of tiles (row-major, per image): tiles resident together on one XCD are
+// neighbours and re-read each other's halo rows from that XCD's L2, not from HBM.
+__device__ __forceinline__ int xcd_tile(int id, int nb) {
+    const int xcd = id & 7, local = id >> 3, per = nb >> 3, rem = nb & 7;
+    return xcd < rem ? xcd * (per + 1) + local : rem * (per + 1) + (xcd - rem) * per + local;
+}
+template <int STEP>
+__global__ __launch_bounds__(STEP == 1 ? 256 : 512) void surf_hessian_tile_kernel(
+    const int32_t* __restrict__ sum, int W, int H, const SurfLayer* __restrict__ layers, int lb,
+    int le, int max_size, size_t det_per_img, float* __restrict__ det) {
+    extern __shared__ int32_t T[];
+    constexpr int IS = 16 / STEP;        // sample rows per block
+    constexpr int NW = STEP == 1 ? 4 : 8;  // waves per block
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int TW = kHTJ * STEP + max_size, TH = IS * STEP + max_size;
+    const int TWs = (TW + STEP - 1) / STEP, THs = (TH + STEP - 1) / STEP, PL = TWs * THs;
+    const int nbx = ((W / STEP) + kHTJ - 1) / kHTJ, nby = ((H / STEP) + IS - 1) / IS;
+    const int t = xcd_tile(blockIdx.x, gridDim.x), bx = t % nbx, by = (t / nbx) % nby;
+    const int j0 = bx * kHTJ, i0 = by * IS, img = t / (nbx * nby);
+    const int32_t* S = sum + (size_t)img * (H + 1) * (W + 1);
+    for (int r = wv; r < TH; r += NW) {
+        const int gi = i0 * STEP + r;
+        int32_t* Tr = T + (r % STEP) * STEP * PL + (r / STEP) * TWs;
+        for (int c = lane; c < TW; c += 64) {
+            const int gj = j0 * STEP + c;
+            Tr[(c % STEP) * PL + c / STEP] = (gi <= H && gj <= W) ? S[(size_t)gi * (W + 1) + gj] : 0;
+        }
+    }
+    __syncthreads();
+    const int j = lane, ib = wv;
+    float* D = det + (size_t)img * det_per_img;
+    for (int l = lb; l < le; l++) {
+        const SurfLayer& L = layers[l];
+        const int si = L.samples_i, sj = L.samples_j;
+        if (si <= 0 || j0 + j >= sj) continue;
+        int off[10][4];
+        float w[10];
+        auto at = [&](int y, int x) { return ((y % STEP) * STEP + x % STEP) * PL + (y / STEP) * TWs + x / STEP; };
+#pragma unroll
+        for (int b = 0; b < 10; b++) {
+            off[b][0] = at(L.box[b][1], L.box[b][0]);  // p0 = (y1, x1)
+            off[b][1] = at(L.box[b][3], L.box[b][0]);  // p1 = (y2, x1)
+            off[b][2] = at(L.box[b][1], L.box[b][2]);  // p2 = (y1, x2)
+            off[b][3] = at(L.box[b][3], L.box[b][2]);  // p3 = (y2, x2)
+            w[b] = b < 3 ? L.dx[b].w : b < 6 ? L.dy[b - 3].w : L.dxy[b - 6].w;
+        }
+#pragma unroll
+        for (int q = 0; q < IS / NW; q++) {
+            const int ti = ib + NW * q, i = i0 + ti;
+            if (i >= si) break;
+            const int32_t* o = T + ti * TWs + j;  // sample (ti, j) -> tile (ti STEP, j STEP)
+            double hx = 0, hy = 0, hxy = 0;
+#pragma unroll
+            for (int b = 0; b < 3; b++)
+                hx += (float)(o[off[b][0]] + o[off[b][3]] - o[off[b][1]] - o[off[b][2]]) * w[b];
+#pragma unroll
+            for (int b = 3; b < 6; b++)
+                hy += (float)(o[off[b][0]] + o[off[b][3]] - o[off[b][1]] - o[off[b][2]]) * w[b];
+#pragma unroll
+            for (int b = 6; b < 10; b++)
+                hxy += (float)(o[off[b][0]] + o[off[b][3]] - o[off[b][1]] - o[off[b][2]]) * w[b];
+            const float dx = (float)hx, dy = (float)hy, dxy = (float)hxy;
+            D[L.off + (size_t)(i + L.margin) * L.cols + j0 + j + L.margin] = dx * dy - 0.81f * dxy * dxy;
+        }
+    }
+}
+
+// the remaining octaves: one thread per sample; the layers [l0, nT) own consecutive runs of blocks
+// (SurfLayer.sample_pre, in blocks), so the layer is uniform per block and its filter table
+// is read by scalar loads (no empty blocks, none of the per-layer grid padding)
+__global__ __launch_bounds__(256) void surf_hessian_hi_kernel(const int32_t* __restrict__ sum, int W,
+                                                              int H,
+                                                              const SurfLayer* __restrict__ layers,
+                                                              int l0, int nT,
+                                                              size_t det_per_img,
+                                                              float* __restrict__ det) {
+    const int img = blockIdx.y, b = blockIdx.x;
+    int l = l0;
+    while (l + 1 < nT && b >= layers[l + 1].sample_pre) l++;
+    l = __builtin_amdgcn_readfirstlane(l);
+    const SurfLayer& L = layers[l];
+    const int r = (b - L.sample_pre) * 256 + (int)threadIdx.x;
+    if (r >= L.samples_i * L.samples_j) return;
+    const int i = r / L.samples_j, j = r - i * L.samples_j;
     const int32_t* o = sum + (size_t)img * (H + 1) * (W + 1) + (size_t)i * L.step * (W + 1) +
                        (size_t)j * L.step;
     const float dx = haar(o, L.dx, 3);
@@ -144,22 +228,22 @@ __device__ bool surf_interpolate(const float (&N9)[3][9], int dx, int dy, int ds
     return true;
 }
 
-// findMaximaInLayer over every middle layer (blockIdx.y indexes the middle layers)
+// findMaximaInLayer over every middle layer: one thread per cell; the middle layers own
+// consecutive runs of blocks (SurfLayer.cell_pre, in blocks: layer uniform per block)
 __global__ __launch_bounds__(256) void surf_extrema_kernel(
     const int32_t* __restrict__ sum, int W, int H, const SurfLayer* __restrict__ layers,
-    const int* __restrict__ mid, size_t det_per_img, const float* __restrict__ det, float thr,
-    int max_kp, erp_keypoint* __restrict__ raw, int32_t* __restrict__ counts) {
-    const int li = mid[blockIdx.y], img = blockIdx.z;
-    const SurfLayer L = layers[li];
-    const SurfLayer& Lu = layers[li + 1];
-    const int size = L.size, step = L.step, lr = L.rows, lc = L.cols;
-    const int margin = (Lu.size / 2) / step + 1;
-    if (Lu.size > H || Lu.size > W) return;
-    const int nr = lr - 2 * margin, ncol = lc - 2 * margin;
-    if (nr <= 0 || ncol <= 0) return;
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= nr * ncol) return;
-    const int i = margin + idx / ncol, j = margin + idx % ncol;
+    const int* __restrict__ mid, int n_mid, size_t det_per_img,
+    const float* __restrict__ det, float thr, int max_kp, erp_keypoint* __restrict__ raw,
+    int32_t* __restrict__ counts) {
+    const int img = blockIdx.y, b = blockIdx.x;
+    int m = 0;
+    while (m + 1 < n_mid && b >= layers[mid[m + 1]].cell_pre) m++;
+    const int li = __builtin_amdgcn_readfirstlane(mid[m]);
+    const SurfLayer& L = layers[li];
+    const int size = L.size, step = L.step, lc = L.cols;
+    const int r = (b - L.cell_pre) * 256 + (int)threadIdx.x;
+    if (r >= L.cells) return;
+    const int i = L.cell_margin + r / L.cell_cols, j = L.cell_margin + r % L.cell_cols;
     const float* base = det + (size_t)img * det_per_img;
     const size_t c = (size_t)i * lc + j;
     const float v = base[L.off + c];
@@ -667,14 +751,30 @@ hipError_t launch_surf_detect(const uint8_t* images, int n_images, int W, int H,
                        W, H, scr.sum);
     hipError_t e = hipMemsetAsync(scr.det, 0, plan.det_per_img * n_images * sizeof(float), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(surf_hessian_kernel, dim3((plan.max_samples + 255) / 256, plan.n_layers, n_images),
-                       dim3(256), 0, st, scr.sum, W, H, plan.d_layers, plan.det_per_img, scr.det);
+    for (int o = 0; o < plan.n_tiled; o++) {
+        const int lb = o * plan.n_layers0, le = std::min(lb + plan.n_layers0, plan.n_layers);
+        const int ms = plan.max_size0 << o;
+        if (o == 0) {
+            const size_t lds = sizeof(int32_t) * (kHTJ + ms) * (16 + ms);
+            hipLaunchKernelGGL(surf_hessian_tile_kernel<1>,
+                               dim3(((W + kHTJ - 1) / kHTJ) * ((H + 15) / 16) * n_images), dim3(256), lds, st, scr.sum, W, H, plan.d_layers, lb, le, ms, plan.det_per_img,
+                               scr.det);
+        } else if (W >= 2 && H >= 2) {
+            const size_t lds = sizeof(int32_t) * 4 * ((2 * kHTJ + ms + 1) / 2) * ((16 + ms + 1) / 2);
+            hipLaunchKernelGGL(surf_hessian_tile_kernel<2>,
+                               dim3(((W / 2 + kHTJ - 1) / kHTJ) * ((H / 2 + 7) / 8) * n_images), dim3(512), lds, st,
+                               scr.sum, W, H, plan.d_layers, lb, le, ms, plan.det_per_img, scr.det);
+        }
+    }
+    if (plan.samples_hi > 0)
+        hipLaunchKernelGGL(surf_hessian_hi_kernel, dim3(plan.samples_hi, n_images), dim3(256), 0, st,
+                           scr.sum, W, H, plan.d_layers, plan.n_tiled * plan.n_layers0, plan.n_layers,
+                           plan.det_per_img, scr.det);
     e = hipMemsetAsync(counts, 0, sizeof(int32_t) * n_images, st);
     if (e != hipSuccess) return e;
-    if (plan.n_mid > 0)
-        hipLaunchKernelGGL(surf_extrema_kernel, dim3((plan.max_mid_cells + 255) / 256, plan.n_mid, n_images),
-                           dim3(256), 0, st, scr.sum, W, H, plan.d_layers, plan.d_mid, plan.det_per_img,
-                           scr.det, plan.threshold, max_kp, scr.raw, counts);
+    if (plan.mid_cells > 0)
+        hipLaunchKernelGGL(surf_extrema_kernel, dim3(plan.mid_cells, n_images), dim3(256), 0, st,
+                           scr.sum, W, H, plan.d_layers, plan.d_mid, plan.n_mid, plan.det_per_img, scr.det, plan.threshold, max_kp, scr.raw, counts);
     hipLaunchKernelGGL(surf_sort_kernel, dim3((max_kp + 255) / 256, n_images), dim3(256), 0, st, scr.raw,
                        counts, max_kp, scr.sorted);
     return hipGetLastError();
