@@ -314,7 +314,8 @@ void erp_surf_params_default(erp_surf_params* p);
 /* n_images images of H x W (channels 1 = gray, 3 = BGR), contiguous, device pointers ->
    per image up to max_kp keypoints [n][max_kp] in OpenCV's KeypointGreater order (descending
    response) and their unit 64-D descriptors [n][max_kp][64]; d_count[n] = keypoints found, or
-   -(needed) when max_kp was too small (rerun larger).  Asynchronous on `stream`. */
+   -(needed) when max_kp was too small (rerun larger).  Enqueued on `stream`; synchronises
+   it once inside (the detected counts size the descriptor pass). */
 erp_status erp_surf_detect_compute_dev(erp_ctx* ctx, const uint8_t* d_images, int32_t n_images,
                                        int32_t W, int32_t H, int32_t channels,
                                        const erp_surf_params* params, int32_t max_kp,
