@@ -105,8 +105,12 @@ def stage_work(stage, B, kpts, iters, res):
         ops = float(np.sum(2.0 * iters * 32 * nb * 216))  # 6 int8 limbs x 36 Gram entries
         return ops, "TOP/s", PEAK_I8_MFMA, "mfma", "2*I*32*nb*216 int8 MFMA ops per pair"
     if stage == "consensus_bounds":
-        flops = float(np.sum(K * K * 8.0))  # 3 sub, 3 mul, 2 add per squared distance, K^2
-        return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", "8 fp32 ops per squared distance, K^2"
+        # binned rows x K squared distances (the reference rows + the rows that Lipschitz
+        # pre-pruning kept; the pruning test itself is not counted)
+        nb = res["binned_rows"].astype(np.float64)
+        flops = float(np.sum(nb * K * 8.0))  # 3 sub, 3 mul, 2 add per squared distance
+        return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", \
+            "8 fp32 ops per binned squared distance (binned_rows x K)"
     if stage == "sampler":
         ops = float(np.sum((M - 1) * iters * 4.0))  # per draw: recurrence, shift, remainder, test
         return ops, "Top/s", PEAK_VALU_OPS, "valu", "4 int/fp64 ops per rand() draw (floor)"

@@ -52,7 +52,7 @@ class PairResult(C.Structure):
     _fields_ = [("R", C.c_float * 3), ("T", C.c_float * 3), ("status", C.c_int32),
                 ("M", C.c_int32), ("K", C.c_int32), ("min_idx", C.c_int32),
                 ("sample_n", C.c_int32), ("near_ties", C.c_int32), ("survivors", C.c_int32),
-                ("reserved", C.c_int32), ("min_dist", C.c_double)]
+                ("binned_rows", C.c_int32), ("min_dist", C.c_double)]
 
 
 class PairBatch(C.Structure):
@@ -72,7 +72,7 @@ HYP_DTYPE = np.dtype([("R1", "<f4", 3), ("R2", "<f4", 3), ("T", "<f4", 3), ("R1_
                       ("R2_valid", "<i4"), ("E", "<f8", 9)], align=True)
 RESULT_DTYPE = np.dtype([("R", "<f4", 3), ("T", "<f4", 3), ("status", "<i4"), ("M", "<i4"),
                          ("K", "<i4"), ("min_idx", "<i4"), ("sample_n", "<i4"),
-                         ("near_ties", "<i4"), ("survivors", "<i4"), ("reserved", "<i4"),
+                         ("near_ties", "<i4"), ("survivors", "<i4"), ("binned_rows", "<i4"),
                          ("min_dist", "<f8")], align=True)
 assert DMATCH_DTYPE.itemsize == C.sizeof(DMatch) == 16
 assert HYP_DTYPE.itemsize == C.sizeof(Hypothesis) == 120

@@ -303,7 +303,7 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->dscale, P * 4) && ensure(c->lb, P * 2 * sh.iters * 8) &&
               ensure(c->ub, P * 2 * sh.iters * 8) && ensure(c->surv, P * 2 * sh.iters * 4) &&
               ensure(c->bsel, P * 2 * sh.iters * 8) && ensure(c->edges, erp::consensus_edges_bytes((int)P)) &&
-              ensure(c->nsurv, P * 4) && ensure(c->vchunk, erp::valid_chunk_bytes(sh));
+              ensure(c->nsurv, P * 8) && ensure(c->vchunk, erp::valid_chunk_bytes(sh));
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
     if (ok && !(out && out->dist)) ok = ensure(c->tmean, P * 2 * sh.iters * 8);
@@ -408,9 +408,12 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         ERP_CK(erp::launch_consensus_bounds((int32_t*)c->kcount.p, (float*)c->rv.p,
                                             (float*)c->dscale.p, (float*)c->edges.p, sh,
                                             cfg->trim_lo, cfg->trim_hi, lbp, ubp, bselp, shard,
-                                            nshards, st));
+                                            nshards, (int32_t*)c->surv.p,
+                                            (int32_t*)c->nsurv.p + sh.n_pairs, st));
     }
     if (phase == 1) return ERP_OK;
+    if (phase == 2)  // the bounds ran per shard (no pre-pruning): binned_rows = K
+        ERP_CK(hipMemsetAsync((int32_t*)c->nsurv.p + sh.n_pairs, 0xFF, sizeof(int32_t) * sh.n_pairs, st));
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
         ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, lbp,
@@ -443,7 +446,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_FINAL, st);
         ERP_CK(erp::launch_consensus_final(counts, (int32_t*)c->kcount.p, (float*)c->rv.p, tv, tmean,
-                                           flags, (int32_t*)c->nsurv.p, sh, cfg->sample_frac, cfg->trim_lo, cfg->trim_hi,
+                                           flags, (int32_t*)c->nsurv.p,
+                                           (int32_t*)c->nsurv.p + sh.n_pairs, sh, cfg->sample_frac, cfg->trim_lo, cfg->trim_hi,
                                            (float*)c->sortbuf.p, results, st));
     }
     return ERP_OK;

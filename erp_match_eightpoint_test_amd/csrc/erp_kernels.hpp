@@ -131,7 +131,8 @@ size_t consensus_edges_bytes(int n_pairs);
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
-                                   int shard, int nshards, hipStream_t st);
+                                   int shard, int nshards, int32_t* rlist, int32_t* rcount,
+                                   hipStream_t st);
 // survivors = rows with LB <= min UB (again = 1: only pairs the refine pass touched)
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
                                    const BatchShape& sh, double trim_lo, double trim_hi,
@@ -148,9 +149,9 @@ hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const f
                                  double* tmean, hipStream_t st);
 hipError_t launch_consensus_final(const int32_t* counts, const int32_t* kcount, const float* rv,
                                   const float* tv, const double* tmean, const int32_t* flags,
-                                  const int32_t* nsurv, const BatchShape& sh, double sample_frac,
-                                  double trim_lo, double trim_hi, float* sortbuf,
-                                  erp_pair_result* results, hipStream_t st);
+                                  const int32_t* nsurv, const int32_t* nbin, const BatchShape& sh,
+                                  double sample_frac, double trim_lo, double trim_hi,
+                                  float* sortbuf, erp_pair_result* results, hipStream_t st);
 int sortbuf_len(int iters);        // power of two >= 2*iters (exact tie re-scoring scratch)
 
 }  // namespace erp

@@ -1831,7 +1831,9 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
                                                                double* __restrict__ lb,
                                                                double* __restrict__ ub,
                                                                int32_t* __restrict__ bsel,
-                                                               int shard, int nshards) {
+                                                               int shard, int nshards, int rstep,
+                                                               const int32_t* __restrict__ rlist,
+                                                               const int32_t* __restrict__ rcount) {
     constexpr int R = kBoundRows;
     constexpr int NS = 256 / R;        // epilogue slices per row
     constexpr int per = kNB / NS;      // bins per slice
@@ -1844,11 +1846,15 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
     // rows [ra, rb) of this shard (hypothesis-block sharding of one find over ranks; 0 / 1
-    // otherwise); every column
+    // otherwise), every rstep-th of them (the reference rows of the Lipschitz pre-pruning), or
+    // the rows of a per-pair list (the rows that pre-pruning kept); every column
     const int ra = (int)((int64_t)K * shard / nshards);
     const int rb = (int)((int64_t)K * (shard + 1) / nshards);
-    const int r0 = ra + blockIdx.x * R;
-    if (r0 >= rb) return;
+    const int nloc = rlist ? rcount[p] : (rb > ra ? (rb - ra + rstep - 1) / rstep : 0);
+    const int l0 = blockIdx.x * R;
+    if (l0 >= nloc) return;
+    const int32_t* RL = rlist ? rlist + (size_t)p * stride : nullptr;
+    auto rowof = [&](int l) { return RL ? (int)RL[l] : ra + l * rstep; };
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
@@ -1861,7 +1867,7 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
 #pragma unroll
     for (int t = 0; t < R; t++) {
         const int r = (lane + t) & (R - 1);
-        const int row = min(r0 + r, K - 1);
+        const int row = rowof(min(l0 + r, nloc - 1));
         xi[t >> 1][t & 1] = X[row];
         yi[t >> 1][t & 1] = Y[row];
         zi[t >> 1][t & 1] = Z[row];
@@ -1945,7 +1951,8 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     __syncthreads();
     int cum = 0;
     for (int q = 0; q < sl; q++) cum += part[q][r];
-    const int row = r0 + r;
+    const bool rvalid = l0 + r < nloc;
+    const int row = rvalid ? rowof(l0 + r) : 0;
     float L = 0.f, U = 0.f;
     int sel_a = -1, sel_b = -1;  // bins holding ranks lo and hi-1 (for the exact pass)
     if (cum < hi && cum + c > lo) {
@@ -1963,14 +1970,14 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
             c0 = c1;
         }
     }
-    if (row < rb) {
+    if (rvalid) {
         if (sel_a >= 0) bsel[((size_t)p * stride + row) * 2] = sel_a;
         if (sel_b >= 0) bsel[((size_t)p * stride + row) * 2 + 1] = sel_b;
     }
     partL[sl][r] = L;
     partU[sl][r] = U;
     __syncthreads();
-    if (sl == 0 && row < rb) {
+    if (sl == 0 && rvalid) {
         for (int q = 1; q < NS; q++) {
             L += partL[q][r];
             U += partU[q][r];
@@ -1980,6 +1987,93 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
         // sequential sum
         lb[(size_t)p * stride + row] = hi > lo ? ((double)L / w) * (1.0 - 2e-4) : 0.0;
         ub[(size_t)p * stride + row] = hi > lo ? ((double)U / w) * (1.0 + 2e-4) : 0.0;
+    }
+}
+
+// Lipschitz pre-pruning (before the full bounds pass).  The trimmed mean T(x) of the distances
+// from x to the set is 1-Lipschitz in x (every distance is, so are the order statistics and
+// their mean): T(i) >= T(c) - d(i, c).  The bounds kernel first runs on the reference rows
+// c = 0, kLipStep, 2 kLipStep, ... (1/16 of the rows); with U = their smallest UB, a row i with
+// d(i, c) < LB(c) - U for some reference c has T(i) > U >= the final min UB, so it cannot be the
+// argmin and skips the K-column histogram pass.  The test runs in squared f32 distances against
+// per-reference thresholds thr_c = (LB_c (1 - 1e-5) - U (1 + 1e-5))^2 (1 - 1e-5): the 1e-5
+// margins cover the f32 rounding of s (<= 5u), the reference's own f32 distances and fp64 sum
+// (<= 4u relative) and the rounding of thr, so a pruned row's LB = U (1 + 5e-6) is rigorous and
+// strictly above every UB that select compares against.  Pruned rows get [LB, +inf) and no
+// boundary bins (select drops them); the others are appended (any order) to the per-pair list
+// that the second bounds pass reads.  Synthetic configs[1] pairs (one cluster of ~1e4 valid
+// rotations): ~80 % of the rows are pruned for ~1/16 + ~1/20 of the full pass's distances.
+constexpr int kLipStep = 16;    // every 16th row is a reference row
+constexpr int kLipMinK = 1024;  // smaller sets: no pre-pruning (every non-reference row listed)
+constexpr int kLipChunk = 1024; // reference rows staged in LDS per chunk
+
+__global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride, double trim_lo,
+    double trim_hi, double* __restrict__ lb, double* __restrict__ ub, int32_t* __restrict__ rlist,
+    int32_t* __restrict__ rcount) {
+    __shared__ float4 refs[kLipChunk];
+    __shared__ double red[4];
+    const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
+    const int K = kcount[p];
+    const int i0 = blockIdx.x * 256;
+    if (i0 >= K) return;
+    const float* X = rv + (size_t)p * 3 * stride;
+    const float* Y = X + stride;
+    const float* Z = Y + stride;
+    double* LBp = lb + (size_t)p * stride;
+    double* UBp = ub + (size_t)p * stride;
+    const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
+    const int nref = (K + kLipStep - 1) / kLipStep;
+    bool prune_on = K >= kLipMinK && hi > lo;
+    double U = __builtin_huge_val();
+    if (prune_on) {
+        for (int c = tid; c < nref; c += 256) U = fmin(U, UBp[c * kLipStep]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) U = fmin(U, __shfl_xor(U, o, 64));
+        if (lane == 0) red[tid >> 6] = U;
+        __syncthreads();
+        U = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+        prune_on = U > 0.0 && U < __builtin_huge_val();
+    }
+    const int i = i0 + tid;
+    const bool active = i < K && (i % kLipStep) != 0;
+    const float xi = active ? X[i] : 0.f, yi = active ? Y[i] : 0.f, zi = active ? Z[i] : 0.f;
+    bool pruned = false;
+    if (prune_on) {
+        const double Um = U * (1.0 + 1e-5);
+        for (int c0 = 0; c0 < nref; c0 += kLipChunk) {
+            const int n = min(kLipChunk, nref - c0);
+            __syncthreads();  // the previous chunk's readers are done
+            for (int c = tid; c < n; c += 256) {
+                const int row = (c0 + c) * kLipStep;
+                const double a = LBp[row] * (1.0 - 1e-5) - Um;
+                const float thr = a > 0.0 ? (float)(a * a * (1.0 - 1e-5)) : -1.f;
+                refs[c] = make_float4(X[row], Y[row], Z[row], thr);
+            }
+            __syncthreads();
+            for (int c = 0; c < n; c += 64) {
+                if (__builtin_amdgcn_ballot_w64(active && !pruned) == 0) break;  // wave-uniform
+                const int ce = min(c + 64, n);
+                for (int q = c; q < ce; q++) {
+                    const float4 r = refs[q];
+                    const float dx = xi - r.x, dy = yi - r.y, dz = zi - r.z;
+                    const float s = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+                    pruned = pruned || s < r.w;
+                }
+            }
+        }
+    }
+    if (active && pruned) {
+        LBp[i] = U * (1.0 + 5e-6);
+        UBp[i] = __builtin_huge_val();
+    }
+    const bool keep = active && !pruned;
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
+    if (bal) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&rcount[p], __builtin_popcountll(bal));
+        base = __shfl(base, 0, 64);
+        if (keep) rlist[(size_t)p * stride + base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = i;
     }
 }
 
@@ -2440,9 +2534,9 @@ __device__ double exact_row_mean(const float* X, const float* Y, const float* Z,
 __global__ __launch_bounds__(1024) void consensus_final_kernel(
     const int32_t* __restrict__ counts, const int32_t* __restrict__ kcount,
     const float* __restrict__ rv, const float* __restrict__ tv, const double* __restrict__ tmean,
-    const int32_t* __restrict__ flags, const int32_t* __restrict__ nsurv, int stride, int npow2,
-    double sample_frac, double trim_lo, double trim_hi, float* __restrict__ sortbuf,
-    erp_pair_result* __restrict__ results) {
+    const int32_t* __restrict__ flags, const int32_t* __restrict__ nsurv,
+    const int32_t* __restrict__ nbin, int stride, int npow2, double sample_frac, double trim_lo,
+    double trim_hi, float* __restrict__ sortbuf, erp_pair_result* __restrict__ results) {
     __shared__ double sv[1024];
     __shared__ int si[1024];
     __shared__ int cand[64];
@@ -2463,7 +2557,7 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     r.min_idx = -1;
     r.near_ties = 0;
     r.survivors = nsurv[p];
-    r.reserved = 0;
+    r.binned_rows = nbin[p] < 0 ? K : (K + kLipStep - 1) / kLipStep + nbin[p];
     r.min_dist = 0.0;
     const int fl = flags ? flags[p] : 0;
     if (fl & 1) r.status = ERP_TOO_FEW_POINTS;
@@ -2798,12 +2892,37 @@ size_t consensus_edges_bytes(int n_pairs) { return (size_t)n_pairs * 2 * kNB * s
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
-                                   int shard, int nshards, hipStream_t st) {
+                                   int shard, int nshards, int32_t* rlist, int32_t* rcount,
+                                   hipStream_t st) {
     hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
-    const int rows = (2 * sh.iters + nshards - 1) / nshards + 1;  // >= any shard's rows
-    dim3 grid((rows + kBoundRows - 1) / kBoundRows, sh.n_pairs);
-    hipLaunchKernelGGL(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale, edges,
-                       2 * sh.iters, trim_lo, trim_hi, lb, ub, bsel, shard, nshards);
+    const int stride = 2 * sh.iters;
+    if (nshards > 1 || !rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
+        if (rcount) {
+            const hipError_t me = hipMemsetAsync(rcount, 0xFF, sizeof(int32_t) * sh.n_pairs, st);
+            if (me != hipSuccess) return me;
+        }
+        const int rows = (stride + nshards - 1) / nshards + 1;  // >= any shard's rows
+        dim3 grid((rows + kBoundRows - 1) / kBoundRows, sh.n_pairs);
+        hipLaunchKernelGGL(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
+                           edges, stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, 1,
+                           (const int32_t*)nullptr, (const int32_t*)nullptr);
+        return hipGetLastError();
+    }
+    // reference rows, Lipschitz pre-pruning, then the rows it kept
+    const int nref = (stride + kLipStep - 1) / kLipStep;
+    dim3 g1((nref + kBoundRows - 1) / kBoundRows, sh.n_pairs);
+    hipLaunchKernelGGL(consensus_bounds_kernel, g1, dim3(256), 0, st, kcount, rv, dscale, edges,
+                       stride, trim_lo, trim_hi, lb, ub, bsel, 0, 1, kLipStep,
+                       (const int32_t*)nullptr, (const int32_t*)nullptr);
+    const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * sh.n_pairs, st);
+    if (me != hipSuccess) return me;
+    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 255) / 256, sh.n_pairs),
+                       dim3(256), 0, st, kcount, rv, stride, trim_lo, trim_hi, lb, ub, rlist,
+                       rcount);
+    dim3 g2((stride + kBoundRows - 1) / kBoundRows, sh.n_pairs);
+    hipLaunchKernelGGL(consensus_bounds_kernel, g2, dim3(256), 0, st, kcount, rv, dscale, edges,
+                       stride, trim_lo, trim_hi, lb, ub, bsel, 0, 1, 1, (const int32_t*)rlist,
+                       (const int32_t*)rcount);
     return hipGetLastError();
 }
 
@@ -2842,11 +2961,11 @@ int sortbuf_len(int iters) {
 
 hipError_t launch_consensus_final(const int32_t* counts, const int32_t* kcount, const float* rv,
                                   const float* tv, const double* tmean, const int32_t* flags,
-                                  const int32_t* nsurv, const BatchShape& sh, double sample_frac,
-                                  double trim_lo, double trim_hi, float* sortbuf,
-                                  erp_pair_result* results, hipStream_t st) {
+                                  const int32_t* nsurv, const int32_t* nbin, const BatchShape& sh,
+                                  double sample_frac, double trim_lo, double trim_hi,
+                                  float* sortbuf, erp_pair_result* results, hipStream_t st) {
     hipLaunchKernelGGL(consensus_final_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, kcount,
-                       rv, tv, tmean, flags, nsurv, 2 * sh.iters, sortbuf_len(sh.iters), sample_frac,
+                       rv, tv, tmean, flags, nsurv, nbin, 2 * sh.iters, sortbuf_len(sh.iters), sample_frac,
                        trim_lo, trim_hi, sortbuf, results);
     return hipGetLastError();
 }

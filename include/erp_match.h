@@ -107,7 +107,8 @@ typedef struct erp_pair_result {
     int32_t sample_n;    /* (int)(M * sample_frac) */
     int32_t near_ties;   /* rows re-scored exactly by the near-tie resolver */
     int32_t survivors;   /* rows whose trimmed-mean bounds did not exclude them */
-    int32_t reserved;
+    int32_t binned_rows; /* rows whose K-column distance histogram was built (K, or the
+                            reference rows + the rows Lipschitz pre-pruning kept) */
     double min_dist;     /* trimmed-mean distance of the winner */
 } erp_pair_result;
 

@@ -555,3 +555,51 @@ def test_consensus_bounds_wide_dynamic_range(ctx, oracle, case):
     assert res["status"] == 0 and res["K"] == K
     assert res["min_idx"] == mi or np.array_equal(rv[res["min_idx"]], rv[mi])
     assert abs(res["min_dist"] - dref[mi]) <= 1e-12 * abs(dref[mi])
+
+
+@pytest.mark.parametrize("case", ["cluster", "cluster_outliers", "shell", "uniform_cube",
+                                  "two_clusters"])
+def test_consensus_lipschitz_prepruning(ctx, oracle, case):
+    """K >= 1024: the bounds pass first bins every 16th row, rows provably beaten through the
+    1-Lipschitz bound T(i) >= T(c) - d(i, c) skip the histogram pass.  The winner and its mean
+    stay exact; on a single cluster most rows are pruned (binned_rows well below K); on a shell
+    (every mean nearly equal) little is pruned and the result is still exact."""
+    from erp_match_eightpoint_test_amd import dist as D
+    rng = np.random.default_rng({"cluster": 11, "cluster_outliers": 12, "shell": 13,
+                                 "uniform_cube": 14, "two_clusters": 15}[case])
+    K = 6000
+    if case == "cluster":
+        rv = rng.standard_normal((K, 3)) * 6e-5 + np.array([0.09, 0.24, 0.26])
+    elif case == "cluster_outliers":
+        rv = rng.standard_normal((K, 3)) * 6e-5 + np.array([0.09, 0.24, 0.26])
+        far = rng.choice(K, 300, replace=False)
+        rv[far] = rng.uniform(-1.5, 1.5, (300, 3))
+    elif case == "shell":
+        v = rng.standard_normal((K, 3))
+        rv = 0.01 * v / np.linalg.norm(v, axis=1, keepdims=True) + 0.2
+    elif case == "uniform_cube":
+        rv = rng.uniform(-1.0, 1.0, (K, 3))
+    else:
+        a = rng.standard_normal((K // 2, 3)) * 6e-5 + np.array([0.1, 0.2, 0.3])
+        b = rng.standard_normal((K - K // 2, 3)) * 6e-5 + np.array([-1.2, 0.9, 0.4])
+        rv = np.concatenate([a, b])[rng.permutation(K)]
+    rv = rv.astype(np.float32)
+    tv = rng.standard_normal((K, 3)).astype(np.float32)
+    _, mi, dref = oracle.consensus(rv)
+    res = D.gpu_consensus(ctx, "cuda")(rv, tv)
+    assert res["status"] == 0 and res["K"] == K
+    assert res["min_idx"] == mi or np.array_equal(rv[res["min_idx"]], rv[mi])
+    assert abs(res["min_dist"] - dref[mi]) <= 1e-12 * abs(dref[mi])
+    assert (K + 15) // 16 <= res["binned_rows"] <= K
+    if case in ("cluster", "cluster_outliers", "uniform_cube"):
+        assert res["binned_rows"] < K // 2, res["binned_rows"]
+
+
+def test_consensus_small_set_bins_every_row(ctx, oracle):
+    """below 1024 rows there is no pre-pruning: every row is binned."""
+    from erp_match_eightpoint_test_amd import dist as D
+    rng = np.random.default_rng(31)
+    rv = (rng.standard_normal((900, 3)) * 0.01).astype(np.float32)
+    _, mi, _ = oracle.consensus(rv)
+    res = D.gpu_consensus(ctx, "cuda")(rv, np.zeros_like(rv))
+    assert res["min_idx"] == mi and res["binned_rows"] == 900
