@@ -1822,7 +1822,7 @@ __global__ __launch_bounds__(256) void consensus_edges_kernel(const float* __res
     }
 }
 
-__global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __restrict__ kcount,
+__device__ __forceinline__ void consensus_bounds_unit(const int32_t* __restrict__ kcount,
                                                                const float* __restrict__ rv,
                                                                const float* __restrict__ dscale,
                                                                const float* __restrict__ edges,
@@ -1833,7 +1833,7 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
                                                                int32_t* __restrict__ bsel,
                                                                int shard, int nshards, int rstep,
                                                                const int32_t* __restrict__ rlist,
-                                                               const int32_t* __restrict__ rcount) {
+                                                               const int32_t* __restrict__ rcount, int p, int bx) {
     constexpr int R = kBoundRows;
     constexpr int NS = 256 / R;        // epilogue slices per row
     constexpr int per = kNB / NS;      // bins per slice
@@ -1843,7 +1843,7 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     int (*part)[R] = reinterpret_cast<int (*)[R]>(hist);
     float (*partL)[R] = reinterpret_cast<float (*)[R]>(hist + NS * R);
     float (*partU)[R] = reinterpret_cast<float (*)[R]>(hist + 2 * NS * R);
-    const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
+    const int tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
     // rows [ra, rb) of this shard (hypothesis-block sharding of one find over ranks; 0 / 1
     // otherwise), every rstep-th of them (the reference rows of the Lipschitz pre-pruning), or
@@ -1851,7 +1851,7 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
     const int ra = (int)((int64_t)K * shard / nshards);
     const int rb = (int)((int64_t)K * (shard + 1) / nshards);
     const int nloc = rlist ? rcount[p] : (rb > ra ? (rb - ra + rstep - 1) / rstep : 0);
-    const int l0 = blockIdx.x * R;
+    const int l0 = bx * R;
     if (l0 >= nloc) return;
     const int32_t* RL = rlist ? rlist + (size_t)p * stride : nullptr;
     auto rowof = [&](int l) { return RL ? (int)RL[l] : ra + l * rstep; };
@@ -1988,6 +1988,16 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(const int32_t* __
         lb[(size_t)p * stride + row] = hi > lo ? ((double)L / w) * (1.0 - 2e-4) : 0.0;
         ub[(size_t)p * stride + row] = hi > lo ? ((double)U / w) * (1.0 + 2e-4) : 0.0;
     }
+}
+
+// one unit (R rows) per block: every row of a shard, or every rstep-th row
+__global__ __launch_bounds__(256) void consensus_bounds_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv,
+    const float* __restrict__ dscale, const float* __restrict__ edges, int stride, double trim_lo,
+    double trim_hi, double* __restrict__ lb, double* __restrict__ ub, int32_t* __restrict__ bsel,
+    int shard, int nshards, int rstep) {
+    consensus_bounds_unit(kcount, rv, dscale, edges, stride, trim_lo, trim_hi, lb, ub, bsel, shard,
+                          nshards, rstep, nullptr, nullptr, blockIdx.y, blockIdx.x);
 }
 
 // Lipschitz pre-pruning (before the full bounds pass).  The trimmed mean T(x) of the distances
@@ -2253,6 +2263,57 @@ __device__ bool item_to_pair(int g, int n_pairs, UNITS units, int* p_out, int* u
         base += n;
     }
     return false;
+}
+
+// the rows of the per-pair lists (Lipschitz survivors): (pair, unit) items of all pairs
+// flattened, so the live units are the first blocks of the grid (the list lengths are only
+// known on the device; a [unit][pair] grid sized for full lists would interleave ~80 % empty
+// blocks with the live ones).  uoff = exclusive prefix of the per-pair unit counts
+// (list_prefix_kernel); item g belongs to the pair p with uoff[p] <= g < uoff[p + 1].
+__global__ __launch_bounds__(1024) void list_prefix_kernel(const int32_t* __restrict__ rcount,
+                                                           int n_pairs,
+                                                           int32_t* __restrict__ uoff) {
+    __shared__ int ws[16];
+    __shared__ int carry;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (int q0 = 0; q0 < n_pairs; q0 += 1024) {
+        const int q = q0 + tid;
+        const int u = q < n_pairs ? (rcount[q] + kBoundRows - 1) / kBoundRows : 0;
+        int x = u;  // inclusive wave scan
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) ws[w] = x;
+        __syncthreads();
+        int before = carry;
+        for (int k = 0; k < w; k++) before += ws[k];
+        if (q < n_pairs) uoff[q] = before + x - u;
+        __syncthreads();
+        if (tid == 1023) carry = before + x;
+        __syncthreads();
+    }
+    if (tid == 0) uoff[n_pairs] = carry;
+}
+
+__global__ __launch_bounds__(256) void consensus_bounds_list_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv,
+    const float* __restrict__ dscale, const float* __restrict__ edges, int stride, double trim_lo,
+    double trim_hi, double* __restrict__ lb, double* __restrict__ ub, int32_t* __restrict__ bsel,
+    const int32_t* __restrict__ rlist, const int32_t* __restrict__ rcount,
+    const int32_t* __restrict__ uoff, int n_pairs) {
+    const int g = blockIdx.x;  // one unit per block (a loop over units doubles the VGPRs)
+    if (g >= uoff[n_pairs]) return;
+    int a = 0, b = n_pairs;  // largest p with uoff[p] <= g
+    while (b - a > 1) {
+        const int m = (a + b) >> 1;
+        if (uoff[m] <= g) a = m; else b = m;
+    }
+    consensus_bounds_unit(kcount, rv, dscale, edges, stride, trim_lo, trim_hi, lb, ub, bsel, 0, 1,
+                          1, rlist, rcount, a, g - uoff[a]);
 }
 
 __global__ __launch_bounds__(256) void consensus_refine_kernel(
@@ -2904,25 +2965,29 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
         const int rows = (stride + nshards - 1) / nshards + 1;  // >= any shard's rows
         dim3 grid((rows + kBoundRows - 1) / kBoundRows, sh.n_pairs);
         hipLaunchKernelGGL(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
-                           edges, stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, 1,
-                           (const int32_t*)nullptr, (const int32_t*)nullptr);
+                           edges, stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, 1);
         return hipGetLastError();
     }
     // reference rows, Lipschitz pre-pruning, then the rows it kept
     const int nref = (stride + kLipStep - 1) / kLipStep;
     dim3 g1((nref + kBoundRows - 1) / kBoundRows, sh.n_pairs);
     hipLaunchKernelGGL(consensus_bounds_kernel, g1, dim3(256), 0, st, kcount, rv, dscale, edges,
-                       stride, trim_lo, trim_hi, lb, ub, bsel, 0, 1, kLipStep,
-                       (const int32_t*)nullptr, (const int32_t*)nullptr);
+                       stride, trim_lo, trim_hi, lb, ub, bsel, 0, 1, kLipStep);
     const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * sh.n_pairs, st);
     if (me != hipSuccess) return me;
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 255) / 256, sh.n_pairs),
                        dim3(256), 0, st, kcount, rv, stride, trim_lo, trim_hi, lb, ub, rlist,
                        rcount);
-    dim3 g2((stride + kBoundRows - 1) / kBoundRows, sh.n_pairs);
-    hipLaunchKernelGGL(consensus_bounds_kernel, g2, dim3(256), 0, st, kcount, rv, dscale, edges,
-                       stride, trim_lo, trim_hi, lb, ub, bsel, 0, 1, 1, (const int32_t*)rlist,
-                       (const int32_t*)rcount);
+    int32_t* uoff = rcount + sh.n_pairs;  // [n_pairs + 1] after the counts
+    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)rcount,
+                       sh.n_pairs, uoff);
+    // one block per unit of the longest possible lists: the live units come first in dispatch
+    // order, the trailing blocks exit after one load
+    const int max_units = sh.n_pairs * ((stride + kBoundRows - 1) / kBoundRows);
+    hipLaunchKernelGGL(consensus_bounds_list_kernel, dim3(max_units), dim3(256), 0, st,
+                       kcount, rv, dscale, edges, stride, trim_lo, trim_hi, lb, ub, bsel,
+                       (const int32_t*)rlist, (const int32_t*)rcount, (const int32_t*)uoff,
+                       sh.n_pairs);
     return hipGetLastError();
 }
 

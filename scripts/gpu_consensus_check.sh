@@ -16,3 +16,6 @@ for K in (2000, 6000, 20000):
 PY
 echo "== bench" && timeout -k 10 600 python bench.py --no-cpu-baseline > gpurun_out/bench_dev.json 2> gpurun_out/bench_dev.err || { tail -20 gpurun_out/bench_dev.err; exit 1; }
 python -c "import json; d=json.loads(open('gpurun_out/bench_dev.json').read().strip().splitlines()[-1]); print(d['value'], d['roofline_stages']['consensus_bounds'], d['stages_ms_serial_step']['consensus_bounds'])"
+export TMPDIR=/tmp
+echo "== rocprof" && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dev -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 0 --warmup 1 --pairs 128 --streams 1 > gpurun_out/prof_dev.log 2>&1 || { tail -20 gpurun_out/prof_dev.log; exit 1; }
+find gpurun_out/prof_dev -name "*kernel_stats.csv" | head -1 | xargs -I{} sh -c 'cut -d, -f1-5 {} | head -30'
