@@ -2023,9 +2023,10 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     int32_t* __restrict__ rcount) {
     __shared__ float4 refs[kLipChunk];
     __shared__ double red[4];
+    __shared__ int nlive;
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
-    const int i0 = blockIdx.x * 256;
+    const int i0 = blockIdx.x * 512;  // two rows per thread: i0 + tid and i0 + 256 + tid
     if (i0 >= K) return;
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
@@ -2045,45 +2046,67 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
         U = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
         prune_on = U > 0.0 && U < __builtin_huge_val();
     }
-    const int i = i0 + tid;
-    const bool active = i < K && (i % kLipStep) != 0;
-    const float xi = active ? X[i] : 0.f, yi = active ? Y[i] : 0.f, zi = active ? Z[i] : 0.f;
-    bool pruned = false;
+    int ii[2];
+    bool active[2];
+    f32x2 xi, yi, zi;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        ii[h] = i0 + 256 * h + tid;
+        active[h] = ii[h] < K && (ii[h] % kLipStep) != 0;
+        xi[h] = active[h] ? X[ii[h]] : 0.f;
+        yi[h] = active[h] ? Y[ii[h]] : 0.f;
+        zi[h] = active[h] ? Z[ii[h]] : 0.f;
+    }
+    // sign bits of s - thr over the references: negative for some c = pruned
+    uint32_t neg0 = 0u, neg1 = 0u;
     if (prune_on) {
         const double Um = U * (1.0 + 1e-5);
         for (int c0 = 0; c0 < nref; c0 += kLipChunk) {
             const int n = min(kLipChunk, nref - c0);
             __syncthreads();  // the previous chunk's readers are done
+            if (tid == 0) nlive = 0;
+            __syncthreads();
+            // only references with LB_c > U (1 + 1e-5) can prune: compacted (any order)
             for (int c = tid; c < n; c += 256) {
                 const int row = (c0 + c) * kLipStep;
                 const double a = LBp[row] * (1.0 - 1e-5) - Um;
-                const float thr = a > 0.0 ? (float)(a * a * (1.0 - 1e-5)) : -1.f;
-                refs[c] = make_float4(X[row], Y[row], Z[row], thr);
+                if (a > 0.0) {
+                    const float thr = (float)(a * a * (1.0 - 1e-5));
+                    refs[atomicAdd(&nlive, 1)] = make_float4(X[row], Y[row], Z[row], thr);
+                }
             }
             __syncthreads();
-            for (int c = 0; c < n; c += 64) {
-                if (__builtin_amdgcn_ballot_w64(active && !pruned) == 0) break;  // wave-uniform
-                const int ce = min(c + 64, n);
-                for (int q = c; q < ce; q++) {
-                    const float4 r = refs[q];
-                    const float dx = xi - r.x, dy = yi - r.y, dz = zi - r.z;
-                    const float s = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
-                    pruned = pruned || s < r.w;
-                }
+            const int m = nlive;
+            for (int q = 0; q < m; q++) {
+                const float4 r = refs[q];
+                const f32x2 dx = xi - r.x, dy = yi - r.y, dz = zi - r.z;
+                f32x2 s = dx * dx;
+                s = __builtin_elementwise_fma(dy, dy, s);
+                s = __builtin_elementwise_fma(dz, dz, s);
+                const f32x2 t = s - r.w;
+                neg0 |= __float_as_uint(t[0]);
+                neg1 |= __float_as_uint(t[1]);
             }
         }
     }
-    if (active && pruned) {
-        LBp[i] = U * (1.0 + 5e-6);
-        UBp[i] = __builtin_huge_val();
-    }
-    const bool keep = active && !pruned;
-    const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
-    if (bal) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&rcount[p], __builtin_popcountll(bal));
-        base = __shfl(base, 0, 64);
-        if (keep) rlist[(size_t)p * stride + base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = i;
+    const bool pr[2] = {(neg0 >> 31) != 0u, (neg1 >> 31) != 0u};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int i = ii[h];
+        const bool pruned = active[h] && pr[h];
+        if (pruned) {
+            LBp[i] = U * (1.0 + 5e-6);
+            UBp[i] = __builtin_huge_val();
+        }
+        const bool keep = active[h] && !pr[h];
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
+        if (bal) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(&rcount[p], __builtin_popcountll(bal));
+            base = __shfl(base, 0, 64);
+            if (keep)
+                rlist[(size_t)p * stride + base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = i;
+        }
     }
 }
 
@@ -2975,7 +2998,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                        stride, trim_lo, trim_hi, lb, ub, bsel, 0, 1, kLipStep);
     const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * sh.n_pairs, st);
     if (me != hipSuccess) return me;
-    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 255) / 256, sh.n_pairs),
+    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, sh.n_pairs),
                        dim3(256), 0, st, kcount, rv, stride, trim_lo, trim_hi, lb, ub, rlist,
                        rcount);
     int32_t* uoff = rcount + sh.n_pairs;  // [n_pairs + 1] after the counts
