@@ -2273,6 +2273,19 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
 // Work items of all pairs flattened: item g of the batch = (pair p, unit u); the per-pair unit
 // counts are only known on the device, so every block forms their prefix sums and strides
 // over the items (one launch of a fixed grid, no empty blocks, pairs balanced).
+// the same from uoff = exclusive prefix of the per-pair unit counts (list_prefix_kernel; one
+// binary search instead of a sequential walk over the pairs' counts per item)
+__device__ __forceinline__ void pair_of_item(const int32_t* __restrict__ uoff, int n_pairs, int g,
+                                             int* p_out, int* u_out) {
+    int a = 0, b = n_pairs;  // largest p with uoff[p] <= g
+    while (b - a > 1) {
+        const int m = (a + b) >> 1;
+        if (uoff[m] <= g) a = m; else b = m;
+    }
+    *p_out = a;
+    *u_out = g - uoff[a];
+}
+
 template <typename UNITS>
 __device__ bool item_to_pair(int g, int n_pairs, UNITS units, int* p_out, int* u_out) {
     int base = 0;
@@ -2294,7 +2307,7 @@ __device__ bool item_to_pair(int g, int n_pairs, UNITS units, int* p_out, int* u
 // blocks with the live ones).  uoff = exclusive prefix of the per-pair unit counts
 // (list_prefix_kernel); item g belongs to the pair p with uoff[p] <= g < uoff[p + 1].
 __global__ __launch_bounds__(1024) void list_prefix_kernel(const int32_t* __restrict__ rcount,
-                                                           int n_pairs,
+                                                           int n_pairs, int div, int minc,
                                                            int32_t* __restrict__ uoff) {
     __shared__ int ws[16];
     __shared__ int carry;
@@ -2303,7 +2316,8 @@ __global__ __launch_bounds__(1024) void list_prefix_kernel(const int32_t* __rest
     __syncthreads();
     for (int q0 = 0; q0 < n_pairs; q0 += 1024) {
         const int q = q0 + tid;
-        const int u = q < n_pairs ? (rcount[q] + kBoundRows - 1) / kBoundRows : 0;
+        const int c = q < n_pairs ? rcount[q] : 0;  // units: ceil(c / div), none if c <= minc
+        const int u = c > minc ? (c + div - 1) / div : 0;
         int x = u;  // inclusive wave scan
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
@@ -2344,16 +2358,11 @@ __global__ __launch_bounds__(256) void consensus_refine_kernel(
     const float* __restrict__ dscale, int stride, double trim_lo, double trim_hi,
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
     const int32_t* __restrict__ bsel, double* __restrict__ lb, double* __restrict__ ub,
-    int n_pairs) {
-    auto units = [&](int p) {
-        const int ns = nsurv[p];
-        return ns > kRefineMin ? (ns + kRefineRows - 1) / kRefineRows : 0;
-    };
-    int total = 0;
-    for (int p = 0; p < n_pairs; p++) total += units(p);
+    const int32_t* __restrict__ uoff, int n_pairs) {
+    const int total = uoff[n_pairs];  // units: ceil(nsurv / kRefineRows) where nsurv > kRefineMin
     for (int g = blockIdx.x; g < total; g += gridDim.x) {
         int p, u;
-        item_to_pair(g, n_pairs, units, &p, &u);
+        pair_of_item(uoff, n_pairs, g, &p, &u);
         __syncthreads();  // the previous item's LDS readers are done
         consensus_refine_block(kcount, rv, dscale, stride, trim_lo, trim_hi, surv, nsurv, bsel,
                                lb, ub, p, u);
@@ -2508,13 +2517,12 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv,
     const float* __restrict__ dscale, int stride, double trim_lo, double trim_hi,
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
-    const int32_t* __restrict__ bsel, double* __restrict__ tmean, int n_pairs) {
-    auto units = [&](int p) { return nsurv[p]; };
-    int total = 0;
-    for (int p = 0; p < n_pairs; p++) total += units(p);
+    const int32_t* __restrict__ bsel, double* __restrict__ tmean, const int32_t* __restrict__ uoff,
+    int n_pairs) {
+    const int total = uoff[n_pairs];  // one unit per survivor
     for (int g = blockIdx.x; g < total; g += gridDim.x) {
         int p, u;
-        item_to_pair(g, n_pairs, units, &p, &u);
+        pair_of_item(uoff, n_pairs, g, &p, &u);
         __syncthreads();  // the previous row's LDS readers are done
         consensus_rows_block(kcount, rv, dscale, stride, trim_lo, trim_hi, surv, nsurv, bsel,
                              tmean, p, u);
@@ -3003,7 +3011,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                        rcount);
     int32_t* uoff = rcount + sh.n_pairs;  // [n_pairs + 1] after the counts
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)rcount,
-                       sh.n_pairs, uoff);
+                       sh.n_pairs, kBoundRows, 0, uoff);
     // one block per unit of the longest possible lists: the live units come first in dispatch
     // order, the trailing blocks exit after one load
     const int max_units = sh.n_pairs * ((stride + kBoundRows - 1) / kBoundRows);
@@ -3027,8 +3035,13 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
                                    const BatchShape& sh, double trim_lo, double trim_hi,
                                    const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
                                    double* lb, double* ub, hipStream_t st) {
+    // unit prefix in the scratch after nsurv[n_pairs] and the list counts[n_pairs]
+    int32_t* uoff = const_cast<int32_t*>(nsurv) + 2 * sh.n_pairs;
+    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, sh.n_pairs,
+                       kRefineRows, kRefineMin, uoff);
     hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
-                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, sh.n_pairs);
+                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub,
+                       (const int32_t*)uoff, sh.n_pairs);
     return hipGetLastError();
 }
 
@@ -3036,8 +3049,12 @@ hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const f
                                  const BatchShape& sh, double trim_lo, double trim_hi,
                                  const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
                                  double* tmean, hipStream_t st) {
+    int32_t* uoff = const_cast<int32_t*>(nsurv) + 2 * sh.n_pairs;  // as in launch_consensus_refine
+    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, sh.n_pairs, 1, 0,
+                       uoff);
     hipLaunchKernelGGL(consensus_rows_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
-                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, tmean, sh.n_pairs);
+                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, tmean,
+                       (const int32_t*)uoff, sh.n_pairs);
     return hipGetLastError();
 }
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # consensus GPU tests + binned-row counts of single-cluster sets (Lipschitz pre-pruning)
-cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread -k "consensus_lipschitz or consensus_small" > gpurun_out/pytest_cons.log 2>&1; rc=$?; tail -15 gpurun_out/pytest_cons.log; [ $rc -ne 0 ] && exit $rc
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -p no:cacheprovider --timeout 200 --timeout-method thread -k "consensus or batch or find" > gpurun_out/pytest_cons.log 2>&1; rc=$?; tail -15 gpurun_out/pytest_cons.log; [ $rc -ne 0 ] && exit $rc
 python - <<'PY'
 import numpy as np, sys
 sys.path.insert(0, ".")
