@@ -303,7 +303,7 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->dscale, P * 4) && ensure(c->lb, P * 2 * sh.iters * 8) &&
               ensure(c->ub, P * 2 * sh.iters * 8) && ensure(c->surv, P * 2 * sh.iters * 4) &&
               ensure(c->bsel, P * 2 * sh.iters * 8) && ensure(c->edges, erp::consensus_edges_bytes((int)P)) &&
-              ensure(c->nsurv, P * 12 + 4) && ensure(c->vchunk, erp::valid_chunk_bytes(sh));
+              ensure(c->nsurv, P * 16 + 4) && ensure(c->vchunk, erp::valid_chunk_bytes(sh));
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
     if (ok && !(out && out->dist)) ok = ensure(c->tmean, P * 2 * sh.iters * 8);
@@ -427,7 +427,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
                                             bselp, lbp,
-                                            ubp, st));
+                                            ubp, (int32_t*)c->sortbuf.p, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);

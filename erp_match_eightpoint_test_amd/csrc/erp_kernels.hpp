@@ -142,7 +142,7 @@ hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, cons
 hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const float* dscale,
                                    const BatchShape& sh, double trim_lo, double trim_hi,
                                    const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
-                                   double* lb, double* ub, hipStream_t st);
+                                   double* lb, double* ub, int32_t* list2, hipStream_t st);
 hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const float* dscale,
                                  const BatchShape& sh, double trim_lo, double trim_hi,
                                  const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,

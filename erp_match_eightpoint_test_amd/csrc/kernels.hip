@@ -2019,26 +2019,34 @@ constexpr int kLipChunk = 1024; // reference rows staged in LDS per chunk
 
 __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride, double trim_lo,
-    double trim_hi, double* __restrict__ lb, double* __restrict__ ub, int32_t* __restrict__ rlist,
-    int32_t* __restrict__ rcount) {
+    double trim_hi, double* __restrict__ lb, double* __restrict__ ub,
+    const int32_t* __restrict__ slist, const int32_t* __restrict__ scount,
+    int32_t* __restrict__ rlist, int olstride, int32_t* __restrict__ rcount) {
+    // slist == nullptr: the K rows (before the histogram pass); else the per-pair survivor list
+    // slist[p][0 .. scount[p]) after the first select (before the refine pass, whose reference
+    // survivors, every 16th, are already refined)
     __shared__ float4 refs[kLipChunk];
     __shared__ double red[4];
     __shared__ int nlive;
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
-    const int i0 = blockIdx.x * 512;  // two rows per thread: i0 + tid and i0 + 256 + tid
-    if (i0 >= K) return;
+    const int n = slist ? scount[p] : K;
+    const int i0 = blockIdx.x * 512;  // two positions per thread: i0 + tid and i0 + 256 + tid
+    if (i0 >= n) return;
+    if (slist && n <= kRefineMin) return;  // few survivors: no refine pass, nothing to list
+    const int32_t* SL = slist ? slist + (size_t)p * stride : nullptr;
+    auto rowpos = [&](int k) { return SL ? (int)SL[k] : k; };
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
     double* LBp = lb + (size_t)p * stride;
     double* UBp = ub + (size_t)p * stride;
     const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
-    const int nref = (K + kLipStep - 1) / kLipStep;
-    bool prune_on = K >= kLipMinK && hi > lo;
+    const int nref = (n + kLipStep - 1) / kLipStep;
+    bool prune_on = (SL ? n > kRefineMin : K >= kLipMinK) && hi > lo;
     double U = __builtin_huge_val();
     if (prune_on) {
-        for (int c = tid; c < nref; c += 256) U = fmin(U, UBp[c * kLipStep]);
+        for (int c = tid; c < nref; c += 256) U = fmin(U, UBp[rowpos(c * kLipStep)]);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) U = fmin(U, __shfl_xor(U, o, 64));
         if (lane == 0) red[tid >> 6] = U;
@@ -2051,8 +2059,9 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     f32x2 xi, yi, zi;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        ii[h] = i0 + 256 * h + tid;
-        active[h] = ii[h] < K && (ii[h] % kLipStep) != 0;
+        const int k = i0 + 256 * h + tid;
+        active[h] = k < n && (k % kLipStep) != 0;
+        ii[h] = active[h] ? rowpos(k) : 0;
         xi[h] = active[h] ? X[ii[h]] : 0.f;
         yi[h] = active[h] ? Y[ii[h]] : 0.f;
         zi[h] = active[h] ? Z[ii[h]] : 0.f;
@@ -2062,13 +2071,13 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     if (prune_on) {
         const double Um = U * (1.0 + 1e-5);
         for (int c0 = 0; c0 < nref; c0 += kLipChunk) {
-            const int n = min(kLipChunk, nref - c0);
+            const int nc = min(kLipChunk, nref - c0);
             __syncthreads();  // the previous chunk's readers are done
             if (tid == 0) nlive = 0;
             __syncthreads();
             // only references with LB_c > U (1 + 1e-5) can prune: compacted (any order)
-            for (int c = tid; c < n; c += 256) {
-                const int row = (c0 + c) * kLipStep;
+            for (int c = tid; c < nc; c += 256) {
+                const int row = rowpos((c0 + c) * kLipStep);
                 const double a = LBp[row] * (1.0 - 1e-5) - Um;
                 if (a > 0.0) {
                     const float thr = (float)(a * a * (1.0 - 1e-5));
@@ -2105,7 +2114,7 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
             if (lane == 0) base = atomicAdd(&rcount[p], __builtin_popcountll(bal));
             base = __shfl(base, 0, 64);
             if (keep)
-                rlist[(size_t)p * stride + base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = i;
+                rlist[(size_t)p * olstride + base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = i;
         }
     }
 }
@@ -2127,22 +2136,29 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
                                        const int32_t* __restrict__ surv,
                                        const int32_t* __restrict__ nsurv,
                                        const int32_t* __restrict__ bsel, double* __restrict__ lb,
-                                       double* __restrict__ ub, int p, int vb) {
+                                       double* __restrict__ ub, const int32_t* __restrict__ list,
+                                       int lstride, const int32_t* __restrict__ lcount, int step,
+                                       int p, int vb) {
     __shared__ uint32_t sub[kRefineRows][2][kNS];
     __shared__ double inner[kRefineRows];
     __shared__ int below[kRefineRows][2];
     const int tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
     const int ns = nsurv[p];
+    if (ns <= kRefineMin) return;  // few survivors: the exact pass is cheaper
+    // the rows refined here: every step-th survivor (step > 1: the Lipschitz references) or the
+    // per-pair list of the survivors the references did not prune (lcount)
+    const int nl = lcount ? lcount[p] : (ns + step - 1) / step;
     const int s0 = vb * kRefineRows;
-    if (s0 >= ns || ns <= kRefineMin) return;  // few survivors: the exact pass is cheaper
+    if (s0 >= nl) return;
     const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
     if (hi <= lo) return;
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
     const int base = bounds_elo(dscale[p]) << kMantBits;
-    const int32_t* S = surv + (size_t)p * stride;
+    const int32_t* S = list + (size_t)p * lstride;
+    auto srow = [&](int k) { return (int)S[(size_t)k * step]; };
     float xi[kRefineRows], yi[kRefineRows], zi[kRefineRows];
     int ba[kRefineRows], bb[kRefineRows];
     double acc[kRefineRows];
@@ -2150,7 +2166,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
 #pragma unroll
     for (int t = 0; t < kRefineRows; t++) {
         const int r = (lane + t) & (kRefineRows - 1);
-        const int row = S[min(s0 + r, ns - 1)];
+        const int row = srow(min(s0 + r, nl - 1));
         xi[t] = X[row];
         yi[t] = Y[row];
         zi[t] = Z[row];
@@ -2194,8 +2210,8 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     __syncthreads();
     // per row (one wave): bracket the window's part inside the two boundary bins
     const int r = tid >> 6, sl = tid & 63;
-    if (s0 + r >= ns) return;
-    const int row = S[s0 + r];
+    if (s0 + r >= nl) return;
+    const int row = srow(s0 + r);
     const int bA = bsel[((size_t)p * stride + row) * 2] + base;
     const int bB = bsel[((size_t)p * stride + row) * 2 + 1] + base;
     const int cA = below[r][0], cB = below[r][1];
@@ -2358,14 +2374,15 @@ __global__ __launch_bounds__(256) void consensus_refine_kernel(
     const float* __restrict__ dscale, int stride, double trim_lo, double trim_hi,
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
     const int32_t* __restrict__ bsel, double* __restrict__ lb, double* __restrict__ ub,
+    const int32_t* __restrict__ list, int lstride, const int32_t* __restrict__ lcount, int step,
     const int32_t* __restrict__ uoff, int n_pairs) {
-    const int total = uoff[n_pairs];  // units: ceil(nsurv / kRefineRows) where nsurv > kRefineMin
+    const int total = uoff[n_pairs];  // units of kRefineRows listed rows, pairs with > kRefineMin
     for (int g = blockIdx.x; g < total; g += gridDim.x) {
         int p, u;
         pair_of_item(uoff, n_pairs, g, &p, &u);
         __syncthreads();  // the previous item's LDS readers are done
         consensus_refine_block(kcount, rv, dscale, stride, trim_lo, trim_hi, surv, nsurv, bsel,
-                               lb, ub, p, u);
+                               lb, ub, list, lstride, lcount, step, p, u);
     }
 }
 
@@ -3007,8 +3024,8 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
     const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * sh.n_pairs, st);
     if (me != hipSuccess) return me;
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, sh.n_pairs),
-                       dim3(256), 0, st, kcount, rv, stride, trim_lo, trim_hi, lb, ub, rlist,
-                       rcount);
+                       dim3(256), 0, st, kcount, rv, stride, trim_lo, trim_hi, lb, ub,
+                       (const int32_t*)nullptr, (const int32_t*)nullptr, rlist, stride, rcount);
     int32_t* uoff = rcount + sh.n_pairs;  // [n_pairs + 1] after the counts
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)rcount,
                        sh.n_pairs, kBoundRows, 0, uoff);
@@ -3034,14 +3051,30 @@ hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, cons
 hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const float* dscale,
                                    const BatchShape& sh, double trim_lo, double trim_hi,
                                    const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
-                                   double* lb, double* ub, hipStream_t st) {
-    // unit prefix in the scratch after nsurv[n_pairs] and the list counts[n_pairs]
-    int32_t* uoff = const_cast<int32_t*>(nsurv) + 2 * sh.n_pairs;
-    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, sh.n_pairs,
-                       kRefineRows, kRefineMin, uoff);
+                                   double* lb, double* ub, int32_t* list2, hipStream_t st) {
+    // scratch after nsurv[n_pairs] and the bounds-list counts[n_pairs]: the unit prefix
+    // [n_pairs + 1], then the counts of list2 [n_pairs]
+    const int P = sh.n_pairs, stride = 2 * sh.iters, l2stride = sortbuf_len(sh.iters);
+    int32_t* uoff = const_cast<int32_t*>(nsurv) + 2 * P;
+    int32_t* n2 = uoff + P + 1;
+    // (A) the reference survivors (every kLipStep-th) of pairs with > kRefineMin survivors
+    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, P,
+                       kRefineRows * kLipStep, kRefineMin, uoff);
     hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
-                       2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub,
-                       (const int32_t*)uoff, sh.n_pairs);
+                       stride, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, surv, stride,
+                       (const int32_t*)nullptr, kLipStep, (const int32_t*)uoff, P);
+    // (B) Lipschitz pruning of the other survivors against the refined references
+    const hipError_t me = hipMemsetAsync(n2, 0, sizeof(int32_t) * P, st);
+    if (me != hipSuccess) return me;
+    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, P), dim3(256), 0, st,
+                       kcount, rv, stride, trim_lo, trim_hi, lb, ub, surv, nsurv, list2, l2stride,
+                       n2);
+    // (C) the survivors the references did not prune
+    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)n2, P,
+                       kRefineRows, 0, uoff);
+    hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
+                       stride, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, (const int32_t*)list2,
+                       l2stride, (const int32_t*)n2, 1, (const int32_t*)uoff, P);
     return hipGetLastError();
 }
 
