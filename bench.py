@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--seed", type=int, default=20200423)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--profile-tag", default="r01i")
+    ap.add_argument("--profile-tag", default="r01j")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
     ap.add_argument("--no-shard-consensus", action="store_true",
