@@ -2287,10 +2287,10 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
 }
 
 // Work items of all pairs flattened: item g of the batch = (pair p, unit u); the per-pair unit
-// counts are only known on the device, so every block forms their prefix sums and strides
-// over the items (one launch of a fixed grid, no empty blocks, pairs balanced).
-// the same from uoff = exclusive prefix of the per-pair unit counts (list_prefix_kernel; one
-// binary search instead of a sequential walk over the pairs' counts per item)
+// counts are only known on the device, so list_prefix_kernel writes their exclusive prefix uoff
+// and the item kernels stride over a fixed grid (no empty blocks, pairs balanced), finding
+// each item's pair by one binary search (a walk over the pairs' counts per item costs up to
+// n_pairs dependent scalar loads)
 __device__ __forceinline__ void pair_of_item(const int32_t* __restrict__ uoff, int n_pairs, int g,
                                              int* p_out, int* u_out) {
     int a = 0, b = n_pairs;  // largest p with uoff[p] <= g
@@ -2300,21 +2300,6 @@ __device__ __forceinline__ void pair_of_item(const int32_t* __restrict__ uoff, i
     }
     *p_out = a;
     *u_out = g - uoff[a];
-}
-
-template <typename UNITS>
-__device__ bool item_to_pair(int g, int n_pairs, UNITS units, int* p_out, int* u_out) {
-    int base = 0;
-    for (int p = 0; p < n_pairs; p++) {
-        const int n = units(p);
-        if (g < base + n) {
-            *p_out = p;
-            *u_out = g - base;
-            return true;
-        }
-        base += n;
-    }
-    return false;
 }
 
 // the rows of the per-pair lists (Lipschitz survivors): (pair, unit) items of all pairs
