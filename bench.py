@@ -49,9 +49,13 @@ def parse():
     ap.add_argument("--iters", type=int, default=10000)
     ap.add_argument("--kpts", type=int, default=4096)
     ap.add_argument("--seed", type=int, default=20200423)
+    ap.add_argument("--inlier-frac", type=float, default=0.8,
+                    help="pairs workload: fraction of left keypoints with a true partner")
+    ap.add_argument("--sigma", type=float, default=0.03,
+                    help="pairs workload: descriptor noise of the true partners")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--profile-tag", default="r01j")
+    ap.add_argument("--profile-tag", default="r02a")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
     ap.add_argument("--no-shard-consensus", action="store_true",
@@ -68,9 +72,11 @@ def parse():
     return ap.parse_args()
 
 
-def make_batch(rank: int, B: int, kpts: int, seed: int):
+def make_batch(rank: int, B: int, kpts: int, seed: int, inlier_frac: float = 0.8,
+               sigma: float = 0.03):
     from erp_match_eightpoint_test_amd import synth
-    pairs = [synth.make_pair(seed + 1000 * rank + i, n_kpts=kpts) for i in range(B)]
+    pairs = [synth.make_pair(seed + 1000 * rank + i, n_kpts=kpts, inlier_frac=inlier_frac,
+                             sigma=sigma) for i in range(B)]
     return pairs
 
 
@@ -117,28 +123,76 @@ def stage_work(stage, B, kpts, iters, res):
     return None
 
 
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(pairs, iters, budget_s):
     """the oracle (CPU restatement, exact brute force + OpenCV-style SVD) on host cores: whole
-    pairs of the same workload, as many as fit in ~budget_s (at least one)."""
+    pairs of the same workload, as many as fit in ~budget_s (at least one), with OpenMP over
+    the box's CPU share (the matcher is the parallel part; find() is serial like the
+    reference's), then ONE pair again on a single thread.  Returns (record, oracle results of
+    the pairs it ran) -- the results are the parity check of the timed workload (main())."""
     import oracle as O
     O.build()
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     os.environ["OMP_NUM_THREADS"] = str(threads)
-    t0 = time.perf_counter()
-    n = 0
-    for p in pairs:
-        mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=threads)
+
+    def one(p, nth):
+        mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=nth)
         kl = p["kp_l"][mt["queryIdx"]]
         kr = p["kp_r"][mt["trainIdx"]]
-        O.find(p["W"], p["H"], kl, kr, O.make_cfg(iters=iters))
-        n += 1
+        r = O.find(p["W"], p["H"], kl, kr, O.make_cfg(iters=iters))
+        r["matches"] = mt
+        return r
+
+    t0 = time.perf_counter()
+    got = []
+    for p in pairs:
+        got.append(one(p, threads))
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{n} whole pair(s) of the bench workload ({len(pairs[0]['desc_l'])}x"
-                      f"{len(pairs[0]['desc_r'])} kpts, {iters} iters) through oracle/ "
-                      f"(exact-BF CPU restatement, OpenMP {threads} threads), {dt:.1f} s"}
+    n = len(got)
+    t1 = time.perf_counter()
+    one(pairs[0], 1)
+    dt1 = time.perf_counter() - t1
+    rec = {"value": n / dt, "unit": "pairs/s", "cores": threads, "kind": "port",
+           "sample": f"{n} whole pair(s) of the bench workload ({len(pairs[0]['desc_l'])}x"
+                     f"{len(pairs[0]['desc_r'])} kpts, {iters} iters) through oracle/ "
+                     f"(exact-BF CPU restatement, OpenMP {threads} threads), {dt:.1f} s",
+           "value_1core": 1.0 / dt1,
+           "sample_1core": f"pair 0 again on 1 thread, {dt1:.2f} s",
+           "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
+    return rec, got
+
+
+def parity_check(gpu_res, gpu_matches, ora):
+    """the timed workload against the oracle, pair by pair (the pairs cpu_baseline ran): M, K,
+    min_idx and status equal, R / T within 2e-6, the match list (queryIdx, trainIdx,
+    distance bits) bit-exact.  gpu_res: result records of the timed step (same pairs, same
+    order); gpu_matches: [pairs, max_nq, 4] int32 from an untimed pass with the matches out."""
+    bad = []
+    for i, o in enumerate(ora):
+        r = gpu_res[i]
+        M = len(o["matches"])
+        ok = (int(r["status"]) == o["status"] == 0 and int(r["M"]) == M and int(r["K"]) == o["K"]
+              and int(r["min_idx"]) == o["min_idx"]
+              and float(np.abs(r["R"] - o["R"]).max()) <= 2e-6
+              and float(np.abs(r["T"] - o["T"]).max()) <= 2e-6
+              and np.array_equal(gpu_matches[i, :M].view(np.uint32).reshape(-1)[: 4 * M],
+                                 o["matches"].view(np.uint32).reshape(-1)))
+        if not ok:
+            bad.append(i)
+    return {"pairs_checked": len(ora), "all_equal": not bad, "mismatched_pairs": bad,
+            "fields": "status, M, K, min_idx equal; R, T within 2e-6; matches bit-exact"}
 
 
 def load_pmc(tag, stage):
@@ -405,9 +459,44 @@ def run_e2e(args):
     print(json.dumps(line))
 
 
+def _launch_ranks(args) -> int:
+    """--gpus N > 1 without a torch.distributed launcher: start N ranks (one process per GPU)
+    via torch.distributed.run as a CHILD process -- before anything here touches the GPU -- and
+    return its exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench.py: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr)
+    return subprocess.call(cmd)
+
+
+def check_world(args) -> int:
+    """the world size this process runs in; fails loudly when it disagrees with --gpus."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch with "
+                         f"torch.distributed.run --nproc-per-node {args.gpus} (or without a "
+                         "launcher and let bench.py start the ranks)")
+    return world
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_launch_ranks(args))
+    check_world(args)
+    if args.gpus > 1 and args.workload in ("dense", "remap", "e2e"):
+        raise SystemExit(f"bench.py: workload {args.workload} is single-GPU (--gpus 1)")
     import torch
+    if torch.cuda.device_count() < args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} "
+                         "HIP device(s) visible")
     if args.workload == "dense":
         return run_dense(args)
     if args.workload == "manual":
@@ -424,11 +513,13 @@ def main():
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+        world = dist.get_world_size()  # the RCCL world actually formed
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
     from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
-    pairs = make_batch(rank, args.pairs, args.kpts, args.seed)
+    from erp_match_eightpoint_test_amd import dist as D
+    pairs = make_batch(rank, args.pairs, args.kpts, args.seed, args.inlier_frac, args.sigma)
     S = max(1, min(args.streams, args.pairs))
     parts = [pairs[i * args.pairs // S:(i + 1) * args.pairs // S] for i in range(S)]
     subs = []
@@ -454,8 +545,6 @@ def main():
         return torch.cat([sb["res"] for sb in subs])
 
     gathered = None
-    if dist is not None:
-        gathered = torch.empty((world, args.pairs, 64), dtype=torch.uint8, device=dev)
     def call_serial():  # the sub-batches one after the other (no stream overlap)
         for sb in subs:
             b = sb["b"]
@@ -472,7 +561,7 @@ def main():
             continue
         out = call()
         if dist is not None:
-            dist.all_gather_into_tensor(gathered, out)
+            gathered = D.gather_records(out)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -481,7 +570,7 @@ def main():
     for _ in range(args.steps):
         out = call()
         if dist is not None:
-            dist.all_gather_into_tensor(gathered, out)
+            gathered = D.gather_records(out)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -560,8 +649,22 @@ def main():
         lat = {"single_pair_ms": float(np.median(ts)) * 1e3,
                "note": "one 4096x4096 pair, 10k iterations, batch of 1, host-timed, median of 20"}
     cpu = None
+    parity = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(pairs, args.iters, args.cpu_seconds)
+        cpu, ora = cpu_baseline(pairs, args.iters, args.cpu_seconds)
+        # untimed pass of sub-batch 0 (the first pairs, the ones the oracle ran) with the match
+        # lists out; its records must also equal the timed step's (nothing cached between runs)
+        sb = subs[0]
+        b = sb["b"]
+        o = sb["runner"].run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"],
+                             b["off_r"], b["width"], b["height"], b["max_nq"], b["max_nt"],
+                             want=("matches",))
+        torch.cuda.synchronize()
+        n0 = len(ora)
+        rerun = results_to_numpy(o["results"])
+        parity = parity_check(res, o["matches"][:n0].cpu().numpy(), ora)
+        parity["rerun_records_identical"] = bool(
+            np.array_equal(rerun.view(np.uint8), res[:len(rerun)].view(np.uint8)))
     line = {
         "metric": "ERP image-pairs/sec (4k x 4k kpts, 10k RANSAC iters); match-set bit-exact",
         "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
@@ -572,7 +675,9 @@ def main():
                                f"batch of {args.pairs} independent pairs per step per GPU",
                    "kpts": args.kpts, "iters": args.iters, "pairs_per_step_per_gpu": args.pairs,
                    "streams": S, "matcher": args.matcher,
-                   "parallelism": f"pair-sharded x{world}", "sampler": "glibc replay (seed 1)"},
+                   "parallelism": f"pair-sharded x{world}", "sampler": "glibc replay (seed 1)",
+                   "rccl_world": world if dist is not None else None,
+                   "inlier_frac": args.inlier_frac, "sigma": args.sigma},
         "roofline": roof,
         "roofline_stages": stage_roofs,
         "cpu_baseline": cpu,
@@ -581,7 +686,8 @@ def main():
         "check": {"all_status_ok": ok, "mean_abs_euler_err_deg_max": max(err_deg),
                   "M_mean": float(res["M"].mean()), "K_mean": float(res["K"].mean()),
                   "consensus_survivors": res["survivors"].tolist(),
-                  "near_ties": res["near_ties"].tolist()},
+                  "near_ties": res["near_ties"].tolist(), "parity": parity,
+                  "gathered_records": None if gathered is None else int(gathered.shape[0])},
     }
     print(json.dumps(line))
     if dist is not None:

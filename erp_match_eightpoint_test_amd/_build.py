@@ -50,15 +50,23 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return LIB_PATH
     os.makedirs(LIB_DIR, exist_ok=True)
-    objs = []
+    objs, cmds = [], []
     for src in SOURCES:
         obj = os.path.join(LIB_DIR, os.path.splitext(src)[0] + ".o")
-        cmd = [HIPCC, *CXXFLAGS, "-I", os.path.join(ROOT, "include"), "-c",
-               os.path.join(CSRC, src), "-o", obj]
+        cmds.append([HIPCC, *CXXFLAGS, "-I", os.path.join(ROOT, "include"), "-c",
+                     os.path.join(CSRC, src), "-o", obj])
+        objs.append(obj)
+    # one hipcc per source, in parallel (kernels.hip dominates; the rest overlap it)
+    jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "0") or 0) or os.cpu_count() or 1))
+    from concurrent.futures import ThreadPoolExecutor
+
+    def run(cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-        objs.append(obj)
+    with ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(run, c) for c in cmds]:
+            f.result()
     tmp = LIB_PATH + ".tmp"
     subprocess.run([HIPCC, *CXXFLAGS, "-shared", "-o", tmp, *objs], check=True)
     os.replace(tmp, LIB_PATH)

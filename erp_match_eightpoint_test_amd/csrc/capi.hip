@@ -62,7 +62,14 @@ void host_glibc_window(uint32_t seed, uint64_t offset, uint32_t out[31]) {
 
 struct erp_ctx {
     int device = 0;
-    std::mutex mu;
+    // one lock per context; recursive so the host-pointer entry points hold it across their
+    // copies AND the device entry point they call
+    std::recursive_mutex mu;
+    // stream ordering between calls (the scratch below is shared by every call): the end of
+    // the last call's work, and the stream it was enqueued on
+    hipEvent_t done = nullptr;
+    hipStream_t last = nullptr;
+    bool pending = false;
     // stage timing
     bool profiling = false;
     int32_t matcher = ERP_MATCHER_MFMA_FILTER;
@@ -111,6 +118,29 @@ struct StageTimer {
     }
 };
 
+// A call's enqueue section on a context: holds the context lock, makes this call's stream wait
+// for the previous call's work when that went to another stream (every call shares the
+// context's scratch, so two calls on different streams would otherwise race on it), and on
+// exit records the end of this call's work.  Calls on one stream stay in stream order for free.
+struct CtxCall {
+    erp_ctx* c;
+    hipStream_t st;
+    CtxCall(erp_ctx* c_, hipStream_t st_) : c(c_), st(st_) {
+        c->mu.lock();
+        if (c->pending && st != c->last) (void)hipStreamWaitEvent(st, c->done, 0);
+    }
+    ~CtxCall() {
+        if (!c->done) (void)hipEventCreateWithFlags(&c->done, hipEventDisableTiming);
+        if (c->done && hipEventRecord(c->done, st) == hipSuccess) {
+            c->last = st;
+            c->pending = true;
+        }
+        c->mu.unlock();
+    }
+    CtxCall(const CtxCall&) = delete;
+    CtxCall& operator=(const CtxCall&) = delete;
+};
+
 }  // namespace
 
 extern "C" {
@@ -120,12 +150,16 @@ int32_t erp_abi_version(void) { return ERP_MATCH_ABI_VERSION; }
 }  // extern "C"
 
 int32_t erp_ctx_device_internal(erp_ctx* ctx) { return ctx->device; }  // remap_api.hip
+
+// CtxCall for the entry points of remap_api.hip / surf_api.hip
+void* erp_ctx_call_begin_internal(erp_ctx* ctx, hipStream_t st) { return new CtxCall(ctx, st); }
+void erp_ctx_call_end_internal(void* call) { delete (CtxCall*)call; }
 uint64_t* erp_ctx_surf_key_internal(erp_ctx* ctx) { return &ctx->surf_key; }  // surf_api.hip
 
 // grow-only scratch slots for remap_api.hip / surf_api.hip (slot 0: remap boundary list;
 // 1..: SURF buffers)
 void* erp_ctx_scratch_internal(erp_ctx* ctx, int which, size_t bytes) {
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     if (which < 0 || which >= (int)(sizeof(ctx->extra) / sizeof(ctx->extra[0]))) return nullptr;
     DevBuf& b = which == 0 ? ctx->remap_scr : ctx->extra[which];
     return ensure(b, bytes) ? b.p : nullptr;
@@ -191,6 +225,7 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
     for (DevBuf& b : ctx->extra)
         if (b.p) (void)hipFree(b.p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
+    if (ctx->done) (void)hipEventDestroy(ctx->done);
     delete ctx;
     return ERP_OK;
 }
@@ -467,7 +502,7 @@ extern "C" {
 
 erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable) {
     if (!ctx) return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     ctx->profiling = enable != 0;
     return ERP_OK;
 }
@@ -476,7 +511,7 @@ erp_status erp_ctx_set_matcher(erp_ctx* ctx, int32_t method) {
     if (!ctx) return ERP_INVALID_ARG;
     if (method != ERP_MATCHER_MFMA_FILTER && method != ERP_MATCHER_VALU_EXACT)
         return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     ctx->matcher = method;
     return ERP_OK;
 }
@@ -492,7 +527,7 @@ const char* erp_stage_name(int32_t stage) {
 
 erp_status erp_ctx_stage_times(erp_ctx* ctx, double* total_ms, int64_t* launches) {
     if (!ctx || !total_ms || !launches) return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     for (int k = 0; k < ERP_STAGE_COUNT; k++) {
         total_ms[k] = 0;
@@ -513,7 +548,7 @@ erp_status erp_ctx_stage_times(erp_ctx* ctx, double* total_ms, int64_t* launches
 erp_status erp_ctx_reserve(erp_ctx* ctx, int32_t n_pairs, int32_t max_nq, int32_t max_nt,
                            int32_t iters) {
     if (!ctx || n_pairs < 1 || max_nq < 0 || max_nt < 0 || iters < 1) return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     const erp::BatchShape sh = make_shape(n_pairs, max_nq, max_nt, iters, 0.25);
     if (!ensure_matcher(ctx, sh) ||
@@ -530,9 +565,9 @@ erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* b, float ratio
         b->max_nq > 65535 || !b->desc_l || !b->desc_r || !b->kp_l || !b->kp_r || !b->off_l ||
         !b->off_r || !b->width || !b->height)
         return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    CtxCall call(ctx, st);
     const erp::BatchShape sh = make_shape(b->n_pairs, b->max_nq, b->max_nt, cfg->iters,
                                           cfg->sample_frac);
     if (!ensure_matcher(ctx, sh)) return ERP_OUT_OF_MEMORY;
@@ -566,9 +601,9 @@ erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,
     if (!ctx || nq < 0 || nt < 0 || dim != erp::kDim || !d_out || !d_count) return ERP_INVALID_ARG;
     if (nq > 0 && (!d_query || !d_train)) return ERP_INVALID_ARG;
     if (nq > 0 && nt < 2) return ERP_TOO_FEW_POINTS;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    CtxCall call(ctx, st);
     if (nq == 0) {
         ERP_CK(hipMemsetAsync(d_count, 0, 4, st));
         return ERP_OK;
@@ -590,15 +625,14 @@ erp_status erp_match_two_image(erp_ctx* ctx, const float* h_desc1, int32_t n1, c
     if (n1 > 0 && n2 < 2) return ERP_TOO_FEW_POINTS;
     *h_count = 0;
     if (n1 == 0) return ERP_OK;
-    {
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        ERP_CK(hipSetDevice(ctx->device));
-        if (!ensure(ctx->in_a, (size_t)n1 * dim * 4) || !ensure(ctx->in_b, (size_t)n2 * dim * 4) ||
-            !ensure(ctx->in_c, (size_t)n1 * sizeof(erp_dmatch) + 16))
-            return ERP_OUT_OF_MEMORY;
-        ERP_CK(hipMemcpy(ctx->in_a.p, h_desc1, (size_t)n1 * dim * 4, hipMemcpyHostToDevice));
-        ERP_CK(hipMemcpy(ctx->in_b.p, h_desc2, (size_t)n2 * dim * 4, hipMemcpyHostToDevice));
-    }
+    // one lock across upload, match and download: the staging buffers are the context's
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    if (!ensure(ctx->in_a, (size_t)n1 * dim * 4) || !ensure(ctx->in_b, (size_t)n2 * dim * 4) ||
+        !ensure(ctx->in_c, (size_t)n1 * sizeof(erp_dmatch) + 16))
+        return ERP_OUT_OF_MEMORY;
+    ERP_CK(hipMemcpy(ctx->in_a.p, h_desc1, (size_t)n1 * dim * 4, hipMemcpyHostToDevice));
+    ERP_CK(hipMemcpy(ctx->in_b.p, h_desc2, (size_t)n2 * dim * 4, hipMemcpyHostToDevice));
     int32_t* d_count = (int32_t*)((char*)ctx->in_c.p + (size_t)n1 * sizeof(erp_dmatch));
     erp_status s = erp_match_knn2_ratio(ctx, (const float*)ctx->in_a.p, n1, (const float*)ctx->in_b.p,
                                         n2, dim, 0.3f, (erp_dmatch*)ctx->in_c.p, d_count, nullptr);
@@ -618,9 +652,9 @@ erp_status erp_eight_point_find_dev(erp_ctx* ctx, int32_t W, int32_t H, const er
     if (!ctx || W <= 0 || H <= 0 || m < 0 || m > 65535 || !d_result || !cfg_ok(cfg))
         return ERP_INVALID_ARG;
     if (m > 0 && (!d_kl || !d_kr)) return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    CtxCall call(ctx, st);
     const erp::BatchShape sh = make_shape(1, m, m, cfg->iters, cfg->sample_frac);
     erp_batch_outputs out{};
     out.results = d_result;
@@ -646,9 +680,9 @@ erp_status erp_eight_point_hypotheses_dev(erp_ctx* ctx, int32_t W, int32_t H,
         return ERP_INVALID_ARG;
     if (m > 0 && (!d_kl || !d_kr)) return ERP_INVALID_ARG;
     if ((int32_t)(m * cfg->sample_frac) < 1) return ERP_TOO_FEW_POINTS;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    CtxCall call(ctx, st);
     const erp::BatchShape sh = make_shape(1, m, m, cfg->iters, cfg->sample_frac);
     erp_batch_outputs out{};
     out.hyps = d_hyps;
@@ -671,9 +705,9 @@ erp_status erp_consensus_dev(erp_ctx* ctx, const float* d_rvec, const float* d_t
     if (!ctx || K < 0 || !d_result || (K > 0 && (!d_rvec || !d_tvec)) || trim_lo < 0 ||
         trim_hi > 1 || trim_lo > trim_hi)
         return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    CtxCall call(ctx, st);
     erp_ransac_cfg cfg;
     erp_ransac_cfg_default(&cfg);
     cfg.trim_lo = trim_lo;
@@ -693,9 +727,9 @@ erp_status erp_consensus_hyps_dev(erp_ctx* ctx, int32_t m, const erp_hypothesis*
                                   erp_pair_result* d_result, void* stream) {
     if (!ctx || m < 0 || m > 65535 || n_hyps < 1 || !d_hyps || !d_result || !cfg_ok(cfg))
         return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    CtxCall call(ctx, st);
     const erp::BatchShape sh = make_shape(1, std::max(m, 1), std::max(m, 1), n_hyps,
                                           cfg->sample_frac);
     erp_batch_outputs out{};
@@ -714,9 +748,9 @@ erp_status erp_consensus_hyps_shard_dev(erp_ctx* ctx, int32_t m, const erp_hypot
     if (!ctx || m < 0 || m > 65535 || n_hyps < 1 || !d_hyps || !cfg_ok(cfg) || nshards < 1 ||
         shard < 0 || shard >= nshards || !d_lb || !d_ub || !d_bsel)
         return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    CtxCall call(ctx, st);
     const erp::BatchShape sh = make_shape(1, std::max(m, 1), std::max(m, 1), n_hyps,
                                           cfg->sample_frac);
     erp_batch_outputs out{};
@@ -740,9 +774,9 @@ erp_status erp_consensus_hyps_finish_dev(erp_ctx* ctx, int32_t m, const erp_hypo
     if (!ctx || m < 0 || m > 65535 || n_hyps < 1 || !d_hyps || !cfg_ok(cfg) || !d_lb || !d_ub ||
         !d_bsel || !d_result)
         return ERP_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     hipStream_t st = (hipStream_t)stream;
+    CtxCall call(ctx, st);
     const erp::BatchShape sh = make_shape(1, std::max(m, 1), std::max(m, 1), n_hyps,
                                           cfg->sample_frac);
     erp_batch_outputs out{};
@@ -756,16 +790,15 @@ erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_po
                                 const erp_point2f* h_kr, int32_t m, const erp_ransac_cfg* cfg,
                                 float R_out[3], float T_out[3], erp_pair_result* h_result) {
     if (!ctx || m < 0 || (m > 0 && (!h_kl || !h_kr))) return ERP_INVALID_ARG;
-    {
-        std::lock_guard<std::mutex> lk(ctx->mu);
-        ERP_CK(hipSetDevice(ctx->device));
-        if (!ensure(ctx->in_a, (size_t)m * 8 + 8) || !ensure(ctx->in_b, (size_t)m * 8 + 8) ||
-            !ensure(ctx->in_c, sizeof(erp_pair_result)))
-            return ERP_OUT_OF_MEMORY;
-        if (m > 0) {
-            ERP_CK(hipMemcpy(ctx->in_a.p, h_kl, (size_t)m * 8, hipMemcpyHostToDevice));
-            ERP_CK(hipMemcpy(ctx->in_b.p, h_kr, (size_t)m * 8, hipMemcpyHostToDevice));
-        }
+    // one lock across upload, find and download: the staging buffers are the context's
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    ERP_CK(hipSetDevice(ctx->device));
+    if (!ensure(ctx->in_a, (size_t)m * 8 + 8) || !ensure(ctx->in_b, (size_t)m * 8 + 8) ||
+        !ensure(ctx->in_c, sizeof(erp_pair_result)))
+        return ERP_OUT_OF_MEMORY;
+    if (m > 0) {
+        ERP_CK(hipMemcpy(ctx->in_a.p, h_kl, (size_t)m * 8, hipMemcpyHostToDevice));
+        ERP_CK(hipMemcpy(ctx->in_b.p, h_kr, (size_t)m * 8, hipMemcpyHostToDevice));
     }
     erp_status s = erp_eight_point_find_dev(ctx, W, H, (const erp_point2f*)ctx->in_a.p,
                                             (const erp_point2f*)ctx->in_b.p, m, cfg,
@@ -788,7 +821,7 @@ erp_status erp_initial_guess(erp_ctx* ctx, const double* h_bl, const double* h_b
         return ERP_INVALID_ARG;
     erp_pair_result r;
     {
-        std::lock_guard<std::mutex> lk(ctx->mu);
+        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
         ERP_CK(hipSetDevice(ctx->device));
         const erp::BatchShape sh = make_shape(1, m, m, cfg->iters, cfg->sample_frac);
         erp_status es = ensure_estimator(ctx, sh, nullptr);
@@ -821,7 +854,7 @@ erp_status erp_eight_point_estimation(erp_ctx* ctx, const double* h_bl, const do
                                       int32_t m, erp_hypothesis* h_out) {
     if (!ctx || m < 0 || !h_out || (m > 0 && (!h_bl || !h_br))) return ERP_INVALID_ARG;
     if (m < 1) return ERP_TOO_FEW_POINTS;
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
     if (!ensure(ctx->in_d, (size_t)m * 48 + 36 * 8 * 2 + sizeof(erp_hypothesis) + 64))
         return ERP_OUT_OF_MEMORY;

@@ -15,6 +15,17 @@
 
 int32_t erp_ctx_device_internal(erp_ctx* ctx);  // capi.hip
 void* erp_ctx_scratch_internal(erp_ctx* ctx, int which, size_t bytes);  // capi.hip (grow-only)
+// capi.hip: the context's call section (lock + stream order after the previous call, whose
+// scratch this call reuses; records the end of this call's work on exit)
+void* erp_ctx_call_begin_internal(erp_ctx* ctx, hipStream_t st);
+void erp_ctx_call_end_internal(void* call);
+namespace {
+struct CtxCallGuard {
+    void* h;
+    CtxCallGuard(erp_ctx* c, hipStream_t st) : h(erp_ctx_call_begin_internal(c, st)) {}
+    ~CtxCallGuard() { erp_ctx_call_end_internal(h); }
+};
+}  // namespace
 
 namespace {
 
@@ -138,6 +149,7 @@ erp_status erp_crop_rotated_image_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t
     if (!d_im || !d_out || !dims_ok(W, H) || H < 4) return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    CtxCallGuard call(ctx, (hipStream_t)stream);
     erp::RemapScratch scr;
     if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     erp::RemapJobs jobs{};
@@ -158,6 +170,7 @@ erp_status erp_spherical_bands_dev(erp_ctx* ctx, const uint8_t* d_ims, int32_t n
         return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    CtxCallGuard call(ctx, (hipStream_t)stream);
     erp::RemapScratch scr;
     if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     static const float pitch[4] = {45.f, 0.f, -45.f, -90.f};  // do_all :77-83 (n1 unrotated)
@@ -190,6 +203,7 @@ erp_status erp_rotate_keypoints_dev(erp_ctx* ctx, erp_point2f* d_kp, int32_t n, 
     if (n < 0 || (n > 0 && !d_kp) || !dims_ok(W, H)) return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    CtxCallGuard call(ctx, (hipStream_t)stream);
     erp::BandKeypointArgs a{};
     for (int b = 0; b < 4; b++) {
         pitch_matrix(pitch_deg, a.m[b]);
@@ -214,6 +228,7 @@ erp_status erp_unrotate_band_keypoints_dev(erp_ctx* ctx, erp_point2f* d_kp,
     if (total > INT32_MAX || (total > 0 && !d_kp)) return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    CtxCallGuard call(ctx, (hipStream_t)stream);
     static const float pitch[4] = {45.f, 0.f, -45.f, -90.f};  // do_all :121-126
     erp::BandKeypointArgs a{};
     int32_t e = 0;
@@ -234,6 +249,7 @@ erp_status erp_rotate_image_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W, in
     if (!d_im || !d_out || !rot_mat || !dims_ok(W, H)) return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    CtxCallGuard call(ctx, (hipStream_t)stream);
     erp::RemapScratch scr;
     if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     erp::RemapJobs jobs{};
@@ -255,6 +271,7 @@ erp_status erp_rectify_dev(erp_ctx* ctx, const uint8_t* d_left, const uint8_t* d
         return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    CtxCallGuard call(ctx, (hipStream_t)stream);
     erp::RemapScratch scr;
     if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     erp::RemapJobs jobs{};
@@ -277,6 +294,7 @@ erp_status erp_vertical_rotate_dev(erp_ctx* ctx, const uint8_t* d_im, int32_t W,
     if (!d_im || !d_out || !dims_ok(W, H)) return ERP_INVALID_ARG;
     erp_status s = set_dev(ctx);
     if (s != ERP_OK) return s;
+    CtxCallGuard call(ctx, (hipStream_t)stream);
     erp::RemapScratch scr;
     if (!scratch(ctx, (size_t)W * H, &scr)) return ERP_OUT_OF_MEMORY;
     // rot_mat_90deg = eular2rot(Vec3d(RAD(89.999), 0, 0)).inv(); rotate_image inverts it again

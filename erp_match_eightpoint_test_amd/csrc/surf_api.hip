@@ -15,6 +15,17 @@
 
 int32_t erp_ctx_device_internal(erp_ctx* ctx);
 void* erp_ctx_scratch_internal(erp_ctx* ctx, int which, size_t bytes);
+// capi.hip: the context's call section (lock + stream order after the previous call, whose
+// scratch this call reuses; records the end of this call's work on exit)
+void* erp_ctx_call_begin_internal(erp_ctx* ctx, hipStream_t st);
+void erp_ctx_call_end_internal(void* call);
+namespace {
+struct CtxCallGuard {
+    void* h;
+    CtxCallGuard(erp_ctx* c, hipStream_t st) : h(erp_ctx_call_begin_internal(c, st)) {}
+    ~CtxCallGuard() { erp_ctx_call_end_internal(h); }
+};
+}  // namespace
 uint64_t* erp_ctx_surf_key_internal(erp_ctx* ctx);
 
 namespace {
@@ -84,6 +95,7 @@ erp_status erp_surf_detect_compute_dev(erp_ctx* ctx, const uint8_t* d_images, in
     if (!d_images || !d_kp || !d_desc || !d_count) return ERP_INVALID_ARG;
     if (hipSetDevice(erp_ctx_device_internal(ctx)) != hipSuccess) return ERP_HIP_ERROR;
     hipStream_t st = (hipStream_t)stream;
+    CtxCallGuard call(ctx, st);
     const int nO = prm->n_octaves, nL = prm->n_octave_layers, nT = (nL + 2) * nO;
     // layer table (host)
     std::vector<erp::SurfLayer> layers(nT);

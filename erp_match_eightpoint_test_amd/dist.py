@@ -13,8 +13,9 @@ Two partitions, each with a single collective at the end (no data-path exchange)
   R_vec_arr push order of src/eight_point.cpp:113-126 is preserved) and every rank runs the
   same consensus on the merged list.
 
-The compute callables are pluggable: on GPUs they are the C ABI (`gpu_hypotheses`,
-`gpu_consensus`); the CPU tests plug in the oracle to check the partition semantics.
+The compute is pluggable: on GPUs it is the C ABI (`CapiShardBackend` for the device-resident
+path `sharded_find`, `gpu_hypotheses` / `gpu_consensus` for the host variant); the gloo tests
+plug in the oracle and run the very same collective code on CPU tensors.
 """
 from __future__ import annotations
 
@@ -78,75 +79,147 @@ def padded_block(iters: int, world: int, rank: int) -> tuple[int, int, int]:
     return blk, a, min(iters, a + blk)
 
 
-def find_hypothesis_sharded_dev(ctx, W: int, H: int, d_kl, d_kr, m: int, iters: int,
-                                cfg_kwargs: dict | None = None, group=None, stream=None,
-                                shard_consensus: bool = True, emulate_world: int = 0):
-    """configs[4] on GPUs, device-resident end to end: rank r computes iterations
-    [r B, (r+1) B) (B = ceil(iters / world)) into a zero-padded block of B records
-    (erp_eight_point_hypotheses_dev at glibc offset base + r B (m-1)), the blocks are
-    all-gathered over RCCL in rank order (= iteration order; zero records push nothing), and
-    every rank runs the valid-list compaction + consensus on the merged records.  With
-    shard_consensus the consensus's K^2 bounds pass is split too: rank r bounds the rows
-    [K r / world, K (r+1) / world) (erp_consensus_hyps_shard_dev), one RCCL all_reduce(SUM)
-    combines the per-row [LB, UB] and boundary bins, and every rank finishes the selection
-    (erp_consensus_hyps_finish_dev) -- the same result as erp_consensus_hyps_dev.
-    emulate_world > 1 (tests, one process): run every shard of the consensus locally in turn and
-    sum them, as the all_reduce would.  Returns (result record tensor [64] uint8, merged)."""
-    import ctypes as C
+class CapiShardBackend:
+    """the per-rank compute of the device-resident configs[4] path through the C ABI, all on
+    one HIP stream `st` (hypotheses -> consensus or bounds shard -> finish)."""
 
+    def __init__(self, ctx, W: int, H: int, d_kl, d_kr, m: int, cfg_kwargs: dict | None = None,
+                 stream=None):
+        import torch
+        self.ctx, self.W, self.H, self.d_kl, self.d_kr, self.m = ctx, W, H, d_kl, d_kr, m
+        self.cfg_kwargs = dict(cfg_kwargs or {})
+        self.base = int(self.cfg_kwargs.pop("offset", 0))
+        self.device = d_kl.device
+        self.st = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+
+    def stream(self):
+        """context manager: torch's current stream = the compute stream, so the collectives
+        (issued on torch's current stream) are ordered after the kernels that fill their
+        inputs, and the kernels after the collectives that fill theirs."""
+        import torch
+        return torch.cuda.stream(torch.cuda.ExternalStream(self.st, device=self.device))
+
+    def _cfg(self, **kw):
+        from .capi import default_cfg
+        return default_cfg(**dict(self.cfg_kwargs, **kw))
+
+    def hyps(self, a: int, b: int, out):
+        import ctypes as C
+
+        from .capi import check
+        cfg = self._cfg(iters=b - a, offset=self.base + a * (self.m - 1))
+        check(self.ctx.L.erp_eight_point_hypotheses_dev(
+            self.ctx.h, self.W, self.H, self.d_kl.data_ptr(), self.d_kr.data_ptr(), self.m,
+            C.byref(cfg), out.data_ptr(), self.st), "erp_eight_point_hypotheses_dev")
+
+    def consensus(self, merged, iters: int, res):
+        import ctypes as C
+
+        from .capi import check
+        cfg = self._cfg(iters=iters)
+        check(self.ctx.L.erp_consensus_hyps_dev(self.ctx.h, self.m, merged.data_ptr(),
+                                                merged.shape[0], C.byref(cfg), res.data_ptr(),
+                                                self.st), "erp_consensus_hyps_dev")
+
+    def shard(self, merged, iters: int, sh: int, nsh: int, part):
+        import ctypes as C
+
+        from .capi import check
+        cfg = self._cfg(iters=iters)
+        check(self.ctx.L.erp_consensus_hyps_shard_dev(
+            self.ctx.h, self.m, merged.data_ptr(), merged.shape[0], C.byref(cfg), sh, nsh,
+            part[0].data_ptr(), part[1].data_ptr(), part[2].data_ptr(), self.st),
+            "erp_consensus_hyps_shard_dev")
+
+    def finish(self, merged, iters: int, bounds, res):
+        import ctypes as C
+
+        from .capi import check
+        cfg = self._cfg(iters=iters)
+        check(self.ctx.L.erp_consensus_hyps_finish_dev(
+            self.ctx.h, self.m, merged.data_ptr(), merged.shape[0], C.byref(cfg),
+            bounds[0].data_ptr(), bounds[1].data_ptr(), bounds[2].data_ptr(), res.data_ptr(),
+            self.st), "erp_consensus_hyps_finish_dev")
+
+
+def sharded_find(backend, iters: int, group=None, shard_consensus: bool = True,
+                 emulate_world: int = 0):
+    """The collective skeleton of configs[4] (hypothesis blocks), independent of where the
+    compute runs: rank r computes iterations [r B, (r+1) B) (B = ceil(iters / world)) into a
+    zero-padded block of B records, the blocks are all_gather_into_tensor'ed in rank order
+    (= iteration order; zero records push nothing, so R_vec_arr's order is the single-process
+    one, src/eight_point.cpp:113-126), and every rank runs the valid-list compaction +
+    consensus on the merged records.  With shard_consensus the K^2 bounds pass is split too:
+    rank r bounds its rows, one all_reduce(SUM) over the [LB, UB] doubles and one over the
+    boundary-bin words (two int32 per row, summed as int64 words: one rank writes each row,
+    the others hold 0, so the sums are exact), and every rank finishes the selection.
+    emulate_world > 1 (one process): run every shard locally in turn and sum them, as the
+    all_reduce would.  `backend` supplies device, stream() and the compute (hyps, consensus,
+    shard, finish): CapiShardBackend on GPUs, the oracle in the gloo tests.
+    Returns (result record tensor [64] uint8, merged records [world B, 120] uint8)."""
     import torch
     import torch.distributed as dist
 
-    from .capi import HYP_DTYPE, RESULT_DTYPE, check, default_cfg
-    cfg_kwargs = dict(cfg_kwargs or {})
+    from .capi import HYP_DTYPE, RESULT_DTYPE
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     blk, a, b = padded_block(iters, world, rank)
-    dev = d_kl.device
-    st = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-    local = torch.zeros((blk, HYP_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-    base = int(cfg_kwargs.pop("offset", 0))
-    if b > a:
-        cfg = default_cfg(**dict(cfg_kwargs, iters=b - a, offset=base + a * (m - 1)))
-        check(ctx.L.erp_eight_point_hypotheses_dev(ctx.h, W, H, d_kl.data_ptr(), d_kr.data_ptr(),
-                                                   m, C.byref(cfg), local.data_ptr(), st),
-              "erp_eight_point_hypotheses_dev")
-    if world > 1:
-        merged = torch.empty((world * blk, HYP_DTYPE.itemsize), dtype=torch.uint8, device=dev)
-        dist.all_gather_into_tensor(merged, local, group=group)
-    else:
-        merged = local
-    res = torch.zeros(RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
-    cfg = default_cfg(**dict(cfg_kwargs, iters=iters))
-    n = merged.shape[0]
-    nsh = world if world > 1 else max(emulate_world, 1)
-    if not shard_consensus or nsh == 1:
-        check(ctx.L.erp_consensus_hyps_dev(ctx.h, m, merged.data_ptr(), n, C.byref(cfg),
-                                           res.data_ptr(), st), "erp_consensus_hyps_dev")
-        return res, merged
-    bounds = torch.zeros((3, 2 * n), dtype=torch.float64, device=dev)  # lb, ub, bsel (2 x i32)
-    shards = [rank] if world > 1 else list(range(nsh))
-    part = torch.empty_like(bounds)
-    for sh in shards:
-        check(ctx.L.erp_consensus_hyps_shard_dev(ctx.h, m, merged.data_ptr(), n, C.byref(cfg), sh,
-                                                 nsh, part[0].data_ptr(), part[1].data_ptr(),
-                                                 part[2].data_ptr(), st),
-              "erp_consensus_hyps_shard_dev")
+    dev = backend.device
+    with backend.stream():
+        local = torch.zeros((blk, HYP_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+        if b > a:
+            backend.hyps(a, b, local)
         if world > 1:
-            bounds = part
-        else:  # emulation: integer bsel halves summed as int64 words (disjoint rows, no carry)
-            bounds[:2] += part[:2]
-            bounds[2].view(torch.int64).add_(part[2].view(torch.int64))
-    if world > 1:
-        # lb / ub as doubles; bsel's int32 pairs as int64 words (one rank writes each row, the
-        # others hold 0: the sums are exact)
-        dist.all_reduce(bounds[:2], group=group)
-        dist.all_reduce(bounds[2].view(torch.int64), group=group)
-    check(ctx.L.erp_consensus_hyps_finish_dev(ctx.h, m, merged.data_ptr(), n, C.byref(cfg),
-                                              bounds[0].data_ptr(), bounds[1].data_ptr(),
-                                              bounds[2].data_ptr(), res.data_ptr(), st),
-          "erp_consensus_hyps_finish_dev")
+            merged = torch.empty((world * blk, HYP_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+            dist.all_gather_into_tensor(merged, local, group=group)
+        else:
+            merged = local
+        res = torch.zeros(RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+        n = merged.shape[0]
+        nsh = world if world > 1 else max(emulate_world, 1)
+        if not shard_consensus or nsh == 1:
+            backend.consensus(merged, iters, res)
+            return res, merged
+        bounds = torch.zeros((3, 2 * n), dtype=torch.float64, device=dev)  # lb, ub, bsel (2 x i32)
+        part = torch.empty_like(bounds)
+        for sh in ([rank] if world > 1 else range(nsh)):
+            backend.shard(merged, iters, sh, nsh, part)
+            if world > 1:
+                bounds = part
+            else:  # emulation: the same sums the all_reduce does
+                bounds[:2] += part[:2]
+                bounds[2].view(torch.int64).add_(part[2].view(torch.int64))
+        if world > 1:
+            dist.all_reduce(bounds[:2], group=group)
+            dist.all_reduce(bounds[2].view(torch.int64), group=group)
+        backend.finish(merged, iters, bounds, res)
     return res, merged
+
+
+def find_hypothesis_sharded_dev(ctx, W: int, H: int, d_kl, d_kr, m: int, iters: int,
+                                cfg_kwargs: dict | None = None, group=None, stream=None,
+                                shard_consensus: bool = True, emulate_world: int = 0):
+    """configs[4] on GPUs, device-resident end to end (sharded_find over the C ABI:
+    erp_eight_point_hypotheses_dev at glibc offset base + r B (m-1), RCCL all_gather of the
+    blocks, erp_consensus_hyps_dev, or erp_consensus_hyps_shard_dev + RCCL all_reduce +
+    erp_consensus_hyps_finish_dev) -- the same result as the unsharded
+    erp_eight_point_find_dev.  Everything, collectives included, is ordered on `stream`.
+    Returns (result record tensor [64] uint8, merged)."""
+    be = CapiShardBackend(ctx, W, H, d_kl, d_kr, m, cfg_kwargs, stream)
+    return sharded_find(be, iters, group, shard_consensus, emulate_world)
+
+
+def gather_records(local, group=None):
+    """the pair path's only collective (configs[1]/[2], the "best-model gather"): every rank's
+    [B, 64] block of erp_pair_result records, concatenated in rank order with one
+    all_gather_into_tensor (RCCL on the GPUs).  Equal B on every rank."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    out = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device=local.device)
+    dist.all_gather_into_tensor(out, local.contiguous(), group=group)
+    return out
 
 
 def shard_pairs(n_pairs: int, group=None) -> range:

@@ -28,6 +28,11 @@
  *
  * Conventions: plain C types only; `void* stream` is a hipStream_t (NULL = default stream);
  * device-pointer entry points are asynchronous on that stream, host-pointer ones synchronous.
+ * A context (erp_ctx) owns grow-only scratch that every call on it reuses, so calls on one
+ * context are serialised on the device: a call enqueued on a different stream than the previous
+ * call on the same context first waits (hipStreamWaitEvent) for that call's work to finish.
+ * Independent work that should overlap needs one context per stream.  Calls are thread-safe
+ * (one lock per context; host-pointer calls hold it across upload, run and download).
  * No C++ exception crosses this boundary; every call returns an erp_status.  The reference's
  * undefined behaviour cases are given explicit statuses (see erp_status).
  */
