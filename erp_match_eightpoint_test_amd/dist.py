@@ -96,7 +96,11 @@ class CapiShardBackend:
         """context manager: torch's current stream = the compute stream, so the collectives
         (issued on torch's current stream) are ordered after the kernels that fill their
         inputs, and the kernels after the collectives that fill theirs."""
+        import contextlib
+
         import torch
+        if self.st == torch.cuda.current_stream(self.device).cuda_stream:
+            return contextlib.nullcontext()  # already torch's current stream
         return torch.cuda.stream(torch.cuda.ExternalStream(self.st, device=self.device))
 
     def _cfg(self, **kw):
