@@ -923,13 +923,20 @@ __device__ __forceinline__ uint32_t mod_rup(uint32_t x, double r, double dd) {
     const double q = __builtin_trunc(xd * r);
     return (uint32_t)(int32_t)__builtin_fma(-q, dd, xd);
 }
-// d >= 256: q = floor(x/d) < 2^23, so x - q*d is one 24-bit multiply-add
+// d >= 256: q = floor(x/d) < 2^23, so x - q*d is one 24-bit multiply-add.  The sampler runs
+// with the fp64 rounding mode set to round-toward-zero (sampler_kernel's prologue), so
+// t = fma(x, r, 2^52) = 2^52 + floor(x r) EXACTLY (x r < 2^31: the sum lies in [2^52, 2^53),
+// where the fp64 grid is the integers, and one truncating rounding of the exact x r + 2^52 is
+// its floor) and q is t's low word: the fma does the multiply, the truncation and the
+// conversion (3 VALU per draw for the modulo instead of 4).
 __device__ __forceinline__ uint32_t mod_rup_i24(uint32_t x, double r, int d) {
-    const int q = (int)((double)x * r);  // v_cvt_i32_f64 truncates
+    const double t = __builtin_fma((double)x, r, 0x1p52);
+    const int q = (int)(uint32_t)__builtin_bit_cast(uint64_t, t);
     int j;
     asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(j) : "v"(q), "s"(-d), "v"(x));
     return (uint32_t)j;
 }
+
 
 // One block of 31 reverse steps i0, i0-1, ..., i0-30 of one lane's replay (ring = the 31-word
 // glibc window, advanced backwards in place).  Returns the block's selection word: bit u set
@@ -950,6 +957,138 @@ __device__ __forceinline__ uint32_t atomicOr_lds_word(uint32_t bm_lane, uint32_t
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// replay blocks consume a step's LDS return `kReplayLag` steps after issuing it (fewer live
+// registers than consuming all 31 after the block: occupancy)
+constexpr int kReplayLag = 8;
+
+// nw | (b << u) as one v_lshl_or_b32 (u a compile-time constant)
+template <int U>
+__device__ __forceinline__ uint32_t lshl_or_c(uint32_t b, uint32_t nw) {
+    uint32_t r;
+    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "i"(U), "v"(nw));
+    return r;
+}
+template <int U>
+__device__ __forceinline__ void collect_bits(const uint32_t (&olds)[31], const uint32_t (&pos)[31],
+                                             uint32_t& nw) {
+    if constexpr (U < 31) {
+        nw = lshl_or_c<U>(__builtin_amdgcn_ubfe(olds[U], pos[U], 1), nw);
+        collect_bits<U + 1>(olds, pos, nw);
+    }
+}
+
+// LDS masked OR with return: old = bm[a]; bm[a] = (old & ~mask) | data (one DS op for the
+// "T[j] := T[i]" bit copy).  The compiler does not track the asm's result, so every use goes
+// through lds_wait31 (an lgkmcnt(0) wait that carries the results as operands).
+__device__ __forceinline__ uint32_t lds_mskor_rtn(uint32_t addr, uint32_t mask, uint32_t data) {
+    uint32_t old;
+    asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(old) : "v"(addr), "v"(mask), "v"(data)
+                 : "memory");
+    return old;
+}
+__device__ __forceinline__ void lds_wait31(uint32_t (&o)[31]) {
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5]),
+                   "+v"(o[6]), "+v"(o[7]), "+v"(o[8]), "+v"(o[9]), "+v"(o[10]), "+v"(o[11]),
+                   "+v"(o[12]), "+v"(o[13]), "+v"(o[14]), "+v"(o[15])
+                 :
+                 : "memory");
+    asm volatile(""
+                 : "+v"(o[16]), "+v"(o[17]), "+v"(o[18]), "+v"(o[19]), "+v"(o[20]),
+                   "+v"(o[21]), "+v"(o[22]), "+v"(o[23]), "+v"(o[24]), "+v"(o[25]),
+                   "+v"(o[26]), "+v"(o[27]), "+v"(o[28]), "+v"(o[29]), "+v"(o[30])
+                 :
+                 : "memory");
+}
+
+// MODE 1 (every step 1 <= i < s) with the block's own 31 bits T[i0-30 .. i0] (bm bits, set =
+// resolved) in one register: bm[i] is a constant-position bit extract instead of a two-word
+// register mirror, the bit copy bm[j] := bm[i] is one masked OR (returning old bm[j]), and a
+// step that writes inside the window updates it with one bfi (out-of-window j lands on the
+// unused bit 31).  ~17 VALU + 1 DS per step (the mirror version: ~27 VALU + 2 DS).
+template <bool I24>
+__device__ __forceinline__ uint32_t replay_block_prefix(uint32_t (&ring)[31], uint32_t* bm,
+                                                        int lane, int i0,
+                                                        const double* __restrict__ rtab) {
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
+    double rt[31];
+#pragma unroll
+    for (int u = 0; u < 31; u++) rt[u] = rtab[i0 - u + 1];
+    const int base = i0 - 30;  // >= 1
+    const int wA = i0 >> 5, wB = base >> 5;
+    const uint32_t hi = bm[wA * 64 + lane], lo = bm[wB * 64 + lane];
+    uint32_t win = wA == wB ? (lo >> (base & 31)) : __builtin_amdgcn_alignbit(hi, lo, base & 31);
+    uint32_t olds[31], pos[31];
+    uint32_t nw = 0;  // steps whose position was already resolved
+#pragma unroll
+    for (int u = 0; u < 31 + kReplayLag; u++) {
+        if (u < 31) {
+            const int ii = i0 - u;
+            const int slot = 30 - u;
+            const uint32_t rv = ring[slot];
+            ring[slot] = rv - ring[(slot + 28) % 31];
+            const uint32_t j = I24 ? mod_rup_i24(rv >> 1, rt[u], ii + 1)
+                                   : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
+            const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)win, 30 - u, 1);  // bm[i]
+            const uint32_t bit = 1u << (j & 31);
+            uint32_t a;
+            asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(a) : "v"(j >> 5), "v"(bm_lane));
+            olds[u] = lds_mskor_rtn(a, bit, bsp & bit);
+            pos[u] = j;
+            const uint32_t t = min(j - (uint32_t)base, 31u);
+            const uint32_t m = 1u << t;
+            win = (win & ~m) | (bsp & m);
+        }
+        // consume step v = u - lag: at most `lag` masked ORs may still be in flight after it
+        // (LDS returns in order; SMEM in the count only makes the wait stricter)
+        const int v = u - kReplayLag;
+        if (v >= 0) {
+            const int inflight = min(30 - v, kReplayLag);
+            if (inflight >= 8)
+                asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(olds[v]) : : "memory");
+            else
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(olds[v]) : : "memory");
+            nw |= __builtin_amdgcn_ubfe(olds[v], pos[v], 1) << v;
+        }
+    }
+    return ~nw & 0x7fffffffu;
+}
+
+// MODE 2 (the block that straddles s, and the last block that runs below step 1): at most two
+// per iteration, so each step is done on its own (no mirrors, no arrays of in-flight results;
+// keeps the kernel's register budget at the other modes' level).  Steps i >= s as MODE 0,
+// steps 1 <= i < s as replay_block_prefix (bm[i] read back from LDS: the lane's LDS ops are in
+// order), steps below 1 do nothing.
+__device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uint32_t* bm,
+                                                       int lane, int i0, int s,
+                                                       const double* __restrict__ rtab) {
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
+    uint32_t word = 0;
+#pragma unroll
+    for (int u = 0; u < 31; u++) {
+        const int ii = i0 - u;  // uniform
+        const int slot = 30 - u;
+        const uint32_t rv = ring[slot];
+        ring[slot] = rv - ring[(slot + 28) % 31];
+        if (ii < 1) continue;
+        const double r = rtab[ii + 1];
+        const uint32_t j = mod_rup(rv >> 1, r, (double)(ii + 1));
+        uint32_t old, jt;
+        if (ii >= s) {
+            jt = min(j, (uint32_t)s);
+            old = atomicOr_lds_word(bm_lane, jt, 1u << (jt & 31));
+        } else {
+            jt = j;
+            const uint32_t bi = (bm[(ii >> 5) * 64 + lane] >> (ii & 31)) & 1u;
+            uint32_t* wp = &bm[(j >> 5) * 64 + lane];
+            old = atomicAnd(wp, ~(1u << (j & 31)));
+            atomicOr(wp, bi << (j & 31));
+        }
+        word |= (__builtin_amdgcn_ubfe(old, jt, 1) ^ 1u) << u;
+    }
+    return word;
+}
+
 template <int MODE, bool I24>
 __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t* bm, int lane,
                                                  int i0, int s, const double* __restrict__ rtab) {
@@ -966,6 +1105,7 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
         curB = bm[wB * 64 + lane];
     }
     uint32_t olds[31], sel[31];
+    uint32_t nw0 = 0;  // MODE 0: steps whose position was already taken
 #pragma unroll
     for (int u = 0; u < 31; u++) {
         const int ii = i0 - u;  // uniform
@@ -984,6 +1124,10 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
             const uint32_t bc = 1u << (jc & 31);
             olds[u] = atomicOr_lds_word(bm_lane, jc, bc);
             sel[u] = jc;  // (MODE 0: the bit position)
+            if (u >= kReplayLag) {  // consume step u - lag (the compiler places the wait)
+                const int v = u - kReplayLag;
+                nw0 |= __builtin_amdgcn_ubfe(olds[v], sel[v], 1) << v;
+            }
         } else {
             const uint32_t cw = ((ii >> 5) == wA) ? curA : curB;
             const uint32_t bi = (cw >> (ii & 31)) & 1u;
@@ -1004,9 +1148,10 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
     if (MODE == 0) {
         // selected iff bit sel of the old word was clear: collect the SET bits (one bfe and one
         // lshl_or per step), complement once
-        uint32_t nw = 0;
+        uint32_t nw = nw0;
 #pragma unroll
-        for (int u = 0; u < 31; u++) nw |= __builtin_amdgcn_ubfe(olds[u], sel[u], 1) << u;
+        for (int v = 31 - kReplayLag; v < 31; v++)
+            nw |= __builtin_amdgcn_ubfe(olds[v], sel[v], 1) << v;
         word = ~nw & 0x7fffffffu;
     } else {
         // selected iff the step's bit was not yet set: sel & ~old != 0 (sel is 0 or one bit)
@@ -1027,6 +1172,11 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;
+    // fp64 round-toward-zero for the rest of the wave (mod_rup_i24's fma; mod_rup stays exact
+    // under it: trunc of a one-sided product, then an exact fma residual)
+    // (inline asm: the compiler's mode-register pass would otherwise put the default mode back
+    // in front of every fp64 instruction; nothing else in this kernel depends on fp64 rounding)
+    asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\ts_nop 3" ::: "memory");
     const int nwords = (s >> 5) + 1;  // positions 0..s (s: the always-set sentinel)
     for (int k = 0; k < nwords; k++) bm[k * 64 + lane] = (k == (s >> 5)) ? (1u << (s & 31)) : 0u;
     uint32_t ring[31];
@@ -1045,10 +1195,12 @@ __global__ __launch_bounds__(64) void sampler_kernel(
             word = replay_block<0, true>(ring, bm, lane, i, s, rtab);
         else if (i - 30 >= s)
             word = replay_block<0, false>(ring, bm, lane, i, s, rtab);
+        else if (i < s && i - 30 >= 255)
+            word = replay_block_prefix<true>(ring, bm, lane, i, rtab);
         else if (i < s && i - 30 >= 1)
-            word = replay_block<1, false>(ring, bm, lane, i, s, rtab);
+            word = replay_block_prefix<false>(ring, bm, lane, i, rtab);
         else
-            word = replay_block<2, false>(ring, bm, lane, i, s, rtab);
+            word = replay_block_mixed(ring, bm, lane, i, s, rtab);
         emitted += __builtin_popcount(word);
         if (b == b0) lastw = word;
         else out[(size_t)b * 64] = word;
