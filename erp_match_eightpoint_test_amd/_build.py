@@ -75,5 +75,23 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB_PATH
 
 
+DRIVER_SRC = os.path.join(ROOT, "tests", "cpp", "class_api_driver.cpp")
+DRIVER_BIN = os.path.join(ROOT, "tests", "cpp", "class_api_driver")
+
+
+def build_driver(force: bool = False) -> str:
+    """the C++ class-API driver (tests/cpp): host code only, g++ against liberp_match.so -- the
+    link a reference maintainer would do."""
+    if (not force and os.path.exists(DRIVER_BIN)
+            and os.path.getmtime(DRIVER_BIN) >= max(os.path.getmtime(DRIVER_SRC),
+                                                    os.path.getmtime(LIB_PATH))):
+        return DRIVER_BIN
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), DRIVER_SRC,
+                    "-o", DRIVER_BIN, "-L", LIB_DIR, "-lerp_match", f"-Wl,-rpath,{LIB_DIR}",
+                    "-Wl,-rpath,$ORIGIN/../../erp_match_eightpoint_test_amd/lib",
+                    "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    return DRIVER_BIN
+
+
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
