@@ -54,6 +54,10 @@ def parse():
     ap.add_argument("--sigma", type=float, default=0.03,
                     help="pairs workload: descriptor noise of the true partners")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--hard-steps", type=int, default=3,
+                    help="pairs workload: timed steps of a second, harder batch (half the left "
+                         "keypoints without a partner, descriptor noise 0.035, 30%% of the true "
+                         "matches at wrong positions) reported beside the headline; 0 = off")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--profile-tag", default="r02a")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
@@ -73,10 +77,10 @@ def parse():
 
 
 def make_batch(rank: int, B: int, kpts: int, seed: int, inlier_frac: float = 0.8,
-               sigma: float = 0.03):
+               sigma: float = 0.03, mismatch_frac: float = 0.0):
     from erp_match_eightpoint_test_amd import synth
     pairs = [synth.make_pair(seed + 1000 * rank + i, n_kpts=kpts, inlier_frac=inlier_frac,
-                             sigma=sigma) for i in range(B)]
+                             sigma=sigma, mismatch_frac=mismatch_frac) for i in range(B)]
     return pairs
 
 
@@ -532,9 +536,9 @@ def main():
         subs.append(dict(b=b, ctx=ctx, runner=runner, stream=torch.cuda.Stream(dev),
                          res=torch.empty((len(part), 64), dtype=torch.uint8, device=dev)))
 
-    def call():
-        for sb in subs:
-            b = sb["b"]
+    def call(batch=None):
+        for i, sb in enumerate(subs):
+            b = sb["b"] if batch is None else batch[i]
             with torch.cuda.stream(sb["stream"]):
                 out = sb["runner"].run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"],
                                        b["off_r"], b["width"], b["height"], b["max_nq"],
@@ -648,6 +652,36 @@ def main():
                 ts.append(time.perf_counter() - ta)
         lat = {"single_pair_ms": float(np.median(ts)) * 1e3,
                "note": "one 4096x4096 pair, 10k iterations, batch of 1, host-timed, median of 20"}
+    # a harder batch through the same contexts and streams (beside the headline, not `value`):
+    # half the left keypoints without a true partner, more descriptor noise (0.035: much more
+    # and the 0.3 ratio test rejects the true partners too), 30 % of the true matches at wrong
+    # positions (outliers the consensus must reject)
+    hard = None
+    if args.steps > 0 and args.hard_steps > 0:
+        hpairs = make_batch(rank, args.pairs, args.kpts, args.seed + 7777, 0.5, 0.035, 0.3)
+        hparts = [hpairs[i * args.pairs // S:(i + 1) * args.pairs // S] for i in range(S)]
+        hb = [to_device(part, dev) for part in hparts]
+        for sb, b in zip(subs, hb):
+            sb["runner"].reserve(len(b["width"]), b["max_nq"], b["max_nt"])
+        call(hb)
+        torch.cuda.synchronize()
+        th0 = time.perf_counter()
+        for _ in range(args.hard_steps):
+            hout = call(hb)
+        torch.cuda.synchronize()
+        th = (time.perf_counter() - th0) / args.hard_steps
+        hres = results_to_numpy(hout)
+        hard = {"value": args.pairs / th, "unit": "pairs/s", "ms_per_step": th * 1e3,
+                "steps": args.hard_steps, "inlier_frac": 0.5, "sigma": 0.035,
+                "mismatch_frac": 0.3,
+                "mean_abs_euler_err_deg_max": max(
+                    float(np.degrees(np.abs(r["R"] - p["euler_gt"])).mean())
+                    for r, p in zip(hres, hpairs)),
+                "all_status_ok": bool(np.all(hres["status"] == 0)),
+                "M_mean": float(hres["M"].mean()), "K_mean": float(hres["K"].mean()),
+                "survivors_mean": float(hres["survivors"].mean()),
+                "survivors_max": int(hres["survivors"].max()),
+                "binned_rows_mean": float(hres["binned_rows"].mean())}
     cpu = None
     parity = None
     if world == 1 and not args.no_cpu_baseline:
@@ -682,6 +716,7 @@ def main():
         "roofline_stages": stage_roofs,
         "cpu_baseline": cpu,
         "latency": lat,
+        "hard_data": hard,
         "stages_ms_serial_step": {k: v[0] for k, v in stages.items()},
         "check": {"all_status_ok": ok, "mean_abs_euler_err_deg_max": max(err_deg),
                   "M_mean": float(res["M"].mean()), "K_mean": float(res["K"].mean()),

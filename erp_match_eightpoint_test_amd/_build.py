@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(LIB_DIR, "liberp_match.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ERP_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["kernels.hip", "capi.hip", "remap.hip", "remap_api.hip", "surf.hip", "surf_api.hip",
+SOURCES = ["kernels.hip", "matcher.hip", "capi.hip", "remap.hip", "remap_api.hip", "surf.hip", "surf_api.hip",
            "host_api.cpp"]
 HEADERS = ["erp_device.hpp", "erp_kernels.hpp", "erp_remap.hpp", "erp_surf.hpp"]
 PUBLIC_HEADERS = ["erp_match.h", os.path.join("erp", "feature_matcher.hpp"),
@@ -30,6 +30,10 @@ PUBLIC_HEADERS = ["erp_match.h", os.path.join("erp", "feature_matcher.hpp"),
 # correctly rounded for bit-exact DMatch.distance.
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
             "-Wno-unused-function", f"--offload-arch={ARCH}"]
+# per-source extras: the matcher's MFMA accumulators in VGPRs (the filter's bounds read them
+# directly; the default AGPR form costs one v_accvgpr_read per element) and no NaN quieting in
+# its min trees (finite descriptors; matcher.hip header)
+EXTRA_FLAGS = {"matcher.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-fno-honor-nans"]}
 
 
 def _inputs():
@@ -46,15 +50,20 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(f) <= t for f in _inputs() if os.path.exists(f))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+def build(force: bool = False, verbose: bool = False, lib_path: str = LIB_PATH,
+          src_override: dict | None = None) -> str:
+    """src_override / lib_path: development variants (a source file replaced by another path,
+    built into another library; see capi.lib_path's ERP_LIB_PATH)."""
+    if not force and lib_path == LIB_PATH and up_to_date():
         return LIB_PATH
-    os.makedirs(LIB_DIR, exist_ok=True)
+    lib_dir = os.path.dirname(lib_path)
+    os.makedirs(lib_dir, exist_ok=True)
     objs, cmds = [], []
     for src in SOURCES:
-        obj = os.path.join(LIB_DIR, os.path.splitext(src)[0] + ".o")
-        cmds.append([HIPCC, *CXXFLAGS, "-I", os.path.join(ROOT, "include"), "-c",
-                     os.path.join(CSRC, src), "-o", obj])
+        obj = os.path.join(lib_dir, os.path.splitext(src)[0] + ".o")
+        path = (src_override or {}).get(src, os.path.join(CSRC, src))
+        cmds.append([HIPCC, *CXXFLAGS, *EXTRA_FLAGS.get(src, []), "-I", os.path.join(ROOT, "include"),
+                     "-I", CSRC, "-c", path, "-o", obj])
         objs.append(obj)
     # one hipcc per source, in parallel (kernels.hip dominates; the rest overlap it)
     jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", "0") or 0) or os.cpu_count() or 1))
@@ -67,12 +76,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
     with ThreadPoolExecutor(jobs) as ex:
         for f in [ex.submit(run, c) for c in cmds]:
             f.result()
-    tmp = LIB_PATH + ".tmp"
+    tmp = lib_path + ".tmp"
     subprocess.run([HIPCC, *CXXFLAGS, "-shared", "-o", tmp, *objs], check=True)
-    os.replace(tmp, LIB_PATH)
+    os.replace(tmp, lib_path)
     for o in objs:
         os.remove(o)
-    return LIB_PATH
+    return lib_path
 
 
 DRIVER_SRC = os.path.join(ROOT, "tests", "cpp", "class_api_driver.cpp")

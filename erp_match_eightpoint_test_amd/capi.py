@@ -120,7 +120,8 @@ _lib = None
 
 
 def lib_path() -> str:
-    return _build.LIB_PATH
+    # ERP_LIB_PATH: a development build elsewhere (A/B experiments); default: the in-tree library
+    return os.environ.get("ERP_LIB_PATH") or _build.LIB_PATH
 
 
 def load(build_if_missing: bool = False):

@@ -239,17 +239,19 @@ erp::BatchShape make_shape(int n_pairs, int max_nq, int max_nt, int iters, doubl
     sh.n_pairs = n_pairs;
     sh.max_nq = std::max(max_nq, 1);
     sh.max_nt = std::max(max_nt, 1);
-    // matcher filter grid: 128 queries x one train chunk per block, >= ~2048 blocks
-    const int qblocks = (sh.max_nq + 127) / 128;
-    const int tmax = (sh.max_nt + 31) / 32;
-    int chunks = (2048 + qblocks * n_pairs - 1) / (qblocks * n_pairs);
+    // matcher filter grid: 256 queries x one train chunk per block, >= ~1024 blocks, chunks of
+    // >= 256 rows (the filter's first stage of every chunk runs twice, bounds then candidates)
+    const int qblocks = (sh.max_nq + 255) / 256;
+    const int tmax = std::max(1, (sh.max_nt + 255) / 256);
+    int chunks = (1024 + qblocks * n_pairs - 1) / (qblocks * n_pairs);
     chunks = std::max(1, std::min(chunks, tmax));
     int chunk_len = (sh.max_nt + chunks - 1) / chunks;
     chunk_len = (chunk_len + 31) / 32 * 32;
     sh.fchunk_len = chunk_len;
     sh.fchunks = (sh.max_nt + chunk_len - 1) / chunk_len;
     // exact VALU sweep: 128 queries x one chunk (multiple of 128 train rows) per block
-    int xch = (2048 + qblocks * n_pairs - 1) / (qblocks * n_pairs);
+    const int xqblocks = (sh.max_nq + 127) / 128;
+    int xch = (2048 + xqblocks * n_pairs - 1) / (xqblocks * n_pairs);
     xch = std::max(1, std::min(xch, (sh.max_nt + 127) / 128));
     sh.xchunk_len = ((sh.max_nt + xch - 1) / xch + 127) / 128 * 128;
     sh.xchunks = (sh.max_nt + sh.xchunk_len - 1) / sh.xchunk_len;
@@ -268,7 +270,7 @@ bool ensure_matcher(erp_ctx* c, const erp::BatchShape& sh) {
     return ensure(c->part, PQ * sh.fchunks * sizeof(erp::Top2)) && ensure(c->part1, fold) &&
            ensure(c->pu, PQ * sh.fchunks * sizeof(float2)) &&
            ensure(c->ccount, PQ * sh.fchunks * 2 * 4) &&
-           ensure(c->cand, PQ * sh.fchunks * 2 * erp::kCandSub * 4) &&
+           ensure(c->cand, erp::knn2_cand_bytes(sh)) &&
            ensure(c->tsplit, erp::knn2_split_bytes(sh)) &&
            ensure(c->ovf, 4 + 12 * PQ * sh.fchunks);
 }
@@ -290,7 +292,7 @@ erp_status fold_and_merge(erp_ctx* ctx, const int64_t* oq, const int64_t* ot,
     return ERP_OK;
 }
 
-// exact k=2 + ratio test: MFMA filter (upper bounds), candidates, exact rescoring, merge -- or
+// exact k=2 + ratio test: MFMA filter (bounds + provisional candidates), exact rescoring, merge -- or
 // the exact packed-FP32 sweep, merge
 erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int64_t* oq,
                        const int64_t* ot, const erp::BatchShape& sh, float ratio,
@@ -305,19 +307,15 @@ erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int
     }
     auto* pu = (float2*)ctx->pu.p;
     auto* cc = (int32_t*)ctx->ccount.p;
-    auto* cand = (int32_t*)ctx->cand.p;
+    void* cand = ctx->cand.p;
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_FILTER, st);
-        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand, 1, st));
-    }
-    {
-        StageTimer _t(ctx, ERP_STAGE_KNN2_CANDIDATES, st);
-        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand, 2, st));
+        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_RESCORE, st);
-        ERP_CK(erp::launch_knn2_rescore(dq, dt, oq, ot, sh, cc, cand, (erp::Top2*)ctx->part.p,
-                                        (int32_t*)ctx->ovf.p, st));
+        ERP_CK(erp::launch_knn2_rescore(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand,
+                                        (erp::Top2*)ctx->part.p, (int32_t*)ctx->ovf.p, st));
     }
     return fold_and_merge(ctx, oq, ot, sh, sh.fchunk_len, sh.fchunks, ratio, matches, counts,
                           flags, st);

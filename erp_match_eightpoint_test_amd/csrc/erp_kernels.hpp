@@ -1,4 +1,5 @@
-// erp_kernels.hpp -- launchers of the gfx950 kernels (implemented in kernels.hip).
+// erp_kernels.hpp -- launchers of the gfx950 kernels (matcher.hip: the matcher; kernels.hip:
+// the rest of the hot path).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -11,8 +12,8 @@ namespace erp {
 constexpr int kDim = 64;          // SURF descriptor length (extended=false)
 constexpr int kMaxQ = 24;         // jump polynomials x^(64(M-1)2^k): waves per pair < 2^24
 constexpr int kPolyWords = 31;    // glibc TYPE_3 degree
-constexpr int kCandSub = 32;      // matcher candidates kept per (query, train chunk, lane half)
-                                  // (more: exact sweep of the query)
+constexpr int kCandSlots = 28;    // matcher: tiles with candidate rows kept per (query, train
+                                  // chunk, lane half) (more: exact sweep of the chunk)
 
 struct Top2 {                     // partial k=2 result of one train chunk for one query
     float d0;                     // best squared distance
@@ -42,7 +43,7 @@ struct Workspace {
 struct BatchShape {
     int n_pairs;
     int max_nq, max_nt;
-    int fchunks, fchunk_len;      // train chunks of the matcher's filter passes
+    int fchunks, fchunk_len;      // train chunks of the matcher's MFMA filter
     int xchunks, xchunk_len;      // train chunks of the exact VALU sweep (multiples of 128)
     int iters;
     int max_s;                    // (int)(max_nq * sample_frac)
@@ -55,20 +56,23 @@ hipError_t launch_set_i64x4(int64_t* p, int64_t a, int64_t b, int64_t c, int64_t
                             hipStream_t st);                                       // lifetime)
 void init_constants();            // reduction table for the jump polynomials (once per device)
 
-// matcher: pass 1 (per-chunk top-2 upper bounds pu), pass 2 (candidates; ccount zeroed
-// before), rescore (exact Top2 per query into part[pairs][max_nq]), merge (ratio + compaction)
-// split = scratch of knn2_split_bytes(sh): the train rows as bf16 hi / lo pieces + norms
-// (pass 1 fills it)
+// matcher: knn2_filter (train rows split to bf16, then ONE MFMA pass: per-(query, chunk) top-2
+// upper bounds pu, and per (query, chunk, lane half) up to kCandSlots tiles that may hold
+// candidates: the tile and its 16 bounds of the lane's rows; counts in ccount), rescore (exact
+// Top2 per (query, chunk) of the stored rows under the final bound into
+// part[pairs][fchunks][max_nq]), merge (ratio + compaction).  split = scratch of
+// knn2_split_bytes(sh) (bf16 rows, norms, per-pair max norm); cand = knn2_cand_bytes(sh).
 size_t knn2_split_bytes(const BatchShape& sh);
+size_t knn2_cand_bytes(const BatchShape& sh);
 hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
                               const int64_t* off_t, const BatchShape& sh, void* split,
-                              float2* pu, int32_t* ccount, int32_t* cand, int pass,
-                              hipStream_t st);
-// rescore -> per-chunk exact partials part[pairs][fchunks][max_nq]; ovf = scratch of
-// 4 + 12 * n_pairs * max_nq * fchunks bytes: overflowed (pair, query, chunk) for the exact sweep
+                              float2* pu, int32_t* ccount, void* cand, hipStream_t st);
+// ovf = scratch of 4 + 12 * n_pairs * max_nq * fchunks bytes: overflowed (pair, query, chunk)
+// for the exact sweep
 hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
-                               const int64_t* off_t, const BatchShape& sh, const int32_t* ccount,
-                               const int32_t* cand, Top2* part, int32_t* ovf, hipStream_t st);
+                               const int64_t* off_t, const BatchShape& sh, void* split,
+                               const float2* pu, const int32_t* ccount, void* cand, Top2* part,
+                               int32_t* ovf, hipStream_t st);
 // exact sweep on packed FP32 VALU (no MFMA filter): per-(chunk, query) exact k=2 into
 // xpart[pairs][xchunks][max_nq]
 hipError_t launch_knn2_exact(const float* desc_q, const float* desc_t, const int64_t* off_q,

@@ -70,619 +70,6 @@ __device__ int block_exclusive_scan(int v, int* ws, int* total) {
     return base + x - v;
 }
 
-// ===================================================================== matcher =========
-// Exact k=2 in three steps (the result is identical to a brute-force sweep in the flann::L2
-// order, lowest train index winning ties):
-//  1. knn2_filter<1>: approximate squared distances a = |q|^2 + |t|^2 - 2 qh.th from ONE bf16
-//     MFMA product of the rounded rows (qh = bf16(q), th = bf16(t); f32 accumulation).
-//     Bound: with |q_i - qh_i| <= 2^-8 |q_i| (bf16 round-to-nearest, 8 significant bits),
-//     |q.t - qh.th| <= sum |qh_i||t_i - th_i| + |q_i - qh_i||t_i| <= 2^-7 (1 + 2^-9) |q||t|
-//     <= 2^-8 (1 + 2^-9) (|q|^2 + |t|^2); the MFMA's f32 accumulation of 64 exact products,
-//     the f32 norms, the reference's own rounding of e (64 f32 squares summed: <= 2^-16.9 S)
-//     and the bound's own f32 formation add < 1.7e-5 (|q|^2 + |t|^2).  So
-//     |a - e| <= 0.0078444 (|q|^2 + |t|^2) < eps(q,t) = 0x1.08p-7 (|q|^2 + |t|^2) = 0.0080566
-//     (|q|^2 + |t|^2) for the reference's exact f32 value e.  Each query keeps the two
-//     smallest u = a + eps per chunk.
-//  2. knn2_filter<2>: U2 = the second smallest u over all chunks bounds e of the true second
-//     neighbour from above; every train row with l = a - eps <= U2 (which includes every row
-//     with e <= e_(2), i.e. both true neighbours and all their ties) is a candidate (a few per
-//     query on SURF-like data: the rows within 4 eps of the second neighbour).  Candidates go
-//     to per-(query, chunk, lane half) lists with a register counter: no atomics.
-//  3. knn2_rescore: exact flann::L2 distances of the candidates (a full exact sweep if a query
-//     ever has more than kCandSub in one list), giving (d0, j0, d1) exactly.
-// The train rows are rounded to bf16 ONCE per batch (knn2_split: bf16 rows and |t|^2, dense
-// [pair][row] layout) and staged per 32-row tile into LDS by plain copies.
-// Matrix layout for v_mfma_f32_32x32x16_bf16: A = 32 train rows x 16 dims (LDS), B = 16 dims x
-// 32 queries (registers, rounded once), D = 32 x 32 with the query on the lane (col = lane & 31)
-// and 16 train rows in the registers (row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)).  Block = 4
-// waves x 32 queries x one train chunk.  The bounds are formed with packed f32 math:
-//   u = fma(-2, qh.th, qu + tu),  qu = |q|^2 (1 + eps) + tiny,  tu = |t|^2 (1 + eps)
-//   l = fma(-2, qh.th, ql + tl),  ql = |q|^2 (1 - eps) - tiny,  tl = |t|^2 (1 - eps)
-// (= a +- (eps (|q|^2 + |t|^2) + tiny) up to four more f32 roundings, <= 2^-21 (|q|^2 + |t|^2),
-// inside the bound's slack).  Pass 1 keeps two group minima of u per lane (v_min3), whose top-2
-// over the query's lanes and chunks bounds its second smallest u; pass 2 takes the minimum l of
-// the lane's 16 rows and only builds the candidate mask when it reaches U2.
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-constexpr int kFQ = 128;            // queries per block
-constexpr int kFT = 32;             // train rows per tile
-constexpr int kFRow = 72;           // bf16 per LDS row: 64 + 8 pad (conflict-free b128 reads)
-constexpr float kFEps = 0x1.08p-7f;
-constexpr float kFTiny = 0x1p-100f; // absolute floor (flushed denormals)
-
-constexpr int kFST = 4;             // 32-row tiles per LDS stage (one barrier per stage)
-struct FilterLds {
-    bf16x8 hi[2][kFST * kFT * kFRow / 8];
-    float tb[2][kFST * kFT];        // tu (pass 1) or tl (pass 2) of the stage's rows
-};
-
-__device__ __forceinline__ bf16x8 round8(const float4 a, const float4 b) {
-    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    bf16x8 h;
-#pragma unroll
-    for (int k = 0; k < 8; k++) h[k] = (__bf16)v[k];
-    return h;
-}
-
-__device__ __forceinline__ float sq8(const float4 a, const float4 b) {
-    return a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z +
-           b.w * b.w;
-}
-
-// train rows -> thi [pair][max_nt][64] bf16 (round to nearest) and tn [pair][max_nt] = |t|^2;
-// four threads per row (16 dims each)
-__global__ __launch_bounds__(256) void knn2_split_kernel(const float* __restrict__ dt,
-                                                         const int64_t* __restrict__ off_t,
-                                                         int max_nt, bf16x8* __restrict__ thi,
-                                                         float* __restrict__ tn) {
-    const int p = blockIdx.y, tid = threadIdx.x;
-    const int j = blockIdx.x * 64 + (tid >> 2), part = tid & 3;
-    const int64_t tbase = off_t[p];
-    const int nt = (int)(off_t[p + 1] - tbase);
-    if (blockIdx.x * 64 >= nt) return;  // uniform
-    float ss = 0.f;
-    const size_t o = ((size_t)p * max_nt + j) * 8 + 2 * part;  // in bf16x8 units
-    if (j < nt) {
-        const float4* tp = reinterpret_cast<const float4*>(dt + (tbase + j) * kDim + 16 * part);
-        const float4 a = tp[0], b = tp[1], c = tp[2], d = tp[3];
-        thi[o] = round8(a, b);
-        thi[o + 1] = round8(c, d);
-        ss = sq8(a, b) + sq8(c, d);
-    }
-    ss += __shfl_xor(ss, 1, 64);
-    ss += __shfl_xor(ss, 2, 64);
-    if (part == 0 && j < nt) tn[(size_t)p * max_nt + j] = ss;
-}
-
-template <int PASS>
-__global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restrict__ dq,
-                                                          const bf16x8* __restrict__ thi,
-                                                          const float* __restrict__ tn,
-                                                          const int64_t* __restrict__ off_q,
-                                                          const int64_t* __restrict__ off_t,
-                                                          int chunk_len, int chunks, int max_nq,
-                                                          int max_nt,
-                                                          float2* __restrict__ pu,
-                                                          int32_t* __restrict__ ccount,
-                                                          int32_t* __restrict__ cand) {
-    __shared__ FilterLds sm;
-    const int p = blockIdx.z;
-    const int64_t qbase = off_q[p];
-    const int nq = (int)(off_q[p + 1] - qbase);
-    const int nt = (int)(off_t[p + 1] - off_t[p]);
-    const int q0 = blockIdx.x * kFQ;
-    const int t0 = blockIdx.y * chunk_len;
-    if (q0 >= nq || t0 >= nt) return;  // uniform over the block
-    const int t1 = min(t0 + chunk_len, nt);
-    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5;
-    const int q = q0 + (tid >> 6) * 32 + (lane & 31);
-    const bool qv = q < nq;
-    // query fragments (B operand): dims 16c + 8h .. +7 of query q, rounded once
-    bf16x8 qh[4];
-    float qq = 0.f;
-    {
-        const float* qp = dq + (qbase + (qv ? q : 0)) * kDim + 8 * h;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const float4 a = *reinterpret_cast<const float4*>(qp + 16 * c);
-            const float4 b = *reinterpret_cast<const float4*>(qp + 16 * c + 4);
-            qq += sq8(a, b);
-            qh[c] = round8(a, b);
-        }
-        qq += __shfl_xor(qq, 32, 64);
-    }
-    const float qb = PASS == 1 ? __builtin_fmaf(qq, kFEps, qq) + kFTiny
-                               : __builtin_fmaf(qq, -kFEps, qq) - kFTiny;
-    const f32x2 qb2 = {qb, qb};
-    const f32x2 m2x = {-2.f, -2.f};
-    float U2 = 0.f;
-    if (PASS == 2) {
-        const int nch = (nt + chunk_len - 1) / chunk_len;
-        float m1 = kInf, m2 = kInf;
-        for (int c = 0; c < nch; c++) {
-            const float2 v = pu[((size_t)p * chunks + c) * max_nq + (qv ? q : 0)];
-            m2 = fminf(fmaxf(m1, v.x), fminf(m2, v.y));
-            m1 = fminf(m1, v.x);
-        }
-        U2 = m2;
-    }
-    float gm0 = kInf, gm1 = kInf;  // pass 1: group minima
-    // pass 2: this lane's candidate list (query q, this chunk, lane half h)
-    const size_t cl = (((size_t)p * max_nq + (qv ? q : 0)) * chunks + blockIdx.y) * 2 + h;
-    int32_t* clist = cand + cl * kCandSub;
-    int ncand = 0;
-    // staging: thread -> train rows (tid >> 3) + 32 u of the stage (u < kFST), 16 bytes
-    // (tid & 7) of each; the next stage is loaded into registers while this one is computed
-    // (kFST tiles of MFMA work cover an L2 miss), one barrier per stage
-    const int srow = tid >> 3, spart = tid & 7;
-    const bf16x8* thp = thi + (size_t)p * max_nt * 8;
-    const float* tnp = tn + (size_t)p * max_nt;
-    const bf16x8 z8 = {};
-    bf16x8 gh[kFST];
-    float gn[kFST];
-    auto gload = [&](int st) {
-#pragma unroll
-        for (int u = 0; u < kFST; u++) {
-            const int j = t0 + (st * kFST + u) * kFT + srow;
-            if (j < t1) {
-                gh[u] = thp[(size_t)j * 8 + spart];
-                gn[u] = spart == 0 ? tnp[j] : kInf;
-            } else {
-                gh[u] = z8;
-                gn[u] = kInf;
-            }
-        }
-    };
-    const int ntiles = (t1 - t0 + kFT - 1) / kFT;
-    const int nstages = (ntiles + kFST - 1) / kFST;
-    gload(0);
-    const int r = lane & 31;
-    auto tile_step = [&](int k, int buf, int u) {
-        const int tile0 = t0 + k * kFT;
-        f32x16 acc = {};
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            const bf16x8 ah = sm.hi[buf][((u * kFT + r) * kFRow + 16 * c + 8 * h) / 8];
-            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, qh[c], acc, 0, 0, 0);
-        }
-        f32x2 b2[8];
-#pragma unroll
-        for (int g = 0; g < 4; g++) {
-            const float4 t4 = *reinterpret_cast<const float4*>(&sm.tb[buf][u * kFT + 8 * g + 4 * h]);
-            const f32x2 ta = {t4.x, t4.y}, tb = {t4.z, t4.w};
-            const f32x2 a0 = {acc[4 * g], acc[4 * g + 1]}, a1 = {acc[4 * g + 2], acc[4 * g + 3]};
-            b2[2 * g] = __builtin_elementwise_fma(m2x, a0, qb2 + ta);
-            b2[2 * g + 1] = __builtin_elementwise_fma(m2x, a1, qb2 + tb);
-        }
-        if (PASS == 1) {
-            // two running group minima per lane (elements c = 0 / c = 1 of the packed pairs):
-            // minima of different groups are different rows, so the second smallest of the
-            // query's group minima (4 per chunk: 2 lanes x 2 groups) bounds the second smallest
-            // u from above -- as tight unless both nearest rows fall into one group.  One
-            // v_min3 per two elements instead of v_med3 + v_min per element.
-#pragma unroll
-            for (int e = 0; e < 8; e += 2) {
-                gm0 = fminf(gm0, fminf(b2[e][0], b2[e + 1][0]));
-                gm1 = fminf(gm1, fminf(b2[e][1], b2[e + 1][1]));
-            }
-        } else {
-            float mn = kInf;
-#pragma unroll
-            for (int e = 0; e < 8; e++) mn = fminf(mn, fminf(b2[e][0], b2[e][1]));
-            const bool any = qv && mn <= U2;
-            if (__builtin_amdgcn_ballot_w64(any)) {  // most tiles have no candidate
-                uint32_t cmask = 0;  // element 2e + c <-> register 4 (e >> 1) + 2 (e & 1) + c
-#pragma unroll
-                for (int e = 0; e < 8; e++)
-#pragma unroll
-                    for (int c = 0; c < 2; c++)
-                        cmask |= (qv && b2[e][c] <= U2) ? (1u << (2 * e + c)) : 0u;
-                while (cmask) {
-                    const int bit = __builtin_ctz(cmask);  // = accumulator register index
-                    cmask &= cmask - 1u;
-                    if (ncand < kCandSub) clist[ncand] = tile0 + 8 * (bit >> 2) + 4 * h + (bit & 3);
-                    ncand++;
-                }
-            }
-        }
-    };
-    for (int st = 0; st < nstages; st++) {
-        const int buf = st & 1;
-#pragma unroll
-        for (int u = 0; u < kFST; u++) {
-            sm.hi[buf][((u * kFT + srow) * kFRow) / 8 + spart] = gh[u];
-            if (spart == 0)
-                sm.tb[buf][u * kFT + srow] =
-                    gn[u] == kInf ? kInf : __builtin_fmaf(gn[u], PASS == 1 ? kFEps : -kFEps, gn[u]);
-        }
-        __syncthreads();
-        if (st + 1 < nstages) gload(st + 1);
-#pragma unroll
-        for (int u = 0; u < kFST; u++)
-            if (st * kFST + u < ntiles) tile_step(st * kFST + u, buf, u);
-    }
-    if (PASS == 1) {
-        // top-2 of the query's four group minima (this lane's two and the other half's two)
-        const float m1 = fminf(gm0, gm1), m2 = fmaxf(gm0, gm1);
-        const float o1 = __shfl_xor(m1, 32, 64), o2 = __shfl_xor(m2, 32, 64);
-        const float n2 = fminf(fmaxf(m1, o1), fminf(m2, o2));
-        const float n1 = fminf(m1, o1);
-        if (h == 0 && qv) pu[((size_t)p * chunks + blockIdx.y) * max_nq + q] = make_float2(n1, n2);
-    } else if (qv) {
-        ccount[cl] = ncand;
-    }
-}
-
-// exact squared distance in the flann::L2<float> order: per group of 4,
-// acc += d0*d0 + d1*d1 + d2*d2 + d3*d3 (no FMA)
-__device__ __forceinline__ float exact_l2(const float4* qr, const float4* __restrict__ tp) {
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < 16; c++) {
-        const float4 tv = tp[c];
-        const float d0 = qr[c].x - tv.x;
-        const float d1 = qr[c].y - tv.y;
-        const float d2 = qr[c].z - tv.z;
-        const float d3 = qr[c].w - tv.w;
-        acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
-    }
-    return acc;
-}
-
-// k=2 update with the sweep's tie rule (lowest train index first among equal distances)
-__device__ __forceinline__ void top2_consider(float acc, int j, float& b0, int& j0, float& b1) {
-    if (acc < b0 || (acc == b0 && j < j0)) {
-        b1 = b0;
-        b0 = acc;
-        j0 = j;
-    } else if (acc < b1) {
-        b1 = acc;
-    }
-}
-
-// one lane per (query, train chunk): exact distances of its candidates (~2 per query on
-// SURF-like data) -> the chunk's exact k=2 in part[pair][chunk][query]; a (query, chunk) whose
-// candidate list overflowed goes to the overflow list (exact sweep of that chunk,
-// knn2_sweep_kernel).  Chunks with no candidates write an empty Top2.
-__global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restrict__ dq,
-                                                           const float* __restrict__ dt,
-                                                           const int64_t* __restrict__ off_q,
-                                                           const int64_t* __restrict__ off_t,
-                                                           int max_nq, int chunk_len, int chunks,
-                                                           const int32_t* __restrict__ ccount,
-                                                           const int32_t* __restrict__ cand,
-                                                           Top2* __restrict__ part,
-                                                           int32_t* __restrict__ ovf) {
-    const int p = blockIdx.z, c = blockIdx.y;
-    const int q = blockIdx.x * 256 + threadIdx.x;
-    const int64_t qbase = off_q[p];
-    const int nq = (int)(off_q[p + 1] - qbase);
-    const int64_t tbase = off_t[p];
-    const int nt = (int)(off_t[p + 1] - tbase);
-    if (q >= nq || c * chunk_len >= nt) return;
-    const size_t l0 = (((size_t)p * max_nq + q) * chunks + c) * 2;
-    const int n0 = ccount[l0], n1 = ccount[l0 + 1];
-    Top2* out = part + ((size_t)p * chunks + c) * max_nq + q;
-    if (n0 > kCandSub || n1 > kCandSub) {
-        const int slot = atomicAdd(&ovf[0], 1);
-        ovf[1 + 3 * slot] = p;
-        ovf[2 + 3 * slot] = q;
-        ovf[3 + 3 * slot] = c;
-        return;
-    }
-    float b0 = kInf, b1 = kInf;
-    int j0 = 0x7fffffff;
-    if (n0 + n1 > 0) {
-        float4 qr[16];
-        const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
-#pragma unroll
-        for (int k = 0; k < 16; k++) qr[k] = qp[k];
-        for (int h = 0; h < 2; h++) {
-            const int n = h ? n1 : n0;
-            const int32_t* cl = cand + (l0 + h) * kCandSub;
-            for (int k = 0; k < n; k++) {
-                const int j = cl[k];
-                top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim)),
-                              j, b0, j0, b1);
-            }
-        }
-    }
-    *out = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
-}
-
-// exact sweep over the train rows of one chunk for the overflowed (query, chunk) entries: one
-// wave per entry, a fixed grid striding over the list
-__global__ __launch_bounds__(256) void knn2_sweep_kernel(const float* __restrict__ dq,
-                                                         const float* __restrict__ dt,
-                                                         const int64_t* __restrict__ off_q,
-                                                         const int64_t* __restrict__ off_t,
-                                                         int max_nq, int chunk_len, int chunks,
-                                                         const int32_t* __restrict__ ovf,
-                                                         Top2* __restrict__ part) {
-    const int lane = wave_lane();
-    const int nov = ovf[0];
-    for (int w = blockIdx.x * 4 + (threadIdx.x >> 6); w < nov; w += gridDim.x * 4) {
-        const int p = ovf[1 + 3 * w], q = ovf[2 + 3 * w], c = ovf[3 + 3 * w];
-        const int64_t qbase = off_q[p], tbase = off_t[p];
-        const int nt = (int)(off_t[p + 1] - tbase);
-        const int ja = c * chunk_len, jb = min(nt, ja + chunk_len);
-        float4 qr[16];
-        const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
-#pragma unroll
-        for (int k = 0; k < 16; k++) qr[k] = qp[k];
-        float b0 = kInf, b1 = kInf;
-        int j0 = 0x7fffffff;
-        for (int j = ja + lane; j < jb; j += 64)
-            top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim)), j,
-                          b0, j0, b1);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const float ob0 = __shfl_xor(b0, o, 64), ob1 = __shfl_xor(b1, o, 64);
-            const int oj = __shfl_xor(j0, o, 64);
-            if (ob0 < b0 || (ob0 == b0 && oj < j0)) {
-                b1 = fminf(b0, ob1);
-                b0 = ob0;
-                j0 = oj;
-            } else {
-                b1 = fminf(b1, ob0);
-            }
-        }
-        if (lane == 0)
-            part[((size_t)p * chunks + c) * max_nq + q] = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
-    }
-}
-
-// ---- LDS-tiled exact sweep on packed FP32 VALU (the non-MFMA matcher, configs[3]) ----------
-// Every (query, train) distance in the flann::L2<float> order, no filter: per group of 4 dims
-// acc += ((d0*d0 + d1*d1) + d2*d2) + d3*d3, each operation rounded (no FMA).  Two train rows
-// share every instruction (v_pk_add_f32 / v_pk_mul_f32 with the query value broadcast), so an
-// element costs 1.5 VALU instructions: sub, mul, add.
-// Block = 256 threads = 16 (tq) x 16 (tt); tile = 128 queries (resident in LDS for the whole
-// chunk) x 128 train rows per step.  Thread (tq, tt) owns queries tq + 16 k (k < 8) and the
-// train row pairs tt + 16 k (k < 4): 64 accumulators.  Train rows sit in LDS as row pairs,
-// dims interleaved ([pair][dim][2]), so one ds_read_b128 yields 2 dims x 2 rows = two packed
-// operands; query rows are [row][68] (the 16 rows a wave reads per instruction fall on 64
-// distinct banks).  The next tile is prefetched into registers during the current one.
-// Output: per (pair, chunk, query) the chunk's exact k=2 (Top2, lowest index among ties);
-// knn2_merge folds chunks in train order.
-constexpr int kXQ = 128, kXT = 128;
-constexpr int kXQRow = 68;             // floats per query row in LDS
-constexpr int kXPair = 2 * kDim + 4;   // floats per train row pair in LDS
-
-struct ExactLds {
-    float q[kXQ * kXQRow];
-    float t[kXT / 2 * kXPair];
-    Top2 red[4][kXQ];                  // cross-wave fold of the k=2 partials
-};
-
-__global__ __launch_bounds__(256) void knn2_exact_kernel(const float* __restrict__ dq,
-                                                         const float* __restrict__ dt,
-                                                         const int64_t* __restrict__ off_q,
-                                                         const int64_t* __restrict__ off_t,
-                                                         int chunk_len, int chunks, int max_nq,
-                                                         Top2* __restrict__ xpart) {
-    __shared__ ExactLds sm;
-    const int p = blockIdx.z;
-    const int64_t qbase = off_q[p], tbase = off_t[p];
-    const int nq = (int)(off_q[p + 1] - qbase);
-    const int nt = (int)(off_t[p + 1] - tbase);
-    const int q0 = blockIdx.x * kXQ;
-    const int t0 = blockIdx.y * chunk_len;
-    if (q0 >= nq || t0 >= nt) return;  // uniform over the block
-    const int t1 = min(t0 + chunk_len, nt);
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int tq = lane & 15, tt = (lane >> 4) + 4 * wid;
-    // query tile: 128 rows x 16 float4, 8 float4 per thread (rows beyond nq read as 0)
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-        const int e = tid + 256 * u, row = e >> 4, c = e & 15;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (q0 + row < nq) v = reinterpret_cast<const float4*>(dq + (qbase + q0 + row) * kDim)[c];
-        *reinterpret_cast<float4*>(&sm.q[row * kXQRow + 4 * c]) = v;
-    }
-    // train staging: thread -> row pair (tid >> 2) of the tile, dims 16 (tid & 3) .. +15
-    const int spair = tid >> 2, sdim = 16 * (tid & 3);
-    float4 ga[4], gb[4];
-    auto gload = [&](int tile0) {
-        const int ra = tile0 + 2 * spair, rb = ra + 1;
-        const float4* pa = reinterpret_cast<const float4*>(dt + (tbase + min(ra, t1 - 1)) * kDim + sdim);
-        const float4* pb = reinterpret_cast<const float4*>(dt + (tbase + min(rb, t1 - 1)) * kDim + sdim);
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            ga[c] = pa[c];
-            gb[c] = pb[c];
-        }
-    };
-    float b0[8], b1[8];
-    int j0[8];
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        b0[k] = kInf;
-        b1[k] = kInf;
-        j0[k] = 0x7fffffff;
-    }
-    const int ntiles = (t1 - t0 + kXT - 1) / kXT;
-    gload(t0);
-    for (int s = 0; s < ntiles; s++) {
-        const int tile0 = t0 + s * kXT;
-        __syncthreads();  // previous tile's reads are done
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-            float* w = &sm.t[spair * kXPair + 2 * (sdim + 4 * c)];
-            *reinterpret_cast<float4*>(w) = make_float4(ga[c].x, gb[c].x, ga[c].y, gb[c].y);
-            *reinterpret_cast<float4*>(w + 4) = make_float4(ga[c].z, gb[c].z, ga[c].w, gb[c].w);
-        }
-        __syncthreads();
-        if (s + 1 < ntiles) gload(tile0 + kXT);
-        f32x2 acc[8][4];
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++) acc[k][kk] = f32x2{0.f, 0.f};
-#pragma unroll 2
-        for (int g = 0; g < 16; g++) {
-            float4 tv[4][2];
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++) {
-                const float* tp = &sm.t[(tt + 16 * kk) * kXPair + 8 * g];
-                tv[kk][0] = *reinterpret_cast<const float4*>(tp);
-                tv[kk][1] = *reinterpret_cast<const float4*>(tp + 4);
-            }
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const float4 qv = *reinterpret_cast<const float4*>(&sm.q[(tq + 16 * k) * kXQRow + 4 * g]);
-                const f32x2 qx = {qv.x, qv.x}, qy = {qv.y, qv.y}, qz = {qv.z, qv.z},
-                            qw = {qv.w, qv.w};
-#pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-                    const f32x2 e0 = qx - f32x2{tv[kk][0].x, tv[kk][0].y};
-                    const f32x2 e1 = qy - f32x2{tv[kk][0].z, tv[kk][0].w};
-                    const f32x2 e2 = qz - f32x2{tv[kk][1].x, tv[kk][1].y};
-                    const f32x2 e3 = qw - f32x2{tv[kk][1].z, tv[kk][1].w};
-                    acc[k][kk] = acc[k][kk] + (((e0 * e0 + e1 * e1) + e2 * e2) + e3 * e3);
-                }
-            }
-        }
-        // k=2 update, branch-free: a thread sees its rows in increasing train index, so a later
-        // row never wins a tie (strict <); second = med3(b0, b1, d).  Rows >= t1 count as +inf.
-#pragma unroll
-        for (int kk = 0; kk < 4; kk++) {
-            const int ja = tile0 + 2 * (tt + 16 * kk);
-            const bool va = ja < t1, vb = ja + 1 < t1;
-#pragma unroll
-            for (int k = 0; k < 8; k++) {
-#pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    const float d = (h ? vb : va) ? acc[k][kk][h] : kInf;
-                    b1[k] = __builtin_amdgcn_fmed3f(b0[k], b1[k], d);
-                    j0[k] = d < b0[k] ? ja + h : j0[k];
-                    b0[k] = fminf(b0[k], d);
-                }
-            }
-        }
-    }
-    // fold the 16 threads of a query: lanes tq + 16 m of a wave (xor 16, 32), then 4 waves
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-#pragma unroll
-        for (int o = 16; o < 64; o <<= 1) {
-            const float ob0 = __shfl_xor(b0[k], o, 64), ob1 = __shfl_xor(b1[k], o, 64);
-            const int oj = __shfl_xor(j0[k], o, 64);
-            if (ob0 < b0[k] || (ob0 == b0[k] && oj < j0[k])) {
-                b1[k] = fminf(b0[k], ob1);
-                b0[k] = ob0;
-                j0[k] = oj;
-            } else {
-                b1[k] = fminf(b1[k], ob0);
-            }
-        }
-        if (lane < 16) sm.red[wid][tq + 16 * k] = Top2{b0[k], j0[k], b1[k]};
-    }
-    __syncthreads();
-    if (tid < kXQ && q0 + tid < nq) {
-        Top2 r = sm.red[0][tid];
-#pragma unroll
-        for (int w = 1; w < 4; w++) {
-            const Top2 o = sm.red[w][tid];
-            if (o.d0 < r.d0 || (o.d0 == r.d0 && o.j0 < r.j0)) {
-                r.d1 = fminf(r.d0, o.d1);
-                r.d0 = o.d0;
-                r.j0 = o.j0;
-            } else {
-                r.d1 = fminf(r.d1, o.d0);
-            }
-        }
-        if (r.j0 == 0x7fffffff) r.j0 = -1;
-        xpart[((size_t)p * chunks + blockIdx.y) * max_nq + q0 + tid] = r;
-    }
-}
-
-// Fold of per-chunk partials part[pair][chunk][query] into one exact k=2 per query
-// (out[pair][query]), chunks in train order (an earlier chunk wins ties): one lane per query,
-// so a single large pair uses the whole chip (the merge below is one block per pair).
-__device__ __forceinline__ void merge_query(const Top2* part, size_t stride, int nch, int q,
-                                            float& B0, int& J, float& B1);
-
-__global__ __launch_bounds__(256) void knn2_fold_kernel(const Top2* __restrict__ part,
-                                                        const int64_t* __restrict__ off_q,
-                                                        const int64_t* __restrict__ off_t,
-                                                        int chunk_len, int chunks, int max_nq,
-                                                        Top2* __restrict__ out) {
-    const int p = blockIdx.y;
-    const int q = blockIdx.x * 256 + threadIdx.x;
-    const int nq = (int)(off_q[p + 1] - off_q[p]);
-    const int nt = (int)(off_t[p + 1] - off_t[p]);
-    if (q >= nq) return;
-    float B0, B1;
-    int J;
-    merge_query(part + (size_t)p * chunks * max_nq, (size_t)max_nq,
-                max(1, (nt + chunk_len - 1) / chunk_len), q, B0, J, B1);
-    out[(size_t)p * max_nq + q] = Top2{B0, J, B1};
-}
-
-// Fold chunk partials in train order (lowest index wins ties), apply the ratio test
-// d0 < ratio * d1 on the sqrt'd distances (convertToDMatches + feature_matcher.cpp:52), and
-// compact the survivors in ascending queryIdx order.  One block (1024 threads) per pair.
-__device__ __forceinline__ void merge_query(const Top2* part, size_t stride, int nch, int q,
-                                            float& B0, int& J, float& B1) {
-    B0 = kInf;
-    B1 = kInf;
-    J = -1;
-    for (int c = 0; c < nch; c++) {
-        const Top2 t = part[(size_t)c * stride + q];
-        if (t.d0 < B0) {
-            B1 = fminf(B0, t.d1);
-            B0 = t.d0;
-            J = t.j0;
-        } else {
-            B1 = fminf(B1, t.d0);
-        }
-    }
-}
-
-__global__ __launch_bounds__(1024) void knn2_merge_kernel(const Top2* __restrict__ part,
-                                                          const int64_t* __restrict__ off_q,
-                                                          const int64_t* __restrict__ off_t,
-                                                          int chunk_len, int chunks, int max_nq,
-                                                          float ratio, erp_dmatch* __restrict__ out,
-                                                          int32_t* __restrict__ counts,
-                                                          int32_t* __restrict__ flags) {
-    __shared__ int ws[16];
-    const int p = blockIdx.x;
-    const int nq = (int)(off_q[p + 1] - off_q[p]);
-    const int nt = (int)(off_t[p + 1] - off_t[p]);
-    if (nt < 2 || nq <= 0) {
-        if (threadIdx.x == 0) {
-            counts[p] = 0;
-            if (nq > 0) flags[p] |= 1;  // knn_matches[i][1] would not exist (UB in the reference)
-        }
-        return;
-    }
-    const int nch = (nt + chunk_len - 1) / chunk_len;
-    const Top2* pp = part + (size_t)p * chunks * max_nq;
-    const int per = (nq + 1023) / 1024;
-    const int qa = min(nq, (int)threadIdx.x * per), qb = min(nq, qa + per);
-    int cnt = 0;
-    for (int q = qa; q < qb; q++) {
-        float B0, B1;
-        int J;
-        merge_query(pp, (size_t)max_nq, nch, q, B0, J, B1);
-        const float d0 = __builtin_sqrtf(B0), d1 = __builtin_sqrtf(B1);
-        cnt += (d0 < ratio * d1) ? 1 : 0;
-    }
-    int total;
-    int pos = block_exclusive_scan<1024>(cnt, ws, &total);
-    erp_dmatch* o = out + (size_t)p * max_nq;
-    for (int q = qa; q < qb; q++) {
-        float B0, B1;
-        int J;
-        merge_query(pp, (size_t)max_nq, nch, q, B0, J, B1);
-        const float d0 = __builtin_sqrtf(B0), d1 = __builtin_sqrtf(B1);
-        if (d0 < ratio * d1) o[pos++] = erp_dmatch{q, J, 0, d0};
-    }
-    if (threadIdx.x == 0) counts[p] = total;
-}
-
 // ============================================================== gather + bearings =======
 __global__ void bearings_from_matches_kernel(const erp_dmatch* __restrict__ matches,
                                              const int32_t* __restrict__ counts,
@@ -2952,68 +2339,6 @@ void init_constants() {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_red), red, sizeof(red));
 }
 
-size_t knn2_split_bytes(const BatchShape& sh) {
-    return (size_t)sh.n_pairs * sh.max_nt * (kDim * sizeof(__bf16) + sizeof(float));
-}
-
-hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
-                              const int64_t* off_t, const BatchShape& sh, void* split,
-                              float2* pu, int32_t* ccount, int32_t* cand, int pass,
-                              hipStream_t st) {
-    bf16x8* thi = (bf16x8*)split;
-    float* tn = (float*)(thi + (size_t)sh.n_pairs * sh.max_nt * 8);
-    if (pass == 1)
-        hipLaunchKernelGGL(knn2_split_kernel, dim3((sh.max_nt + 63) / 64, sh.n_pairs), dim3(256), 0,
-                           st, desc_t, off_t, sh.max_nt, thi, tn);
-    dim3 grid((sh.max_nq + kFQ - 1) / kFQ, sh.fchunks, sh.n_pairs);
-    if (pass == 1)
-        hipLaunchKernelGGL(knn2_filter_kernel<1>, grid, dim3(256), 0, st, desc_q, thi, tn,
-                           off_q, off_t, sh.fchunk_len, sh.fchunks, sh.max_nq, sh.max_nt, pu,
-                           ccount, cand);
-    else
-        hipLaunchKernelGGL(knn2_filter_kernel<2>, grid, dim3(256), 0, st, desc_q, thi, tn,
-                           off_q, off_t, sh.fchunk_len, sh.fchunks, sh.max_nq, sh.max_nt, pu,
-                           ccount, cand);
-    return hipGetLastError();
-}
-
-hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
-                               const int64_t* off_t, const BatchShape& sh, const int32_t* ccount,
-                               const int32_t* cand, Top2* part, int32_t* ovf, hipStream_t st) {
-    hipLaunchKernelGGL(set_i32_kernel, dim3(1), dim3(1), 0, st, ovf, 0);
-    dim3 grid((sh.max_nq + 255) / 256, sh.fchunks, sh.n_pairs);
-    hipLaunchKernelGGL(knn2_rescore_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
-                       sh.max_nq, sh.fchunk_len, sh.fchunks, ccount, cand, part, ovf);
-    hipLaunchKernelGGL(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
-                       sh.max_nq, sh.fchunk_len, sh.fchunks, ovf, part);
-    return hipGetLastError();
-}
-
-hipError_t launch_knn2_exact(const float* desc_q, const float* desc_t, const int64_t* off_q,
-                             const int64_t* off_t, const BatchShape& sh, Top2* xpart,
-                             hipStream_t st) {
-    dim3 grid((sh.max_nq + kXQ - 1) / kXQ, sh.xchunks, sh.n_pairs);
-    hipLaunchKernelGGL(knn2_exact_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
-                       sh.xchunk_len, sh.xchunks, sh.max_nq, xpart);
-    return hipGetLastError();
-}
-
-hipError_t launch_knn2_fold(const Top2* part, const int64_t* off_q, const int64_t* off_t,
-                            const BatchShape& sh, int chunk_len, int chunks, Top2* out,
-                            hipStream_t st) {
-    hipLaunchKernelGGL(knn2_fold_kernel, dim3((sh.max_nq + 255) / 256, sh.n_pairs), dim3(256), 0,
-                       st, part, off_q, off_t, chunk_len, chunks, sh.max_nq, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
-                             const BatchShape& sh, int chunk_len, int chunks, float ratio,
-                             erp_dmatch* matches, int32_t* counts, int32_t* flags,
-                             hipStream_t st) {
-    hipLaunchKernelGGL(knn2_merge_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, part, off_q, off_t,
-                       chunk_len, chunks, sh.max_nq, ratio, matches, counts, flags);
-    return hipGetLastError();
-}
 
 hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t* counts,
                                         const erp_point2f* kp_l, const erp_point2f* kp_r,

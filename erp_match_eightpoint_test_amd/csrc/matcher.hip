@@ -1,0 +1,924 @@
+// matcher.hip -- gfx950 kernels of the exact k=2 + ratio-0.3 matcher
+// (src/feature_matcher.cpp:42-59, FlannBasedMatcher::knnMatch(k = 2) + the ratio test; the
+// exact brute-force limit of FLANN's randomized KD-tree, distances in flann::L2<float>'s order).
+//
+// Compiled with -ffp-contract=off (the flann::L2 accumulation, the ratio test and sqrtf must
+// round like the reference's x86-64 code), -mllvm -amdgpu-mfma-vgpr-form (the filter's MFMA
+// accumulators live in VGPRs: no v_accvgpr_read per element before the bounds epilogue) and
+// -fno-honor-nans (descriptors are finite: no NaN-quieting ops in the filter's min trees).
+//
+// Kernels: knn2_split (train rows -> bf16(-2 t), |t|^2), knn2_filter (ONE bf16 MFMA pass:
+// per-query upper bounds + provisional candidates), knn2_rescore (exact distances of the
+// candidates that survive the final bound), knn2_sweep (exact sweep for overflowed lists),
+// knn2_exact (the packed-FP32 sweep: the non-MFMA matcher), knn2_fold / knn2_merge (chunk fold,
+// ratio test, order-preserving compaction).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "erp_kernels.hpp"
+
+namespace erp {
+
+namespace {
+
+constexpr float kInf = __builtin_huge_valf();
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int wave_lane() { return threadIdx.x & 63; }
+
+// exclusive scan over a block of BLOCK threads (BLOCK multiple of 64, <= 1024)
+template <int BLOCK>
+__device__ int block_exclusive_scan(int v, int* ws, int* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) ws[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        int t = lane < BLOCK / 64 ? ws[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < BLOCK / 64; o <<= 1) {
+            const int y = __shfl_up(t, o, 64);
+            if (lane >= o) t += y;
+        }
+        if (lane < BLOCK / 64) ws[lane] = t;
+    }
+    __syncthreads();
+    const int base = wid ? ws[wid - 1] : 0;
+    *total = ws[BLOCK / 64 - 1];
+    __syncthreads();
+    return base + x - v;
+}
+
+// ===================================================================== matcher =========
+// Exact k=2 in two steps (the result is identical to a brute-force sweep in the flann::L2
+// order, lowest train index winning ties):
+//  1. knn2_filter: ONE bf16 MFMA product per (query, train) pair gives u' = tu - 2 qh.th with
+//     qh = bf16(q), th = bf16(t) (|q_i - qh_i| <= 2^-8 |q_i|) and tu = |t|^2 (1 + eps) loaded
+//     as the MFMA's C operand (the B operand holds bf16(-2 t), exact scaling), so the element
+//     needs no epilogue arithmetic.  With S = |q|^2 + |t|^2 and a = |q|^2 + |t|^2 - 2 qh.th,
+//       |q.t - qh.th| <= 2^-7 (1 + 2^-9) |q||t| <= 2^-8 (1 + 2^-9) S,
+//     and the f32 accumulation of the 64 exact bf16 products, the f32 norms, e's own rounding
+//     (64 f32 squares summed: <= 2^-16.9 S) and the few f32 roundings of u' and the bounds
+//     (each <= 2^-24 3 S) add < 2e-5 S, so |a - e| <= 0.0078444 S for the reference's exact
+//     f32 value e, against eps = 0x1.08p-7 = 0.0080566: u = a + eps S >= e + 2.1e-4 S and
+//     l = a - eps S <= e - 2.1e-4 S.  QB = |q|^2 (1 + eps) + tiny turns u' into u = u' + QB.
+//     Running bound: every lane keeps two group minima of u' (its elements 0-7 and 8-15 are
+//     disjoint train rows), so the second smallest of a query's four group minima (both lane
+//     halves) G bounds the chunk's second smallest u' from above, and G + QB >= e_(2) (the
+//     true second-neighbour distance).  A row t with e_t <= e_(2) (both neighbours and all
+//     their ties) has l_t <= e_(2) - 2.1e-4 S_t <= G + QB, i.e.
+//       u'_t <= G + (QB - QL) + 2 eps |t|^2 <= thr := G + (QB - QL) + teM,
+//     QL = |q|^2 (1 - eps) - tiny, teM = 2 eps max_t |t|^2 (per pair, rounded up): every such
+//     row is stored as a provisional candidate with the lower bound l* = u'_t + QL - teM <= l_t.
+//     G only falls as the chunk proceeds, so the set stored is a superset of the rows with
+//     l_t <= the chunk's final bound.  The first stage of the chunk runs bounds-only (with no
+//     bound yet every row would qualify) and is recomputed for candidates after the last.
+//  2. knn2_rescore: U2 = the second smallest bound over all chunks (>= e_(2)); candidates with
+//     l* <= U2 are re-scored exactly in the flann order, one lane per (query, chunk); a list
+//     that overflowed kCandSlots gets an exact sweep of its chunk.
+// Matrix layout for v_mfma_f32_32x32x16_bf16: A = 32 train rows x 16 dims (LDS), B = 16 dims x
+// 32 queries (registers, rounded once), C/D = 32 x 32 with the query on the lane (col = lane &
+// 31) and 16 train rows in the registers (row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)).  A wave
+// owns 64 queries (two B operands share every A fragment and the C operand), a block 4 waves x
+// 64 queries x one train chunk.  Per 32-row tile a wave issues 8 MFMAs (256 cycles) against
+// 8 ds_read_b128 and ~24 VALU (the two group-minimum trees and the candidate test).
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kFW = 64;             // queries per wave
+constexpr int kFQ = 4 * kFW;        // queries per block
+constexpr int kFT = 32;             // train rows per tile
+constexpr int kFRow = 72;           // bf16 per LDS row: 64 + 8 pad (conflict-free b128 reads)
+constexpr int kFST = 4;             // 32-row tiles per LDS stage (one barrier per stage)
+constexpr float kFEps = 0x1.08p-7f;
+constexpr float kFTiny = 0x1p-100f; // absolute floor (flushed denormals)
+constexpr float kFMargin = 0x1p-20f;
+
+// LDS stage (one of two): 128 train rows x 144 B (64 bf16 + 16 B pad: the b128 fragment reads
+// of a wave fall on distinct banks), then their tu = |t|^2 (1 + eps) (+inf past the chunk)
+constexpr int kFRowB = kFRow * 2;                 // 144
+constexpr int kFHiB = kFST * kFT * kFRowB;        // 18432
+constexpr int kFStageB = kFHiB + kFST * kFT * 4;  // + 512
+
+__device__ __forceinline__ bf16x8 round8(const float4 a, const float4 b, float s) {
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    bf16x8 h;
+#pragma unroll
+    for (int k = 0; k < 8; k++) h[k] = (__bf16)(v[k] * s);
+    return h;
+}
+
+__device__ __forceinline__ float sq8(const float4 a, const float4 b) {
+    return a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w + b.x * b.x + b.y * b.y + b.z * b.z +
+           b.w * b.w;
+}
+
+// train rows -> thi [pair][max_nt][64] = bf16(-2 t) (round to nearest; exact scaling of
+// bf16(t)), tn [pair][max_nt] = |t|^2, tmax[pair] = max |t|^2 (float bits; zeroed before);
+// four threads per row (16 dims each)
+__global__ __launch_bounds__(256) void knn2_split_kernel(const float* __restrict__ dt,
+                                                         const int64_t* __restrict__ off_t,
+                                                         int max_nt, bf16x8* __restrict__ thi,
+                                                         float* __restrict__ tn,
+                                                         uint32_t* __restrict__ tmax) {
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const int j = blockIdx.x * 64 + (tid >> 2), part = tid & 3;
+    const int64_t tbase = off_t[p];
+    const int nt = (int)(off_t[p + 1] - tbase);
+    if (blockIdx.x * 64 >= nt) return;  // uniform
+    float ss = 0.f;
+    const size_t o = ((size_t)p * max_nt + j) * 8 + 2 * part;  // in bf16x8 units
+    if (j < nt) {
+        const float4* tp = reinterpret_cast<const float4*>(dt + (tbase + j) * kDim + 16 * part);
+        const float4 a = tp[0], b = tp[1], c = tp[2], d = tp[3];
+        thi[o] = round8(a, b, -2.f);
+        thi[o + 1] = round8(c, d, -2.f);
+        ss = sq8(a, b) + sq8(c, d);
+    }
+    ss += __shfl_xor(ss, 1, 64);
+    ss += __shfl_xor(ss, 2, 64);
+    if (part == 0 && j < nt) tn[(size_t)p * max_nt + j] = ss;
+    __shared__ float wmax[4];
+    float m = (j < nt) ? ss : 0.f;
+#pragma unroll
+    for (int s = 4; s < 64; s <<= 1) m = fmaxf(m, __shfl_xor(m, s, 64));
+    if ((tid & 63) == 0) wmax[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0)  // |t|^2 >= 0: the float bits order like the values
+        atomicMax(&tmax[p], __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
+}
+
+// min trees of the filter (v_min3_f32 / v_min_f32: the file is built with -fno-honor-nans, so
+// the compiler drops the sNaN-quieting v_max_f32 it would put in front of every operand; the
+// bounds of finite descriptors are never NaN).  Not inline asm: the hazard recognizer must see
+// these reads of MFMA results (an asm v_min3 read them before the MFMA had written them).
+__device__ __forceinline__ float min3f(float a, float b, float c) { return fminf(fminf(a, b), c); }
+__device__ __forceinline__ float min2f(float a, float b) { return fminf(a, b); }
+
+// second smallest of {a0, a1, b0, b1} given a0/a1 and b0/b1 in any order
+__device__ __forceinline__ float second4(float a0, float a1, float b0, float b1) {
+    const float m1 = fminf(a0, a1), m2 = fmaxf(a0, a1);
+    const float o1 = fminf(b0, b1), o2 = fmaxf(b0, b1);
+    return fminf(fmaxf(m1, o1), fminf(m2, o2));
+}
+
+__global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restrict__ dq,
+                                                          const bf16x8* __restrict__ thi,
+                                                          const float* __restrict__ tn,
+                                                          const uint32_t* __restrict__ tmax,
+                                                          const int64_t* __restrict__ off_q,
+                                                          const int64_t* __restrict__ off_t,
+                                                          int chunk_len, int chunks, int max_nq,
+                                                          int max_nt, int qblocks,
+                                                          float2* __restrict__ pu,
+                                                          int32_t* __restrict__ ccount,
+                                                          int32_t* __restrict__ ctile,
+                                                          bf16x8* __restrict__ cval) {
+    __shared__ __align__(16) char sm[2 * kFStageB];
+    // XCD-aware block order: workgroups are dealt to the 8 XCDs round-robin by linear id, so
+    // XCD x gets the contiguous logical range [x NB/8, (x+1) NB/8) (query blocks fastest, then
+    // chunks, then pairs): all blocks of a pair share one XCD's L2, which holds the pair's bf16
+    // train rows (512 KB at 4096 rows) for every query block instead of refetching them from
+    // HBM per XCD.  (Identity when NB is not a multiple of 8.)
+    const int NB = gridDim.x;
+    const int lb = (NB & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (NB >> 3) + (blockIdx.x >> 3));
+    const int qb = lb % qblocks, ch = (lb / qblocks) % chunks, p = lb / (qblocks * chunks);
+    const int64_t qbase = off_q[p];
+    const int nq = (int)(off_q[p + 1] - qbase);
+    const int nt = (int)(off_t[p + 1] - off_t[p]);
+    const int q0 = qb * kFQ;
+    const int t0 = ch * chunk_len;
+    if (q0 >= nq || t0 >= nt) return;  // uniform over the block
+    const int t1 = min(t0 + chunk_len, nt);
+    const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
+    // teM >= 2 eps |t|^2 for every row of the pair
+    const float teM = __uint_as_float(tmax[p]) * (2.f * kFEps) * (1.f + kFMargin) + kFTiny;
+    // the wave's two 32-query column blocks: fragments dims 16c + 8h .. +7, rounded once
+    bf16x8 qh[2][4];
+    float QB[2], cq[2];
+    bool qv[2];
+    int qi[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const int q = q0 + (tid >> 6) * kFW + 32 * j + r;
+        qv[j] = q < nq;
+        qi[j] = qv[j] ? q : 0;
+        const float* qp = dq + (qbase + qi[j]) * kDim + 8 * h;
+        float qq = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            const float4 a = *reinterpret_cast<const float4*>(qp + 16 * c);
+            const float4 b = *reinterpret_cast<const float4*>(qp + 16 * c + 4);
+            qq += sq8(a, b);
+            qh[j][c] = round8(a, b, 1.f);
+        }
+        qq += __shfl_xor(qq, 32, 64);
+        QB[j] = __builtin_fmaf(qq, kFEps, qq) + kFTiny;
+        const float QL = __builtin_fmaf(qq, -kFEps, qq) - kFTiny;
+        cq[j] = QB[j] - (QL - teM);       // thr = G + cq (rounded up below)
+    }
+    float gm[2][2] = {{kInf, kInf}, {kInf, kInf}};
+    float thr[2] = {-kInf, -kInf};
+    int ncand[2] = {0, 0};
+    size_t cl[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++)
+        cl[j] = (((size_t)p * max_nq + qi[j]) * chunks + ch) * 2 + h;
+    // staging: thread -> train rows (tid >> 3) + 32 u of the stage (u < kFST), 16 bytes
+    // (tid & 7) of each; the next stage is loaded into registers while this one is computed
+    const int srow = tid >> 3, spart = tid & 7;
+    const bf16x8* thp = thi + (size_t)p * max_nt * 8;
+    const float* tnp = tn + (size_t)p * max_nt;
+    const bf16x8 z8 = {};
+    bf16x8 gh[kFST];
+    float gn[kFST];
+    auto gload = [&](int st) {
+#pragma unroll
+        for (int u = 0; u < kFST; u++) {
+            const int j = t0 + (st * kFST + u) * kFT + srow;
+            if (j < t1) {
+                gh[u] = thp[(size_t)j * 8 + spart];
+                gn[u] = spart == 0 ? tnp[j] : kInf;
+            } else {
+                gh[u] = z8;
+                gn[u] = kInf;
+            }
+        }
+    };
+    const int nstages = (t1 - t0 + kFST * kFT - 1) / (kFST * kFT);  // rows past t1: +inf
+    // per-lane slot bases: slot s of list j at cvbase[j] + 2 s (values), ctbase[j] + s (tile)
+    bf16x8* cvbase[2];
+    int32_t* ctbase[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        cvbase[j] = cval + cl[j] * kCandSlots * 2;
+        ctbase[j] = ctile + cl[j] * kCandSlots;
+    }
+    // LDS byte addresses: A fragment (row r, dims 16 c + 8 h) and the C operand rows 8 g + 4 h
+    const int rd_hi = r * kFRowB + 16 * h;
+    const int rd_tu = kFHiB + 16 * h;
+    const int wr_hi = srow * kFRowB + 16 * spart;
+    const int wr_tu = kFHiB + 4 * srow;
+    // one tile: the A fragments and C operand from LDS, two 4-MFMA chains (the wave's two query
+    // blocks), the epilogue (group minima; with `extract`, the candidate test and slot stores)
+    auto tile = [&](const char* sb, int u, int tile0, bool extract) {
+        bf16x8 ah[4];
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            ah[c] = *reinterpret_cast<const bf16x8*>(sb + rd_hi + u * kFT * kFRowB + 32 * c);
+        f32x16 ci;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const float4 t4 = *reinterpret_cast<const float4*>(sb + rd_tu + 4 * (u * kFT + 8 * g));
+            ci[4 * g] = t4.x;
+            ci[4 * g + 1] = t4.y;
+            ci[4 * g + 2] = t4.z;
+            ci[4 * g + 3] = t4.w;
+        }
+        f32x16 acc[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[0], qh[j][0], ci, 0, 0, 0);
+#pragma unroll
+            for (int c = 1; c < 4; c++)
+                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[c], qh[j][c], acc[j], 0, 0, 0);
+        }
+        float tmin[2];
+#pragma unroll
+        for (int j = 0; j < 2; j++) {
+            const f32x16 e = acc[j];
+            float ta = min3f(e[0], e[1], e[2]);
+            ta = min3f(ta, e[3], e[4]);
+            ta = min3f(ta, e[5], e[6]);
+            ta = min2f(ta, e[7]);
+            float tb = min3f(e[8], e[9], e[10]);
+            tb = min3f(tb, e[11], e[12]);
+            tb = min3f(tb, e[13], e[14]);
+            tb = min2f(tb, e[15]);
+            gm[j][0] = min2f(gm[j][0], ta);
+            gm[j][1] = min2f(gm[j][1], tb);
+            tmin[j] = min2f(ta, tb);
+        }
+        if (extract) {
+            // a lane whose 16 rows of the tile may hold a candidate stores them whole (tile,
+            // 16 bounds as bf16: two 16-B stores); knn2_rescore picks the rows under the final
+            // bound (widening each stored value by its bf16 rounding)
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                if (tmin[j] <= thr[j]) {
+                    const int sl = ncand[j]++;
+                    if (sl < kCandSlots) {
+                        ctbase[j][sl] = tile0;
+#pragma unroll
+                        for (int g = 0; g < 2; g++) {
+                            bf16x8 b;
+#pragma unroll
+                            for (int i = 0; i < 8; i++) b[i] = (__bf16)acc[j][8 * g + i];
+                            cvbase[j][2 * sl + g] = b;
+                        }
+                    }
+                }
+            }
+        }
+    };
+    // one stage: its staged rows into LDS buffer BUF, barrier, the next stage's loads, 4 tiles,
+    // then (except in the final recompute) the query's running bound and candidate threshold
+    auto stage = [&](auto bufc, int it) {
+        constexpr int BUF = decltype(bufc)::value;
+        char* sb = sm + BUF * kFStageB;
+        const int st = it == nstages ? 0 : it;
+#pragma unroll
+        for (int u = 0; u < kFST; u++) {
+            *reinterpret_cast<bf16x8*>(sb + wr_hi + u * kFT * kFRowB) = gh[u];
+            if (spart == 0)
+                *reinterpret_cast<float*>(sb + wr_tu + 4 * u * kFT) =
+                    gn[u] == kInf ? kInf : __builtin_fmaf(gn[u], kFEps, gn[u]);
+        }
+        __syncthreads();
+        if (it < nstages) gload(it + 1 == nstages ? 0 : it + 1);
+#pragma unroll
+        for (int u = 0; u < kFST; u++) tile(sb, u, t0 + (st * kFST + u) * kFT, it > 0);
+        if (it < nstages) {
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const float G = second4(gm[j][0], gm[j][1], __shfl_xor(gm[j][0], 32, 64),
+                                        __shfl_xor(gm[j][1], 32, 64));
+                thr[j] = qv[j] ? (G + cq[j]) + (fabsf(G) + cq[j]) * kFMargin : -kInf;
+            }
+        }
+    };
+    // stage sequence: 0 (bounds only), 1 .. nstages - 1, then 0 again (candidates only, against
+    // the chunk's final bound); LDS buffers alternate
+    gload(0);
+    for (int it = 0; it <= nstages; it += 2) {
+        stage(std::integral_constant<int, 0>{}, it);
+        if (it + 1 <= nstages) stage(std::integral_constant<int, 1>{}, it + 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        const float m1 = fminf(gm[j][0], gm[j][1]), m2 = fmaxf(gm[j][0], gm[j][1]);
+        const float o1 = __shfl_xor(m1, 32, 64), o2 = __shfl_xor(m2, 32, 64);
+        const float n2 = fminf(fmaxf(m1, o1), fminf(m2, o2));
+        const float n1 = fminf(m1, o1);
+        if (h == 0 && qv[j])
+            pu[((size_t)p * chunks + ch) * max_nq + qi[j]] =
+                make_float2(n1 + QB[j], n2 + QB[j]);
+        if (qv[j]) ccount[cl[j]] = ncand[j];
+    }
+}
+
+// exact squared distance in the flann::L2<float> order: per group of 4,
+// acc += d0*d0 + d1*d1 + d2*d2 + d3*d3 (no FMA)
+__device__ __forceinline__ float exact_l2(const float4* qr, const float4* __restrict__ tp) {
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 16; c++) {
+        const float4 tv = tp[c];
+        const float d0 = qr[c].x - tv.x;
+        const float d1 = qr[c].y - tv.y;
+        const float d2 = qr[c].z - tv.z;
+        const float d3 = qr[c].w - tv.w;
+        acc += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+    }
+    return acc;
+}
+
+// k=2 update with the sweep's tie rule (lowest train index first among equal distances)
+__device__ __forceinline__ void top2_consider(float acc, int j, float& b0, int& j0, float& b1) {
+    if (acc < b0 || (acc == b0 && j < j0)) {
+        b1 = b0;
+        b0 = acc;
+        j0 = j;
+    } else if (acc < b1) {
+        b1 = acc;
+    }
+}
+
+constexpr int kPassList = 24;  // rows under the final bound per (query, chunk) (more: sweep)
+
+// k=2 fold with the lowest-index tie rule (chunks / lanes / waves in any order)
+__device__ __forceinline__ void top2_fold(float& b0, int& j0, float& b1, float ob0, int oj, float ob1) {
+    if (ob0 < b0 || (ob0 == b0 && oj < j0)) {
+        b1 = fminf(b0, ob1);
+        b0 = ob0;
+        j0 = oj;
+    } else {
+        b1 = fminf(b1, ob0);
+    }
+}
+
+// one lane per (query, train chunk): U2 = the second smallest bound over all chunks, then the
+// stored rows with l* = u' + QL - teM <= U2 (u' widened by its bf16 rounding) into the lane's
+// LDS list, then their exact distances in increasing l*: once l* > b1 (the exact second
+// smallest so far) the row's e > b1 >= b0 cannot change (j0, d0, d1), nor can any later row
+// -> the chunk's exact k=2 in part[pair][chunk][query].  A (query, chunk) whose slot list
+// overflowed in knn2_filter (or with more than kPassList rows) goes to the overflow list
+// (exact sweep of that chunk, knn2_sweep_kernel).  Chunks with no candidates write an empty
+// Top2.
+__global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restrict__ dq,
+                                                           const float* __restrict__ dt,
+                                                           const int64_t* __restrict__ off_q,
+                                                           const int64_t* __restrict__ off_t,
+                                                           int max_nq, int chunk_len, int chunks,
+                                                           const uint32_t* __restrict__ tmax,
+                                                           const float2* __restrict__ pu,
+                                                           const int32_t* __restrict__ ccount,
+                                                           const int32_t* __restrict__ ctile,
+                                                           const bf16x8* __restrict__ cval,
+                                                           Top2* __restrict__ part,
+                                                           int32_t* __restrict__ ovf, int qblocks) {
+    __shared__ int32_t plist[kPassList * 256];
+    __shared__ float plb[kPassList * 256];
+    // XCD-aware block order as in knn2_filter (a pair's blocks on one XCD: its f32 train rows,
+    // gathered by the exact distances, stay in that XCD's L2)
+    const int NB = gridDim.x;
+    const int lb = (NB & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (NB >> 3) + (blockIdx.x >> 3));
+    const int c = (lb / qblocks) % chunks, p = lb / (qblocks * chunks);
+    const int q = (lb % qblocks) * 256 + threadIdx.x;
+    const int64_t qbase = off_q[p];
+    const int nq = (int)(off_q[p + 1] - qbase);
+    const int64_t tbase = off_t[p];
+    const int nt = (int)(off_t[p + 1] - tbase);
+    if (q >= nq || c * chunk_len >= nt) return;
+    const size_t l0 = (((size_t)p * max_nq + q) * chunks + c) * 2;
+    const int n0 = ccount[l0], n1 = ccount[l0 + 1];
+    Top2* out = part + ((size_t)p * chunks + c) * max_nq + q;
+    auto overflow = [&]() {
+        const int slot = atomicAdd(&ovf[0], 1);
+        ovf[1 + 3 * slot] = p;
+        ovf[2 + 3 * slot] = q;
+        ovf[3 + 3 * slot] = c;
+    };
+    if (n0 > kCandSlots || n1 > kCandSlots) {
+        overflow();
+        return;
+    }
+    float b0 = kInf, b1 = kInf;
+    int j0 = 0x7fffffff;
+    if (n0 + n1 > 0) {
+        const int nch = (nt + chunk_len - 1) / chunk_len;
+        float m1 = kInf, m2 = kInf;
+        for (int cc = 0; cc < nch; cc++) {
+            const float2 v = pu[((size_t)p * chunks + cc) * max_nq + q];
+            m2 = fminf(fmaxf(m1, v.x), fminf(m2, v.y));
+            m1 = fminf(m1, v.x);
+        }
+        const float U2 = m2;
+        float4 qr[16];
+        const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
+        float qq = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            qr[k] = qp[k];
+            qq += qr[k].x * qr[k].x + qr[k].y * qr[k].y + qr[k].z * qr[k].z + qr[k].w * qr[k].w;
+        }
+        // l* = u' + lq <= the row's l (knn2_filter header; lq's rounding is inside the slack)
+        const float teM = __uint_as_float(tmax[p]) * (2.f * kFEps) * (1.f + kFMargin) + kFTiny;
+        const float lq = (__builtin_fmaf(qq, -kFEps, qq) - kFTiny) - teM;
+        int npass = 0;
+        for (int h = 0; h < 2; h++) {
+            const int n = h ? n1 : n0;
+            for (int k = 0; k < n; k++) {
+                const size_t slot = (l0 + h) * kCandSlots + k;
+                const int tile0 = ctile[slot];
+                const bf16x8 v0 = cval[slot * 2], v1 = cval[slot * 2 + 1];
+#pragma unroll
+                for (int e = 0; e < 16; e++) {
+                    // bf16 round to nearest: |v - u'| <= 2^-9 |u'|, so v - 2^-8 |v| <= u'
+                    const float x = (float)(e < 8 ? v0[e] : v1[e - 8]);
+                    const float lo = __builtin_fmaf(-0x1p-8f, fabsf(x), x) + lq;
+                    const int row = tile0 + (e & 3) + 8 * (e >> 2) + 4 * h;
+                    if (lo <= U2 && row < nt) {
+                        if (npass < kPassList) {
+                            plist[npass * 256 + threadIdx.x] = row;
+                            plb[npass * 256 + threadIdx.x] = lo;
+                        }
+                        npass++;
+                    }
+                }
+            }
+        }
+        if (npass > kPassList) {  // (never seen on SURF-like data) exact sweep of the chunk
+            overflow();
+            return;
+        }
+        for (int k = 0; k < npass; k++) {
+            int kb = k;
+            float lbest = plb[k * 256 + threadIdx.x];
+            for (int m = k + 1; m < npass; m++) {
+                const float v = plb[m * 256 + threadIdx.x];
+                if (v < lbest) {
+                    lbest = v;
+                    kb = m;
+                }
+            }
+            if (lbest > b1) break;
+            const int row = plist[kb * 256 + threadIdx.x];
+            if (kb != k) {  // swap the chosen entry into position k
+                plist[kb * 256 + threadIdx.x] = plist[k * 256 + threadIdx.x];
+                plb[kb * 256 + threadIdx.x] = plb[k * 256 + threadIdx.x];
+            }
+            top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + row) * kDim)),
+                          row, b0, j0, b1);
+        }
+    }
+    *out = Top2{b0, j0 == 0x7fffffff ? -1 : j0, b1};
+}
+
+// exact sweep over the train rows of one chunk for the overflowed (query, chunk) entries: one
+// 256-thread block per entry (rows strided over the threads, two rows in flight per thread),
+// a fixed grid striding over the list
+
+__global__ __launch_bounds__(256) void knn2_sweep_kernel(const float* __restrict__ dq,
+                                                         const float* __restrict__ dt,
+                                                         const int64_t* __restrict__ off_q,
+                                                         const int64_t* __restrict__ off_t,
+                                                         int max_nq, int chunk_len, int chunks,
+                                                         const int32_t* __restrict__ ovf,
+                                                         Top2* __restrict__ part) {
+    __shared__ Top2 red[4];
+    const int lane = wave_lane(), wid = threadIdx.x >> 6;
+    const int nov = ovf[0];
+    for (int w = blockIdx.x; w < nov; w += gridDim.x) {
+        const int p = ovf[1 + 3 * w], q = ovf[2 + 3 * w], c = ovf[3 + 3 * w];
+        const int64_t qbase = off_q[p], tbase = off_t[p];
+        const int nt = (int)(off_t[p + 1] - tbase);
+        const int ja = c * chunk_len, jb = min(nt, ja + chunk_len);
+        float4 qr[16];
+        const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
+#pragma unroll
+        for (int k = 0; k < 16; k++) qr[k] = qp[k];
+        float b0 = kInf, b1 = kInf;
+        int j0 = 0x7fffffff;
+        for (int j = ja + (int)threadIdx.x; j < jb; j += 512) {
+            const float da = exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j) * kDim));
+            const int j2 = j + 256;
+            const float db = j2 < jb
+                                 ? exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + j2) * kDim))
+                                 : kInf;
+            top2_consider(da, j, b0, j0, b1);
+            if (j2 < jb) top2_consider(db, j2, b0, j0, b1);
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1)
+            top2_fold(b0, j0, b1, __shfl_xor(b0, o, 64), __shfl_xor(j0, o, 64), __shfl_xor(b1, o, 64));
+        if (lane == 0) red[wid] = Top2{b0, j0, b1};
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            Top2 r = red[0];
+            for (int k = 1; k < 4; k++) top2_fold(r.d0, r.j0, r.d1, red[k].d0, red[k].j0, red[k].d1);
+            part[((size_t)p * chunks + c) * max_nq + q] = Top2{r.d0, r.j0 == 0x7fffffff ? -1 : r.j0, r.d1};
+        }
+        __syncthreads();
+    }
+}
+
+// ---- LDS-tiled exact sweep on packed FP32 VALU (the non-MFMA matcher, configs[3]) ----------
+// Every (query, train) distance in the flann::L2<float> order, no filter: per group of 4 dims
+// acc += ((d0*d0 + d1*d1) + d2*d2) + d3*d3, each operation rounded (no FMA).  Two train rows
+// share every instruction (v_pk_add_f32 / v_pk_mul_f32 with the query value broadcast), so an
+// element costs 1.5 VALU instructions: sub, mul, add.
+// Block = 256 threads = 16 (tq) x 16 (tt); tile = 128 queries (resident in LDS for the whole
+// chunk) x 128 train rows per step.  Thread (tq, tt) owns queries tq + 16 k (k < 8) and the
+// train row pairs tt + 16 k (k < 4): 64 accumulators.  Train rows sit in LDS as row pairs,
+// dims interleaved ([pair][dim][2]), so one ds_read_b128 yields 2 dims x 2 rows = two packed
+// operands; query rows are [row][68] (the 16 rows a wave reads per instruction fall on 64
+// distinct banks).  The next tile is prefetched into registers during the current one.
+// Output: per (pair, chunk, query) the chunk's exact k=2 (Top2, lowest index among ties);
+// knn2_merge folds chunks in train order.
+constexpr int kXQ = 128, kXT = 128;
+constexpr int kXQRow = 68;             // floats per query row in LDS
+constexpr int kXPair = 2 * kDim + 4;   // floats per train row pair in LDS
+
+struct ExactLds {
+    float q[kXQ * kXQRow];
+    float t[kXT / 2 * kXPair];
+    Top2 red[4][kXQ];                  // cross-wave fold of the k=2 partials
+};
+
+__global__ __launch_bounds__(256) void knn2_exact_kernel(const float* __restrict__ dq,
+                                                         const float* __restrict__ dt,
+                                                         const int64_t* __restrict__ off_q,
+                                                         const int64_t* __restrict__ off_t,
+                                                         int chunk_len, int chunks, int max_nq,
+                                                         Top2* __restrict__ xpart) {
+    __shared__ ExactLds sm;
+    const int p = blockIdx.z;
+    const int64_t qbase = off_q[p], tbase = off_t[p];
+    const int nq = (int)(off_q[p + 1] - qbase);
+    const int nt = (int)(off_t[p + 1] - tbase);
+    const int q0 = blockIdx.x * kXQ;
+    const int t0 = blockIdx.y * chunk_len;
+    if (q0 >= nq || t0 >= nt) return;  // uniform over the block
+    const int t1 = min(t0 + chunk_len, nt);
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tq = lane & 15, tt = (lane >> 4) + 4 * wid;
+    // query tile: 128 rows x 16 float4, 8 float4 per thread (rows beyond nq read as 0)
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+        const int e = tid + 256 * u, row = e >> 4, c = e & 15;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (q0 + row < nq) v = reinterpret_cast<const float4*>(dq + (qbase + q0 + row) * kDim)[c];
+        *reinterpret_cast<float4*>(&sm.q[row * kXQRow + 4 * c]) = v;
+    }
+    // train staging: thread -> row pair (tid >> 2) of the tile, dims 16 (tid & 3) .. +15
+    const int spair = tid >> 2, sdim = 16 * (tid & 3);
+    float4 ga[4], gb[4];
+    auto gload = [&](int tile0) {
+        const int ra = tile0 + 2 * spair, rb = ra + 1;
+        const float4* pa = reinterpret_cast<const float4*>(dt + (tbase + min(ra, t1 - 1)) * kDim + sdim);
+        const float4* pb = reinterpret_cast<const float4*>(dt + (tbase + min(rb, t1 - 1)) * kDim + sdim);
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            ga[c] = pa[c];
+            gb[c] = pb[c];
+        }
+    };
+    float b0[8], b1[8];
+    int j0[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        b0[k] = kInf;
+        b1[k] = kInf;
+        j0[k] = 0x7fffffff;
+    }
+    const int ntiles = (t1 - t0 + kXT - 1) / kXT;
+    gload(t0);
+    for (int s = 0; s < ntiles; s++) {
+        const int tile0 = t0 + s * kXT;
+        __syncthreads();  // previous tile's reads are done
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            float* w = &sm.t[spair * kXPair + 2 * (sdim + 4 * c)];
+            *reinterpret_cast<float4*>(w) = make_float4(ga[c].x, gb[c].x, ga[c].y, gb[c].y);
+            *reinterpret_cast<float4*>(w + 4) = make_float4(ga[c].z, gb[c].z, ga[c].w, gb[c].w);
+        }
+        __syncthreads();
+        if (s + 1 < ntiles) gload(tile0 + kXT);
+        f32x2 acc[8][4];
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) acc[k][kk] = f32x2{0.f, 0.f};
+#pragma unroll 2
+        for (int g = 0; g < 16; g++) {
+            float4 tv[4][2];
+#pragma unroll
+            for (int kk = 0; kk < 4; kk++) {
+                const float* tp = &sm.t[(tt + 16 * kk) * kXPair + 8 * g];
+                tv[kk][0] = *reinterpret_cast<const float4*>(tp);
+                tv[kk][1] = *reinterpret_cast<const float4*>(tp + 4);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const float4 qv = *reinterpret_cast<const float4*>(&sm.q[(tq + 16 * k) * kXQRow + 4 * g]);
+                const f32x2 qx = {qv.x, qv.x}, qy = {qv.y, qv.y}, qz = {qv.z, qv.z},
+                            qw = {qv.w, qv.w};
+#pragma unroll
+                for (int kk = 0; kk < 4; kk++) {
+                    const f32x2 e0 = qx - f32x2{tv[kk][0].x, tv[kk][0].y};
+                    const f32x2 e1 = qy - f32x2{tv[kk][0].z, tv[kk][0].w};
+                    const f32x2 e2 = qz - f32x2{tv[kk][1].x, tv[kk][1].y};
+                    const f32x2 e3 = qw - f32x2{tv[kk][1].z, tv[kk][1].w};
+                    acc[k][kk] = acc[k][kk] + (((e0 * e0 + e1 * e1) + e2 * e2) + e3 * e3);
+                }
+            }
+        }
+        // k=2 update, branch-free: a thread sees its rows in increasing train index, so a later
+        // row never wins a tie (strict <); second = med3(b0, b1, d).  Rows >= t1 count as +inf.
+#pragma unroll
+        for (int kk = 0; kk < 4; kk++) {
+            const int ja = tile0 + 2 * (tt + 16 * kk);
+            const bool va = ja < t1, vb = ja + 1 < t1;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const float d = (h ? vb : va) ? acc[k][kk][h] : kInf;
+                    b1[k] = __builtin_amdgcn_fmed3f(b0[k], b1[k], d);
+                    j0[k] = d < b0[k] ? ja + h : j0[k];
+                    b0[k] = fminf(b0[k], d);
+                }
+            }
+        }
+    }
+    // fold the 16 threads of a query: lanes tq + 16 m of a wave (xor 16, 32), then 4 waves
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+#pragma unroll
+        for (int o = 16; o < 64; o <<= 1) {
+            const float ob0 = __shfl_xor(b0[k], o, 64), ob1 = __shfl_xor(b1[k], o, 64);
+            const int oj = __shfl_xor(j0[k], o, 64);
+            if (ob0 < b0[k] || (ob0 == b0[k] && oj < j0[k])) {
+                b1[k] = fminf(b0[k], ob1);
+                b0[k] = ob0;
+                j0[k] = oj;
+            } else {
+                b1[k] = fminf(b1[k], ob0);
+            }
+        }
+        if (lane < 16) sm.red[wid][tq + 16 * k] = Top2{b0[k], j0[k], b1[k]};
+    }
+    __syncthreads();
+    if (tid < kXQ && q0 + tid < nq) {
+        Top2 r = sm.red[0][tid];
+#pragma unroll
+        for (int w = 1; w < 4; w++) {
+            const Top2 o = sm.red[w][tid];
+            if (o.d0 < r.d0 || (o.d0 == r.d0 && o.j0 < r.j0)) {
+                r.d1 = fminf(r.d0, o.d1);
+                r.d0 = o.d0;
+                r.j0 = o.j0;
+            } else {
+                r.d1 = fminf(r.d1, o.d0);
+            }
+        }
+        if (r.j0 == 0x7fffffff) r.j0 = -1;
+        xpart[((size_t)p * chunks + blockIdx.y) * max_nq + q0 + tid] = r;
+    }
+}
+
+// Fold of per-chunk partials part[pair][chunk][query] into one exact k=2 per query
+// (out[pair][query]), chunks in train order (an earlier chunk wins ties): one lane per query,
+// so a single large pair uses the whole chip (the merge below is one block per pair).
+__device__ __forceinline__ void merge_query(const Top2* part, size_t stride, int nch, int q,
+                                            float& B0, int& J, float& B1);
+
+__global__ __launch_bounds__(256) void knn2_fold_kernel(const Top2* __restrict__ part,
+                                                        const int64_t* __restrict__ off_q,
+                                                        const int64_t* __restrict__ off_t,
+                                                        int chunk_len, int chunks, int max_nq,
+                                                        Top2* __restrict__ out) {
+    const int p = blockIdx.y;
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    const int nq = (int)(off_q[p + 1] - off_q[p]);
+    const int nt = (int)(off_t[p + 1] - off_t[p]);
+    if (q >= nq) return;
+    float B0, B1;
+    int J;
+    merge_query(part + (size_t)p * chunks * max_nq, (size_t)max_nq,
+                max(1, (nt + chunk_len - 1) / chunk_len), q, B0, J, B1);
+    out[(size_t)p * max_nq + q] = Top2{B0, J, B1};
+}
+
+// Fold chunk partials in train order (lowest index wins ties), apply the ratio test
+// d0 < ratio * d1 on the sqrt'd distances (convertToDMatches + feature_matcher.cpp:52), and
+// compact the survivors in ascending queryIdx order.  One block (1024 threads) per pair.
+__device__ __forceinline__ void merge_query(const Top2* part, size_t stride, int nch, int q,
+                                            float& B0, int& J, float& B1) {
+    B0 = kInf;
+    B1 = kInf;
+    J = -1;
+    for (int c = 0; c < nch; c++) {
+        const Top2 t = part[(size_t)c * stride + q];
+        if (t.d0 < B0) {
+            B1 = fminf(B0, t.d1);
+            B0 = t.d0;
+            J = t.j0;
+        } else {
+            B1 = fminf(B1, t.d0);
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void knn2_merge_kernel(const Top2* __restrict__ part,
+                                                          const int64_t* __restrict__ off_q,
+                                                          const int64_t* __restrict__ off_t,
+                                                          int chunk_len, int chunks, int max_nq,
+                                                          float ratio, erp_dmatch* __restrict__ out,
+                                                          int32_t* __restrict__ counts,
+                                                          int32_t* __restrict__ flags) {
+    __shared__ int ws[16];
+    const int p = blockIdx.x;
+    const int nq = (int)(off_q[p + 1] - off_q[p]);
+    const int nt = (int)(off_t[p + 1] - off_t[p]);
+    if (nt < 2 || nq <= 0) {
+        if (threadIdx.x == 0) {
+            counts[p] = 0;
+            if (nq > 0) flags[p] |= 1;  // knn_matches[i][1] would not exist (UB in the reference)
+        }
+        return;
+    }
+    const int nch = (nt + chunk_len - 1) / chunk_len;
+    const Top2* pp = part + (size_t)p * chunks * max_nq;
+    const int per = (nq + 1023) / 1024;
+    const int qa = min(nq, (int)threadIdx.x * per), qb = min(nq, qa + per);
+    int cnt = 0;
+    for (int q = qa; q < qb; q++) {
+        float B0, B1;
+        int J;
+        merge_query(pp, (size_t)max_nq, nch, q, B0, J, B1);
+        const float d0 = __builtin_sqrtf(B0), d1 = __builtin_sqrtf(B1);
+        cnt += (d0 < ratio * d1) ? 1 : 0;
+    }
+    int total;
+    int pos = block_exclusive_scan<1024>(cnt, ws, &total);
+    erp_dmatch* o = out + (size_t)p * max_nq;
+    for (int q = qa; q < qb; q++) {
+        float B0, B1;
+        int J;
+        merge_query(pp, (size_t)max_nq, nch, q, B0, J, B1);
+        const float d0 = __builtin_sqrtf(B0), d1 = __builtin_sqrtf(B1);
+        if (d0 < ratio * d1) o[pos++] = erp_dmatch{q, J, 0, d0};
+    }
+    if (threadIdx.x == 0) counts[p] = total;
+}
+
+
+__global__ void set_i32_kernel(int32_t* p, int32_t v) { *p = v; }
+
+}  // namespace
+
+// ====================================================================== launchers =======
+size_t knn2_cand_bytes(const BatchShape& sh) {
+    return (size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 * kCandSlots * (2 * sizeof(bf16x8) + 4);
+}
+
+size_t knn2_split_bytes(const BatchShape& sh) {
+    return (size_t)sh.n_pairs * sh.max_nt * (kDim * sizeof(__bf16) + sizeof(float)) +
+           (size_t)sh.n_pairs * sizeof(uint32_t);
+}
+
+static void cand_split(const BatchShape& sh, void* cand, int32_t** ctile, bf16x8** cval) {
+    const size_t lists = (size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 * kCandSlots;
+    *cval = (bf16x8*)cand;
+    *ctile = (int32_t*)(*cval + lists * 2);
+}
+
+static uint32_t* split_tmax(const BatchShape& sh, void* split) {
+    return (uint32_t*)((char*)split + (size_t)sh.n_pairs * sh.max_nt * (kDim * sizeof(__bf16) + sizeof(float)));
+}
+
+hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                              const int64_t* off_t, const BatchShape& sh, void* split,
+                              float2* pu, int32_t* ccount, void* cand, hipStream_t st) {
+    bf16x8* thi = (bf16x8*)split;
+    float* tn = (float*)(thi + (size_t)sh.n_pairs * sh.max_nt * 8);
+    uint32_t* tmax = split_tmax(sh, split);
+    hipError_t e = hipMemsetAsync(tmax, 0, (size_t)sh.n_pairs * sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(knn2_split_kernel, dim3((sh.max_nt + 63) / 64, sh.n_pairs), dim3(256), 0,
+                       st, desc_t, off_t, sh.max_nt, thi, tn, tmax);
+    int32_t* ctile;
+    bf16x8* cval;
+    cand_split(sh, cand, &ctile, &cval);
+    const int qblocks = (sh.max_nq + kFQ - 1) / kFQ;
+    hipLaunchKernelGGL(knn2_filter_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
+                       st, desc_q, thi, tn, tmax, off_q, off_t, sh.fchunk_len, sh.fchunks,
+                       sh.max_nq, sh.max_nt, qblocks, pu, ccount, ctile, cval);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                               const int64_t* off_t, const BatchShape& sh, void* split,
+                               const float2* pu, const int32_t* ccount, void* cand, Top2* part,
+                               int32_t* ovf, hipStream_t st) {
+    int32_t* ctile;
+    bf16x8* cval;
+    cand_split(sh, cand, &ctile, &cval);
+    hipLaunchKernelGGL(set_i32_kernel, dim3(1), dim3(1), 0, st, ovf, 0);
+    const int qblocks = (sh.max_nq + 255) / 256;
+    hipLaunchKernelGGL(knn2_rescore_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
+                       st, desc_q, desc_t, off_q, off_t, sh.max_nq, sh.fchunk_len, sh.fchunks,
+                       split_tmax(sh, split), pu, ccount, ctile, cval, part, ovf, qblocks);
+    hipLaunchKernelGGL(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
+                       sh.max_nq, sh.fchunk_len, sh.fchunks, ovf, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn2_exact(const float* desc_q, const float* desc_t, const int64_t* off_q,
+                             const int64_t* off_t, const BatchShape& sh, Top2* xpart,
+                             hipStream_t st) {
+    dim3 grid((sh.max_nq + kXQ - 1) / kXQ, sh.xchunks, sh.n_pairs);
+    hipLaunchKernelGGL(knn2_exact_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
+                       sh.xchunk_len, sh.xchunks, sh.max_nq, xpart);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn2_fold(const Top2* part, const int64_t* off_q, const int64_t* off_t,
+                            const BatchShape& sh, int chunk_len, int chunks, Top2* out,
+                            hipStream_t st) {
+    hipLaunchKernelGGL(knn2_fold_kernel, dim3((sh.max_nq + 255) / 256, sh.n_pairs), dim3(256), 0,
+                       st, part, off_q, off_t, chunk_len, chunks, sh.max_nq, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
+                             const BatchShape& sh, int chunk_len, int chunks, float ratio,
+                             erp_dmatch* matches, int32_t* counts, int32_t* flags,
+                             hipStream_t st) {
+    hipLaunchKernelGGL(knn2_merge_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, part, off_q, off_t,
+                       chunk_len, chunks, sh.max_nq, ratio, matches, counts, flags);
+    return hipGetLastError();
+}
+
+}  // namespace erp

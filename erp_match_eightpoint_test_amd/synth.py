@@ -59,8 +59,12 @@ def _quantise(rng: np.random.Generator, px: np.ndarray, integer_frac: float) -> 
 
 def make_pair(seed: int, n_kpts: int = 4096, n_train: int | None = None, W: int = W_REF,
               H: int = H_REF, inlier_frac: float = 0.8, sigma: float = 0.03,
-              euler_max_deg: float = 15.0, integer_frac: float = 0.75, dim: int = 64) -> dict:
-    """One synthetic ERP pair: descriptors + keypoints for left (queries) and right (train)."""
+              euler_max_deg: float = 15.0, integer_frac: float = 0.75, dim: int = 64,
+              mismatch_frac: float = 0.0) -> dict:
+    """One synthetic ERP pair: descriptors + keypoints for left (queries) and right (train).
+    mismatch_frac: that fraction of the true partners keep their descriptor but get a random
+    right keypoint (wrong matches that pass the ratio test: geometric outliers for the
+    consensus); drawn from a second generator, so the other outputs do not change."""
     rng = np.random.default_rng(seed)
     N = n_kpts
     T = n_kpts if n_train is None else n_train
@@ -91,6 +95,11 @@ def make_pair(seed: int, n_kpts: int = 4096, n_train: int | None = None, W: int 
         desc_r[perm[n_in:]] = random_descriptors(rng, n_out, dim)
         ro = rng.standard_normal((n_out, 3))
         kp_r[perm[n_in:]] = _quantise(rng, bearing_to_pixel(ro, W, H), integer_frac)
+    if mismatch_frac > 0 and n_in:
+        rng2 = np.random.default_rng(seed + 1_000_003)
+        bad = rng2.random(n_in) < mismatch_frac
+        rb = rng2.standard_normal((int(bad.sum()), 3))
+        kp_r[perm[:n_in][bad]] = _quantise(rng2, bearing_to_pixel(rb, W, H), integer_frac)
     gt_partner = np.full(N, -1, np.int64)
     gt_partner[:n_in] = perm[:n_in]
     return {"desc_l": desc_l, "desc_r": desc_r, "kp_l": kp_l, "kp_r": kp_r, "W": W, "H": H,

@@ -165,7 +165,7 @@ erp_status erp_ctx_reserve(erp_ctx* ctx, int32_t n_pairs, int32_t max_nq, int32_
 /* ---- stage timing (the reference's START_TIME/STOP_TIME, src/debug_print.h:9-13, applied to
    the hot path): HIP events recorded around every kernel on the pipeline's stream. ---- */
 typedef enum erp_stage {
-    ERP_STAGE_KNN2_FILTER = 0,  /* MFMA pass 1: per-query upper bounds of the 2nd neighbour */
+    ERP_STAGE_KNN2_FILTER = 0,  /* bf16 split + the one MFMA pass: bounds + provisional candidates */
     ERP_STAGE_KNN2_MERGE = 1,   /* chunk fold + ratio test + compaction */
     ERP_STAGE_BEARINGS = 2,     /* gather + pixel -> bearing */
     ERP_STAGE_JUMP_PREP = 3,    /* glibc jump-ahead polynomials */
@@ -178,7 +178,7 @@ typedef enum erp_stage {
     ERP_STAGE_CONSENSUS_SELECT = 10,
     ERP_STAGE_WINDOWS = 11,         /* per-iteration glibc end windows (jump-ahead) */
     ERP_STAGE_GRAM = 12,            /* A^T A of every sample (fp64) */
-    ERP_STAGE_KNN2_CANDIDATES = 13, /* MFMA pass 2: candidate train rows per query */
+    ERP_STAGE_KNN2_CANDIDATES = 13, /* unused since r02 (the two MFMA passes were fused) */
     ERP_STAGE_KNN2_RESCORE = 14,    /* exact flann::L2 distances of the candidates */
     ERP_STAGE_CONSENSUS_REFINE = 15, /* tighter bounds for the survivors (sub-bins) */
     ERP_STAGE_KNN2_EXACT = 16,      /* exact sweep on packed FP32 VALU (ERP_MATCHER_VALU_EXACT) */

@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Real-image fixtures from the reference's own data files (run in the build container, where
+/root/reference exists; the GPU box only reads the committed outputs).
+
+  python tests/golden/gen_real.py
+
+* tests/golden/real/left_building.jpg, right_building.jpg: the reference's input pair
+  (/root/reference/build/*.jpg, 5376 x 2688, copied byte for byte: data files, not source).
+* tests/golden/real/ref_rectified_{left,right}.jpg: the reference's own OUTPUT of the automatic
+  pipeline (src/automatic.cpp:117-157, rectify) on that pair at 2048 x 1024
+  (/root/reference/build/output_20200423/rectified_*.png), re-encoded as JPEG quality 95 to keep
+  the repository small (the test compares geometry -- a residual rotation from matched SURF
+  features -- not pixel values).  The pairing output_20200423 <-> *_building.jpg was checked:
+  the rectified left image differs from left_building.jpg resized to 2048 x 1024 by 14.0 grey
+  levels on average, from left_building2.jpg by 42.8 (output_20200423_2 <-> building2: 10.2 /
+  40.7; right_building2.jpg is not in the reference, so only the first pair is usable).
+* tests/golden/real/MANIFEST.json: sha256 of every source and output file.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import shutil
+
+from PIL import Image
+
+REF = "/root/reference/build"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "real")
+
+
+def sha(path: str) -> str:
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    man = {"sources": {}, "outputs": {}}
+    for name in ("left_building.jpg", "right_building.jpg"):
+        src = os.path.join(REF, name)
+        shutil.copyfile(src, os.path.join(OUT, name))
+        man["sources"][name] = sha(src)
+    for side in ("left", "right"):
+        src = os.path.join(REF, "output_20200423", f"rectified_{side}.png")
+        dst = os.path.join(OUT, f"ref_rectified_{side}.jpg")
+        Image.open(src).convert("RGB").save(dst, quality=95, subsampling=0)
+        man["sources"][f"output_20200423/rectified_{side}.png"] = sha(src)
+    for name in sorted(os.listdir(OUT)):
+        if name.endswith(".jpg"):
+            man["outputs"][name] = sha(os.path.join(OUT, name))
+    with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
+        json.dump(man, f, indent=1)
+    print(json.dumps(man, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,135 @@
+"""The reference's own data end to end.
+
+Inputs: /root/reference/build/{left,right}_building.jpg (5376 x 2688), committed under
+tests/golden/real/ by tests/golden/gen_real.py together with the reference's OUTPUT of its
+automatic pipeline on that pair at 2048 x 1024 (output_20200423/rectified_{left,right}.png:
+do_all -> eight_point::find -> rectify, src/automatic.cpp:117-145).
+
+1. test_real_building_matches_reference_output: our GPU pipeline (spherical_surf.do_all,
+   eight_point.find with the reference defaults, erp_rotation.rectify) on the same pair at
+   2048 x 1024.  Both rectified images are the input sphere rotated by a matrix built from the
+   estimated (R, T); ours and the reference's may differ only by the estimate.  The residual is
+   measured geometrically: SURF matches between our rectified image and the reference's
+   (do_all on the two), their bearings, and the rotation that best maps ours onto the
+   reference's (Kabsch, trimmed).  The left images differ by a rotation that depends on the
+   estimated T alone; the right ones add the estimated R, so inv(Q_left) Q_right isolates the
+   disagreement in R (up to the ~1 % non-orthogonality of rot_from_vec's (1/1+c) quirk, which
+   shows as the 0.19 degree median fit error).  The bar: R within 1.5 degrees of the
+   reference's (measured 0.90; the T residual, ~9 degrees, is reported, not asserted: T of this
+   pair is poorly conditioned -- short baseline, M ~ 260 matches, 80 iterations).  OpenCV's
+   SURF / FLANN / SVD are absent here and the reference's estimate is one glibc-seeded
+   80-iteration RANSAC over ITS matches, so this is a tolerance KAT, not bit parity.
+2. test_real_building_fullres_keypoints: do_all + find at the full 5376 x 2688 -- keypoint
+   counts per band against the 65 535 cap of the C ABI (erp_eight_point_find: m <= 65535).
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REAL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "real")
+
+
+def _bgr(path, size=None):
+    from PIL import Image
+    im = Image.open(path).convert("RGB")
+    if size is not None and im.size != size:
+        im = im.resize(size, Image.BILINEAR)
+    return np.ascontiguousarray(np.asarray(im)[..., ::-1])  # RGB -> BGR (cv::imread order)
+
+
+def _dev(a):
+    import torch
+    return torch.from_numpy(a).cuda().contiguous()
+
+
+def _residual(ss, W, H, im_a, im_b):
+    """rotation Q that best maps the sphere of image a onto image b (b ~ Q a on the bearings of
+    do_all's SURF matches; Kabsch with two trimming rounds keeping the best 50 %) ->
+    (Q, matches, median fit error in degrees)."""
+    import oracle as O
+    kl, kr, M, _ = ss.do_all(im_a, im_b)
+    a = O.pixel_to_bearing(W, H, kl.cpu().numpy())
+    b = O.pixel_to_bearing(W, H, kr.cpu().numpy())
+    keep = np.ones(len(a), bool)
+    for _ in range(3):
+        Hm = b[keep].T @ a[keep]
+        U, _, Vt = np.linalg.svd(Hm)
+        D = np.diag([1.0, 1.0, np.sign(np.linalg.det(U @ Vt))])
+        Q = U @ D @ Vt
+        err = np.linalg.norm(b - a @ Q.T, axis=1)
+        keep = err <= np.quantile(err, 0.5)
+    return Q, int(M), float(np.degrees(np.median(err)))
+
+
+def _angle(Q) -> float:
+    return float(np.degrees(np.arccos(np.clip((np.trace(Q) - 1) / 2, -1, 1))))
+
+
+@pytest.fixture(scope="module")
+def api(gpu_lib):
+    from erp_match_eightpoint_test_amd import Context, eight_point, erp_rotation, spherical_surf
+    ctx = Context(0)
+    return spherical_surf(ctx=ctx), eight_point(ctx=ctx), erp_rotation(ctx=ctx)
+
+
+def test_real_fixture_manifest():
+    import hashlib
+    man = json.load(open(os.path.join(REAL, "MANIFEST.json")))
+    for name, h in man["outputs"].items():
+        with open(os.path.join(REAL, name), "rb") as f:
+            assert hashlib.sha256(f.read()).hexdigest() == h, name
+
+
+def test_real_building_matches_reference_output(api):
+    ss, ep, er = api
+    W, H = 2048, 1024
+    left = _dev(_bgr(os.path.join(REAL, "left_building.jpg"), (W, H)))
+    right = _dev(_bgr(os.path.join(REAL, "right_building.jpg"), (W, H)))
+    kl, kr, M, total = ss.do_all(left, right)
+    R, T = ep.find(W, H, kl.cpu().numpy(), kr.cpu().numpy())
+    assert ep.last_result["status"] == 0
+    lo, ro = er.rectify(left, right, R.astype(np.float64), T.astype(np.float64))
+    ref_l = _dev(_bgr(os.path.join(REAL, "ref_rectified_left.jpg")))
+    ref_r = _dev(_bgr(os.path.join(REAL, "ref_rectified_right.jpg")))
+    Ql, ml, el = _residual(ss, W, H, lo, ref_l)
+    Qr, mr, erm = _residual(ss, W, H, ro, ref_r)
+    # left: both rectifications rotate the left sphere by a matrix of T alone (rot_from_vec), so
+    # angle(Ql) is the T disagreement; right: they add the estimated relative rotation E, and
+    # inv(Ql) Qr is conjugate to E_ref inv(E_ours): its angle is the R disagreement, whatever T
+    rel = _angle(Ql.T @ Qr)
+    base_l = _angle(_residual(ss, W, H, left, ref_l)[0])  # the rectification itself
+    print(f"\nreal pair 2048x1024: {total} left keypoints, M={M}, K={int(ep.last_result['K'])}, "
+          f"R={np.degrees(R)} deg, T={T}\n  vs the reference's output: relative rotation "
+          f"{rel:.3f} deg; T-dependent residual left {_angle(Ql):.2f} deg / right {_angle(Qr):.2f}"
+          f" deg ({ml} / {mr} matches, median fit error {el:.3f} / {erm:.3f} deg); the reference's"
+          f" left rectification itself {base_l:.2f} deg")
+    assert ml > 100 and mr > 100 and el < 0.5 and erm < 0.5  # the residuals are rotations
+    # measured: 0.90 deg (two 80-iteration estimates over different match sets: OpenCV's SURF +
+    # FLANN there, the restatement + exact k=2 here); the rectifying rotation itself is ~4.8 deg
+    assert rel < 1.5, rel
+
+
+def test_real_building_fullres_keypoints(api):
+    import torch
+    from erp_match_eightpoint_test_amd import feature_matcher
+    ss, ep, er = api
+    left = _dev(_bgr(os.path.join(REAL, "left_building.jpg")))
+    right = _dev(_bgr(os.path.join(REAL, "right_building.jpg")))
+    H, W = left.shape[:2]
+    assert (W, H) == (5376, 2688)
+    bands = ss.bands(torch.stack([left, right]).contiguous())
+    fm = feature_matcher(ctx=ss.ctx)
+    _, _, counts = fm.surf_dev(bands.reshape(8, H // 4, W, 3))
+    kl, kr, M, total = ss.do_all(left, right)
+    R, T = ep.find(W, H, kl.cpu().numpy(), kr.cpu().numpy())
+    print(f"\nreal pair 5376x2688: band keypoints {counts.tolist()}, left total {total}, M={M}, "
+          f"R={np.degrees(R)} deg, T={T}")
+    assert ep.last_result["status"] == 0
+    assert total == int(counts[:4].sum())
+    assert max(int(counts[:4].sum()), int(counts[4:].sum())) < 65535  # the C ABI's m / nq cap
