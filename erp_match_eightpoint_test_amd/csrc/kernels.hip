@@ -694,13 +694,20 @@ __global__ __launch_bounds__(256, 3) void gram_mfma_kernel(const int32_t* __rest
                                                            const uint32_t* __restrict__ selw,
                                                            int iters, int nwaves, int nbw,
                                                            double sample_frac,
-                                                           double* __restrict__ gram) {
+                                                           double* __restrict__ gram, int nhb) {
     __shared__ __align__(16) int8_t lds[kGramRing * kGramSlotBytes];
-    const int p = blockIdx.y, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // XCD-aware block order (1-D grid of nhb iteration blocks x pairs): workgroups go to the 8
+    // XCDs round-robin by linear id, so XCD x takes the contiguous logical range
+    // [x NB/8, (x+1) NB/8) -- all iteration blocks of a pair on one XCD, whose L2 then holds the
+    // pair's limb images (7 KB per selection word) for every block instead of each XCD
+    // fetching them from HBM (identity when NB is not a multiple of 8)
+    const int NB = gridDim.x;
+    const int lbk = (NB & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (NB >> 3) + (blockIdx.x >> 3));
+    const int p = lbk / nhb, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;
-    const int hb = blockIdx.x * 128;
+    const int hb = (lbk % nhb) * 128;
     if (hb >= iters) return;  // uniform over the block
     const int nb = (M - 1) / 31 + 1;
     const int nsteps = (nb + kGramWords - 1) / kGramWords;  // words read: <= 2 nsteps - 1 <= nb < nbw
@@ -2407,8 +2414,9 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
     const int nwaves = (sh.iters + 63) / 64;
     hipLaunchKernelGGL(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
                        pts, sh.max_nq, sh.sel_words, limbs);
-    hipLaunchKernelGGL(gram_mfma_kernel, dim3((sh.iters + 127) / 128, sh.n_pairs), dim3(256), 0, st,
-                       counts, limbs, selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram);
+    const int nhb = (sh.iters + 127) / 128;
+    hipLaunchKernelGGL(gram_mfma_kernel, dim3(nhb * sh.n_pairs), dim3(256), 0, st, counts, limbs,
+                       selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb);
     if (samples)
         hipLaunchKernelGGL(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
                            sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);

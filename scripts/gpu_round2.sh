@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 TAG=${TAG:-r02c}
 PROF="python3 bench.py --no-cpu-baseline --steps 0 --warmup 2 ${BENCH_ARGS}"
 if [ -z "$SKIP_TESTS" ]; then
-echo "== gpu tests" && timeout -k 10 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_K} > gpurun_out/pytest_gpu_${TAG}.log 2>&1 || { tail -60 gpurun_out/pytest_gpu_${TAG}.log; exit 1; }
+echo "== gpu tests" && timeout -k 10 900 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu_${TAG}.log 2>&1 || { tail -60 gpurun_out/pytest_gpu_${TAG}.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu_${TAG}.log
 fi
 echo "== bench" && timeout -k 10 600 python bench.py --profile-tag ${TAG} ${BENCH_ARGS} ${BENCH_CPU} > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { tail -30 gpurun_out/bench_${TAG}.err; exit 1; }
