@@ -27,9 +27,9 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# pipeline stage -> kernel symbol (short name; knn2_filter_kernel<1>/<2> are the two MFMA passes)
+# pipeline stage -> kernel symbol (short name; since r02 the matcher has one MFMA pass)
 STAGE_KERNEL = {
-    "knn2_filter": "knn2_filter_kernel<1>", "knn2_candidates": "knn2_filter_kernel<2>",
+    "knn2_filter": "knn2_filter_kernel",
     "knn2_rescore": "knn2_rescore_kernel", "knn2_merge": "knn2_merge_kernel",
     "bearings": "bearings_from_matches_kernel", "jump_prep": "jump_prep_kernel",
     "windows": "sampler_window_kernel", "sampler": "sampler_kernel", "gram": "gram_mfma_kernel",
@@ -78,6 +78,9 @@ def main():
     ap.add_argument("--stats")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--sq", help="dir of an SQ counter pass -> profiles/<tag>_sq.txt")
+    ap.add_argument("--draws", type=float, default=0.0,
+                    help="rand() draws per sampler launch (per-draw VALU / LDS in the SQ table)")
     a = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -109,6 +112,34 @@ def main():
                               indent=1)
         for k, v in sorted(table.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):
             print(f"{k:40s} {v['hbm_bytes_per_launch'] / 1e6:10.3f} MB/launch")
+    if a.sq:
+        path = find_csv(a.sq, "counter_collection.csv")
+        acc = defaultdict(lambda: defaultdict(float))
+        disp = defaultdict(set)
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                k = short(row["Kernel_Name"])
+                acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
+                disp[k].add(row["Dispatch_Id"])
+        lines = ["# SQ counters per kernel: mean per dispatch (rocprofv3 --pmc, one pass, kernel trace",
+                 "# only; SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* in quad-cycles, SQ_INSTS_* in",
+                 "# wave-instructions, summed over the chip)"]
+        for k, v in sorted(acc.items(), key=lambda kv: -kv[1].get("SQ_WAVE_CYCLES", 0)):
+            if k.startswith("__amd"):
+                continue
+            n = len(disp[k])
+            lines.append(f"{k:36s} dispatches={n:3d} " +
+                         " ".join(f"{c}={x / n:.4g}" for c, x in sorted(v.items())))
+        smp = acc.get("sampler_kernel")
+        if smp and a.draws > 0:
+            n = len(disp["sampler_kernel"])
+            wd = a.draws / 64.0  # wave-level draws per launch
+            lines.append(f"# sampler: {a.draws:.4g} draws per launch -> "
+                         f"{smp['SQ_INSTS_VALU'] / n / wd:.2f} VALU and "
+                         f"{smp['SQ_INSTS_LDS'] / n / wd:.2f} LDS wave-instructions per draw")
+        with open(os.path.join(prof, f"{a.tag}_sq.txt"), "w") as f:
+            f.write("\n".join(lines) + "\n")
+        print("\n".join(lines[-3:]))
 
 
 if __name__ == "__main__":
