@@ -94,19 +94,24 @@ __device__ int block_exclusive_scan(int v, int* ws, int* total) {
 // 8 ds_read_b128 and ~24 VALU (the two group-minimum trees and the candidate test).
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef const __attribute__((address_space(1))) void* glb_vptr;
 constexpr int kFW = 64;             // queries per wave
 constexpr int kFQ = 4 * kFW;        // queries per block
 constexpr int kFT = 32;             // train rows per tile
-constexpr int kFRow = 72;           // bf16 per LDS row: 64 + 8 pad (conflict-free b128 reads)
 constexpr int kFST = 4;             // 32-row tiles per LDS stage (one barrier per stage)
 constexpr float kFEps = 0x1.08p-7f;
 constexpr float kFTiny = 0x1p-100f; // absolute floor (flushed denormals)
 constexpr float kFMargin = 0x1p-20f;
 
-// LDS stage (one of two): 128 train rows x 144 B (64 bf16 + 16 B pad: the b128 fragment reads
-// of a wave fall on distinct banks), then their tu = |t|^2 (1 + eps) (+inf past the chunk)
-constexpr int kFRowB = kFRow * 2;                 // 144
-constexpr int kFHiB = kFST * kFT * kFRowB;        // 18432
+// LDS stage (one of two): 128 train rows x 128 B (64 bf16), filled by LDS-DMA
+// (global_load_lds: lane l of a 1-KB wave piece lands at piece + 16 l, so a piece holds 8 rows
+// unpadded).  The 16-B pieces of row r are XOR-swizzled, position c' = c ^ ((r >> 1) & 7), on
+// the global (source) side: the b128 A-fragment reads of a wave (16 rows of one lane group,
+// one piece each) then fall on 16 distinct 4-dword bank slots (rows of either parity take all 8
+// positions).  Then the stage's tu = |t|^2 (1 + eps) (+inf past the chunk).
+constexpr int kFRowB = 128;
+constexpr int kFHiB = kFST * kFT * kFRowB;        // 16384
 constexpr int kFStageB = kFHiB + kFST * kFT * 4;  // + 512
 
 __device__ __forceinline__ bf16x8 round8(const float4 a, const float4 b, float s) {
@@ -123,8 +128,8 @@ __device__ __forceinline__ float sq8(const float4 a, const float4 b) {
 }
 
 // train rows -> thi [pair][max_nt][64] = bf16(-2 t) (round to nearest; exact scaling of
-// bf16(t)), tn [pair][max_nt] = |t|^2, tmax[pair] = max |t|^2 (float bits; zeroed before);
-// four threads per row (16 dims each)
+// bf16(t)), tu [pair][max_nt] = |t|^2 (1 + eps) (the filter's C operand), tmax[pair] =
+// max |t|^2 (float bits; zeroed before); four threads per row (16 dims each)
 __global__ __launch_bounds__(256) void knn2_split_kernel(const float* __restrict__ dt,
                                                          const int64_t* __restrict__ off_t,
                                                          int max_nt, bf16x8* __restrict__ thi,
@@ -146,7 +151,7 @@ __global__ __launch_bounds__(256) void knn2_split_kernel(const float* __restrict
     }
     ss += __shfl_xor(ss, 1, 64);
     ss += __shfl_xor(ss, 2, 64);
-    if (part == 0 && j < nt) tn[(size_t)p * max_nt + j] = ss;
+    if (part == 0 && j < nt) tn[(size_t)p * max_nt + j] = __builtin_fmaf(ss, kFEps, ss);
     __shared__ float wmax[4];
     float m = (j < nt) ? ss : 0.f;
 #pragma unroll
@@ -182,7 +187,9 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
                                                           float2* __restrict__ pu,
                                                           int32_t* __restrict__ ccount,
                                                           int32_t* __restrict__ ctile,
-                                                          bf16x8* __restrict__ cval) {
+                                                          bf16x8* __restrict__ cval,
+                                                          const bf16x8* __restrict__ sent_hi,
+                                                          const float* __restrict__ sent_tu) {
     __shared__ __align__(16) char sm[2 * kFStageB];
     // XCD-aware block order: workgroups are dealt to the 8 XCDs round-robin by linear id, so
     // XCD x gets the contiguous logical range [x NB/8, (x+1) NB/8) (query blocks fastest, then
@@ -229,52 +236,49 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     float gm[2][2] = {{kInf, kInf}, {kInf, kInf}};
     float thr[2] = {-kInf, -kInf};
     int ncand[2] = {0, 0};
-    size_t cl[2];
+    uint32_t cl[2];  // (pair, query, chunk, lane half) list index (< 2^31: the launcher checks)
 #pragma unroll
     for (int j = 0; j < 2; j++)
-        cl[j] = (((size_t)p * max_nq + qi[j]) * chunks + ch) * 2 + h;
-    // staging: thread -> train rows (tid >> 3) + 32 u of the stage (u < kFST), 16 bytes
-    // (tid & 7) of each; the next stage is loaded into registers while this one is computed
-    const int srow = tid >> 3, spart = tid & 7;
+        cl[j] = (((uint32_t)p * (uint32_t)max_nq + (uint32_t)qi[j]) * (uint32_t)chunks + ch) * 2u + h;
+    // staging by LDS-DMA: wave w moves the stage's 1-KB pieces 4 w .. 4 w + 3 (8 rows each;
+    // lane -> row 8 k + (lane >> 3), swizzled source piece) and, waves 0 and 1, 64 tu each;
+    // rows past the chunk read the sentinel row (bf16 zeros, tu = +inf)
+    const int wv = tid >> 6;
     const bf16x8* thp = thi + (size_t)p * max_nt * 8;
-    const float* tnp = tn + (size_t)p * max_nt;
-    const bf16x8 z8 = {};
-    bf16x8 gh[kFST];
-    float gn[kFST];
-    auto gload = [&](int st) {
+    const float* tup = tn + (size_t)p * max_nt;
+    const int drow = lane >> 3;
+    auto dma = [&](char* sb, int st) {
+        const int rb = t0 + st * kFST * kFT;
 #pragma unroll
-        for (int u = 0; u < kFST; u++) {
-            const int j = t0 + (st * kFST + u) * kFT + srow;
-            if (j < t1) {
-                gh[u] = thp[(size_t)j * 8 + spart];
-                gn[u] = spart == 0 ? tnp[j] : kInf;
-            } else {
-                gh[u] = z8;
-                gn[u] = kInf;
-            }
+        for (int k = 0; k < 4; k++) {
+            const int m = 4 * wv + k;  // piece: rows 8 m .. 8 m + 7 of the stage
+            const int row = 8 * m + drow;
+            const int dpc = (lane & 7) ^ ((row >> 1) & 7);  // source piece of LDS position lane & 7
+            const bf16x8* src = rb + row < t1 ? thp + (size_t)(rb + row) * 8 + dpc : sent_hi + dpc;
+            __builtin_amdgcn_global_load_lds((glb_vptr)src,
+                                             (lds_vptr)(sb + (4 * wv + k) * 1024), 16, 0, 0);
+        }
+        if (wv < 2) {
+            const int row = 64 * wv + lane;
+            const float* src = rb + row < t1 ? tup + rb + row : sent_tu;
+            __builtin_amdgcn_global_load_lds((glb_vptr)src, (lds_vptr)(sb + kFHiB + 256 * wv), 4,
+                                             0, 0);
         }
     };
     const int nstages = (t1 - t0 + kFST * kFT - 1) / (kFST * kFT);  // rows past t1: +inf
-    // per-lane slot bases: slot s of list j at cvbase[j] + 2 s (values), ctbase[j] + s (tile)
-    bf16x8* cvbase[2];
-    int32_t* ctbase[2];
+    // LDS byte addresses: A fragment (row r, piece 2 c + h = dims 16 c + 8 h, swizzled) and the
+    // C operand rows 8 g + 4 h
+    int rd_hi[4];
 #pragma unroll
-    for (int j = 0; j < 2; j++) {
-        cvbase[j] = cval + cl[j] * kCandSlots * 2;
-        ctbase[j] = ctile + cl[j] * kCandSlots;
-    }
-    // LDS byte addresses: A fragment (row r, dims 16 c + 8 h) and the C operand rows 8 g + 4 h
-    const int rd_hi = r * kFRowB + 16 * h;
+    for (int c = 0; c < 4; c++) rd_hi[c] = r * kFRowB + (((2 * c + h) ^ ((r >> 1) & 7)) << 4);
     const int rd_tu = kFHiB + 16 * h;
-    const int wr_hi = srow * kFRowB + 16 * spart;
-    const int wr_tu = kFHiB + 4 * srow;
     // one tile: the A fragments and C operand from LDS, two 4-MFMA chains (the wave's two query
     // blocks), the epilogue (group minima; with `extract`, the candidate test and slot stores)
     auto tile = [&](const char* sb, int u, int tile0, bool extract) {
         bf16x8 ah[4];
 #pragma unroll
         for (int c = 0; c < 4; c++)
-            ah[c] = *reinterpret_cast<const bf16x8*>(sb + rd_hi + u * kFT * kFRowB + 32 * c);
+            ah[c] = *reinterpret_cast<const bf16x8*>(sb + rd_hi[c] + u * kFT * kFRowB);
         f32x16 ci;
 #pragma unroll
         for (int g = 0; g < 4; g++) {
@@ -317,34 +321,30 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
                 if (tmin[j] <= thr[j]) {
                     const int sl = ncand[j]++;
                     if (sl < kCandSlots) {
-                        ctbase[j][sl] = tile0;
+                        const size_t slot = (size_t)cl[j] * kCandSlots + sl;
+                        ctile[slot] = tile0;
 #pragma unroll
                         for (int g = 0; g < 2; g++) {
                             bf16x8 b;
 #pragma unroll
                             for (int i = 0; i < 8; i++) b[i] = (__bf16)acc[j][8 * g + i];
-                            cvbase[j][2 * sl + g] = b;
+                            cval[slot * 2 + g] = b;
                         }
                     }
                 }
             }
         }
     };
-    // one stage: its staged rows into LDS buffer BUF, barrier, the next stage's loads, 4 tiles,
+    // one stage: wait for its DMAs (issued during the previous stage), barrier, the next
+    // stage's DMAs into the other buffer (whose reads finished before this barrier), 4 tiles,
     // then (except in the final recompute) the query's running bound and candidate threshold
     auto stage = [&](auto bufc, int it) {
         constexpr int BUF = decltype(bufc)::value;
         char* sb = sm + BUF * kFStageB;
         const int st = it == nstages ? 0 : it;
-#pragma unroll
-        for (int u = 0; u < kFST; u++) {
-            *reinterpret_cast<bf16x8*>(sb + wr_hi + u * kFT * kFRowB) = gh[u];
-            if (spart == 0)
-                *reinterpret_cast<float*>(sb + wr_tu + 4 * u * kFT) =
-                    gn[u] == kInf ? kInf : __builtin_fmaf(gn[u], kFEps, gn[u]);
-        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (it < nstages) gload(it + 1 == nstages ? 0 : it + 1);
+        if (it < nstages) dma(sm + (1 - BUF) * kFStageB, it + 1 == nstages ? 0 : it + 1);
 #pragma unroll
         for (int u = 0; u < kFST; u++) tile(sb, u, t0 + (st * kFST + u) * kFT, it > 0);
         if (it < nstages) {
@@ -358,7 +358,7 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     };
     // stage sequence: 0 (bounds only), 1 .. nstages - 1, then 0 again (candidates only, against
     // the chunk's final bound); LDS buffers alternate
-    gload(0);
+    dma(sm, 0);
     for (int it = 0; it <= nstages; it += 2) {
         stage(std::integral_constant<int, 0>{}, it);
         if (it + 1 <= nstages) stage(std::integral_constant<int, 1>{}, it + 1);
@@ -843,9 +843,9 @@ size_t knn2_cand_bytes(const BatchShape& sh) {
     return (size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 * kCandSlots * (2 * sizeof(bf16x8) + 4);
 }
 
-size_t knn2_split_bytes(const BatchShape& sh) {
+size_t knn2_split_bytes(const BatchShape& sh) {  // rows, tu, tmax, sentinel row (+ align)
     return (size_t)sh.n_pairs * sh.max_nt * (kDim * sizeof(__bf16) + sizeof(float)) +
-           (size_t)sh.n_pairs * sizeof(uint32_t);
+           (size_t)sh.n_pairs * sizeof(uint32_t) + 16 + 128 + 16;
 }
 
 static void cand_split(const BatchShape& sh, void* cand, int32_t** ctile, bf16x8** cval) {
@@ -857,6 +857,11 @@ static void cand_split(const BatchShape& sh, void* cand, int32_t** ctile, bf16x8
 static uint32_t* split_tmax(const BatchShape& sh, void* split) {
     return (uint32_t*)((char*)split + (size_t)sh.n_pairs * sh.max_nt * (kDim * sizeof(__bf16) + sizeof(float)));
 }
+// the sentinel row after tmax (16-B aligned): 64 bf16 zeros, then tu = +inf
+static char* split_sentinel(const BatchShape& sh, void* split) {
+    const size_t o = (size_t)((char*)(split_tmax(sh, split) + sh.n_pairs) - (char*)split);
+    return (char*)split + ((o + 15) & ~(size_t)15);
+}
 
 hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
                               const int64_t* off_t, const BatchShape& sh, void* split,
@@ -864,7 +869,10 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
     bf16x8* thi = (bf16x8*)split;
     float* tn = (float*)(thi + (size_t)sh.n_pairs * sh.max_nt * 8);
     uint32_t* tmax = split_tmax(sh, split);
+    char* sent = split_sentinel(sh, split);
     hipError_t e = hipMemsetAsync(tmax, 0, (size_t)sh.n_pairs * sizeof(uint32_t), st);
+    if (e == hipSuccess) e = hipMemsetAsync(sent, 0, 128, st);
+    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(sent + 128), 0x7f800000u, 1, st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(knn2_split_kernel, dim3((sh.max_nt + 63) / 64, sh.n_pairs), dim3(256), 0,
                        st, desc_t, off_t, sh.max_nt, thi, tn, tmax);
@@ -872,9 +880,11 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
     bf16x8* cval;
     cand_split(sh, cand, &ctile, &cval);
     const int qblocks = (sh.max_nq + kFQ - 1) / kFQ;
+    if ((size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 >= (1ull << 31)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(knn2_filter_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
                        st, desc_q, thi, tn, tmax, off_q, off_t, sh.fchunk_len, sh.fchunks,
-                       sh.max_nq, sh.max_nt, qblocks, pu, ccount, ctile, cval);
+                       sh.max_nq, sh.max_nt, qblocks, pu, ccount, ctile, cval,
+                       (const bf16x8*)sent, (const float*)(sent + 128));
     return hipGetLastError();
 }
 
