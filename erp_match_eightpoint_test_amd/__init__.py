@@ -6,6 +6,8 @@ Host-side mirror of the reference's hot-path classes (Kitsunetic/ERP_match_eight
 * ``eight_point.find / initial_guess / eight_point_estimation`` -- src/eight_point.cpp:16-192
 * ``erp_rotation`` / ``spherical_surf`` -- the ERP remaps either side of the path
   (src/erp_rotation.cpp:14-122, src/spherical_surf.cpp:16-133, src/automatic.cpp:50-79,148-152)
+* ``epipolar_tool`` / ``feature_matcher.draw_match`` -- the visual outputs
+  (src/epipolar_tool.cpp:7-128, src/feature_matcher.cpp:61-86)
 * ``PairBatchRunner`` -- the batched hot path: match -> gather -> find for many ERP pairs,
   i.e. what src/automatic.cpp:117-126 runs per pair, as one sequence of gfx950 kernels.
 
@@ -23,7 +25,8 @@ from . import capi, synth
 from .capi import (DMATCH_DTYPE, HYP_DTYPE, RESULT_DTYPE, Context, ErpError, check,
                    default_cfg)
 
-__all__ = ["feature_matcher", "eight_point", "erp_rotation", "spherical_surf", "PairBatchRunner", "Context", "ErpError",
+__all__ = ["feature_matcher", "eight_point", "erp_rotation", "spherical_surf", "epipolar_tool",
+           "PairBatchRunner", "Context", "ErpError",
            "default_cfg", "DMATCH_DTYPE", "HYP_DTYPE", "RESULT_DTYPE", "results_to_numpy",
            "hyps_to_numpy", "synth", "capi"]
 
@@ -111,6 +114,28 @@ class feature_matcher:  # noqa: N801  (reference class name)
                 return kp, desc, counts
             max_kp = int(-counts.min()) + 16
 
+    def draw_match(self, im_left, im_right, key_left, key_right):
+        """draw_match (src/feature_matcher.cpp:61-86): CUDA uint8 BGR images [H, W, 3] and the
+        matched keypoints (CUDA float32 [M, 2] or anything array-like of (pt.x, pt.y)) -> the
+        overlay [H, W, 3]: grey left / right in channels 0 / 1, a 5-px line per match coloured
+        HSV(i 180 / M, 180, 150), later matches on top."""
+        import torch
+        im_left, im_right = _img_dev(im_left), _img_dev(im_right)
+        if im_left.shape != im_right.shape:
+            raise ValueError("draw_match: the two images differ in size")
+        H, W = im_left.shape[:2]
+        kl, kr = _keys_dev(key_left, im_left.device), _keys_dev(key_right, im_left.device)
+        m = min(kl.shape[0], kr.shape[0])
+        if kl.shape[0] != kr.shape[0]:
+            raise ValueError("draw_match: key_left and key_right differ in length")
+        out = torch.empty_like(im_left)
+        check(self.ctx.L.erp_draw_match_dev(self.ctx.h, im_left.data_ptr(), im_right.data_ptr(),
+                                            W, H, kl.data_ptr() if m else None,
+                                            kr.data_ptr() if m else None, m, out.data_ptr(),
+                                            torch.cuda.current_stream(im_left.device).cuda_stream),
+              "draw_match")
+        return out
+
     def _to_device(self, a):
         import torch
         return torch.from_numpy(a).to(f"cuda:{self.ctx.device}")
@@ -184,6 +209,64 @@ class eight_point:  # noqa: N801  (reference class name)
         r = np.frombuffer(bytes(h), HYP_DTYPE)[0]
         return (r["R1"].copy(), r["R2"].copy(), r["T"].copy(), bool(r["R1_valid"]),
                 bool(r["R2_valid"]), r["E"].copy())
+
+
+def _keys_dev(k, device):
+    """(pt.x, pt.y) rows as a contiguous CUDA float32 tensor [n, 2]"""
+    import torch
+    if isinstance(k, torch.Tensor):
+        t = k.to(device=device, dtype=torch.float32)
+    else:
+        t = torch.from_numpy(np.ascontiguousarray(k, np.float32)).to(device)
+    return t.reshape(-1, 2).contiguous()
+
+
+def _keys_host(k) -> np.ndarray:
+    try:
+        import torch
+        if isinstance(k, torch.Tensor):
+            k = k.detach().cpu().numpy()
+    except ImportError:  # pragma: no cover
+        pass
+    return np.ascontiguousarray(k, np.float32).reshape(-1, 2)
+
+
+class epipolar_tool:  # noqa: N801  (reference class name)
+    """epipolar_tool (src/epipolar_tool.hpp:7-31, .cpp:7-128): picks test_key_num (<= 7) of the
+    matched pairs with std::random_shuffle on the glibc rand() stream -- (seed, offset) = the
+    process-global rand() state, (1, 0) in a fresh process -- and draws, for an essential
+    matrix, the epipolar curves of their left keypoints and dots at their right keypoints on an
+    output_width x output_height ERP canvas (a CUDA uint8 tensor [H, W, 3])."""
+
+    def __init__(self, left_key, right_key, im_width: int, im_height: int, output_width: int,
+                 output_height: int, test_key_num: int, seed: int = 1, offset: int = 0,
+                 device: int = 0, ctx: Context | None = None):
+        self.ctx = ctx or Context(device)
+        self.left_key, self.right_key = _keys_host(left_key), _keys_host(right_key)
+        if self.left_key.shape != self.right_key.shape:
+            raise ValueError("epipolar_tool: left_key and right_key differ in length")
+        self.match_size = self.left_key.shape[0]
+        self.n_key = int(test_key_num)
+        self.im_width, self.im_height = int(im_width), int(im_height)
+        self.epipole_mat_width, self.epipole_mat_height = int(output_width), int(output_height)
+        self.seed, self.offset = int(seed), int(offset)
+        self.random_idx = np.zeros(max(self.n_key, 0), np.int32)
+        if not (1 <= self.match_size and 0 <= self.n_key <= min(7, self.match_size)):
+            raise ErpError(capi.ERP_INVALID_ARG,
+                           "epipolar_tool: need 0 <= test_key_num <= min(7, match_size)")
+
+    def draw_epipole(self, test_E_mat):  # noqa: N803  (reference argument name)
+        import torch
+        E = _m9(test_E_mat)
+        dev = torch.device(f"cuda:{self.ctx.device}")
+        out = torch.empty((self.epipole_mat_height, self.epipole_mat_width, 3), dtype=torch.uint8,
+                          device=dev)
+        check(self.ctx.L.erp_epipolar_draw_dev(
+            self.ctx.h, _np_ptr(self.left_key), _np_ptr(self.right_key), self.match_size,
+            self.im_width, self.im_height, self.epipole_mat_width, self.epipole_mat_height,
+            self.n_key, self.seed, self.offset, _np_ptr(E), out.data_ptr(),
+            _np_ptr(self.random_idx), torch.cuda.current_stream(dev).cuda_stream), "draw_epipole")
+        return out
 
 
 def _m9(a) -> np.ndarray:
@@ -317,12 +400,13 @@ class spherical_surf:  # noqa: N801  (reference class name)
               "rotate_keypoint")
         return key
 
-    def do_all(self, im_left, im_right, max_kp: int = 16384, fill: int = 0):
+    def do_all(self, im_left, im_right, max_kp: int = 16384, fill: int = 0, draw: bool = False):
         """spherical_surf::do_all (src/spherical_surf.cpp:65-180) on two CUDA uint8 BGR ERP
         images [H, W, 3]: bands (:77-93) -> SURF on the 8 bands (:96-118) -> keypoint
         un-rotation + concatenation n0..n3 (:120-150) -> match_two_image (:153) -> gather
         (:155-162).  Returns (left_key [M, 2], right_key [M, 2]) CUDA float32 tensors of the
-        matched ERP pixels, match_size and total_key_num (the left keypoints, :179)."""
+        matched ERP pixels, match_size and total_key_num (the left keypoints, :179); with
+        draw=True also match_output (feature_matcher.draw_match of the two images, :173)."""
         import torch
         H, W = im_left.shape[:2]
         ims = torch.stack([_img_dev(im_left), _img_dev(im_right)]).contiguous()
@@ -340,7 +424,11 @@ class spherical_surf:  # noqa: N801  (reference class name)
             dcat.append(torch.cat([desc[4 * side + b, :c4[b]] for b in range(4)]).contiguous())
         m = fm._match_device(dcat[0], dcat[1], 0.3)            # [M, 4] int32 DMatch rows
         q, t = m[:, 0].long(), m[:, 1].long()
-        return keys[0][q], keys[1][t], int(m.shape[0]), int(keys[0].shape[0])
+        kl, kr = keys[0][q], keys[1][t]
+        if draw:
+            return (kl, kr, int(m.shape[0]), int(keys[0].shape[0]),
+                    fm.draw_match(im_left, im_right, kl, kr))
+        return kl, kr, int(m.shape[0]), int(keys[0].shape[0])
 
     def unrotate_band_keypoints(self, key, counts, width: int, height: int):
         """do_all's keypoint step (src/spherical_surf.cpp:120-144), in place on the band

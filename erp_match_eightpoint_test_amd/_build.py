@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(LIB_DIR, "liberp_match.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("ERP_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["kernels.hip", "matcher.hip", "capi.hip", "remap.hip", "remap_api.hip", "surf.hip", "surf_api.hip",
+SOURCES = ["kernels.hip", "matcher.hip", "capi.hip", "remap.hip", "remap_api.hip", "surf.hip", "surf_api.hip", "viz.hip",
            "host_api.cpp"]
 HEADERS = ["erp_device.hpp", "erp_kernels.hpp", "erp_remap.hpp", "erp_surf.hpp"]
 PUBLIC_HEADERS = ["erp_match.h", os.path.join("erp", "feature_matcher.hpp"),

@@ -34,6 +34,10 @@ bool ensure(DevBuf& b, size_t bytes) {
     return true;
 }
 
+
+}  // namespace
+
+// (global linkage: viz.hip shuffles on the same stream)
 // glibc rand() window before draw `offset` of a stream seeded with `seed` (host, sequential;
 // same recurrence the kernels jump along).  31 words r[n-31..n-1].
 void host_glibc_window(uint32_t seed, uint64_t offset, uint32_t out[31]) {
@@ -58,8 +62,6 @@ void host_glibc_window(uint32_t seed, uint64_t offset, uint32_t out[31]) {
     for (int j = 0; j < 31; j++) out[j] = ring[(end - 31 + j) % 34];
 }
 
-}  // namespace
-
 struct erp_ctx {
     int device = 0;
     // one lock per context; recursive so the host-pointer entry points hold it across their
@@ -79,8 +81,9 @@ struct erp_ctx {
     DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
         rtab, limbs, tsplit, ovf, remap_scr, vchunk;
-    DevBuf extra[12];         // erp_ctx_scratch_internal slots (SURF)
+    DevBuf extra[13];         // erp_ctx_scratch_internal slots (1-11 SURF, 12 viz)
     uint64_t surf_key = 0;    // (W, H, params) of the SURF layer table in extra[1]
+    uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -163,6 +166,20 @@ void* erp_ctx_scratch_internal(erp_ctx* ctx, int which, size_t bytes) {
     if (which < 0 || which >= (int)(sizeof(ctx->extra) / sizeof(ctx->extra[0]))) return nullptr;
     DevBuf& b = which == 0 ? ctx->remap_scr : ctx->extra[which];
     return ensure(b, bytes) ? b.p : nullptr;
+}
+
+// the draw_match line buffer: grown like the other slots, with a per-call epoch for its stamps
+// (epoch << 16 | match index); *fresh = the buffer must be zeroed first (new memory, or the
+// 16-bit epoch wrapped)
+void* erp_ctx_stamp_buffer_internal(erp_ctx* ctx, size_t bytes, uint32_t* epoch, bool* fresh) {
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DevBuf& b = ctx->extra[12];
+    void* before = b.p;
+    if (!ensure(b, bytes)) return nullptr;
+    *fresh = b.p != before || ctx->viz_epoch == 0 || ctx->viz_epoch >= 0xFFFFu;
+    ctx->viz_epoch = *fresh ? 1u : ctx->viz_epoch + 1u;
+    *epoch = ctx->viz_epoch;
+    return b.p;
 }
 
 extern "C" {

@@ -328,6 +328,37 @@ erp_status erp_surf_detect_compute_dev(erp_ctx* ctx, const uint8_t* d_images, in
                                        erp_keypoint* d_kp, float* d_desc, int32_t* d_count,
                                        void* stream);
 
+/* ---- visual outputs, device images ---- */
+/* epipolar_tool (src/epipolar_tool.hpp / .cpp:7-71, constructor + draw_epipole :74-128): n_key
+   (<= 7, the reference's color_set) of the m matched pairs (host keypoints, ERP pixels of an
+   im_width x im_height image) chosen as the first n_key of std::random_shuffle(iota(m)) on the
+   glibc rand() stream at (seed, offset) (the process-global rand() state: 1 / 0 in a fresh
+   process); on an out_width x out_height CV_8UC3 canvas d_out (written whole) the pixels p with
+   |l^T E p| < 0.002 for a chosen left bearing l get that key's colour and 11 x 11 dots mark the
+   chosen right keypoints (resized).  E: row-major 3x3 (test_E_mat).  The reference's OpenMP
+   loop races on overlapping writes; here the sequential order of its loop decides: a pixel
+   shows the last key whose dot covers it, else the last key whose curve passes, else 0 (the
+   corner pixel (H-1, W-1) interleaves curve k and dot k in key order).  A dot pixel lands at
+   its linear address like the unchecked Mat::at (past the left/right edge it wraps into the
+   neighbouring row); writes that would leave the canvas are dropped.
+   h_random_idx (may be NULL): the n_key chosen match indices. */
+erp_status erp_epipolar_draw_dev(erp_ctx* ctx, const erp_point2f* h_key_left,
+                                 const erp_point2f* h_key_right, int32_t m, int32_t im_width,
+                                 int32_t im_height, int32_t out_width, int32_t out_height,
+                                 int32_t n_key, uint32_t seed, uint64_t offset, const double E[9],
+                                 uint8_t* d_out, int32_t* h_random_idx, void* stream);
+/* feature_matcher::draw_match (src/feature_matcher.cpp:61-86): d_out (W x H CV_8UC3) = the
+   grey images of d_left / d_right (cvtColor CV_RGB2GRAY, as the reference calls it on its BGR
+   images) in channels 0 / 1, 0 in channel 2, with a line of thickness 5 from key_left[i] to
+   key_right[i] (device keypoints, rounded like cv::Point(Point2f)) in the colour
+   HSV(i 180 / m, 180, 150) -> BGR, later matches on top.  Lines are the pixels within 2.5 of
+   the segment (cv::line's thickness-5 rasteriser is not restated: parity with OpenCV is
+   unpinned).  m <= 65535; the three image pointers are 4-byte aligned. */
+erp_status erp_draw_match_dev(erp_ctx* ctx, const uint8_t* d_left, const uint8_t* d_right,
+                              int32_t W, int32_t H, const erp_point2f* d_key_left,
+                              const erp_point2f* d_key_right, int32_t m, uint8_t* d_out,
+                              void* stream);
+
 /* host 3x3 geometry (row-major doubles) */
 void erp_eular2rot(const double theta[3], double R[9]);         /* erp_rotation.cpp:14-40 */
 void erp_rot2eular(const double R[9], double e[3]);             /* erp_rotation.cpp:43-63 */

@@ -66,7 +66,8 @@ def build(force: bool = False) -> str:
     """Compile the oracle with its Makefile (gcc only; no reference sources involved)."""
     if force or not os.path.exists(LIB_PATH) or (
             os.path.getmtime(LIB_PATH) < max(os.path.getmtime(os.path.join(HERE, f))
-                                             for f in ("erp_oracle.c", "erp_surf.c", "erp_oracle.h"))):
+                                             for f in ("erp_oracle.c", "erp_surf.c", "erp_viz.c",
+                                                       "erp_oracle.h"))):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
 
@@ -125,6 +126,13 @@ def lib():
         L.erpo_rectify.restype = C.c_int32
         L.erpo_vertical_rotate.argtypes = [P, C.c_int32, C.c_int32, P]
         L.erpo_vertical_rotate.restype = C.c_int32
+        L.erpo_epipolar_draw.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                                         C.c_int32, C.c_int32, C.c_uint32, C.c_uint64, P, P, P, P]
+        L.erpo_epipolar_draw.restype = C.c_int32
+        L.erpo_epipolar_value.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32]
+        L.erpo_epipolar_value.restype = C.c_double
+        L.erpo_hsv2bgr.argtypes = [C.c_int, C.c_int, C.c_int, P]
+        L.erpo_draw_match.argtypes = [P, P, C.c_int32, C.c_int32, P, P, C.c_int32, P]
         _lib = L
     return _lib
 
@@ -409,4 +417,49 @@ def gray_bgr(img):
     H, W = img.shape[:2]
     out = np.zeros((H, W), np.uint8)
     lib().erpo_gray_bgr(_p(img), W, H, _p(out))
+    return out
+
+
+# ---------------- visual outputs (erp_viz.c) ----------------
+def epipolar_draw(key_left, key_right, im_width: int, im_height: int, out_w: int, out_h: int,
+                  n_key: int, E, seed: int = 1, offset: int = 0):
+    """epipolar_tool(...).draw_epipole(E) run sequentially (src/epipolar_tool.cpp:7-128) ->
+    (canvas uint8 [out_h, out_w, 3], random_idx (n_key,), min over pixels and keys of
+    ||l^T E p| - 0.002| -- how close the canvas came to the threshold)."""
+    kl = np.ascontiguousarray(key_left, np.float32).reshape(-1, 2)
+    kr = np.ascontiguousarray(key_right, np.float32).reshape(-1, 2)
+    e = np.ascontiguousarray(E, np.float64).reshape(9)
+    out = np.zeros((out_h, out_w, 3), np.uint8)
+    idx = np.zeros(max(n_key, 1), np.int32)
+    mm = C.c_double(0)
+    rc = lib().erpo_epipolar_draw(_p(kl), _p(kr), kl.shape[0], im_width, im_height, out_w, out_h,
+                                  n_key, seed, offset, _p(e), _p(out), _p(idx), C.byref(mm))
+    if rc:
+        raise ValueError("epipolar_draw: invalid arguments")
+    return out, idx[:n_key], mm.value
+
+
+def epipolar_value(l, E, i: int, j: int, out_w: int, out_h: int) -> float:
+    """l^T E p of canvas pixel (i, j) (src/epipolar_tool.cpp:100-105)"""
+    lv = np.ascontiguousarray(l, np.float64).reshape(3)
+    e = np.ascontiguousarray(E, np.float64).reshape(9)
+    return lib().erpo_epipolar_value(_p(lv), _p(e), i, j, out_w, out_h)
+
+
+def hsv2bgr(h: int, s: int, v: int) -> np.ndarray:
+    o = np.zeros(3, np.uint8)
+    lib().erpo_hsv2bgr(h, s, v, _p(o))
+    return o
+
+
+def draw_match(im_left: np.ndarray, im_right: np.ndarray, key_left, key_right) -> np.ndarray:
+    """feature_matcher::draw_match (src/feature_matcher.cpp:61-86) with lines = the pixels
+    within 2.5 of the segment between the rounded keypoints (parity with cv::line unpinned)."""
+    a = np.ascontiguousarray(im_left, np.uint8)
+    b = np.ascontiguousarray(im_right, np.uint8)
+    kl = np.ascontiguousarray(key_left, np.float32).reshape(-1, 2)
+    kr = np.ascontiguousarray(key_right, np.float32).reshape(-1, 2)
+    H, W = a.shape[:2]
+    out = np.zeros_like(a)
+    lib().erpo_draw_match(_p(a), _p(b), W, H, _p(kl), _p(kr), kl.shape[0], _p(out))
     return out

@@ -178,4 +178,15 @@ int erpo_find(int32_t W, int32_t H, const float* kl, const float* kr, int32_t m,
 #ifdef __cplusplus
 }
 #endif
+/* ---------------- visual outputs (erp_viz.c) ---------------- */
+int32_t erpo_epipolar_draw(const float* key_left, const float* key_right, int32_t m,
+                           int32_t im_width, int32_t im_height, int32_t out_w, int32_t out_h,
+                           int32_t n_key, uint32_t seed, uint64_t offset, const double E[9],
+                           uint8_t* out, int32_t* random_idx, double* min_margin);
+double erpo_epipolar_value(const double l[3], const double E[9], int32_t i, int32_t j, int32_t out_w,
+                           int32_t out_h);
+void erpo_hsv2bgr(int h, int s, int v, uint8_t bgr[3]);
+void erpo_draw_match(const uint8_t* left, const uint8_t* right, int32_t W, int32_t H,
+                     const float* key_left, const float* key_right, int32_t m, uint8_t* out);
+
 #endif
