@@ -312,6 +312,24 @@ def run_manual(args):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     r = results_to_numpy(res.view(1, -1))[0]
+    emu = {}
+    if world == 1 and not args.no_shard_consensus:
+        # the row-sharded consensus of an N-rank run, every shard on this GPU in turn (outside
+        # the timed region): the bounds stage per shard ~ one rank's share of it at N ranks
+        for nsh in (2, 8):
+            D.find_hypothesis_sharded_dev(ctx, c["W"], c["H"], kl, kr, 100, iters, emulate_world=nsh)
+            torch.cuda.synchronize()
+            ctx.stage_times()
+            res_e = D.find_hypothesis_sharded_dev(ctx, c["W"], c["H"], kl, kr, 100, iters,
+                                                  emulate_world=nsh)[0]
+            torch.cuda.synchronize()
+            se = {k: v[0] for k, v in ctx.stage_times().items() if v[1] > 0}
+            re_ = results_to_numpy(res_e.view(1, -1))[0]
+            emu[f"shards{nsh}"] = {
+                "bounds_ms_per_shard": se.get("consensus_bounds", 0.0) / nsh,
+                "stages_ms_all_shards": se,
+                "same_winner": bool(re_["min_idx"] == r["min_idx"] and
+                                    np.array_equal(re_["R"], r["R"]))}
     if rank == 0:
         # the unsharded find() on this GPU must give the same winner (outside the timed region)
         from erp_match_eightpoint_test_amd import eight_point
@@ -328,6 +346,7 @@ def run_manual(args):
                            "parallelism": f"hypothesis blocks x{world}",
                            "iterations_per_s": iters * args.steps / elapsed},
                 "stages_ms_rank0": st,
+                "row_shard_emulation": emu,
                 "check": {"status": int(r["status"]), "K": int(r["K"]),
                           "min_idx": int(r["min_idx"]), "survivors": int(r["survivors"]),
                           "same_as_unsharded": bool(np.array_equal(r["R"], R1) and

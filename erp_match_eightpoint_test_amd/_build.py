@@ -51,9 +51,10 @@ def up_to_date() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, lib_path: str = LIB_PATH,
-          src_override: dict | None = None) -> str:
-    """src_override / lib_path: development variants (a source file replaced by another path,
-    built into another library; see capi.lib_path's ERP_LIB_PATH)."""
+          src_override: dict | None = None, defines: list | None = None) -> str:
+    """src_override / lib_path / defines: development variants (a source file replaced by
+    another path, extra -D flags, built into another library; see capi.lib_path's
+    ERP_LIB_PATH)."""
     if not force and lib_path == LIB_PATH and up_to_date():
         return LIB_PATH
     lib_dir = os.path.dirname(lib_path)
@@ -62,7 +63,8 @@ def build(force: bool = False, verbose: bool = False, lib_path: str = LIB_PATH,
     for src in SOURCES:
         obj = os.path.join(lib_dir, os.path.splitext(src)[0] + ".o")
         path = (src_override or {}).get(src, os.path.join(CSRC, src))
-        cmds.append([HIPCC, *CXXFLAGS, *EXTRA_FLAGS.get(src, []), "-I", os.path.join(ROOT, "include"),
+        cmds.append([HIPCC, *CXXFLAGS, *EXTRA_FLAGS.get(src, []), *[f"-D{d}" for d in defines or []],
+                     "-I", os.path.join(ROOT, "include"),
                      "-I", CSRC, "-c", path, "-o", obj])
         objs.append(obj)
     # one hipcc per source, in parallel (kernels.hip dominates; the rest overlap it)

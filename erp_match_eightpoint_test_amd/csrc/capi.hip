@@ -462,7 +462,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (int32_t*)c->nsurv.p + sh.n_pairs, st));
     }
     if (phase == 1) return ERP_OK;
-    if (phase == 2)  // the bounds ran per shard (no pre-pruning): binned_rows = K
+    if (phase == 2)  // the bounds ran per shard (binned rows not combined): report -1
         ERP_CK(hipMemsetAsync((int32_t*)c->nsurv.p + sh.n_pairs, 0xFF, sizeof(int32_t) * sh.n_pairs, st));
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);

@@ -1559,7 +1559,10 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(
 // boundary bins (select drops them); the others are appended (any order) to the per-pair list
 // that the second bounds pass reads.  Synthetic configs[1] pairs (one cluster of ~1e4 valid
 // rotations): ~80 % of the rows are pruned for ~1/16 + ~1/20 of the full pass's distances.
-constexpr int kLipStep = 16;    // every 16th row is a reference row
+#ifndef ERP_LIP_STEP
+#define ERP_LIP_STEP 16
+#endif
+constexpr int kLipStep = ERP_LIP_STEP;  // every 16th row is a reference row
 constexpr int kLipMinK = 1024;  // smaller sets: no pre-pruning (every non-reference row listed)
 constexpr int kLipChunk = 1024; // reference rows staged in LDS per chunk
 
@@ -1567,21 +1570,26 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride, double trim_lo,
     double trim_hi, double* __restrict__ lb, double* __restrict__ ub,
     const int32_t* __restrict__ slist, const int32_t* __restrict__ scount,
-    int32_t* __restrict__ rlist, int olstride, int32_t* __restrict__ rcount) {
-    // slist == nullptr: the K rows (before the histogram pass); else the per-pair survivor list
-    // slist[p][0 .. scount[p]) after the first select (before the refine pass, whose reference
-    // survivors, every 16th, are already refined)
+    int32_t* __restrict__ rlist, int olstride, int32_t* __restrict__ rcount, int shard,
+    int nshards) {
+    // slist == nullptr: the rows [ra, rb) of row shard `shard` of `nshards` (all K rows when
+    // unsharded) before the histogram pass, against that shard's own reference rows ra, ra + 16,
+    // ... (configs[4]'s row-sharded consensus: U is then the shard's smallest reference UB, still
+    // >= the global minimum of T, so every pruning stays rigorous); else the per-pair survivor
+    // list slist[p][0 .. scount[p]) after the first select (before the refine pass, whose
+    // reference survivors, every 16th, are already refined)
     __shared__ float4 refs[kLipChunk];
     __shared__ double red[4];
     __shared__ int nlive;
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
-    const int n = slist ? scount[p] : K;
+    const int ra = slist ? 0 : (int)((int64_t)K * shard / nshards);
+    const int n = slist ? scount[p] : (int)((int64_t)K * (shard + 1) / nshards) - ra;
     const int i0 = blockIdx.x * 512;  // two positions per thread: i0 + tid and i0 + 256 + tid
     if (i0 >= n) return;
     if (slist && n <= kRefineMin) return;  // few survivors: no refine pass, nothing to list
     const int32_t* SL = slist ? slist + (size_t)p * stride : nullptr;
-    auto rowpos = [&](int k) { return SL ? (int)SL[k] : k; };
+    auto rowpos = [&](int k) { return SL ? (int)SL[k] : ra + k; };
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
@@ -2475,7 +2483,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    hipStream_t st) {
     hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     const int stride = 2 * sh.iters;
-    if (nshards > 1 || !rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
+    if (!rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
         if (rcount) {
             const hipError_t me = hipMemsetAsync(rcount, 0xFF, sizeof(int32_t) * sh.n_pairs, st);
             if (me != hipSuccess) return me;
@@ -2486,16 +2494,19 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                            edges, stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, 1);
         return hipGetLastError();
     }
-    // reference rows, Lipschitz pre-pruning, then the rows it kept
-    const int nref = (stride + kLipStep - 1) / kLipStep;
+    // reference rows, Lipschitz pre-pruning, then the rows it kept -- within the row shard
+    // (nshards > 1: configs[4]'s consensus split over ranks; each rank's rows only)
+    const int srows = (stride + nshards - 1) / nshards + 1;  // >= any shard's rows
+    const int nref = (srows + kLipStep - 1) / kLipStep;
     dim3 g1((nref + kBoundRows - 1) / kBoundRows, sh.n_pairs);
     hipLaunchKernelGGL(consensus_bounds_kernel, g1, dim3(256), 0, st, kcount, rv, dscale, edges,
-                       stride, trim_lo, trim_hi, lb, ub, bsel, 0, 1, kLipStep);
+                       stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, kLipStep);
     const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * sh.n_pairs, st);
     if (me != hipSuccess) return me;
-    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, sh.n_pairs),
+    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((srows + 511) / 512, sh.n_pairs),
                        dim3(256), 0, st, kcount, rv, stride, trim_lo, trim_hi, lb, ub,
-                       (const int32_t*)nullptr, (const int32_t*)nullptr, rlist, stride, rcount);
+                       (const int32_t*)nullptr, (const int32_t*)nullptr, rlist, stride, rcount,
+                       shard, nshards);
     int32_t* uoff = rcount + sh.n_pairs;  // [n_pairs + 1] after the counts
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)rcount,
                        sh.n_pairs, kBoundRows, 0, uoff);
@@ -2538,7 +2549,7 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
     if (me != hipSuccess) return me;
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, P), dim3(256), 0, st,
                        kcount, rv, stride, trim_lo, trim_hi, lb, ub, surv, nsurv, list2, l2stride,
-                       n2);
+                       n2, 0, 1);
     // (C) the survivors the references did not prune
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)n2, P,
                        kRefineRows, 0, uoff);

@@ -426,11 +426,14 @@ def test_hypothesis_sharded_dev_padded_blocks(ctx, world):
     assert np.array_equal(r["R"], R) and np.array_equal(r["T"], T)
 
 
-@pytest.mark.parametrize("world,iters", [(2, 500), (3, 500), (8, 500), (5, 4000)])
+@pytest.mark.parametrize("world,iters", [(2, 500), (3, 500), (8, 500), (5, 4000), (2, 100000),
+                                         (8, 100000)])
 def test_consensus_row_shards_equal_unsharded(ctx, world, iters):
     """configs[4]'s sharded consensus: the K^2 bounds pass split into `world` row shards
-    (erp_consensus_hyps_shard_dev per shard, summed as the RCCL all_reduce would) then
-    erp_consensus_hyps_finish_dev gives the unsharded find's result, field for field."""
+    (erp_consensus_hyps_shard_dev per shard: reference rows, Lipschitz pre-pruning against the
+    shard's own references, the kept rows; summed as the RCCL all_reduce would) then
+    erp_consensus_hyps_finish_dev gives the unsharded find's result, field for field -- up to
+    configs[4]'s 100k iterations (K ~ 89k rows)."""
     import torch
     from erp_match_eightpoint_test_amd import eight_point, results_to_numpy
     from erp_match_eightpoint_test_amd import dist as D

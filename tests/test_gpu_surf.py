@@ -1,11 +1,12 @@
 """GPU SURF against the oracle's restatement (oracle/erp_surf.c).
 
-Bars: keypoints (x, y, size, response, octave, class_id) bit-exact and in the same
-KeypointGreater order -- the detector is integer / float / double work repeated operation for
-operation; orientation angles within 1e-3 degrees and descriptors within 2e-3 (max abs) for
-all but a handful of keypoints: the rotated sampling window uses the device's sin/cos, which
-can differ from glibc's sinf/cosf in the last ulp and move a bilinear sample across a
-rounding boundary.  Parity with OpenCV itself is unpinned (OpenCV is absent)."""
+Bars: keypoints (x, y, size, response, octave, class_id, angle) bit-exact and in the same
+KeypointGreater order -- the detector and the orientation are integer / float / double work
+repeated operation for operation; descriptors bit-exact except for keypoints whose rotated
+window sin / cos differ between glibc's sinf / cosf (the oracle) and the device's double sin /
+cos rounded to float -- certified per keypoint with libm on the host (measured: no such
+keypoint in any test so far, every descriptor bit-exact).  Parity with OpenCV itself is
+unpinned (OpenCV is absent)."""
 from __future__ import annotations
 
 import numpy as np
@@ -33,16 +34,36 @@ def fm(gpu_lib):
     return feature_matcher(ctx=Context(0))
 
 
+def _sincos_differ(angle_deg: np.ndarray) -> np.ndarray:
+    """keypoints whose rotated-window sin/cos may differ between the oracle (glibc sinf / cosf
+    of the float angle in radians) and the device (the double sin / cos rounded to float)"""
+    import ctypes
+    import math
+    libm = ctypes.CDLL("libm.so.6")
+    libm.sinf.restype = libm.cosf.restype = ctypes.c_float
+    libm.sinf.argtypes = libm.cosf.argtypes = [ctypes.c_float]
+    out = np.zeros(len(angle_deg), bool)
+    for k, a in enumerate(angle_deg):
+        d = float(np.float32(a) * np.float32(math.pi / 180))
+        out[k] = (np.float32(libm.sinf(d)) != np.float32(math.sin(d))
+                  or np.float32(libm.cosf(d)) != np.float32(math.cos(d)))
+    return out
+
+
 def _compare(kg, dg, ko, do):
+    """keypoints and angles bit-exact; descriptors bit-exact except where the window's sin / cos
+    provably differ between glibc's sinf / cosf and the device's rounded double (certified per
+    keypoint; none so far)"""
     assert len(kg) == len(ko), (len(kg), len(ko))
-    for f in ("x", "y", "size", "response", "octave", "class_id"):
+    for f in ("x", "y", "size", "response", "octave", "class_id", "angle"):
         assert np.array_equal(kg[f], ko[f]), f
-    da = np.abs(kg["angle"] - ko["angle"])
-    da = np.minimum(da, 360 - da)
-    bad = int((da > 1e-3).sum())
     dd = np.abs(dg - do).max(axis=1) if len(dg) else np.zeros(0)
-    badd = int((dd > 2e-3).sum())
-    assert bad <= max(2, len(kg) // 200) and badd <= max(2, len(kg) // 100), (bad, badd, len(kg))
+    differ = dd != 0
+    certified = _sincos_differ(ko["angle"][differ]) if differ.any() else np.zeros(0, bool)
+    print(f"\n{len(kg)} keypoints: angles exact, {int(differ.sum())} descriptors not bit-exact "
+          f"(max {dd.max() if len(dd) else 0:.3g}), {int(certified.sum())} of them certified")
+    assert certified.all(), np.flatnonzero(differ)[~certified][:10]
+    assert (dd[differ] <= 2e-3).all()
     assert np.allclose(np.linalg.norm(dg, axis=1), 1.0, atol=1e-5)
 
 
