@@ -671,30 +671,53 @@ __global__ __launch_bounds__(256) void gram_limbs_kernel(const int32_t* __restri
     for (int k = tid; k < kGramN * 32 / 16; k += 256) o[k] = reinterpret_cast<const uint4*>(tile)[k];
 }
 
-// Block = 4 waves x 32 iterations (one MFMA row tile each); K loop over the pair's selection
-// words, two words (64 rows, 14 MFMAs per wave) per step.  Operands reach LDS only by LDS-DMA
-// (global_load_lds: the 14 KB limb images of the step's two words and the block's 2 x 128
-// selection words) into a ring of kGramRing slots, issued kGramRing - 1 steps ahead: the
-// selection words stream from HBM once, and their latency is covered by the ring, not by
-// occupancy.  One raw barrier per step after a counted vmcnt (never 0 in the loop); all LDS in
-// one __shared__ array.  All 14 B fragments of a step are read before the first MFMA.
-// gram[p][36][iters] (SoA, the eigen layout).
+// Block = kGramWaves waves x 32 iterations (one MFMA row tile each); K loop over the pair's
+// selection words, two words (64 rows, 14 MFMAs per wave) per step.  Operands reach LDS only by
+// LDS-DMA (global_load_lds: the 14 KB limb images of the step's two words and the block's
+// 2 x 32 kGramWaves selection words) into a ring of kGramRing slots, issued kGramRing - 1 steps
+// ahead: the selection words stream from HBM once, and their latency is covered by the ring, not
+// by occupancy.  The limb images are read once per block and step, so the block's iteration
+// count sets the L2 -> LDS traffic per MFMA.  One raw
+// barrier per step after a counted vmcnt (never 0 in the loop); all LDS in one __shared__ array.
+// All 14 B fragments of a step are read before the first MFMA.  gram[p][36][iters] (SoA, the
+// eigen layout).
+// (measured r02h, per 384-pair step: 4 waves / 3 blocks per CU 2.42 ms; 8 waves -- half the
+// L2 -> LDS image traffic -- 2.44; 6 waves 2.91 (a 6-wave block loads the SIMDs 2/2/1/1); all
+// 14 fragment reads issued before the first MFMA (ERP_GRAM_SCHED, 194 VGPRs) 2.55-2.63)
+#ifndef ERP_GRAM_WAVES
+#define ERP_GRAM_WAVES 4
+#endif
+#ifndef ERP_GRAM_SCHED
+#define ERP_GRAM_SCHED 0
+#endif
+constexpr int kGramWaves = ERP_GRAM_WAVES;                      // waves per block
+constexpr int kGramIters = 32 * kGramWaves;                     // iterations per block
 constexpr int kGramWords = 2;                                   // selection words per K step
 constexpr int kGramWordBytes = kGramN * 32;                     // one word's limb image (7 KB)
 constexpr int kGramSelOff = kGramWords * kGramWordBytes;        // selection words in a slot
-constexpr int kGramSlotBytes = kGramSelOff + kGramWords * 128 * 4;
+constexpr int kGramSlotBytes = kGramSelOff + kGramWords * kGramIters * 4;
 constexpr int kGramRing = 3;
-static_assert(kGramSelOff == 14 * 1024, "14 limb pieces of 1 KB per step");
+constexpr int kGramPieces = kGramSelOff / 1024;                 // 1-KB limb pieces per step
+static_assert(kGramPieces == 14, "14 limb pieces of 1 KB per step");
+static_assert(kGramWaves % 2 == 0 && kGramWaves <= 14, "2 words x (kGramWaves / 2) chunks");
+// limb pieces moved by wave w: the first (14 % W) waves move one more
+constexpr int gram_pieces_of(int w) {
+    return kGramPieces / kGramWaves + (w < kGramPieces % kGramWaves ? 1 : 0);
+}
+constexpr int gram_piece0(int w) {
+    return w * (kGramPieces / kGramWaves) + (w < kGramPieces % kGramWaves ? w : kGramPieces % kGramWaves);
+}
 
 typedef __attribute__((address_space(3))) void* lds_vptr;
 typedef const __attribute__((address_space(1))) void* glb_vptr;
 
-__global__ __launch_bounds__(256, 3) void gram_mfma_kernel(const int32_t* __restrict__ counts,
-                                                           const int8_t* __restrict__ limbs,
-                                                           const uint32_t* __restrict__ selw,
-                                                           int iters, int nwaves, int nbw,
-                                                           double sample_frac,
-                                                           double* __restrict__ gram, int nhb) {
+#ifndef ERP_GRAM_MINBLOCKS
+#define ERP_GRAM_MINBLOCKS 3
+#endif
+__global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma_kernel(
+    const int32_t* __restrict__ counts, const int8_t* __restrict__ limbs,
+    const uint32_t* __restrict__ selw, int iters, int nwaves, int nbw, double sample_frac,
+    double* __restrict__ gram, int nhb) {
     __shared__ __align__(16) int8_t lds[kGramRing * kGramSlotBytes];
     // XCD-aware block order (1-D grid of nhb iteration blocks x pairs): workgroups go to the 8
     // XCDs round-robin by linear id, so XCD x takes the contiguous logical range
@@ -707,18 +730,25 @@ __global__ __launch_bounds__(256, 3) void gram_mfma_kernel(const int32_t* __rest
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;
-    const int hb = (lbk % nhb) * 128;
+    const int hb = (lbk % nhb) * kGramIters;
     if (hb >= iters) return;  // uniform over the block
     const int nb = (M - 1) / 31 + 1;
     const int nsteps = (nb + kGramWords - 1) / kGramWords;  // words read: <= 2 nsteps - 1 <= nb < nbw
     const int h0 = hb + wv * 32;
     const int r = lane & 31, hh = lane >> 5;
     const int8_t* lg = limbs + (size_t)p * nbw * kGramWordBytes + lane * 16;
-    // waves 0, 1 move limb pieces 4 wv .. 4 wv + 3 and selection word wv; waves 2, 3 move limb
-    // pieces 8 + 3 (wv - 2) .. + 2 and selection word wv (word (wv >> 1), 64-iteration chunk
-    // (wv & 1); chunks past the last iteration are clamped: their rows are never stored)
-    const int lp0 = wv < 2 ? 4 * wv : 8 + 3 * (wv - 2);
-    const int chunk = min((hb >> 6) + (wv & 1), nwaves - 1);
+    // wave wv moves limb pieces gram_piece0(wv) .. + gram_pieces_of(wv) - 1 and the selection
+    // word (wv / (W/2)) of 64-iteration chunk (wv % (W/2)) (chunks past the last iteration are
+    // clamped: their rows are never stored)
+    constexpr int kChunks = kGramWaves / 2;
+    const int lp0 = [&] {
+        int v = 0;
+#pragma unroll
+        for (int w = 0; w < kGramWaves; w++) v = (w == wv) ? gram_piece0(w) : v;
+        return v;
+    }();
+    const bool extra = wv < kGramPieces % kGramWaves;  // moves kGramPieces / W + 1 pieces
+    const int chunk = min((hb >> 6) + (wv % kChunks), nwaves - 1);
     const uint32_t* sg = selw + ((size_t)p * nwaves + chunk) * (size_t)nbw * 64 + lane;
     const int soff = kGramSelOff + wv * 256;
     auto issue = [&](int step) {
@@ -726,14 +756,15 @@ __global__ __launch_bounds__(256, 3) void gram_mfma_kernel(const int32_t* __rest
         int8_t* slot = lds + (step % kGramRing) * kGramSlotBytes;
         const int8_t* src = lg + (size_t)sx * kGramSelOff;
 #pragma unroll
-        for (int k = 0; k < 3; k++)
+        for (int k = 0; k < kGramPieces / kGramWaves; k++)
             __builtin_amdgcn_global_load_lds((glb_vptr)(src + (lp0 + k) * 1024),
                                              (lds_vptr)(slot + (lp0 + k) * 1024), 16, 0, 0);
-        if (wv < 2)
-            __builtin_amdgcn_global_load_lds((glb_vptr)(src + (lp0 + 3) * 1024),
-                                             (lds_vptr)(slot + (lp0 + 3) * 1024), 16, 0, 0);
+        if (extra)
+            __builtin_amdgcn_global_load_lds(
+                (glb_vptr)(src + (lp0 + kGramPieces / kGramWaves) * 1024),
+                (lds_vptr)(slot + (lp0 + kGramPieces / kGramWaves) * 1024), 16, 0, 0);
         __builtin_amdgcn_global_load_lds(
-            (glb_vptr)(sg + (size_t)(sx * kGramWords + (wv >> 1)) * 64), (lds_vptr)(slot + soff),
+            (glb_vptr)(sg + (size_t)(sx * kGramWords + wv / kChunks) * 64), (lds_vptr)(slot + soff),
             4, 0, 0);
     };
     i32x16 acc[kGramTiles];
@@ -745,34 +776,46 @@ __global__ __launch_bounds__(256, 3) void gram_mfma_kernel(const int32_t* __rest
     for (int k = 0; k < kGramRing - 1; k++) issue(k);
     const int boff = r * 32 + (((hh ^ (r >> 3)) & 1) << 4);
     for (int st = 0; st < nsteps; st++) {
-        // step st's DMAs retired: the kGramRing - 2 later steps (5 or 4 per step) may fly
+        // step st's DMAs retired: the kGramRing - 2 later steps may fly (pieces + 1 each)
         static_assert(kGramRing == 3, "vmcnt counts");
-        if (wv < 2) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        constexpr int kBase = kGramPieces / kGramWaves + 1;
+        if (extra) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBase + 1) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBase) : "memory");
         __builtin_amdgcn_s_barrier();
         issue(st + kGramRing - 1);  // into the slot every wave finished reading in step st - 1
         const int8_t* slot = lds + (st % kGramRing) * kGramSlotBytes;
-        uint32_t wsel[kGramWords];
+        // every B fragment of the step in flight at once (the MFMAs then wait on counted
+        // lgkmcnts): the step's LDS latency is exposed once, not once per fragment pair
+        i32x4 bf[kGramWords][kGramTiles];
 #pragma unroll
         for (int i = 0; i < kGramWords; i++)
-            wsel[i] = reinterpret_cast<const uint32_t*>(slot + kGramSelOff)[i * 128 + wv * 32 + r];
+#pragma unroll
+            for (int t = 0; t < kGramTiles; t++)
+                bf[i][t] = *reinterpret_cast<const i32x4*>(slot + i * kGramWordBytes +
+                                                           t * 32 * 32 + boff);
+        uint32_t wsel[kGramWords];  // read after the fragments: one wait covers the step
+#pragma unroll
+        for (int i = 0; i < kGramWords; i++)
+            wsel[i] = reinterpret_cast<const uint32_t*>(slot + kGramSelOff)[i * kGramIters + wv * 32 + r];
+        i32x4 a[kGramWords];
 #pragma unroll
         for (int i = 0; i < kGramWords; i++) {
-            i32x4 bf[kGramTiles];
-#pragma unroll
-            for (int t = 0; t < kGramTiles; t++)
-                bf[t] = *reinterpret_cast<const i32x4*>(slot + i * kGramWordBytes + t * 32 * 32 +
-                                                        boff);
             const uint32_t wm = (st * kGramWords + i < nb) ? 0xffffu : 0u;  // words past nb
             const uint32_t bits = (wsel[i] >> (16 * hh)) & wm;
-            i32x4 a;
 #pragma unroll
             for (int v = 0; v < 4; v++)
-                a[v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
+                a[i][v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
+        }
+#if ERP_GRAM_SCHED
+        __builtin_amdgcn_sched_group_barrier(0x100, kGramWords * (kGramTiles + 1), 0);  // LDS reads
+        __builtin_amdgcn_sched_group_barrier(0x002, 4 * kGramWords * 4, 0);            // VALU
+        __builtin_amdgcn_sched_group_barrier(0x008, kGramWords * kGramTiles, 0);       // MFMAs
+#endif
+#pragma unroll
+        for (int i = 0; i < kGramWords; i++)
 #pragma unroll
             for (int t = 0; t < kGramTiles; t++)
-                acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf[t], acc[t], 0, 0, 0);
-        }
+                acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], bf[i][t], acc[t], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's tail DMAs
     // recombine: row = (k & 3) + 8 (k >> 2) + 4 hh; entry r from tiles 0..5 of this lane,
@@ -2422,8 +2465,8 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
     const int nwaves = (sh.iters + 63) / 64;
     hipLaunchKernelGGL(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
                        pts, sh.max_nq, sh.sel_words, limbs);
-    const int nhb = (sh.iters + 127) / 128;
-    hipLaunchKernelGGL(gram_mfma_kernel, dim3(nhb * sh.n_pairs), dim3(256), 0, st, counts, limbs,
+    const int nhb = (sh.iters + kGramIters - 1) / kGramIters;
+    hipLaunchKernelGGL(gram_mfma_kernel, dim3(nhb * sh.n_pairs), dim3(64 * kGramWaves), 0, st, counts, limbs,
                        selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb);
     if (samples)
         hipLaunchKernelGGL(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
