@@ -78,6 +78,7 @@ struct erp_ctx {
     std::vector<hipEvent_t> ev_pool;
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
+    DevBuf mblk;              // knn2_merge's per-block survivor counts
     DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
         rtab, limbs, tsplit, ovf, remap_scr, vchunk;
@@ -229,7 +230,7 @@ erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
 erp_status erp_ctx_destroy(erp_ctx* ctx) {
     if (!ctx) return ERP_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    DevBuf* all[] = {&ctx->part, &ctx->part1, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->edges, &ctx->gfin,
+    DevBuf* all[] = {&ctx->mblk, &ctx->part, &ctx->part1, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->edges, &ctx->gfin,
                      &ctx->matches,
                      &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
                      &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
@@ -282,6 +283,7 @@ erp::BatchShape make_shape(int n_pairs, int max_nq, int max_nt, int iters, doubl
 bool ensure_matcher(erp_ctx* c, const erp::BatchShape& sh) {
     const size_t PQ = (size_t)sh.n_pairs * sh.max_nq;
     const size_t fold = PQ * sizeof(erp::Top2);
+    if (!ensure(c->mblk, erp::knn2_merge_scratch_bytes(sh))) return false;
     if (c->matcher == ERP_MATCHER_VALU_EXACT)
         return ensure(c->part, PQ * sh.xchunks * sizeof(erp::Top2)) && ensure(c->part1, fold);
     return ensure(c->part, PQ * sh.fchunks * sizeof(erp::Top2)) && ensure(c->part1, fold) &&
@@ -305,7 +307,7 @@ erp_status fold_and_merge(erp_ctx* ctx, const int64_t* oq, const int64_t* ot,
     }
     // a single chunk spanning the whole train set
     ERP_CK(erp::launch_knn2_merge(part, oq, ot, sh, sh.max_nt, 1, ratio, matches, counts, flags,
-                                  st));
+                                  (int32_t*)ctx->mblk.p, st));
     return ERP_OK;
 }
 

@@ -84,10 +84,11 @@ hipError_t launch_knn2_fold(const Top2* part, const int64_t* off_q, const int64_
                             hipStream_t st);
 // fold of per-chunk partials part[pairs][chunks][max_nq] (chunk c = train rows
 // [c*chunk_len, (c+1)*chunk_len)), ratio test, compaction
+size_t knn2_merge_scratch_bytes(const BatchShape& sh);
 hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
                              const BatchShape& sh, int chunk_len, int chunks, float ratio,
                              erp_dmatch* matches, int32_t* counts, int32_t* flags,
-                             hipStream_t st);
+                             int32_t* bcount, hipStream_t st);
 hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t* counts,
                                         const erp_point2f* kp_l, const erp_point2f* kp_r,
                                         const int64_t* off_l, const int64_t* off_r,

@@ -772,7 +772,7 @@ __global__ __launch_bounds__(256) void knn2_fold_kernel(const Top2* __restrict__
 
 // Fold chunk partials in train order (lowest index wins ties), apply the ratio test
 // d0 < ratio * d1 on the sqrt'd distances (convertToDMatches + feature_matcher.cpp:52), and
-// compact the survivors in ascending queryIdx order.  One block (1024 threads) per pair.
+// compact the survivors in ascending queryIdx order (knn2_merge_count / knn2_merge below).
 __device__ __forceinline__ void merge_query(const Top2* part, size_t stride, int nch, int q,
                                             float& B0, int& J, float& B1) {
     B0 = kInf;
@@ -790,49 +790,87 @@ __device__ __forceinline__ void merge_query(const Top2* part, size_t stride, int
     }
 }
 
-__global__ __launch_bounds__(1024) void knn2_merge_kernel(const Top2* __restrict__ part,
-                                                          const int64_t* __restrict__ off_q,
-                                                          const int64_t* __restrict__ off_t,
-                                                          int chunk_len, int chunks, int max_nq,
-                                                          float ratio, erp_dmatch* __restrict__ out,
-                                                          int32_t* __restrict__ counts,
-                                                          int32_t* __restrict__ flags) {
+// Two passes over (pair, block of 1024 queries): the survivors of each block counted, then
+// each block places its survivors at (the counts of the pair's earlier blocks) + (its own
+// exclusive scan) -- ascending queryIdx, one query per thread, coalesced partial reads, and
+// the whole grid busy for a single large pair (configs[3]: 16 blocks for 16384 queries).
+constexpr int kMergeBlock = 1024;
+
+__device__ __forceinline__ bool merge_one(const Top2* pp, int max_nq, int nch, int q, int nq,
+                                          float ratio, int& J, float& d0) {
+    if (q >= nq) return false;
+    float B0, B1;
+    merge_query(pp, (size_t)max_nq, nch, q, B0, J, B1);
+    d0 = __builtin_sqrtf(B0);
+    const float d1 = __builtin_sqrtf(B1);
+    return d0 < ratio * d1;
+}
+
+__global__ __launch_bounds__(kMergeBlock) void knn2_merge_count_kernel(
+    const Top2* __restrict__ part, const int64_t* __restrict__ off_q,
+    const int64_t* __restrict__ off_t, int chunk_len, int chunks, int max_nq, float ratio,
+    int32_t* __restrict__ bcount) {
     __shared__ int ws[16];
-    const int p = blockIdx.x;
+    const int p = blockIdx.y, b = blockIdx.x;
+    const int nq = (int)(off_q[p + 1] - off_q[p]);
+    const int nt = (int)(off_t[p + 1] - off_t[p]);
+    if (nt < 2 || b * kMergeBlock >= nq) return;  // uniform over the block
+    const int nch = (nt + chunk_len - 1) / chunk_len;
+    int J;
+    float d0;
+    const bool keep = merge_one(part + (size_t)p * chunks * max_nq, max_nq, nch,
+                                b * kMergeBlock + (int)threadIdx.x, nq, ratio, J, d0);
+    int total;
+    (void)block_exclusive_scan<kMergeBlock>(keep ? 1 : 0, ws, &total);
+    if (threadIdx.x == 0) bcount[(size_t)p * gridDim.x + b] = total;
+}
+
+__global__ __launch_bounds__(kMergeBlock) void knn2_merge_kernel(
+    const Top2* __restrict__ part, const int64_t* __restrict__ off_q,
+    const int64_t* __restrict__ off_t, int chunk_len, int chunks, int max_nq, float ratio,
+    const int32_t* __restrict__ bcount, erp_dmatch* __restrict__ out,
+    int32_t* __restrict__ counts, int32_t* __restrict__ flags) {
+    __shared__ int ws[16];
+    __shared__ int base_s;
+    const int p = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
     const int nq = (int)(off_q[p + 1] - off_q[p]);
     const int nt = (int)(off_t[p + 1] - off_t[p]);
     if (nt < 2 || nq <= 0) {
-        if (threadIdx.x == 0) {
+        if (b == 0 && threadIdx.x == 0) {
             counts[p] = 0;
             if (nq > 0) flags[p] |= 1;  // knn_matches[i][1] would not exist (UB in the reference)
         }
         return;
     }
+    const int nqb = (nq + kMergeBlock - 1) / kMergeBlock;  // this pair's live blocks
+    if (b >= nqb) return;
+    if (threadIdx.x < 64) {  // the pair's earlier blocks (and, for the last one, all of them)
+        const int32_t* bc = bcount + (size_t)p * nb;
+        int pre = 0, all = 0;
+        for (int k = threadIdx.x; k < nqb; k += 64) {
+            const int c = bc[k];
+            pre += k < b ? c : 0;
+            all += c;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            pre += __shfl_xor(pre, o, 64);
+            all += __shfl_xor(all, o, 64);
+        }
+        if (threadIdx.x == 0) {
+            base_s = pre;
+            if (b == nqb - 1) counts[p] = all;
+        }
+    }
     const int nch = (nt + chunk_len - 1) / chunk_len;
-    const Top2* pp = part + (size_t)p * chunks * max_nq;
-    const int per = (nq + 1023) / 1024;
-    const int qa = min(nq, (int)threadIdx.x * per), qb = min(nq, qa + per);
-    int cnt = 0;
-    for (int q = qa; q < qb; q++) {
-        float B0, B1;
-        int J;
-        merge_query(pp, (size_t)max_nq, nch, q, B0, J, B1);
-        const float d0 = __builtin_sqrtf(B0), d1 = __builtin_sqrtf(B1);
-        cnt += (d0 < ratio * d1) ? 1 : 0;
-    }
+    const int q = b * kMergeBlock + (int)threadIdx.x;
+    int J = 0;
+    float d0 = 0.f;
+    const bool keep = merge_one(part + (size_t)p * chunks * max_nq, max_nq, nch, q, nq, ratio, J, d0);
     int total;
-    int pos = block_exclusive_scan<1024>(cnt, ws, &total);
-    erp_dmatch* o = out + (size_t)p * max_nq;
-    for (int q = qa; q < qb; q++) {
-        float B0, B1;
-        int J;
-        merge_query(pp, (size_t)max_nq, nch, q, B0, J, B1);
-        const float d0 = __builtin_sqrtf(B0), d1 = __builtin_sqrtf(B1);
-        if (d0 < ratio * d1) o[pos++] = erp_dmatch{q, J, 0, d0};
-    }
-    if (threadIdx.x == 0) counts[p] = total;
+    const int pos = block_exclusive_scan<kMergeBlock>(keep ? 1 : 0, ws, &total);  // syncs base_s
+    if (keep) out[(size_t)p * max_nq + base_s + pos] = erp_dmatch{q, J, 0, d0};
 }
-
 
 __global__ void set_i32_kernel(int32_t* p, int32_t v) { *p = v; }
 
@@ -922,12 +960,20 @@ hipError_t launch_knn2_fold(const Top2* part, const int64_t* off_q, const int64_
     return hipGetLastError();
 }
 
+size_t knn2_merge_scratch_bytes(const BatchShape& sh) {
+    return (size_t)sh.n_pairs * ((sh.max_nq + kMergeBlock - 1) / kMergeBlock) * sizeof(int32_t) + 4;
+}
+
 hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
                              const BatchShape& sh, int chunk_len, int chunks, float ratio,
                              erp_dmatch* matches, int32_t* counts, int32_t* flags,
-                             hipStream_t st) {
-    hipLaunchKernelGGL(knn2_merge_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, part, off_q, off_t,
-                       chunk_len, chunks, sh.max_nq, ratio, matches, counts, flags);
+                             int32_t* bcount, hipStream_t st) {
+    const dim3 grid(std::max(1, (sh.max_nq + kMergeBlock - 1) / kMergeBlock), sh.n_pairs);
+    hipLaunchKernelGGL(knn2_merge_count_kernel, grid, dim3(kMergeBlock), 0, st, part, off_q, off_t,
+                       chunk_len, chunks, sh.max_nq, ratio, bcount);
+    hipLaunchKernelGGL(knn2_merge_kernel, grid, dim3(kMergeBlock), 0, st, part, off_q, off_t,
+                       chunk_len, chunks, sh.max_nq, ratio, (const int32_t*)bcount, matches, counts,
+                       flags);
     return hipGetLastError();
 }
 
