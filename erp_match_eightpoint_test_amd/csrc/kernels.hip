@@ -1339,7 +1339,10 @@ constexpr int kSubBits = 10;          // 1024 sub-bins per bin (refine / exact p
 constexpr int kNS = 1 << kSubBits;
 constexpr int kLowBits = kBinShift - kSubBits;  // ... and below them the exact values
 constexpr int kRefineRows = 4;        // rows per refine block
-constexpr int kRefineMin = 32;   // survivors per pair below which refining does not pay
+#ifndef ERP_REFINE_MIN
+#define ERP_REFINE_MIN 32
+#endif
+constexpr int kRefineMin = ERP_REFINE_MIN;  // survivors per pair below which refining does not pay
 
 // first s-binade of the bins: the 40 binades ending with the one holding D^2 (D = dscale is
 // the bounding-box diagonal rounded up, >= every distance, so every s <= D^2)
@@ -1699,9 +1702,12 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const int i = ii[h];
-        const bool pruned = active[h] && pr[h];
+        // list mode: a survivor whose own (first-pass) LB already exceeds the refined U cannot
+        // be the argmin either (T_i >= LB_i > U >= min T: not even a tie) -- no refine needed
+        const bool above = SL && prune_on && active[h] && LBp[i] > U * (1.0 + 1e-5);
+        const bool pruned = active[h] && (pr[h] || above);
         if (pruned) {
-            LBp[i] = U * (1.0 + 5e-6);
+            LBp[i] = SL ? fmax(LBp[i], U * (1.0 + 5e-6)) : U * (1.0 + 5e-6);
             UBp[i] = __builtin_huge_val();
         }
         const bool keep = active[h] && !pr[h];
@@ -1758,7 +1764,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     auto srow = [&](int k) { return (int)S[(size_t)k * step]; };
     float xi[kRefineRows], yi[kRefineRows], zi[kRefineRows];
     int ba[kRefineRows], bb[kRefineRows];
-    double acc[kRefineRows];
+    float acc[kRefineRows];  // per-thread partial sums (<= ceil(K/256) terms; bracketed below)
     int bel_a[kRefineRows], bel_b[kRefineRows];
 #pragma unroll
     for (int t = 0; t < kRefineRows; t++) {
@@ -1769,7 +1775,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
         zi[t] = Z[row];
         ba[t] = bsel[((size_t)p * stride + row) * 2] + base;   // as key >> kBinShift
         bb[t] = bsel[((size_t)p * stride + row) * 2 + 1] + base;
-        acc[t] = 0.0;
+        acc[t] = 0.f;
         bel_a[t] = 0;
         bel_b[t] = 0;
     }
@@ -1789,9 +1795,10 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
             const int e = (int)(key >> kBinShift);
             bel_a[t] += e < ba[t];
             bel_b[t] += e < bb[t];
-            if (e > ba[t] && e < bb[t]) {
-                acc[t] += (double)__builtin_amdgcn_sqrtf(s);  // raw v_sqrt_f32, <= 1 ulp
-            } else if (e == ba[t] || e == bb[t]) {
+            // branch-free inner sum (raw v_sqrt_f32, <= 1 ulp; f32 accumulation) -- only the
+            // boundary-bin counts take a (short, divergent) branch
+            acc[t] += (e > ba[t] && e < bb[t]) ? __builtin_amdgcn_sqrtf(s) : 0.f;
+            if (e == ba[t] || e == bb[t]) {
                 const int r = (lane + t) & (kRefineRows - 1);
                 atomicAdd(&sub[r][e == ba[t] ? 0 : 1][(key >> kLowBits) & (kNS - 1u)], 1u);
             }
@@ -1800,7 +1807,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
 #pragma unroll
     for (int t = 0; t < kRefineRows; t++) {
         const int r = (lane + t) & (kRefineRows - 1);
-        atomicAdd(&inner[r], acc[t]);
+        atomicAdd(&inner[r], (double)acc[t]);
         atomicAdd(&below[r][0], bel_a[t]);
         atomicAdd(&below[r][1], bel_b[t]);
     }
@@ -1814,12 +1821,10 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     const int cA = below[r][0], cB = below[r][1];
     // sub-bin k of bin b (as key >> kBinShift) covers keys [((b << kSubBits) | k) << kLowBits,
     // + 2^kLowBits)
+    // (k = 1024 is sub-bin 0 of bin b + 1: every d in sub-bin k is <= sub_lo(b, k + 1), as
+    // sqrtf is monotone)
     auto sub_lo = [&](int b, int k) {
-        return (double)__builtin_sqrtf(__uint_as_float((uint32_t)((b << kSubBits) | k) << kLowBits));
-    };
-    auto sub_hi = [&](int b, int k) {
-        return (double)__builtin_sqrtf(__uint_as_float(
-            ((uint32_t)((b << kSubBits) | k) << kLowBits) + ((1u << kLowBits) - 1u)));
+        return (double)__builtin_sqrtf(__uint_as_float((uint32_t)((b << kSubBits) + k) << kLowBits));
     };
     // the window's ranks inside bin A: [max(lo, cA), min(hi, cA + nA)); inside bin B (when
     // distinct): [cB, hi).  Count per sub-bin, clipped to those rank ranges, times the
@@ -1856,9 +1861,9 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
                 const int k = 16 * sl + q;
                 const int n = (int)hh[k];
                 const int a0 = max(cum, lo), a1 = min(cum + n, hi);
-                if (a1 > a0) {
+                if (a1 > a0) {  // (only the sub-bins the rank window overlaps)
                     L += (double)(a1 - a0) * sub_lo(b, k);
-                    U += (double)(a1 - a0) * sub_hi(b, k);
+                    U += (double)(a1 - a0) * sub_lo(b, k + 1);
                 }
                 cum += n;
             }
@@ -1872,9 +1877,12 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     if (sl == 0 && ok) {
         const double w = (double)(hi - lo);
         const double in = inner[r];
-        // the inner sum used the raw v_sqrt_f32 (<= 2^-23 relative, flushes below 2^-126):
-        // bracket it by 2^-22 relative plus 2^-63 per term (the inner count is at most K)
-        const double inl = in * (1.0 - 0x1p-22), inu = in * (1.0 + 0x1p-22) + (double)K * 0x1p-63;
+        // the inner sum used the raw v_sqrt_f32 (<= 2^-23 relative, flushes below 2^-126) and
+        // per-thread f32 sums of n <= ceil(K/256) non-negative terms (relative error <= n 2^-24,
+        // then exact enough in fp64): bracket it by 2^-22 + (n + 1) 2^-24 relative plus 2^-63
+        // per term (the inner count is at most K)
+        const double rel = 0x1p-22 + (double)((K + 255) / 256 + 1) * 0x1p-24;
+        const double inl = in * (1.0 - rel), inu = in * (1.0 + rel) + (double)K * 0x1p-63;
         const double nl = ((inl + L) / w) * (1.0 - 1e-9), nu = ((inu + U) / w) * (1.0 + 1e-9);
         double* lp = lb + (size_t)p * stride + row;
         double* up = ub + (size_t)p * stride + row;
