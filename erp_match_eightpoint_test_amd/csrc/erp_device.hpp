@@ -763,6 +763,60 @@ ERP_HD ERP_INLINE void gram_ldlt9(const double* g36, int stride, int h, double m
 // step after the iterate moves by < 1e-12 and the vector is then at rounding level.  A lane
 // whose iterate has not settled after kInvIt steps (near-degenerate lambda_1 ~ lambda_2) takes
 // the Jacobi path (eigenvalue shift + inverse iteration, gram_min_eigvec9_jacobi).
+// The inverse-iteration part alone (the device kernel runs the Jacobi fallback in a second,
+// rarely busy kernel so that its registers do not size the common one): false = not settled.
+// D is kept as 1/D on the diagonal of S (the solves only multiply by it).
+ERP_HD ERP_INLINE bool gram_min_eigvec9_inv(const double* g36, int stride, int h, double* e) {
+    constexpr int kInvIt = 10;
+    double S[45];
+    double tr = 0;
+#pragma unroll
+    for (int i = 0; i < 9; i++) tr += g36[(6 * sym3(i / 3, i / 3) + sym3(i % 3, i % 3)) * stride + h];
+    const double tiny = kDblEps * (tr > 0 ? tr : 1.0);
+    gram_ldlt9(g36, stride, h, -16 * tiny, tiny * 1e-3, S);
+#pragma unroll
+    for (int i = 0; i < 9; i++) S[ut9(i, i)] = 1.0 / S[ut9(i, i)];
+    double x[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) x[i] = 1.0 / 3.0;
+    int settled = -1;  // step at which the iterate stopped moving
+    for (int it = 0; it < kInvIt; it++) {
+        double y[9];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {  // L y = x
+            double v = x[i];
+#pragma unroll
+            for (int k = 0; k < i; k++) v -= S[ut9(k, i)] * y[k];
+            y[i] = v;
+        }
+#pragma unroll
+        for (int i = 0; i < 9; i++) y[i] *= S[ut9(i, i)];
+#pragma unroll
+        for (int i = 8; i >= 0; i--)  // L^T z = y
+#pragma unroll
+            for (int k = i + 1; k < 9; k++) y[i] -= S[ut9(i, k)] * y[k];
+        double nrm = 0, dot = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            nrm += y[i] * y[i];
+            dot += y[i] * x[i];
+        }
+        const double inv = (dot < 0 ? -1.0 : 1.0) / sqrt(nrm);  // keep the sign: no flip-flop
+        double dlt = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            const double v = y[i] * inv;
+            dlt = fmax(dlt, fabs(v - x[i]));
+            x[i] = v;
+        }
+        if (settled >= 0) break;     // one more step after settling
+        if (dlt < 1e-12) settled = it;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++) e[i] = x[i];
+    return settled >= 0;
+}
+
 ERP_HD inline void gram_min_eigvec9(const double* g36, int stride, int h, double* e) {
     constexpr int kInvIt = 10;
     double S[45];

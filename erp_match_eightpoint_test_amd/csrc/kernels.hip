@@ -921,15 +921,39 @@ __global__ __launch_bounds__(64) void eigen_kernel(const int32_t* __restrict__ c
         for (int k = 0; k < 36; k++) g36[k] = gi[(size_t)k * iters];
         gram36_to_full(g36, G);
         gram_jacobi9(G, s, e);
-    } else {
-        gram_min_eigvec9(gi, iters, 0, e);
+    } else if (!gram_min_eigvec9_inv(gi, iters, 0, e)) {
+        e[0] = __builtin_nan("");  // not settled: eigen_fallback_kernel takes the Jacobi path
     }
     double* eo = evec + (size_t)p * 9 * iters + h;
 #pragma unroll
     for (int k = 0; k < 9; k++) eo[(size_t)k * iters] = e[k];
 }
 
-__global__ __launch_bounds__(64) void estimate_kernel(const int32_t* __restrict__ counts,
+// the lanes whose inverse iteration did not settle (near-degenerate lambda_1 ~ lambda_2; rare):
+// eigenvalue shift by cyclic Jacobi, then inverse iteration (gram_min_eigvec9_jacobi)
+__global__ __launch_bounds__(64) void eigen_fallback_kernel(const int32_t* __restrict__ counts,
+                                                            const double* __restrict__ gram,
+                                                            int iters, double sample_frac,
+                                                            double* __restrict__ evec) {
+    const int p = blockIdx.y;
+    const int h = blockIdx.x * 64 + threadIdx.x;
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 9 || h >= iters) return;
+    double* eo = evec + (size_t)p * 9 * iters + h;
+    if (!__builtin_isnan(eo[0])) return;
+    double e[9];
+    gram_min_eigvec9_jacobi(gram + (size_t)p * 36 * iters + h, iters, 0, e);
+#pragma unroll
+    for (int k = 0; k < 9; k++) eo[(size_t)k * iters] = e[k];
+}
+
+#ifdef ERP_EST_WAVES
+#define ERP_EST_ATTR __attribute__((amdgpu_waves_per_eu(ERP_EST_WAVES)))
+#else
+#define ERP_EST_ATTR
+#endif
+__global__ __launch_bounds__(64) ERP_EST_ATTR void estimate_kernel(const int32_t* __restrict__ counts,
                                                       const double* __restrict__ evec, int iters,
                                                       double sample_frac, double valid_abs,
                                                       erp_hypothesis* __restrict__ hyps) {
@@ -2492,6 +2516,8 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
                         hipStream_t st) {
     dim3 grid((sh.iters + 63) / 64, sh.n_pairs);
     hipLaunchKernelGGL(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters,
+                       sample_frac, evec);
+    hipLaunchKernelGGL(eigen_fallback_kernel, grid, dim3(64), 0, st, counts, gram, sh.iters,
                        sample_frac, evec);
     // (M is only known on the device: the thin instantiation returns at once for s >= 9)
     hipLaunchKernelGGL(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters,
