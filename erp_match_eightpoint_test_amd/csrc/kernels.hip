@@ -1633,6 +1633,10 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(
 #define ERP_LIP_STEP 16
 #endif
 constexpr int kLipStep = ERP_LIP_STEP;  // every 16th row is a reference row
+#ifndef ERP_REF_STEP
+#define ERP_REF_STEP 16
+#endif
+constexpr int kRefStep = ERP_REF_STEP;  // every 16th survivor is refined first (refine pass)
 constexpr int kLipMinK = 1024;  // smaller sets: no pre-pruning (every non-reference row listed)
 constexpr int kLipChunk = 1024; // reference rows staged in LDS per chunk
 
@@ -1641,7 +1645,7 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     double trim_hi, double* __restrict__ lb, double* __restrict__ ub,
     const int32_t* __restrict__ slist, const int32_t* __restrict__ scount,
     int32_t* __restrict__ rlist, int olstride, int32_t* __restrict__ rcount, int shard,
-    int nshards) {
+    int nshards, int lstep) {
     // slist == nullptr: the rows [ra, rb) of row shard `shard` of `nshards` (all K rows when
     // unsharded) before the histogram pass, against that shard's own reference rows ra, ra + 16,
     // ... (configs[4]'s row-sharded consensus: U is then the shard's smallest reference UB, still
@@ -1666,11 +1670,11 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     double* LBp = lb + (size_t)p * stride;
     double* UBp = ub + (size_t)p * stride;
     const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
-    const int nref = (n + kLipStep - 1) / kLipStep;
+    const int nref = (n + lstep - 1) / lstep;  // every lstep-th position is a reference
     bool prune_on = (SL ? n > kRefineMin : K >= kLipMinK) && hi > lo;
     double U = __builtin_huge_val();
     if (prune_on) {
-        for (int c = tid; c < nref; c += 256) U = fmin(U, UBp[rowpos(c * kLipStep)]);
+        for (int c = tid; c < nref; c += 256) U = fmin(U, UBp[rowpos(c * lstep)]);
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) U = fmin(U, __shfl_xor(U, o, 64));
         if (lane == 0) red[tid >> 6] = U;
@@ -1684,7 +1688,7 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const int k = i0 + 256 * h + tid;
-        active[h] = k < n && (k % kLipStep) != 0;
+        active[h] = k < n && (k % lstep) != 0;
         ii[h] = active[h] ? rowpos(k) : 0;
         xi[h] = active[h] ? X[ii[h]] : 0.f;
         yi[h] = active[h] ? Y[ii[h]] : 0.f;
@@ -1701,7 +1705,7 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
             __syncthreads();
             // only references with LB_c > U (1 + 1e-5) can prune: compacted (any order)
             for (int c = tid; c < nc; c += 256) {
-                const int row = rowpos((c0 + c) * kLipStep);
+                const int row = rowpos((c0 + c) * lstep);
                 const double a = LBp[row] * (1.0 - 1e-5) - Um;
                 if (a > 0.0) {
                     const float thr = (float)(a * a * (1.0 - 1e-5));
@@ -2583,7 +2587,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((srows + 511) / 512, sh.n_pairs),
                        dim3(256), 0, st, kcount, rv, stride, trim_lo, trim_hi, lb, ub,
                        (const int32_t*)nullptr, (const int32_t*)nullptr, rlist, stride, rcount,
-                       shard, nshards);
+                       shard, nshards, kLipStep);
     int32_t* uoff = rcount + sh.n_pairs;  // [n_pairs + 1] after the counts
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)rcount,
                        sh.n_pairs, kBoundRows, 0, uoff);
@@ -2615,18 +2619,18 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
     const int P = sh.n_pairs, stride = 2 * sh.iters, l2stride = sortbuf_len(sh.iters);
     int32_t* uoff = const_cast<int32_t*>(nsurv) + 2 * P;
     int32_t* n2 = uoff + P + 1;
-    // (A) the reference survivors (every kLipStep-th) of pairs with > kRefineMin survivors
+    // (A) the reference survivors (every kRefStep-th) of pairs with > kRefineMin survivors
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, P,
-                       kRefineRows * kLipStep, kRefineMin, uoff);
+                       kRefineRows * kRefStep, kRefineMin, uoff);
     hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
                        stride, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, surv, stride,
-                       (const int32_t*)nullptr, kLipStep, (const int32_t*)uoff, P);
+                       (const int32_t*)nullptr, kRefStep, (const int32_t*)uoff, P);
     // (B) Lipschitz pruning of the other survivors against the refined references
     const hipError_t me = hipMemsetAsync(n2, 0, sizeof(int32_t) * P, st);
     if (me != hipSuccess) return me;
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, P), dim3(256), 0, st,
                        kcount, rv, stride, trim_lo, trim_hi, lb, ub, surv, nsurv, list2, l2stride,
-                       n2, 0, 1);
+                       n2, 0, 1, kRefStep);
     // (C) the survivors the references did not prune
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)n2, P,
                        kRefineRows, 0, uoff);
