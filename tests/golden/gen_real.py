@@ -13,7 +13,17 @@
   features -- not pixel values).  The pairing output_20200423 <-> *_building.jpg was checked:
   the rectified left image differs from left_building.jpg resized to 2048 x 1024 by 14.0 grey
   levels on average, from left_building2.jpg by 42.8 (output_20200423_2 <-> building2: 10.2 /
-  40.7; right_building2.jpg is not in the reference, so only the first pair is usable).
+  40.7).
+* tests/golden/real/ref_rectified_left.png, ref_rectified_left_vertical.png: the reference's
+  own rectified left image of that pair and its vertical view (src/automatic.cpp:148-157:
+  rotate_image by eular2rot(89.999 deg, 0, 0).inv(), then cv::rotate 90 degrees clockwise),
+  copied byte for byte (lossless PNG): the vertical view of the first is the second, pixel for
+  pixel, except the pixels the reference never writes (uninitialised memory in its output).
+* tests/golden/real/left_building2_2048.jpg, right_building2_2048.jpg: the second pair of the
+  reference's data (build/*_building2.jpg, the pair its config_file.ini names), resized to the
+  pipeline's 2048 x 1024 (resize_input, config_file.ini) with PIL's bilinear filter and
+  stored as JPEG quality 95; ref_rectified_{left,right}_2.jpg: the reference's automatic
+  output on that pair (output_20200423_2, re-encoded as JPEG quality 95).
 * tests/golden/real/MANIFEST.json: sha256 of every source and output file.
 """
 from __future__ import annotations
@@ -46,8 +56,21 @@ def main():
         dst = os.path.join(OUT, f"ref_rectified_{side}.jpg")
         Image.open(src).convert("RGB").save(dst, quality=95, subsampling=0)
         man["sources"][f"output_20200423/rectified_{side}.png"] = sha(src)
+    for name in ("rectified_left.png", "rectified_left_vertical.png"):
+        src = os.path.join(REF, "output_20200423", name)
+        shutil.copyfile(src, os.path.join(OUT, "ref_" + name))
+        man["sources"]["output_20200423/" + name] = sha(src)
+    for side in ("left", "right"):
+        src = os.path.join(REF, f"{side}_building2.jpg")
+        Image.open(src).convert("RGB").resize((2048, 1024), Image.BILINEAR).save(
+            os.path.join(OUT, f"{side}_building2_2048.jpg"), quality=95, subsampling=0)
+        man["sources"][f"{side}_building2.jpg"] = sha(src)
+        src = os.path.join(REF, "output_20200423_2", f"rectified_{side}.png")
+        Image.open(src).convert("RGB").save(os.path.join(OUT, f"ref_rectified_{side}_2.jpg"),
+                                            quality=95, subsampling=0)
+        man["sources"][f"output_20200423_2/rectified_{side}.png"] = sha(src)
     for name in sorted(os.listdir(OUT)):
-        if name.endswith(".jpg"):
+        if name.endswith(".jpg") or name.endswith(".png"):
             man["outputs"][name] = sha(os.path.join(OUT, name))
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
         json.dump(man, f, indent=1)

@@ -21,6 +21,10 @@ do_all -> eight_point::find -> rectify, src/automatic.cpp:117-145).
    80-iteration RANSAC over ITS matches, so this is a tolerance KAT, not bit parity.
 2. test_real_building_fullres_keypoints: do_all + find at the full 5376 x 2688 -- keypoint
    counts per band against the 65 535 cap of the C ABI (erp_eight_point_find: m <= 65535).
+3. test_real_building2_matches_reference_output: the same KAT on the second pair (the one the
+   reference's config_file.ini names) against output_20200423_2.
+4. test_real_vertical_view_pixel_exact: the device vertical view of the reference's rectified
+   image against the reference's own vertical view, pixel for pixel.
 """
 from __future__ import annotations
 
@@ -84,6 +88,51 @@ def test_real_fixture_manifest():
     for name, h in man["outputs"].items():
         with open(os.path.join(REAL, name), "rb") as f:
             assert hashlib.sha256(f.read()).hexdigest() == h, name
+
+
+def test_real_vertical_view_pixel_exact(api):
+    """the device vertical view (erp_vertical_rotate_dev) of the reference's own rectified
+    image equals the reference's own vertical view (rectified_left_vertical.png) at every pixel
+    the remap writes; the unwritten ones (the reference leaves them uninitialised) are found by
+    running with two fill values (measured: 1 of 2 097 152)."""
+    ss, ep, er = api
+    src = _dev(_bgr(os.path.join(REAL, "ref_rectified_left.png")))
+    want = _bgr(os.path.join(REAL, "ref_rectified_left_vertical.png"))
+    a = er.vertical_rotate(src, fill=0).cpu().numpy()
+    b = er.vertical_rotate(src, fill=255).cpu().numpy()
+    unwritten = (a != b).any(-1)
+    assert a.shape == want.shape == (2048, 1024, 3)
+    assert int(unwritten.sum()) <= 4, int(unwritten.sum())
+    bad = np.argwhere((a != want).any(-1) & ~unwritten)
+    assert len(bad) == 0, (len(bad), bad[:10])
+
+
+def _kat(api, left_name, right_name, ref_l_name, ref_r_name, size=None):
+    ss, ep, er = api
+    W, H = 2048, 1024
+    left = _dev(_bgr(os.path.join(REAL, left_name), (W, H)))
+    right = _dev(_bgr(os.path.join(REAL, right_name), (W, H)))
+    kl, kr, M, total = ss.do_all(left, right)
+    R, T = ep.find(W, H, kl.cpu().numpy(), kr.cpu().numpy())
+    assert ep.last_result["status"] == 0
+    lo, ro = er.rectify(left, right, R.astype(np.float64), T.astype(np.float64))
+    Ql, ml, el = _residual(ss, W, H, lo, _dev(_bgr(os.path.join(REAL, ref_l_name))))
+    Qr, mr, erm = _residual(ss, W, H, ro, _dev(_bgr(os.path.join(REAL, ref_r_name))))
+    rel = _angle(Ql.T @ Qr)
+    print(f"\n{left_name}: {total} left keypoints, M={M}, K={int(ep.last_result['K'])}, "
+          f"R={np.degrees(R)} deg; vs the reference's output: relative rotation {rel:.3f} deg, "
+          f"T-dependent residual {_angle(Ql):.2f} / {_angle(Qr):.2f} deg ({ml} / {mr} matches, "
+          f"fit error {el:.3f} / {erm:.3f} deg)")
+    assert ml > 100 and mr > 100 and el < 0.5 and erm < 0.5
+    return rel
+
+
+def test_real_building2_matches_reference_output(api):
+    """the pair the reference's config_file.ini names (build/*_building2.jpg, committed resized
+    to the pipeline's 2048 x 1024) against its output_20200423_2: the same geometric KAT"""
+    rel = _kat(api, "left_building2_2048.jpg", "right_building2_2048.jpg",
+               "ref_rectified_left_2.jpg", "ref_rectified_right_2.jpg")
+    assert rel < 1.5, rel
 
 
 def test_real_building_matches_reference_output(api):
