@@ -2,6 +2,7 @@
 // orchestration of the hot-path kernels on one HIP stream.  No host round trip inside a
 // pipeline run (match counts, sample sizes and hypothesis counts stay on the device).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <stdint.h>
 #include <stdlib.h>
@@ -85,6 +86,7 @@ struct erp_ctx {
     DevBuf extra[13];         // erp_ctx_scratch_internal slots (1-11 SURF, 12 viz)
     uint64_t surf_key = 0;    // (W, H, params) of the SURF layer table in extra[1]
     uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
+    bool zoom = getenv("ERP_NO_ZOOM") == nullptr;  // the consensus zoom pass (A/B knob)
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -467,6 +469,20 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     if (phase == 2)  // the bounds ran per shard (binned rows not combined): report -1
         ERP_CK(hipMemsetAsync((int32_t*)c->nsurv.p + sh.n_pairs, 0xFF, sizeof(int32_t) * sh.n_pairs, st));
     {
+        StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
+        ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, lbp,
+                                            ubp, sh, cfg->trim_lo, cfg->trim_hi,
+                                            (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, 0,
+                                            st));
+    }
+    if (c->zoom) {
+        {
+            StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
+            ERP_CK(erp::launch_consensus_zoom((int32_t*)c->kcount.p, (float*)c->rv.p,
+                                              (float*)c->dscale.p, (float*)c->edges.p, sh,
+                                              cfg->trim_lo, cfg->trim_hi, lbp, ubp, bselp,
+                                              (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, st));
+        }
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
         ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, lbp,
                                             ubp, sh, cfg->trim_lo, cfg->trim_hi,

@@ -133,6 +133,10 @@ hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, i
                                   hipStream_t st);
 // per-row [LB, UB] of the trimmed mean and the bins holding ranks lo / hi-1 (bsel[row][2])
 size_t consensus_edges_bytes(int n_pairs);
+hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const float* dscale,
+                                 float* edges, const BatchShape& sh, double trim_lo,
+                                 double trim_hi, double* lb, double* ub, const int32_t* bsel,
+                                 const int32_t* surv, int32_t* nsurv, hipStream_t st);
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,

@@ -1364,7 +1364,7 @@ constexpr int kNS = 1 << kSubBits;
 constexpr int kLowBits = kBinShift - kSubBits;  // ... and below them the exact values
 constexpr int kRefineRows = 4;        // rows per refine block
 #ifndef ERP_REFINE_MIN
-#define ERP_REFINE_MIN 32
+#define ERP_REFINE_MIN 8
 #endif
 constexpr int kRefineMin = ERP_REFINE_MIN;  // survivors per pair below which refining does not pay
 
@@ -1987,6 +1987,216 @@ __global__ __launch_bounds__(256) void consensus_bounds_list_kernel(
                           1, rlist, rcount, a, g - uoff[a]);
 }
 
+// ---- zoom: the first selection's survivors re-binned on a 4x finer grid -------------------
+// The first bounds pass bins s = d^2 at 16 bins per binade over 36 binades (any distance range);
+// its bounds are ~2 % wide in d, so ~150 rows per pair survive the first selection.  The
+// survivors' rank windows (bsel: the bins of ranks lo and hi-1) span a few binades, so a second
+// histogram pass over the survivors only, at 64 bins per binade over 9 binades placed on those
+// windows (per pair: consensus_zoom_prep), tightens LB / UB ~4x; the re-selection then keeps ~8x
+// fewer rows (T grows quadratically near its minimum) for refine / the exact pass.  The zoom
+// bins the reference's own s (rdist2: same operations, no bias), so the d-range of a bin is
+// [sqrtf(s_b), sqrtf(s_b+1)] exactly (sqrtf is monotone); keys below / above the 9 binades are
+// clamped into bins 0 / kNB-1, whose edges are 0 / +inf.  Bounds only ever tighten (LB = max,
+// UB = min with the first pass); bsel (the coarse bins refine and the exact pass use) stays.
+constexpr int kZMant = 6;                      // 64 bins per binade of s
+constexpr int kZShift = 23 - kZMant;
+constexpr int kZBinades = kNB >> kZMant;       // 9 binades: the same 576 bins (LDS layout)
+static_assert(kZBinades * (1 << kZMant) == kNB, "zoom bins");
+#ifndef ERP_ZOOM_MIN
+#define ERP_ZOOM_MIN 32
+#endif
+constexpr int kZoomMin = ERP_ZOOM_MIN;         // survivors per pair below which no zoom pass
+
+// per pair: the zoom grid's first binade zelo[p] (-1: no zoom) and its d-space edges
+__global__ __launch_bounds__(256) void consensus_zoom_prep_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ dscale,
+    const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
+    const int32_t* __restrict__ bsel, int stride, double trim_lo, double trim_hi,
+    int32_t* __restrict__ zelo, float* __restrict__ edz) {
+    __shared__ int red[2][4];
+    const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
+    const int K = kcount[p], n = nsurv[p];
+    const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
+    if (n <= kZoomMin || hi <= lo) {
+        if (tid == 0) zelo[p] = -1;
+        return;
+    }
+    int amin = 1 << 30, bmax = -1;
+    for (int k = tid; k < n; k += 256) {
+        const int row = surv[(size_t)p * stride + k];
+        amin = min(amin, bsel[((size_t)p * stride + row) * 2]);
+        bmax = max(bmax, bsel[((size_t)p * stride + row) * 2 + 1]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        amin = min(amin, __shfl_xor(amin, o, 64));
+        bmax = max(bmax, __shfl_xor(bmax, o, 64));
+    }
+    if (lane == 0) {
+        red[0][tid >> 6] = amin;
+        red[1][tid >> 6] = bmax;
+    }
+    __syncthreads();
+    amin = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
+    bmax = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+    // coarse bin b <-> s-binade elo + b / 16; the grid covers the top 9 binades of the span
+    const int elo = bounds_elo(dscale[p]);
+    const int zlo = elo + (amin >> kMantBits), zhi = elo + (bmax >> kMantBits);
+    const int z = max(max(zlo, zhi - (kZBinades - 1)), 1);
+    if (tid == 0) zelo[p] = z;
+    float* ed = edz + (size_t)p * 2 * kNB;
+    for (int b = tid; b < kNB; b += 256) {
+        const uint32_t key = (uint32_t)((z << kZMant) + b) << kZShift;
+        ed[b] = b == 0 ? 0.f : __builtin_sqrtf(__uint_as_float(key));
+        ed[kNB + b] = b == kNB - 1 ? kInf : __builtin_sqrtf(__uint_as_float(key + (1u << kZShift)));
+    }
+}
+
+// one unit (kBoundRows survivors of one pair) per block; items flattened over the pairs
+__global__ __launch_bounds__(256) void consensus_zoom_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv,
+    const float* __restrict__ edz, const int32_t* __restrict__ zelo, int stride, double trim_lo,
+    double trim_hi, double* __restrict__ lb, double* __restrict__ ub,
+    const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
+    const int32_t* __restrict__ uoff, int n_pairs) {
+    constexpr int R = kBoundRows;
+    constexpr int NS = 256 / R;
+    constexpr int per = kNB / NS;
+    __shared__ __align__(16) uint32_t hist[kNB * R];  // [bin][row]
+    int (*part)[R] = reinterpret_cast<int (*)[R]>(hist);
+    float (*partL)[R] = reinterpret_cast<float (*)[R]>(hist + NS * R);
+    float (*partU)[R] = reinterpret_cast<float (*)[R]>(hist + 2 * NS * R);
+    const int g = blockIdx.x;
+    if (g >= uoff[n_pairs]) return;
+    int p = 0, b = n_pairs;  // largest p with uoff[p] <= g
+    while (b - p > 1) {
+        const int m = (p + b) >> 1;
+        if (uoff[m] <= g) p = m; else b = m;
+    }
+    const int tid = threadIdx.x, lane = wave_lane();
+    const int K = kcount[p], nloc = nsurv[p], zb = zelo[p];
+    const int l0 = (g - uoff[p]) * R;
+    if (zb < 0 || l0 >= nloc) return;  // (uniform)
+    const int32_t* RL = surv + (size_t)p * stride;
+    const float* X = rv + (size_t)p * 3 * stride;
+    const float* Y = X + stride;
+    const float* Z = Y + stride;
+    const int zbase = zb << kZMant;
+    constexpr int kPairs = R / 2;
+    f32x2 xi[kPairs], yi[kPairs], zi[kPairs];
+    uint32_t hoff[R];
+    const uint32_t hist_addr = (uint32_t)(size_t)(lds_u32*)hist;
+#pragma unroll
+    for (int t = 0; t < R; t++) {
+        const int r = (lane + t) & (R - 1);
+        const int row = RL[min(l0 + r, nloc - 1)];
+        xi[t >> 1][t & 1] = X[row];
+        yi[t >> 1][t & 1] = Y[row];
+        zi[t >> 1][t & 1] = Z[row];
+        hoff[t] = hist_addr + 4u * (uint32_t)r;
+    }
+    for (int k = tid; k < kNB * R / 4; k += 256)
+        reinterpret_cast<uint4*>(hist)[k] = make_uint4(0u, 0u, 0u, 0u);
+    __syncthreads();
+    constexpr int CB = 4;
+    float cx[CB], cy[CB], cz[CB], nx[CB], ny[CB], nz[CB];
+    const uint32_t kmax4 = 4u * (uint32_t)(K - 1);
+    auto ld = [](const float* base, uint32_t off) {
+        return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + off);
+    };
+#pragma unroll
+    for (int c = 0; c < CB; c++) {
+        const uint32_t o = min(4u * (uint32_t)(c * 256 + tid), kmax4);
+        cx[c] = ld(X, o);
+        cy[c] = ld(Y, o);
+        cz[c] = ld(Z, o);
+    }
+    for (int j0 = 0; j0 < K; j0 += CB * 256) {
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            const uint32_t o = min(4u * (uint32_t)(j0 + CB * 256 + c * 256 + tid), kmax4);
+            nx[c] = ld(X, o);
+            ny[c] = ld(Y, o);
+            nz[c] = ld(Z, o);
+        }
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            if (j0 + c * 256 + tid < K) {
+                const float xj = cx[c], yj = cy[c], zj = cz[c];
+#pragma unroll
+                for (int t = 0; t < kPairs; t++) {
+                    // rdist2's operations and order, two rows per packed instruction
+                    const f32x2 dx = xi[t] - xj, dy = yi[t] - yj, dz = zi[t] - zj;
+                    const f32x2 s = (dx * dx + dy * dy) + dz * dz;
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int bz = min(max((int)(__float_as_uint(s[h]) >> kZShift) - zbase, 0),
+                                           kNB - 1);  // (one v_med3_i32)
+                        lds_inc(lshl6_add((uint32_t)bz, hoff[2 * t + h]));
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CB; c++) {
+            cx[c] = nx[c];
+            cy[c] = ny[c];
+            cz[c] = nz[c];
+        }
+    }
+    __syncthreads();
+    const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
+    const int r = tid & (R - 1), sl = tid / R;
+    const float* ed = edz + (size_t)p * 2 * kNB + sl * per;
+    float el[per], eu[per];
+    int n[per];
+    int c = 0;
+#pragma unroll
+    for (int q = 0; q < per; q++) {
+        el[q] = ed[q];
+        eu[q] = ed[kNB + q];
+        n[q] = (int)hist[(sl * per + q) * R + r];
+        c += n[q];
+    }
+    __syncthreads();
+    part[sl][r] = c;
+    __syncthreads();
+    int cum = 0;
+    for (int q = 0; q < sl; q++) cum += part[q][r];
+    const bool rvalid = l0 + r < nloc;
+    const int row = rvalid ? RL[l0 + r] : 0;
+    float L = 0.f, U = 0.f;
+    if (cum < hi && cum + c > lo) {
+        int c0 = min(max(cum, lo), hi);
+#pragma unroll
+        for (int q = 0; q < per; q++) {
+            const int nc = cum + n[q];
+            const int c1 = min(max(nc, lo), hi);
+            const float w = (float)(c1 - c0);
+            L = __builtin_fmaf(w, el[q], L);
+            U = w > 0.f ? __builtin_fmaf(w, eu[q], U) : U;  // (0 * inf)
+            cum = nc;
+            c0 = c1;
+        }
+    }
+    partL[sl][r] = L;
+    partU[sl][r] = U;
+    __syncthreads();
+    if (sl == 0 && rvalid) {
+        for (int q = 1; q < NS; q++) {
+            L += partL[q][r];
+            U += partU[q][r];
+        }
+        const double w = (double)(hi - lo);
+        // margins: the f32 accumulation and the reference's own rounding of its sorted
+        // sequential sum (as in the first pass)
+        double* lp = lb + (size_t)p * stride + row;
+        double* up = ub + (size_t)p * stride + row;
+        *lp = fmax(*lp, ((double)L / w) * (1.0 - 2e-4));
+        *up = fmin(*up, ((double)U / w) * (1.0 + 2e-4));
+    }
+}
+
 __global__ __launch_bounds__(256) void consensus_refine_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv,
     const float* __restrict__ dscale, int stride, double trim_lo, double trim_hi,
@@ -2555,7 +2765,29 @@ hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, i
     return hipGetLastError();
 }
 
-size_t consensus_edges_bytes(int n_pairs) { return (size_t)n_pairs * 2 * kNB * sizeof(float); }
+// [P][2][kNB] first-pass edges, [P][2][kNB] zoom edges, [P] zoom grids
+size_t consensus_edges_bytes(int n_pairs) {
+    return (size_t)n_pairs * 4 * kNB * sizeof(float) + (size_t)n_pairs * sizeof(int32_t);
+}
+
+hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const float* dscale,
+                                 float* edges, const BatchShape& sh, double trim_lo,
+                                 double trim_hi, double* lb, double* ub, const int32_t* bsel,
+                                 const int32_t* surv, int32_t* nsurv, hipStream_t st) {
+    const int P = sh.n_pairs, stride = 2 * sh.iters;
+    float* edz = edges + (size_t)P * 2 * kNB;
+    int32_t* zelo = reinterpret_cast<int32_t*>(edges + (size_t)P * 4 * kNB);
+    int32_t* uoff = nsurv + 2 * P;  // free until the refine pass (launch_consensus_refine)
+    hipLaunchKernelGGL(consensus_zoom_prep_kernel, dim3(P), dim3(256), 0, st, kcount, dscale, surv,
+                       (const int32_t*)nsurv, bsel, stride, trim_lo, trim_hi, zelo, edz);
+    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)nsurv, P,
+                       kBoundRows, kZoomMin, uoff);
+    const int max_units = P * ((stride + kBoundRows - 1) / kBoundRows);
+    hipLaunchKernelGGL(consensus_zoom_kernel, dim3(max_units), dim3(256), 0, st, kcount, rv,
+                       (const float*)edz, (const int32_t*)zelo, stride, trim_lo, trim_hi, lb, ub,
+                       surv, (const int32_t*)nsurv, (const int32_t*)uoff, P);
+    return hipGetLastError();
+}
 
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    float* edges, const BatchShape& sh, double trim_lo,
