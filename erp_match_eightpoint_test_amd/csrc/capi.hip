@@ -80,13 +80,15 @@ struct erp_ctx {
     size_t ev_used = 0;
     std::vector<std::pair<int, size_t>> ev_rec;  // (stage, index of start event; end = +1)
     DevBuf mblk;              // knn2_merge's per-block survivor counts
+    DevBuf zsel;              // consensus zoom: the survivors' rank-window bins (level 1 grid)
     DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
         rtab, limbs, tsplit, ovf, remap_scr, vchunk;
     DevBuf extra[13];         // erp_ctx_scratch_internal slots (1-11 SURF, 12 viz)
     uint64_t surf_key = 0;    // (W, H, params) of the SURF layer table in extra[1]
     uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
-    bool zoom = getenv("ERP_NO_ZOOM") == nullptr;  // the consensus zoom pass (A/B knob)
+    // consensus zoom levels (0-2; ERP_ZOOM_LEVELS, an A/B knob)
+    int zoom = getenv("ERP_ZOOM_LEVELS") ? atoi(getenv("ERP_ZOOM_LEVELS")) : 1;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -232,7 +234,7 @@ erp_status erp_ctx_create(int32_t device, erp_ctx** out) {
 erp_status erp_ctx_destroy(erp_ctx* ctx) {
     if (!ctx) return ERP_INVALID_ARG;
     (void)hipSetDevice(ctx->device);
-    DevBuf* all[] = {&ctx->mblk, &ctx->part, &ctx->part1, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->edges, &ctx->gfin,
+    DevBuf* all[] = {&ctx->mblk, &ctx->zsel, &ctx->part, &ctx->part1, &ctx->pu, &ctx->ccount, &ctx->cand, &ctx->bsel, &ctx->edges, &ctx->gfin,
                      &ctx->matches,
                      &ctx->counts, &ctx->flags, &ctx->pts, &ctx->polyR,
                      &ctx->polyQ, &ctx->idx, &ctx->gram, &ctx->hyps, &ctx->rv, &ctx->tv,
@@ -356,7 +358,7 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result)) &&
               ensure(c->dscale, P * 4) && ensure(c->lb, P * 2 * sh.iters * 8) &&
               ensure(c->ub, P * 2 * sh.iters * 8) && ensure(c->surv, P * 2 * sh.iters * 4) &&
-              ensure(c->bsel, P * 2 * sh.iters * 8) && ensure(c->edges, erp::consensus_edges_bytes((int)P)) &&
+              ensure(c->bsel, P * 2 * sh.iters * 8) && ensure(c->zsel, P * 2 * sh.iters * 8) && ensure(c->edges, erp::consensus_edges_bytes((int)P)) &&
               ensure(c->nsurv, P * 16 + 4) && ensure(c->vchunk, erp::valid_chunk_bytes(sh));
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
@@ -475,13 +477,14 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, 0,
                                             st));
     }
-    if (c->zoom) {
+    for (int level = 1; level <= c->zoom; level++) {
         {
             StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
             ERP_CK(erp::launch_consensus_zoom((int32_t*)c->kcount.p, (float*)c->rv.p,
                                               (float*)c->dscale.p, (float*)c->edges.p, sh,
                                               cfg->trim_lo, cfg->trim_hi, lbp, ubp, bselp,
-                                              (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, st));
+                                              (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
+                                              (int32_t*)c->zsel.p, level, st));
         }
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
         ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, lbp,

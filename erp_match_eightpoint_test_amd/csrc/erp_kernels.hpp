@@ -136,7 +136,8 @@ size_t consensus_edges_bytes(int n_pairs);
 hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const float* dscale,
                                  float* edges, const BatchShape& sh, double trim_lo,
                                  double trim_hi, double* lb, double* ub, const int32_t* bsel,
-                                 const int32_t* surv, int32_t* nsurv, hipStream_t st);
+                                 const int32_t* surv, int32_t* nsurv, int32_t* zsel, int level,
+                                 hipStream_t st);
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,

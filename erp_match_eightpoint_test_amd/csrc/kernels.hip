@@ -1998,34 +1998,44 @@ __global__ __launch_bounds__(256) void consensus_bounds_list_kernel(
 // [sqrtf(s_b), sqrtf(s_b+1)] exactly (sqrtf is monotone); keys below / above the 9 binades are
 // clamped into bins 0 / kNB-1, whose edges are 0 / +inf.  Bounds only ever tighten (LB = max,
 // UB = min with the first pass); bsel (the coarse bins refine and the exact pass use) stays.
-constexpr int kZMant = 6;                      // 64 bins per binade of s
-constexpr int kZShift = 23 - kZMant;
-constexpr int kZBinades = kNB >> kZMant;       // 9 binades: the same 576 bins (LDS layout)
-static_assert(kZBinades * (1 << kZMant) == kNB, "zoom bins");
+// Two levels: 64 bins per binade over 9 binades placed on the coarse windows (bsel), then
+// 256 bins per binade over 2.25 binades placed on the level-1 windows (zsel, written by the
+// level-1 pass), each followed by a re-selection.
 #ifndef ERP_ZOOM_MIN
-#define ERP_ZOOM_MIN 32
+#define ERP_ZOOM_MIN 8
 #endif
 constexpr int kZoomMin = ERP_ZOOM_MIN;         // survivors per pair below which no zoom pass
+#ifndef ERP_ZOOM_MAX
+#define ERP_ZOOM_MAX 2048
+#endif
+constexpr int kZoomMax = ERP_ZOOM_MAX;         // ... and above which none either
 
-// per pair: the zoom grid's first binade zelo[p] (-1: no zoom) and its d-space edges
+// per pair: the zoom grid's first bin zbase[p] (absolute, in units of key >> (23 - MANT); -1:
+// no zoom) from the span of the survivors' rank-window bins of the previous grid (SRC_MANT bins
+// per binade, absolute), and its d-space edges
+template <int MANT, int SRC_MANT>
 __global__ __launch_bounds__(256) void consensus_zoom_prep_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ dscale,
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
-    const int32_t* __restrict__ bsel, int stride, double trim_lo, double trim_hi,
-    int32_t* __restrict__ zelo, float* __restrict__ edz) {
+    const int32_t* __restrict__ wsel, int wsel_base_coarse, int stride, double trim_lo,
+    double trim_hi, int32_t* __restrict__ zbase, float* __restrict__ edz) {
+    constexpr int kShift = 23 - MANT;
+    static_assert(MANT >= SRC_MANT, "finer grid");
     __shared__ int red[2][4];
     const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p], n = nsurv[p];
     const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
-    if (n <= kZoomMin || hi <= lo) {
-        if (tid == 0) zelo[p] = -1;
+    // (a pair whose means all lie within ~1 % of each other -- two clusters -- keeps most of its
+    // rows through any grid: the refine pass's Lipschitz stage handles it)
+    if (n <= kZoomMin || n > kZoomMax || hi <= lo) {
+        if (tid == 0) zbase[p] = -1;
         return;
     }
     int amin = 1 << 30, bmax = -1;
     for (int k = tid; k < n; k += 256) {
         const int row = surv[(size_t)p * stride + k];
-        amin = min(amin, bsel[((size_t)p * stride + row) * 2]);
-        bmax = max(bmax, bsel[((size_t)p * stride + row) * 2 + 1]);
+        amin = min(amin, wsel[((size_t)p * stride + row) * 2]);
+        bmax = max(bmax, wsel[((size_t)p * stride + row) * 2 + 1]);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -2039,49 +2049,51 @@ __global__ __launch_bounds__(256) void consensus_zoom_prep_kernel(
     __syncthreads();
     amin = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
     bmax = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
-    // coarse bin b <-> s-binade elo + b / 16; the grid covers the top 9 binades of the span
-    const int elo = bounds_elo(dscale[p]);
-    const int zlo = elo + (amin >> kMantBits), zhi = elo + (bmax >> kMantBits);
-    const int z = max(max(zlo, zhi - (kZBinades - 1)), 1);
-    if (tid == 0) zelo[p] = z;
+    // the first pass's bins are relative to the pair's grid (bsel + (elo << kMantBits));
+    // the zoom passes write absolute bins
+    const int off = wsel_base_coarse ? (bounds_elo(dscale[p]) << kMantBits) : 0;
+    constexpr int up = MANT - SRC_MANT;
+    const int ulo = (amin + off) << up, uhi = ((bmax + off + 1) << up) - 1;  // in this grid's bins
+    const int z = max(max(ulo, uhi - (kNB - 1)), 1 << MANT);                 // top-aligned
+    if (tid == 0) zbase[p] = z;
     float* ed = edz + (size_t)p * 2 * kNB;
     for (int b = tid; b < kNB; b += 256) {
-        const uint32_t key = (uint32_t)((z << kZMant) + b) << kZShift;
+        const uint32_t key = (uint32_t)(z + b) << kShift;
         ed[b] = b == 0 ? 0.f : __builtin_sqrtf(__uint_as_float(key));
-        ed[kNB + b] = b == kNB - 1 ? kInf : __builtin_sqrtf(__uint_as_float(key + (1u << kZShift)));
+        ed[kNB + b] = b == kNB - 1 ? kInf : __builtin_sqrtf(__uint_as_float(key + (1u << kShift)));
     }
 }
 
-// one unit (kBoundRows survivors of one pair) per block; items flattened over the pairs
-__global__ __launch_bounds__(256) void consensus_zoom_kernel(
+// one unit (kBoundRows survivors of one pair) per block; items flattened over the pairs; writes
+// the tightened bounds and the survivors' rank-window bins on this grid (zsel, absolute)
+template <int MANT>
+__device__ __forceinline__ void consensus_zoom_unit(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv,
-    const float* __restrict__ edz, const int32_t* __restrict__ zelo, int stride, double trim_lo,
+    const float* __restrict__ edz, const int32_t* __restrict__ zbase_p, int stride, double trim_lo,
     double trim_hi, double* __restrict__ lb, double* __restrict__ ub,
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
-    const int32_t* __restrict__ uoff, int n_pairs) {
+    const int32_t* __restrict__ uoff, int n_pairs, int32_t* __restrict__ zsel, int g,
+    uint32_t* hist) {
+    constexpr int kShift = 23 - MANT;
     constexpr int R = kBoundRows;
     constexpr int NS = 256 / R;
     constexpr int per = kNB / NS;
-    __shared__ __align__(16) uint32_t hist[kNB * R];  // [bin][row]
     int (*part)[R] = reinterpret_cast<int (*)[R]>(hist);
     float (*partL)[R] = reinterpret_cast<float (*)[R]>(hist + NS * R);
     float (*partU)[R] = reinterpret_cast<float (*)[R]>(hist + 2 * NS * R);
-    const int g = blockIdx.x;
-    if (g >= uoff[n_pairs]) return;
     int p = 0, b = n_pairs;  // largest p with uoff[p] <= g
     while (b - p > 1) {
         const int m = (p + b) >> 1;
         if (uoff[m] <= g) p = m; else b = m;
     }
     const int tid = threadIdx.x, lane = wave_lane();
-    const int K = kcount[p], nloc = nsurv[p], zb = zelo[p];
+    const int K = kcount[p], nloc = nsurv[p], zbase = zbase_p[p];
     const int l0 = (g - uoff[p]) * R;
-    if (zb < 0 || l0 >= nloc) return;  // (uniform)
+    if (zbase < 0 || l0 >= nloc) return;  // (uniform)
     const int32_t* RL = surv + (size_t)p * stride;
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
-    const int zbase = zb << kZMant;
     constexpr int kPairs = R / 2;
     f32x2 xi[kPairs], yi[kPairs], zi[kPairs];
     uint32_t hoff[R];
@@ -2130,7 +2142,7 @@ __global__ __launch_bounds__(256) void consensus_zoom_kernel(
                     const f32x2 s = (dx * dx + dy * dy) + dz * dz;
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
-                        const int bz = min(max((int)(__float_as_uint(s[h]) >> kZShift) - zbase, 0),
+                        const int bz = min(max((int)(__float_as_uint(s[h]) >> kShift) - zbase, 0),
                                            kNB - 1);  // (one v_med3_i32)
                         lds_inc(lshl6_add((uint32_t)bz, hoff[2 * t + h]));
                     }
@@ -2166,6 +2178,7 @@ __global__ __launch_bounds__(256) void consensus_zoom_kernel(
     const bool rvalid = l0 + r < nloc;
     const int row = rvalid ? RL[l0 + r] : 0;
     float L = 0.f, U = 0.f;
+    int sel_a = -1, sel_b = -1;  // bins of ranks lo and hi-1 on this grid
     if (cum < hi && cum + c > lo) {
         int c0 = min(max(cum, lo), hi);
 #pragma unroll
@@ -2175,9 +2188,15 @@ __global__ __launch_bounds__(256) void consensus_zoom_kernel(
             const float w = (float)(c1 - c0);
             L = __builtin_fmaf(w, el[q], L);
             U = w > 0.f ? __builtin_fmaf(w, eu[q], U) : U;  // (0 * inf)
+            sel_a = (cum <= lo && lo < nc) ? sl * per + q : sel_a;
+            sel_b = (cum <= hi - 1 && hi - 1 < nc) ? sl * per + q : sel_b;
             cum = nc;
             c0 = c1;
         }
+    }
+    if (rvalid) {
+        if (sel_a >= 0) zsel[((size_t)p * stride + row) * 2] = zbase + sel_a;
+        if (sel_b >= 0) zsel[((size_t)p * stride + row) * 2 + 1] = zbase + sel_b;
     }
     partL[sl][r] = L;
     partU[sl][r] = U;
@@ -2195,6 +2214,20 @@ __global__ __launch_bounds__(256) void consensus_zoom_kernel(
         *lp = fmax(*lp, ((double)L / w) * (1.0 - 2e-4));
         *up = fmin(*up, ((double)U / w) * (1.0 + 2e-4));
     }
+}
+
+// one unit per block (a loop over units doubles the VGPRs: 122 -> 248), the live units first
+template <int MANT>
+__global__ __launch_bounds__(256) void consensus_zoom_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv,
+    const float* __restrict__ edz, const int32_t* __restrict__ zbase_p, int stride, double trim_lo,
+    double trim_hi, double* __restrict__ lb, double* __restrict__ ub,
+    const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
+    const int32_t* __restrict__ uoff, int n_pairs, int32_t* __restrict__ zsel) {
+    __shared__ __align__(16) uint32_t hist[kNB * kBoundRows];  // [bin][row]
+    if ((int)blockIdx.x >= uoff[n_pairs]) return;
+    consensus_zoom_unit<MANT>(kcount, rv, edz, zbase_p, stride, trim_lo, trim_hi, lb, ub, surv,
+                              nsurv, uoff, n_pairs, zsel, blockIdx.x, hist);
 }
 
 __global__ __launch_bounds__(256) void consensus_refine_kernel(
@@ -2773,19 +2806,31 @@ size_t consensus_edges_bytes(int n_pairs) {
 hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const float* dscale,
                                  float* edges, const BatchShape& sh, double trim_lo,
                                  double trim_hi, double* lb, double* ub, const int32_t* bsel,
-                                 const int32_t* surv, int32_t* nsurv, hipStream_t st) {
+                                 const int32_t* surv, int32_t* nsurv, int32_t* zsel, int level,
+                                 hipStream_t st) {
     const int P = sh.n_pairs, stride = 2 * sh.iters;
     float* edz = edges + (size_t)P * 2 * kNB;
-    int32_t* zelo = reinterpret_cast<int32_t*>(edges + (size_t)P * 4 * kNB);
+    int32_t* zb = reinterpret_cast<int32_t*>(edges + (size_t)P * 4 * kNB);
     int32_t* uoff = nsurv + 2 * P;  // free until the refine pass (launch_consensus_refine)
-    hipLaunchKernelGGL(consensus_zoom_prep_kernel, dim3(P), dim3(256), 0, st, kcount, dscale, surv,
-                       (const int32_t*)nsurv, bsel, stride, trim_lo, trim_hi, zelo, edz);
+    if (level == 1)
+        hipLaunchKernelGGL((consensus_zoom_prep_kernel<6, kMantBits>), dim3(P), dim3(256), 0, st,
+                           kcount, dscale, surv, (const int32_t*)nsurv, bsel, 1, stride, trim_lo,
+                           trim_hi, zb, edz);
+    else  // the level-1 windows (zsel) -> the 256-per-binade grid
+        hipLaunchKernelGGL((consensus_zoom_prep_kernel<8, 6>), dim3(P), dim3(256), 0, st, kcount,
+                           dscale, surv, (const int32_t*)nsurv, (const int32_t*)zsel, 0, stride,
+                           trim_lo, trim_hi, zb, edz);
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)nsurv, P,
                        kBoundRows, kZoomMin, uoff);
     const int max_units = P * ((stride + kBoundRows - 1) / kBoundRows);
-    hipLaunchKernelGGL(consensus_zoom_kernel, dim3(max_units), dim3(256), 0, st, kcount, rv,
-                       (const float*)edz, (const int32_t*)zelo, stride, trim_lo, trim_hi, lb, ub,
-                       surv, (const int32_t*)nsurv, (const int32_t*)uoff, P);
+    if (level == 1)
+        hipLaunchKernelGGL(consensus_zoom_kernel<6>, dim3(max_units), dim3(256), 0, st, kcount, rv,
+                           (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb,
+                           ub, surv, (const int32_t*)nsurv, (const int32_t*)uoff, P, zsel);
+    else
+        hipLaunchKernelGGL(consensus_zoom_kernel<8>, dim3(max_units), dim3(256), 0, st, kcount, rv,
+                           (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb,
+                           ub, surv, (const int32_t*)nsurv, (const int32_t*)uoff, P, zsel);
     return hipGetLastError();
 }
 
