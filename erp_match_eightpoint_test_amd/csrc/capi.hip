@@ -89,6 +89,9 @@ struct erp_ctx {
     uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
     // consensus zoom levels (0-2; ERP_ZOOM_LEVELS, an A/B knob)
     int zoom = getenv("ERP_ZOOM_LEVELS") ? atoi(getenv("ERP_ZOOM_LEVELS")) : 1;
+    // zoomed central references before the pre-pruning (opt-in ERP_ZOOM_REFS=1: measured no
+    // fewer binned rows)
+    bool zoom_refs = getenv("ERP_ZOOM_REFS") != nullptr;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -465,7 +468,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (float*)c->dscale.p, (float*)c->edges.p, sh,
                                             cfg->trim_lo, cfg->trim_hi, lbp, ubp, bselp, shard,
                                             nshards, (int32_t*)c->surv.p,
-                                            (int32_t*)c->nsurv.p + sh.n_pairs, st));
+                                            (int32_t*)c->nsurv.p + sh.n_pairs,
+                                            (int32_t*)c->zsel.p, c->zoom_refs, st));
     }
     if (phase == 1) return ERP_OK;
     if (phase == 2)  // the bounds ran per shard (binned rows not combined): report -1

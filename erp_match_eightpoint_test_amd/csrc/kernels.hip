@@ -2230,6 +2230,39 @@ __global__ __launch_bounds__(256) void consensus_zoom_kernel(
                               nsurv, uoff, n_pairs, zsel, blockIdx.x, hist);
 }
 
+// Before the Lipschitz pre-pruning: the reference rows whose first-pass UB is within 3 % of the
+// smallest (<= kBoundRows of them: one zoom unit per pair) are listed for a zoom pass, so that
+// U = min UB over the references -- the bound every pruning test subtracts -- is ~4x tighter.
+__global__ __launch_bounds__(256) void consensus_pick_central_kernel(
+    const int32_t* __restrict__ kcount, const double* __restrict__ ub, int stride, int shard,
+    int nshards, int32_t* __restrict__ list, int32_t* __restrict__ count) {
+    __shared__ double red[4];
+    __shared__ int n_s;
+    const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
+    const int K = kcount[p];
+    const int ra = (int)((int64_t)K * shard / nshards), rb = (int)((int64_t)K * (shard + 1) / nshards);
+    const int nref = rb > ra ? (rb - ra + kLipStep - 1) / kLipStep : 0;
+    const double* U = ub + (size_t)p * stride;
+    double m = __builtin_huge_val();
+    for (int c = tid; c < nref; c += 256) m = fmin(m, U[ra + c * kLipStep]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o, 64));
+    if (lane == 0) red[tid >> 6] = m;
+    if (tid == 0) n_s = 0;
+    __syncthreads();
+    m = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
+    const double lim = m * 1.03;
+    for (int c = tid; c < nref && m < __builtin_huge_val(); c += 256) {
+        const int row = ra + c * kLipStep;
+        if (U[row] <= lim) {
+            const int k = atomicAdd(&n_s, 1);
+            if (k < kBoundRows) list[(size_t)p * stride + k] = row;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) count[p] = min(n_s, kBoundRows);
+}
+
 __global__ __launch_bounds__(256) void consensus_refine_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv,
     const float* __restrict__ dscale, int stride, double trim_lo, double trim_hi,
@@ -2838,7 +2871,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
-                                   hipStream_t st) {
+                                   int32_t* zsel, bool zoom_refs, hipStream_t st) {
     hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     const int stride = 2 * sh.iters;
     if (!rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
@@ -2859,6 +2892,14 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
     dim3 g1((nref + kBoundRows - 1) / kBoundRows, sh.n_pairs);
     hipLaunchKernelGGL(consensus_bounds_kernel, g1, dim3(256), 0, st, kcount, rv, dscale, edges,
                        stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, kLipStep);
+    if (zoom_refs) {  // the central references on the zoom grid: a tighter U for the pruning
+        int32_t* cnt = rcount - sh.n_pairs;  // (nsurv[0 .. P): free until the first select)
+        hipLaunchKernelGGL(consensus_pick_central_kernel, dim3(sh.n_pairs), dim3(256), 0, st,
+                           kcount, (const double*)ub, stride, shard, nshards, rlist, cnt);
+        const hipError_t ze = launch_consensus_zoom(kcount, rv, dscale, edges, sh, trim_lo,
+                                                    trim_hi, lb, ub, bsel, rlist, cnt, zsel, 1, st);
+        if (ze != hipSuccess) return ze;
+    }
     const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * sh.n_pairs, st);
     if (me != hipSuccess) return me;
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((srows + 511) / 512, sh.n_pairs),
