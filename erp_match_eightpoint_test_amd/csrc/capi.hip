@@ -89,6 +89,8 @@ struct erp_ctx {
     uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
     // consensus zoom levels (0-2; ERP_ZOOM_LEVELS, an A/B knob)
     int zoom = getenv("ERP_ZOOM_LEVELS") ? atoi(getenv("ERP_ZOOM_LEVELS")) : 1;
+    // the matcher's ratio test decided by the bf16 bounds where they suffice (A/B knob)
+    bool bound_ratio = getenv("ERP_NO_BOUND_RATIO") == nullptr;
     // zoomed central references before the pre-pruning (opt-in ERP_ZOOM_REFS=1: measured no
     // fewer binned rows)
     bool zoom_refs = getenv("ERP_ZOOM_REFS") != nullptr;
@@ -341,7 +343,8 @@ erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_RESCORE, st);
         ERP_CK(erp::launch_knn2_rescore(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand,
-                                        (erp::Top2*)ctx->part.p, (int32_t*)ctx->ovf.p, st));
+                                        (erp::Top2*)ctx->part.p, (int32_t*)ctx->ovf.p,
+                                        ctx->bound_ratio ? ratio : -1.f, st));
     }
     return fold_and_merge(ctx, oq, ot, sh, sh.fchunk_len, sh.fchunks, ratio, matches, counts,
                           flags, st);

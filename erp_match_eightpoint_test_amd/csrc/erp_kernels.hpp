@@ -72,7 +72,7 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
 hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
                                const int64_t* off_t, const BatchShape& sh, void* split,
                                const float2* pu, const int32_t* ccount, void* cand, Top2* part,
-                               int32_t* ovf, hipStream_t st);
+                               int32_t* ovf, float ratio, hipStream_t st);
 // exact sweep on packed FP32 VALU (no MFMA filter): per-(chunk, query) exact k=2 into
 // xpart[pairs][xchunks][max_nq]
 hipError_t launch_knn2_exact(const float* desc_q, const float* desc_t, const int64_t* off_q,

@@ -435,7 +435,8 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                                                            const int32_t* __restrict__ ctile,
                                                            const bf16x8* __restrict__ cval,
                                                            Top2* __restrict__ part,
-                                                           int32_t* __restrict__ ovf, int qblocks) {
+                                                           int32_t* __restrict__ ovf, int qblocks,
+                                                           float ratio) {
     __shared__ int32_t plist[kPassList * 256];
     __shared__ float plb[kPassList * 256];
     // XCD-aware block order as in knn2_filter (a pair's blocks on one XCD: its f32 train rows,
@@ -484,7 +485,12 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
         // l* = u' + lq <= the row's l (knn2_filter header; lq's rounding is inside the slack)
         const float teM = __uint_as_float(tmax[p]) * (2.f * kFEps) * (1.f + kFMargin) + kFTiny;
         const float lq = (__builtin_fmaf(qq, -kFEps, qq) - kFTiny) - teM;
+        // u* = v + 2^-8 |v| + |q|^2 (1 + eps) >= u' + |q|^2 (1 + eps) = u >= e (the filter's
+        // upper bound; the f32 roundings here are far inside its 2.1e-4 S slack)
+        const float uq = __builtin_fmaf(qq, kFEps, qq);
         int npass = 0;
+        float l1 = kInf, l2 = kInf, umin = kInf;  // two smallest l*, smallest u*
+        int r1 = -1, ra = -1;                     // their rows
         for (int h = 0; h < 2; h++) {
             const int n = h ? n1 : n0;
             for (int k = 0; k < n; k++) {
@@ -503,6 +509,18 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                             plb[npass * 256 + threadIdx.x] = lo;
                         }
                         npass++;
+                        const float hi = __builtin_fmaf(0x1p-8f, fabsf(x), x) + uq;
+                        if (lo < l1) {
+                            l2 = l1;
+                            l1 = lo;
+                            r1 = row;
+                        } else {
+                            l2 = fminf(l2, lo);
+                        }
+                        if (hi < umin) {
+                            umin = hi;
+                            ra = row;
+                        }
                     }
                 }
             }
@@ -510,6 +528,30 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
         if (npass > kPassList) {  // (never seen on SURF-like data) exact sweep of the chunk
             overflow();
             return;
+        }
+        // The ratio test decided by the bounds (single-chunk launches only: the merge then sees
+        // this lane's record alone).  Every row with e <= e_(2) is listed (unlisted rows have
+        // e >= l* > U2 >= e_(2)), so e_(1) >= l1, e_(2) >= the smallest l* of the rows other than
+        // the one holding e_(1), and e_(2) <= U2.  sqrtf and fl(ratio * x) are monotone, so
+        //  reject: sqrtf(l1) >= fl(ratio sqrtf(U2)) gives d0 >= ratio d1 -- record {inf, -1, inf}
+        //    (the merge's d0 < ratio d1 is false for it, as for the exact values);
+        //  accept: when one row's u* is below every other row's l*, it is the unique nearest;
+        //    its exact e gives d0, and d0 < fl(ratio sqrtf(L_other)) <= fl(ratio d1) -- record
+        //    {e, row, L_other}, on which the merge's test passes just as on {e, row, e_(2)}.
+        if (ratio >= 0.f && npass > 0) {
+            if (__builtin_sqrtf(fmaxf(l1, 0.f)) >= ratio * __builtin_sqrtf(U2)) {
+                *out = Top2{kInf, -1, kInf};
+                return;
+            }
+            const float lother = r1 == ra ? l2 : l1;
+            if (umin < lother) {
+                const float e = exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + ra) * kDim));
+                const float lb2 = fmaxf(lother, 0.f);
+                if (__builtin_sqrtf(e) < ratio * __builtin_sqrtf(lb2)) {
+                    *out = Top2{e, ra, lb2};
+                    return;
+                }
+            }
         }
         for (int k = 0; k < npass; k++) {
             int kb = k;
@@ -929,7 +971,7 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
 hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
                                const int64_t* off_t, const BatchShape& sh, void* split,
                                const float2* pu, const int32_t* ccount, void* cand, Top2* part,
-                               int32_t* ovf, hipStream_t st) {
+                               int32_t* ovf, float ratio, hipStream_t st) {
     int32_t* ctile;
     bf16x8* cval;
     cand_split(sh, cand, &ctile, &cval);
@@ -937,7 +979,8 @@ hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const i
     const int qblocks = (sh.max_nq + 255) / 256;
     hipLaunchKernelGGL(knn2_rescore_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
                        st, desc_q, desc_t, off_q, off_t, sh.max_nq, sh.fchunk_len, sh.fchunks,
-                       split_tmax(sh, split), pu, ccount, ctile, cval, part, ovf, qblocks);
+                       split_tmax(sh, split), pu, ccount, ctile, cval, part, ovf, qblocks,
+                       sh.fchunks == 1 ? ratio : -1.f);  // (bound decisions need one chunk)
     hipLaunchKernelGGL(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
                        sh.max_nq, sh.fchunk_len, sh.fchunks, ovf, part);
     return hipGetLastError();

@@ -90,7 +90,7 @@ int main(int argc, char** argv) {
         CK(erp::launch_knn2_filter(dq, dt, doff, doff, sh, split, (float2*)dpu, dcc, cand, 0));
         CK(hipEventRecord(e1, 0));
         CK(erp::launch_knn2_rescore(dq, dt, doff, doff, sh, split, (const float2*)dpu, dcc, cand,
-                                    part, dovf, 0));
+                                    part, dovf, -1.f, 0));
         CK(hipEventRecord(e2, 0));
         CK(hipEventSynchronize(e2));
         float a, b;
