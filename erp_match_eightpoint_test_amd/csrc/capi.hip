@@ -93,7 +93,7 @@ struct erp_ctx {
     bool bound_ratio = getenv("ERP_NO_BOUND_RATIO") == nullptr;
     // zoomed central references before the pre-pruning (opt-in ERP_ZOOM_REFS=1: measured no
     // fewer binned rows)
-    bool zoom_refs = getenv("ERP_ZOOM_REFS") != nullptr;
+    int zoom_refs = getenv("ERP_ZOOM_REFS") ? atoi(getenv("ERP_ZOOM_REFS")) : 0;  // 2: all refs
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;

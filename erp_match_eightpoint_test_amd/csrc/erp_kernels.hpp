@@ -142,7 +142,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
-                                   int32_t* zsel, bool zoom_refs, hipStream_t st);
+                                   int32_t* zsel, int zoom_refs, hipStream_t st);
 // survivors = rows with LB <= min UB (again = 1: only pairs the refine pass touched)
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
                                    const BatchShape& sh, double trim_lo, double trim_hi,

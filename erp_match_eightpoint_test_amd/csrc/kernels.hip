@@ -2235,7 +2235,7 @@ __global__ __launch_bounds__(256) void consensus_zoom_kernel(
 // U = min UB over the references -- the bound every pruning test subtracts -- is ~4x tighter.
 __global__ __launch_bounds__(256) void consensus_pick_central_kernel(
     const int32_t* __restrict__ kcount, const double* __restrict__ ub, int stride, int shard,
-    int nshards, int32_t* __restrict__ list, int32_t* __restrict__ count) {
+    int nshards, int32_t* __restrict__ list, int32_t* __restrict__ count, int all) {
     __shared__ double red[4];
     __shared__ int n_s;
     const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
@@ -2251,16 +2251,17 @@ __global__ __launch_bounds__(256) void consensus_pick_central_kernel(
     if (tid == 0) n_s = 0;
     __syncthreads();
     m = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
-    const double lim = m * 1.03;
+    const double lim = all ? __builtin_huge_val() : m * 1.03;
+    const int cap = all ? stride : kBoundRows;
     for (int c = tid; c < nref && m < __builtin_huge_val(); c += 256) {
         const int row = ra + c * kLipStep;
         if (U[row] <= lim) {
             const int k = atomicAdd(&n_s, 1);
-            if (k < kBoundRows) list[(size_t)p * stride + k] = row;
+            if (k < cap) list[(size_t)p * stride + k] = row;
         }
     }
     __syncthreads();
-    if (tid == 0) count[p] = min(n_s, kBoundRows);
+    if (tid == 0) count[p] = min(n_s, cap);
 }
 
 __global__ __launch_bounds__(256) void consensus_refine_kernel(
@@ -2871,7 +2872,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
-                                   int32_t* zsel, bool zoom_refs, hipStream_t st) {
+                                   int32_t* zsel, int zoom_refs, hipStream_t st) {
     hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     const int stride = 2 * sh.iters;
     if (!rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
@@ -2895,7 +2896,8 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
     if (zoom_refs) {  // the central references on the zoom grid: a tighter U for the pruning
         int32_t* cnt = rcount - sh.n_pairs;  // (nsurv[0 .. P): free until the first select)
         hipLaunchKernelGGL(consensus_pick_central_kernel, dim3(sh.n_pairs), dim3(256), 0, st,
-                           kcount, (const double*)ub, stride, shard, nshards, rlist, cnt);
+                           kcount, (const double*)ub, stride, shard, nshards, rlist, cnt,
+                           zoom_refs > 1 ? 1 : 0);
         const hipError_t ze = launch_consensus_zoom(kcount, rv, dscale, edges, sh, trim_lo,
                                                     trim_hi, lb, ub, bsel, rlist, cnt, zsel, 1, st);
         if (ze != hipSuccess) return ze;
