@@ -327,72 +327,86 @@ __device__ __forceinline__ uint32_t mod_rup_i24(uint32_t x, double r, int d) {
 
 // One block of 31 reverse steps i0, i0-1, ..., i0-30 of one lane's replay (ring = the 31-word
 // glibc window, advanced backwards in place).  Returns the block's selection word: bit u set
-// iff step i0-u's index ends in the sample.  bm = the lane's s-bit LDS bitmap, [word][lane].
-//   MODE 0 (every step i >= s):      valid = j < s;  old = bm[j] |= bit;     sel = valid && !old
-//   MODE 1 (every step 1 <= i < s):  old = bm[j]; bm[j] := bm[i];            sel = !old
-//   MODE 2 (mixed / steps below 1):  per-step choice of the two (dead steps do nothing)
-// (bm bit set = "resolved": for i >= s the position was taken by a later step; for i < s the
-// reverse-step set T of the header comment is the complement.)  The atomics' old values are
-// consumed after the block, so the LDS traffic streams without waits; MODE 1/2 read bm[i] from
-// registers mirroring the (at most two) words holding i0-30..i0.
-// atomic OR into the lane's bitmap word of position j (bm_lane = LDS byte address of the lane's
-// word 0; words are 256 B apart): the address is one v_lshl_add_u32 of j >> 5
-__device__ __forceinline__ uint32_t atomicOr_lds_word(uint32_t bm_lane, uint32_t j, uint32_t bits) {
+// iff step i0-u's index ends in the sample.  bm = the lane's s-bit LDS bitmap, [word][lane],
+// bit SET = position still unresolved (available):
+//   steps i >= s (replay_block_draws):   sel = bm[j];  bm[j] := 0
+//   steps 1 <= i < s (replay_block_prefix): sel = bm[j];  bm[j] := bm[i]
+//   the block straddling s / running below step 1 (replay_block_mixed): per step
+// A position j >= s needs no clamp: its bit is 0 (positions s .. the allocation's end are
+// cleared by the kernel's prologue) or its word lies beyond the workgroup's LDS allocation,
+// where gfx950 returns 0 and drops the write (scripts/dev/lds_oob.hip: measured up to 512 KB,
+// i.e. j < 65536 = the keypoint cap).  The LDS ops' results are consumed kReplayLag steps
+// after issue, so the traffic streams without waits.
+// (bm_lane = LDS byte address of the lane's word 0; words are 256 B apart: the address is one
+// v_lshl_add_u32 of j >> 5)
+__device__ __forceinline__ uint32_t lds_word_addr(uint32_t bm_lane, uint32_t j) {
     uint32_t a;
     asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(a) : "v"(j >> 5), "v"(bm_lane));
-    return __hip_atomic_fetch_or((lds_u32*)(size_t)a, bits, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+    return a;
 }
 
 // replay blocks consume a step's LDS return `kReplayLag` steps after issuing it (fewer live
 // registers than consuming all 31 after the block: occupancy)
 constexpr int kReplayLag = 8;
 
-// nw | (b << u) as one v_lshl_or_b32 (u a compile-time constant)
-template <int U>
-__device__ __forceinline__ uint32_t lshl_or_c(uint32_t b, uint32_t nw) {
-    uint32_t r;
-    asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(b), "i"(U), "v"(nw));
-    return r;
-}
-template <int U>
-__device__ __forceinline__ void collect_bits(const uint32_t (&olds)[31], const uint32_t (&pos)[31],
-                                             uint32_t& nw) {
-    if constexpr (U < 31) {
-        nw = lshl_or_c<U>(__builtin_amdgcn_ubfe(olds[U], pos[U], 1), nw);
-        collect_bits<U + 1>(olds, pos, nw);
-    }
-}
-
-// LDS masked OR with return: old = bm[a]; bm[a] = (old & ~mask) | data (one DS op for the
-// "T[j] := T[i]" bit copy).  The compiler does not track the asm's result, so every use goes
-// through lds_wait31 (an lgkmcnt(0) wait that carries the results as operands).
+// LDS masked OR with return: old = bm[a]; bm[a] = (old & ~mask) | data (one DS op: the bit
+// clear of the i >= s steps with data = 0, the "T[j] := T[i]" bit copy of the prefix steps).
+// The compiler does not track the asm's result, so every use goes through an explicit
+// lgkmcnt wait that carries the result as an operand.
 __device__ __forceinline__ uint32_t lds_mskor_rtn(uint32_t addr, uint32_t mask, uint32_t data) {
     uint32_t old;
     asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3" : "=v"(old) : "v"(addr), "v"(mask), "v"(data)
                  : "memory");
     return old;
 }
-__device__ __forceinline__ void lds_wait31(uint32_t (&o)[31]) {
-    asm volatile("s_waitcnt lgkmcnt(0)"
-                 : "+v"(o[0]), "+v"(o[1]), "+v"(o[2]), "+v"(o[3]), "+v"(o[4]), "+v"(o[5]),
-                   "+v"(o[6]), "+v"(o[7]), "+v"(o[8]), "+v"(o[9]), "+v"(o[10]), "+v"(o[11]),
-                   "+v"(o[12]), "+v"(o[13]), "+v"(o[14]), "+v"(o[15])
-                 :
-                 : "memory");
-    asm volatile(""
-                 : "+v"(o[16]), "+v"(o[17]), "+v"(o[18]), "+v"(o[19]), "+v"(o[20]),
-                   "+v"(o[21]), "+v"(o[22]), "+v"(o[23]), "+v"(o[24]), "+v"(o[25]),
-                   "+v"(o[26]), "+v"(o[27]), "+v"(o[28]), "+v"(o[29]), "+v"(o[30])
-                 :
-                 : "memory");
+
+// consume step v of a replay block whose steps 0 .. 30 were issued in order (v + lag issued so
+// far): at most `lag` masked ORs may still be in flight after it (LDS returns in order; SMEM in
+// the count only makes the wait stricter)
+__device__ __forceinline__ void lds_wait_step(uint32_t& o, int v) {
+    if (min(30 - v, kReplayLag) >= 8)
+        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(o) : : "memory");
+    else
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(o) : : "memory");
 }
 
-// MODE 1 (every step 1 <= i < s) with the block's own 31 bits T[i0-30 .. i0] (bm bits, set =
-// resolved) in one register: bm[i] is a constant-position bit extract instead of a two-word
-// register mirror, the bit copy bm[j] := bm[i] is one masked OR (returning old bm[j]), and a
-// step that writes inside the window updates it with one bfi (out-of-window j lands on the
-// unused bit 31).  ~17 VALU + 1 DS per step (the mirror version: ~27 VALU + 2 DS).
+// steps i >= s: one LDS op per draw, no clamp, no validity select (~10 VALU per draw)
+template <bool I24>
+__device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uint32_t* bm,
+                                                       int lane, int i0,
+                                                       const double* __restrict__ rtab) {
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
+    double rt[31];  // 1/(i+1) of the block's steps: scalar loads (uniform index)
+#pragma unroll
+    for (int u = 0; u < 31; u++) rt[u] = rtab[i0 - u + 1];
+    const uint32_t zero = 0;
+    uint32_t olds[31], pos[31];
+    uint32_t nw = 0;
+#pragma unroll
+    for (int u = 0; u < 31 + kReplayLag; u++) {
+        if (u < 31) {
+            const int ii = i0 - u;  // uniform, >= s >= 1
+            const int slot = 30 - u;
+            const uint32_t rv = ring[slot];
+            ring[slot] = rv - ring[(slot + 28) % 31];
+            const uint32_t j = I24 ? mod_rup_i24(rv >> 1, rt[u], ii + 1)
+                                   : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
+            olds[u] = lds_mskor_rtn(lds_word_addr(bm_lane, j), 1u << (j & 31), zero);
+            pos[u] = j;
+        }
+        const int v = u - kReplayLag;
+        if (v >= 0) {
+            lds_wait_step(olds[v], v);
+            nw |= __builtin_amdgcn_ubfe(olds[v], pos[v], 1) << v;
+        }
+    }
+    return nw;
+}
+
+// steps 1 <= i < s with the block's own 31 bits bm[i0-30 .. i0] in one register: bm[i] is a
+// constant-position bit extract, the bit copy bm[j] := bm[i] is one masked OR (returning old
+// bm[j]), and a step that writes inside the window updates it with one bfi (out-of-window j
+// lands on the unused bit 31).  ~17 VALU + 1 DS per step.
 template <bool I24>
 __device__ __forceinline__ uint32_t replay_block_prefix(uint32_t (&ring)[31], uint32_t* bm,
                                                         int lane, int i0,
@@ -406,7 +420,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix(uint32_t (&ring)[31], ui
     const uint32_t hi = bm[wA * 64 + lane], lo = bm[wB * 64 + lane];
     uint32_t win = wA == wB ? (lo >> (base & 31)) : __builtin_amdgcn_alignbit(hi, lo, base & 31);
     uint32_t olds[31], pos[31];
-    uint32_t nw = 0;  // steps whose position was already resolved
+    uint32_t nw = 0;
 #pragma unroll
     for (int u = 0; u < 31 + kReplayLag; u++) {
         if (u < 31) {
@@ -418,38 +432,27 @@ __device__ __forceinline__ uint32_t replay_block_prefix(uint32_t (&ring)[31], ui
                                    : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
             const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)win, 30 - u, 1);  // bm[i]
             const uint32_t bit = 1u << (j & 31);
-            uint32_t a;
-            asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(a) : "v"(j >> 5), "v"(bm_lane));
-            olds[u] = lds_mskor_rtn(a, bit, bsp & bit);
+            olds[u] = lds_mskor_rtn(lds_word_addr(bm_lane, j), bit, bsp & bit);
             pos[u] = j;
             const uint32_t t = min(j - (uint32_t)base, 31u);
             const uint32_t m = 1u << t;
             win = (win & ~m) | (bsp & m);
         }
-        // consume step v = u - lag: at most `lag` masked ORs may still be in flight after it
-        // (LDS returns in order; SMEM in the count only makes the wait stricter)
         const int v = u - kReplayLag;
         if (v >= 0) {
-            const int inflight = min(30 - v, kReplayLag);
-            if (inflight >= 8)
-                asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(olds[v]) : : "memory");
-            else
-                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(olds[v]) : : "memory");
+            lds_wait_step(olds[v], v);
             nw |= __builtin_amdgcn_ubfe(olds[v], pos[v], 1) << v;
         }
     }
-    return ~nw & 0x7fffffffu;
+    return nw;
 }
 
-// MODE 2 (the block that straddles s, and the last block that runs below step 1): at most two
-// per iteration, so each step is done on its own (no mirrors, no arrays of in-flight results;
-// keeps the kernel's register budget at the other modes' level).  Steps i >= s as MODE 0,
-// steps 1 <= i < s as replay_block_prefix (bm[i] read back from LDS: the lane's LDS ops are in
-// order), steps below 1 do nothing.
+// the block that straddles s, and the last block that runs below step 1: at most two per
+// iteration, so each step is done on its own (compiler-tracked atomics; keeps the kernel's
+// register budget at the other blocks' level).  Steps below 1 do nothing.
 __device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uint32_t* bm,
                                                        int lane, int i0, int s,
                                                        const double* __restrict__ rtab) {
-    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
     uint32_t word = 0;
 #pragma unroll
     for (int u = 0; u < 31; u++) {
@@ -460,90 +463,12 @@ __device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uin
         if (ii < 1) continue;
         const double r = rtab[ii + 1];
         const uint32_t j = mod_rup(rv >> 1, r, (double)(ii + 1));
-        uint32_t old, jt;
-        if (ii >= s) {
-            jt = min(j, (uint32_t)s);
-            old = atomicOr_lds_word(bm_lane, jt, 1u << (jt & 31));
-        } else {
-            jt = j;
-            const uint32_t bi = (bm[(ii >> 5) * 64 + lane] >> (ii & 31)) & 1u;
-            uint32_t* wp = &bm[(j >> 5) * 64 + lane];
-            old = atomicAnd(wp, ~(1u << (j & 31)));
-            atomicOr(wp, bi << (j & 31));
-        }
-        word |= (__builtin_amdgcn_ubfe(old, jt, 1) ^ 1u) << u;
-    }
-    return word;
-}
-
-template <int MODE, bool I24>
-__device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t* bm, int lane,
-                                                 int i0, int s, const double* __restrict__ rtab) {
-    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
-    double rt[31];  // 1/(i+1) of the block's steps: scalar loads (uniform index)
-#pragma unroll
-    for (int u = 0; u < 31; u++) rt[u] = rtab[max(i0 - u, 1) + 1];
-    int wA = 0, wB = 0;
-    uint32_t curA = 0, curB = 0;
-    if (MODE != 0) {
-        wA = i0 >> 5;
-        wB = (i0 - 30) > 0 ? (i0 - 30) >> 5 : 0;
-        curA = bm[wA * 64 + lane];
-        curB = bm[wB * 64 + lane];
-    }
-    uint32_t olds[31], sel[31];
-    uint32_t nw0 = 0;  // MODE 0: steps whose position was already taken
-#pragma unroll
-    for (int u = 0; u < 31; u++) {
-        const int ii = i0 - u;  // uniform
-        const int slot = 30 - u;
-        const uint32_t rv = ring[slot];
-        ring[slot] = rv - ring[(slot + 28) % 31];
-        const bool live = MODE != 2 || ii >= 1;
-        const int d = live ? ii + 1 : 2;
-        const uint32_t j = I24 ? mod_rup_i24(rv >> 1, rt[u], d) : mod_rup(rv >> 1, rt[u], (double)d);
-        const uint32_t bit = 1u << (j & 31);
-        const bool isB = MODE == 1 || (MODE == 2 && ii < s);
-        if (MODE == 0) {
-            // j >= s is clamped to the sentinel position s, whose bit is always set: the OR is
-            // harmless and the step is never selected (no validity select per step)
-            const uint32_t jc = min(j, (uint32_t)s);
-            const uint32_t bc = 1u << (jc & 31);
-            olds[u] = atomicOr_lds_word(bm_lane, jc, bc);
-            sel[u] = jc;  // (MODE 0: the bit position)
-            if (u >= kReplayLag) {  // consume step u - lag (the compiler places the wait)
-                const int v = u - kReplayLag;
-                nw0 |= __builtin_amdgcn_ubfe(olds[v], sel[v], 1) << v;
-            }
-        } else {
-            const uint32_t cw = ((ii >> 5) == wA) ? curA : curB;
-            const uint32_t bi = (cw >> (ii & 31)) & 1u;
-            const bool validA = live && !isB && j < (uint32_t)s;
-            const bool validB = live && isB;
-            const uint32_t w = (validA || validB) ? (j >> 5) : 0u;
-            const uint32_t andm = validB ? ~bit : 0xffffffffu;
-            const uint32_t orm = validB ? (bi << (j & 31)) : (validA ? bit : 0u);
-            uint32_t* wp = &bm[w * 64 + lane];
-            olds[u] = atomicAnd(wp, andm);
-            atomicOr(wp, orm);
-            curA = (w == (uint32_t)wA) ? ((curA & andm) | orm) : curA;
-            curB = (w == (uint32_t)wB) ? ((curB & andm) | orm) : curB;
-            sel[u] = (validA || validB) ? bit : 0u;
-        }
-    }
-    uint32_t word = 0;
-    if (MODE == 0) {
-        // selected iff bit sel of the old word was clear: collect the SET bits (one bfe and one
-        // lshl_or per step), complement once
-        uint32_t nw = nw0;
-#pragma unroll
-        for (int v = 31 - kReplayLag; v < 31; v++)
-            nw |= __builtin_amdgcn_ubfe(olds[v], sel[v], 1) << v;
-        word = ~nw & 0x7fffffffu;
-    } else {
-        // selected iff the step's bit was not yet set: sel & ~old != 0 (sel is 0 or one bit)
-#pragma unroll
-        for (int u = 0; u < 31; u++) word |= min(sel[u] & ~olds[u], 1u) << u;
+        // bm[i] (read before the clear: j = i keeps the bit)
+        const uint32_t bi = ii < s ? (bm[(ii >> 5) * 64 + lane] >> (ii & 31)) & 1u : 0u;
+        uint32_t* wp = &bm[(j >> 5) * 64 + lane];  // j >= s: a cleared or out-of-allocation word
+        const uint32_t old = atomicAnd(wp, ~(1u << (j & 31)));
+        if (ii < s) atomicOr(wp, bi << (j & 31));
+        word |= __builtin_amdgcn_ubfe(old, j, 1) << u;
     }
     return word;
 }
@@ -553,7 +478,7 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
 __global__ __launch_bounds__(64) void sampler_kernel(
     const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins, int nwaves, int nbw,
     double sample_frac, const double* __restrict__ rtab, uint32_t* __restrict__ selw,
-    int32_t* __restrict__ flags) {
+    int32_t* __restrict__ flags, int nalloc) {
     extern __shared__ uint32_t bm[];  // [nwords][64]
     const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
     const int M = counts[p];
@@ -564,8 +489,10 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     // (inline asm: the compiler's mode-register pass would otherwise put the default mode back
     // in front of every fp64 instruction; nothing else in this kernel depends on fp64 rounding)
     asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\ts_nop 3" ::: "memory");
-    const int nwords = (s >> 5) + 1;  // positions 0..s (s: the always-set sentinel)
-    for (int k = 0; k < nwords; k++) bm[k * 64 + lane] = (k == (s >> 5)) ? (1u << (s & 31)) : 0u;
+    // positions < s available, every other bitmap word of the allocation (nalloc words: the
+    // batch's largest s; + slack for the allocation granule, writes beyond it are dropped) clear
+    for (int k = 0; k < nalloc + 5; k++)
+        bm[k * 64 + lane] = k < (s >> 5) ? ~0u : k == (s >> 5) ? (1u << (s & 31)) - 1u : 0u;
     uint32_t ring[31];
     {
         const uint32_t* wi = wins + ((size_t)p * nwaves + w) * 31 * 64 + lane;
@@ -579,9 +506,9 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     while (i >= 1) {
         uint32_t word;
         if (i - 30 >= s && i - 30 >= 255)
-            word = replay_block<0, true>(ring, bm, lane, i, s, rtab);
+            word = replay_block_draws<true>(ring, bm, lane, i, rtab);
         else if (i - 30 >= s)
-            word = replay_block<0, false>(ring, bm, lane, i, s, rtab);
+            word = replay_block_draws<false>(ring, bm, lane, i, rtab);
         else if (i < s && i - 30 >= 255)
             word = replay_block_prefix<true>(ring, bm, lane, i, rtab);
         else if (i < s && i - 30 >= 1)
@@ -594,7 +521,7 @@ __global__ __launch_bounds__(64) void sampler_kernel(
         i -= 31;
         b++;
     }
-    if (!(bm[lane] & 1u)) {  // position 0 still unresolved: its value 0 stays in the prefix
+    if (bm[lane] & 1u) {  // position 0 still unresolved: its value 0 stays in the prefix
         lastw |= 1u << u0;
         emitted++;
     }
@@ -2755,10 +2682,12 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         hipLaunchKernelGGL(sampler_window_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts,
                            polyR, polyQ, w0, nwaves, sample_frac, wins);
     } else {
-        const int nwords = sh.max_s / 32 + 1;  // + the sentinel position max_s
+        // positions 0 .. max_s, rounded up to the LDS allocation granule (1280 B = 5 words on
+        // gfx950, scripts/dev/lds_oob.hip) so that no word of the allocation goes uncleared
+        const int nwords = (sh.max_s / 32 + 1 + 4) / 5 * 5;
         const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
         hipLaunchKernelGGL(sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
-                           wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags);
+                           wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags, nwords);
     }
     return hipGetLastError();
 }
