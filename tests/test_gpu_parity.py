@@ -357,6 +357,30 @@ def test_batch_full_size_properties(ctx, oracle):
     assert np.degrees(np.abs(r["R"] - p["euler_gt"])).mean() < 1.0
 
 
+def test_sampler_large_match_count(ctx, oracle):
+    """M ~ 27k matches: the sampler's i >= s draws land on bitmap words far beyond the
+    workgroup's LDS allocation (positions up to M-1: byte offsets up to ~220 KB, past the CU's
+    160 KB of LDS),
+    which must read as taken and write nothing (kernels.hip replay_block_draws); the sampled sets
+    of the first iterations and of a wave boundary equal the oracle's glibc replay."""
+    import torch
+    from erp_match_eightpoint_test_amd import PairBatchRunner, results_to_numpy
+    p = synth.make_pair(4242, n_kpts=60000)
+    args = _batch([p])
+    outs = PairBatchRunner(ctx=ctx, iters=130).run(*args, want=("samples",))
+    torch.cuda.synchronize()
+    r = results_to_numpy(outs["results"])[0]
+    M = int(r["M"])
+    assert r["status"] == 0 and M > 25000
+    s = int(M * 0.25)
+    g = oracle.GlibcRand(1)
+    samples = outs["samples"][0].cpu().numpy()
+    for it in range(130):
+        a = g.random_array(M)
+        if it in (0, 1, 2, 63, 64, 129):
+            assert np.array_equal(np.sort(samples[it, :s]), np.sort(a[:s])), it
+
+
 # ---------------------------------------------------------- sharding entry points (GPU)
 def test_hypothesis_blocks_by_offset_match_full_run(ctx, oracle):
     """erp_eight_point_hypotheses_dev on iteration blocks [0,a) and [a,I) with the glibc offset
