@@ -447,6 +447,52 @@ __device__ __forceinline__ uint32_t replay_block_prefix(uint32_t (&ring)[31], ui
     return nw;
 }
 
+// The same steps with bm[i] read back from LDS per step instead of a register window (no
+// window bookkeeping: ~13.5 instead of ~16.5 VALU per step).  A wave's LDS ops complete in
+// order, so the read of bm[i] issued after the previous step's masked OR sees it; the read is
+// issued before the step's modulo, whose VALU work (and the other waves') covers its latency.
+#ifndef ERP_PREFIX_READ
+#define ERP_PREFIX_READ 1
+#endif
+template <bool I24>
+__device__ __forceinline__ uint32_t replay_block_prefix_rd(uint32_t (&ring)[31], uint32_t* bm,
+                                                           int lane, int i0,
+                                                           const double* __restrict__ rtab) {
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
+    // the reads are volatile asm, ordered against the masked ORs as volatile asm; only the
+    // first carries a memory clobber (every earlier bitmap access is emitted before it, and the
+    // block's reciprocal loads above it, where they merge into wide scalar loads -- sunk into
+    // the steps one by one, their 31 addresses spill)
+    double rt[31];
+    uint32_t nw = 0, prev = 0, ppos = 0;
+#pragma unroll
+    for (int u = 0; u < 31; u++) {
+        const int ii = i0 - u;  // uniform, >= 1
+        if (u == 0 || u == 16)  // the reciprocals in two halves (SGPR pressure)
+#pragma unroll
+            for (int k = u; k < (u == 0 ? 16 : 31); k++) rt[k] = rtab[i0 - k + 1];
+        uint32_t rd;
+        const uint32_t ra = bm_lane + ((uint32_t)(ii >> 5) << 8);
+        if (u == 0 || u == 16)  // the memory clobber holds the half's loads (merged) above it
+            asm volatile("ds_read_b32 %0, %1" : "=v"(rd) : "v"(ra) : "memory");
+        else
+            asm volatile("ds_read_b32 %0, %1" : "=v"(rd) : "v"(ra));
+        const int slot = 30 - u;
+        const uint32_t rv = ring[slot];
+        ring[slot] = rv - ring[(slot + 28) % 31];
+        const uint32_t j = I24 ? mod_rup_i24(rv >> 1, rt[u], ii + 1)
+                               : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rd), "+v"(prev));
+        if (u > 0) nw |= __builtin_amdgcn_ubfe(prev, ppos, 1) << (u - 1);
+        const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)rd, ii & 31, 1);  // bm[i]
+        const uint32_t bit = 1u << (j & 31);
+        prev = lds_mskor_rtn(lds_word_addr(bm_lane, j), bit, bsp & bit);
+        ppos = j;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(prev) : : "memory");
+    return nw | (__builtin_amdgcn_ubfe(prev, ppos, 1) << 30);
+}
+
 // the block that straddles s, and the last block that runs below step 1: at most two per
 // iteration, so each step is done on its own (compiler-tracked atomics; keeps the kernel's
 // register budget at the other blocks' level).  Steps below 1 do nothing.
@@ -510,9 +556,11 @@ __global__ __launch_bounds__(64) void sampler_kernel(
         else if (i - 30 >= s)
             word = replay_block_draws<false>(ring, bm, lane, i, rtab);
         else if (i < s && i - 30 >= 255)
-            word = replay_block_prefix<true>(ring, bm, lane, i, rtab);
+            word = ERP_PREFIX_READ ? replay_block_prefix_rd<true>(ring, bm, lane, i, rtab)
+                                   : replay_block_prefix<true>(ring, bm, lane, i, rtab);
         else if (i < s && i - 30 >= 1)
-            word = replay_block_prefix<false>(ring, bm, lane, i, rtab);
+            word = ERP_PREFIX_READ ? replay_block_prefix_rd<false>(ring, bm, lane, i, rtab)
+                                   : replay_block_prefix<false>(ring, bm, lane, i, rtab);
         else
             word = replay_block_mixed(ring, bm, lane, i, s, rtab);
         emitted += __builtin_popcount(word);
