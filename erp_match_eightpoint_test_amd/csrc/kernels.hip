@@ -2445,8 +2445,18 @@ __global__ __launch_bounds__(1024) void consensus_select_kernel(const int32_t* _
         if (tid == 0) nsurv[p] = 0;
         return;
     }
+    // 4 independent loads in flight per thread (one block per pair: at configs[4]'s K ~ 89k
+    // the loops are load-latency bound)
     double m = __builtin_huge_val();
-    for (int k = tid; k < K; k += 1024) m = fmin(m, U[k]);
+    for (int k0 = 0; k0 < K; k0 += 4096) {
+        double u[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = k0 + j * 1024 + tid;
+            u[j] = k < K ? U[k] : __builtin_huge_val();
+        }
+        m = fmin(m, fmin(fmin(u[0], u[1]), fmin(u[2], u[3])));
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o, 64));
     if ((tid & 63) == 0) sm[tid >> 6] = m;
@@ -2458,16 +2468,25 @@ __global__ __launch_bounds__(1024) void consensus_select_kernel(const int32_t* _
     if (tid == 0) ws[0] = 0;
     __syncthreads();
     const int lane = tid & 63;
-    for (int k0 = 0; k0 < K; k0 += 1024) {
-        const int k = k0 + tid;
-        const bool keep = k < K && L[k] <= minub;
-        if (k < K && !keep) Tm[k] = __builtin_huge_val();
-        const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
-        if (bal) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&ws[0], __builtin_popcountll(bal));
-            base = __shfl(base, 0, 64);
-            if (keep) S[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = k;
+    for (int k0 = 0; k0 < K; k0 += 4096) {
+        double l[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = k0 + j * 1024 + tid;
+            l[j] = k < K ? L[k] : __builtin_huge_val();
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = k0 + j * 1024 + tid;
+            const bool keep = k < K && l[j] <= minub;
+            if (k < K && !keep) Tm[k] = __builtin_huge_val();
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
+            if (bal) {
+                int base = 0;
+                if (lane == 0) base = atomicAdd(&ws[0], __builtin_popcountll(bal));
+                base = __shfl(base, 0, 64);
+                if (keep) S[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = k;
+            }
         }
     }
     __syncthreads();
@@ -2566,12 +2585,19 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     } else {
         double v = __builtin_huge_val();
         int bi = 0x7fffffff;
-        for (int k = tid; k < K; k += 1024) {
-            const double t = Tm[k];
-            if (t < v) {  // NaN never compares less; strided order keeps the first index
-                v = t;
-                bi = k;
+        for (int k0 = 0; k0 < K; k0 += 4096) {  // 4 loads in flight per thread
+            double t[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = k0 + j * 1024 + tid;
+                t[j] = k < K ? Tm[k] : __builtin_huge_val();
             }
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                if (t[j] < v) {  // NaN never compares less; increasing k keeps the first index
+                    v = t[j];
+                    bi = k0 + j * 1024 + tid;
+                }
         }
         sv[tid] = v;
         si[tid] = bi;
@@ -2594,14 +2620,45 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
         // them in row order (contiguous row ranges per thread + an ordered scan: deterministic,
         // and the lowest index of a run of identical rows is always kept)
         const double tol = 1e-9 * fabs(bv) + 1e-300;
-        const int per = (K + 1023) / 1024;
-        const int ka = min(K, tid * per), kb = min(K, ka + per);
+        // count (coalesced); at most 64 candidates (the usual case: 1) are gathered in any order
+        // and ranked by row index; more take the ordered contiguous-range scan
         int cnt = 0;
-        for (int k = ka; k < kb; k++) cnt += Tm[k] <= bv + tol;
+        for (int k0 = 0; k0 < K; k0 += 4096) {
+            double t[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = k0 + j * 1024 + tid;
+                t[j] = k < K ? Tm[k] : __builtin_huge_val();
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) cnt += t[j] <= bv + tol;
+        }
         int nc;
-        int pos = block_exclusive_scan<1024>(cnt, ws, &nc);
-        for (int k = ka; k < kb && pos < 64; k++)
-            if (Tm[k] <= bv + tol) cand[pos++] = k;
+        block_exclusive_scan<1024>(cnt, ws, &nc);
+        if (nc <= 64) {
+            __shared__ int gat[64];
+            __shared__ int ng;
+            if (tid == 0) ng = 0;
+            __syncthreads();
+            for (int k = tid; k < K; k += 1024)
+                if (Tm[k] <= bv + tol) gat[atomicAdd(&ng, 1)] = k;
+            __syncthreads();
+            if (tid < nc) {
+                const int me = gat[tid];
+                int rank = 0;
+                for (int d = 0; d < nc; d++) rank += gat[d] < me;
+                cand[rank] = me;
+            }
+        } else {
+            const int per = (K + 1023) / 1024;
+            const int ka = min(K, tid * per), kb = min(K, ka + per);
+            int c2 = 0;
+            for (int k = ka; k < kb; k++) c2 += Tm[k] <= bv + tol;
+            int nc2;
+            int pos = block_exclusive_scan<1024>(c2, ws, &nc2);
+            for (int k = ka; k < kb && pos < 64; k++)
+                if (Tm[k] <= bv + tol) cand[pos++] = k;
+        }
         __syncthreads();
         if (nc > 1) {
             const int n = nc < 64 ? nc : 64;
