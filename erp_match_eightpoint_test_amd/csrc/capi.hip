@@ -16,6 +16,13 @@
 #include "../../include/erp_match.h"
 #include "erp_kernels.hpp"
 
+// eigen stage fused into the Gram kernel (kernels.hip gram_mfma_kernel: no Gram round trip
+// through HBM for the common s >= 9 pairs): 1 = the inverse iteration, 2 = and the estimate;
+// 0 = the separate eigen_kernel / estimate_kernel, for A/B
+#ifndef ERP_FUSE_EIGEN
+#define ERP_FUSE_EIGEN 0
+#endif
+
 namespace {
 
 struct DevBuf {
@@ -430,12 +437,14 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
         StageTimer _t(ctx, ERP_STAGE_GRAM, st);
         ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
                                      cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
-                                     out ? out->samples : nullptr, st));
+                                     out ? out->samples : nullptr,
+                                     ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr,
+                                     ERP_FUSE_EIGEN == 2 ? hyps : nullptr, cfg->valid_abs, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
-        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh,
-                                 cfg->sample_frac, cfg->valid_abs, (double*)c->gfin.p, hyps, st));
+        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
+                                 cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN));
     }
     return ERP_OK;
 }

@@ -109,17 +109,23 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
 constexpr int kRecipTable = 65538;
 hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st);
 // Gram of every iteration's sample on int8 MFMA (exact fixed-point sums) -> gram[p][36][iters];
-// limbs = scratch of gram_limbs_bytes(sh); samples (debug, may be NULL) = the sampled indices
+// limbs = scratch of gram_limbs_bytes(sh); samples (debug, may be NULL) = the sampled indices.
+// evec != NULL fuses the eigen stage's inverse iteration (pairs with s >= 9) into the Gram
+// kernel: evec[p][9][iters] written there, and the Gram written to HBM only for pairs with
+// s < 9 and for the iterations whose inverse iteration did not settle (evec NaN); then call
+// launch_eigen with fused = 1.  hyps != NULL as well: the settled lanes' estimates too (fused = 2:
+// the fallback and thin eigen kernels then write their own lanes' records, no estimate_kernel)
 size_t gram_limbs_bytes(const BatchShape& sh);
 hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint32_t* selw,
                             const BatchShape& sh, double sample_frac, int8_t* limbs,
-                            double* gram, int32_t* samples, hipStream_t st);
+                            double* gram, int32_t* samples, double* evec,
+                            erp_hypothesis* hyps, double valid_abs, hipStream_t st);
 
 // selected singular vector per iteration from the Grams gram[p][36][iters] -> evec[p][9][iters],
 // then the estimate (rank-2 fix, decomposition, Euler angles, validity) -> hyps
 hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
                         double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
-                        hipStream_t st);
+                        hipStream_t st, int fused = 0);
 // R_vec_arr / T_vec_arr in push order + K + bounding-box scale; vchunk = scratch of
 // valid_chunk_bytes(sh) (per 1024-iteration chunk: count and bounding box)
 size_t valid_chunk_bytes(const BatchShape& sh);

@@ -577,6 +577,24 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     if (emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
 }
 
+// the estimate of one iteration from its selected vector e (rank-2 fix, decomposition, Euler
+// angles, validity) into its hypothesis record
+__device__ __forceinline__ void estimate_store(const double* e, double valid_abs,
+                                               erp_hypothesis* __restrict__ o) {
+    Hyp hy;
+    estimate_from_e(e, valid_abs, hy);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        o->R1[k] = hy.R1[k];
+        o->R2[k] = hy.R2[k];
+        o->T[k] = hy.T[k];
+    }
+    o->R1_valid = hy.R1_valid;
+    o->R2_valid = hy.R2_valid;
+#pragma unroll
+    for (int k = 0; k < 9; k++) o->E[k] = hy.E[k];
+}
+
 // ---- Gram on int8 MFMA: exact fixed-point sums -------------------------------------------
 // G_h = sum over the sampled rows i of P_i, P_i = (l l^T) x (r r^T) (36 distinct values), is a
 // product of the 0/1 selection matrix (iterations x rows) with P (rows x 36).  Each P_i value
@@ -692,7 +710,8 @@ typedef const __attribute__((address_space(1))) void* glb_vptr;
 __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma_kernel(
     const int32_t* __restrict__ counts, const int8_t* __restrict__ limbs,
     const uint32_t* __restrict__ selw, int iters, int nwaves, int nbw, double sample_frac,
-    double* __restrict__ gram, int nhb) {
+    double* __restrict__ gram, int nhb, double* __restrict__ evec,
+    erp_hypothesis* __restrict__ hyps, double valid_abs) {
     __shared__ __align__(16) int8_t lds[kGramRing * kGramSlotBytes];
     // XCD-aware block order (1-D grid of nhb iteration blocks x pairs): workgroups go to the 8
     // XCDs round-robin by linear id, so XCD x takes the contiguous logical range
@@ -796,6 +815,50 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
     // recombine: row = (k & 3) + 8 (k >> 2) + 4 hh; entry r from tiles 0..5 of this lane,
     // entries 32..35 from tile 6 (lane 4 limb + e)
     double* go = gram + (size_t)p * 36 * iters;
+    if (evec && s >= 9) {  // uniform over the block
+        // fused eigen stage: the block's 128 Grams go through LDS (the ring, now idle) instead
+        // of an HBM round trip; waves 0 and 1 then run the inverse iteration of eigen_kernel
+        // on one iteration per lane.  Only the lanes that do not settle write their Gram to HBM
+        // (for eigen_fallback_kernel, which finds them by the NaN in evec).  hyps != NULL: the
+        // settled lanes also run the estimate (estimate_kernel's work) here.
+        constexpr int kStg = kGramIters + 1;  // [36][kStg] doubles: odd stride, no bank conflicts
+        static_assert(36 * kStg * 8 <= kGramRing * kGramSlotBytes, "Gram stage fits the ring");
+        double* stg = reinterpret_cast<double*>(lds);
+        __syncthreads();  // every wave's last fragment reads have returned
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const int row = wv * 32 + (k & 3) + 8 * (k >> 2) + 4 * hh;
+            long long v = 0;
+#pragma unroll
+            for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[t][k] << (8 * t);
+            long long v2 = 0;
+            const int x = acc[kGramLimbs][k];
+#pragma unroll
+            for (int t = 0; t < kGramLimbs; t++)
+                v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
+            stg[r * kStg + row] = (double)v * (1.0 / kGramScale);
+            if (r < 4) stg[(32 + r) * kStg + row] = (double)v2 * (1.0 / kGramScale);
+        }
+        __syncthreads();
+        if (wv >= kGramIters / 64) return;
+        const int hl = wv * 64 + lane, h = hb + hl;
+        double e[9];
+        const bool ok = gram_min_eigvec9_inv(stg, kStg, hl, e);
+        if (h >= iters) return;
+        if (!ok) {
+            e[0] = __builtin_nan("");
+#pragma unroll 4
+            for (int k = 0; k < 36; k++) go[(size_t)k * iters + h] = stg[k * kStg + hl];
+        } else if (hyps) {
+            estimate_store(e, valid_abs, hyps + (size_t)p * iters + h);
+            evec[(size_t)p * 9 * iters + h] = 0.0;  // settled (eigen_fallback_kernel skips it)
+            return;
+        }
+        double* eo = evec + (size_t)p * 9 * iters + h;
+#pragma unroll
+        for (int k = 0; k < 9; k++) eo[(size_t)k * iters] = e[k];
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const int row = (k & 3) + 8 * (k >> 2) + 4 * hh;
@@ -880,7 +943,9 @@ template <bool THIN>
 __global__ __launch_bounds__(64) void eigen_kernel(const int32_t* __restrict__ counts,
                                                    const double* __restrict__ gram, int iters,
                                                    double sample_frac,
-                                                   double* __restrict__ evec) {
+                                                   double* __restrict__ evec,
+                                                   erp_hypothesis* __restrict__ hyps,
+                                                   double valid_abs) {
     const int p = blockIdx.y;
     const int h = blockIdx.x * 64 + threadIdx.x;
     const int M = counts[p];
@@ -899,6 +964,10 @@ __global__ __launch_bounds__(64) void eigen_kernel(const int32_t* __restrict__ c
     } else if (!gram_min_eigvec9_inv(gi, iters, 0, e)) {
         e[0] = __builtin_nan("");  // not settled: eigen_fallback_kernel takes the Jacobi path
     }
+    if (THIN && hyps) {  // the fused pipeline has no estimate_kernel
+        estimate_store(e, valid_abs, hyps + (size_t)p * iters + h);
+        return;
+    }
     double* eo = evec + (size_t)p * 9 * iters + h;
 #pragma unroll
     for (int k = 0; k < 9; k++) eo[(size_t)k * iters] = e[k];
@@ -909,7 +978,9 @@ __global__ __launch_bounds__(64) void eigen_kernel(const int32_t* __restrict__ c
 __global__ __launch_bounds__(64) void eigen_fallback_kernel(const int32_t* __restrict__ counts,
                                                             const double* __restrict__ gram,
                                                             int iters, double sample_frac,
-                                                            double* __restrict__ evec) {
+                                                            double* __restrict__ evec,
+                                                            erp_hypothesis* __restrict__ hyps,
+                                                            double valid_abs) {
     const int p = blockIdx.y;
     const int h = blockIdx.x * 64 + threadIdx.x;
     const int M = counts[p];
@@ -919,6 +990,10 @@ __global__ __launch_bounds__(64) void eigen_fallback_kernel(const int32_t* __res
     if (!__builtin_isnan(eo[0])) return;
     double e[9];
     gram_min_eigvec9_jacobi(gram + (size_t)p * 36 * iters + h, iters, 0, e);
+    if (hyps) {  // the fused pipeline has no estimate_kernel
+        estimate_store(e, valid_abs, hyps + (size_t)p * iters + h);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < 9; k++) eo[(size_t)k * iters] = e[k];
 }
@@ -941,19 +1016,7 @@ __global__ __launch_bounds__(64) ERP_EST_ATTR void estimate_kernel(const int32_t
     double e[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) e[k] = ei[(size_t)k * iters];
-    Hyp hy;
-    estimate_from_e(e, valid_abs, hy);
-    erp_hypothesis* o = hyps + (size_t)p * iters + h;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        o->R1[k] = hy.R1[k];
-        o->R2[k] = hy.R2[k];
-        o->T[k] = hy.T[k];
-    }
-    o->R1_valid = hy.R1_valid;
-    o->R2_valid = hy.R2_valid;
-#pragma unroll
-    for (int k = 0; k < 9; k++) o->E[k] = hy.E[k];
+    estimate_store(e, valid_abs, hyps + (size_t)p * iters + h);
 }
 
 // push R1 (if valid) then R2 (if valid) per iteration, in iteration order
@@ -2808,13 +2871,15 @@ size_t gram_limbs_bytes(const BatchShape& sh) {
 
 hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint32_t* selw,
                             const BatchShape& sh, double sample_frac, int8_t* limbs,
-                            double* gram, int32_t* samples, hipStream_t st) {
+                            double* gram, int32_t* samples, double* evec,
+                            erp_hypothesis* hyps, double valid_abs, hipStream_t st) {
     const int nwaves = (sh.iters + 63) / 64;
     hipLaunchKernelGGL(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
                        pts, sh.max_nq, sh.sel_words, limbs);
     const int nhb = (sh.iters + kGramIters - 1) / kGramIters;
     hipLaunchKernelGGL(gram_mfma_kernel, dim3(nhb * sh.n_pairs), dim3(64 * kGramWaves), 0, st, counts, limbs,
-                       selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb);
+                       selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb, evec, hyps,
+                       valid_abs);
     if (samples)
         hipLaunchKernelGGL(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
                            sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);
@@ -2828,17 +2893,22 @@ hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream
 
 hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
                         double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
-                        hipStream_t st) {
+                        hipStream_t st, int fused) {
     dim3 grid((sh.iters + 63) / 64, sh.n_pairs);
-    hipLaunchKernelGGL(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters,
-                       sample_frac, evec);
+    // fused >= 1: gram_mfma_kernel ran the inverse iteration (s >= 9) already; fused == 2: and
+    // the estimate of its settled lanes, the fallback / thin kernels estimate their own lanes
+    erp_hypothesis* own = fused == 2 ? hyps : nullptr;
+    if (!fused)
+        hipLaunchKernelGGL(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters,
+                           sample_frac, evec, nullptr, valid_abs);
     hipLaunchKernelGGL(eigen_fallback_kernel, grid, dim3(64), 0, st, counts, gram, sh.iters,
-                       sample_frac, evec);
+                       sample_frac, evec, own, valid_abs);
     // (M is only known on the device: the thin instantiation returns at once for s >= 9)
     hipLaunchKernelGGL(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters,
-                       sample_frac, evec);
-    hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
-                       sample_frac, valid_abs, hyps);
+                       sample_frac, evec, own, valid_abs);
+    if (fused != 2)
+        hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
+                           sample_frac, valid_abs, hyps);
     return hipGetLastError();
 }
 
