@@ -20,7 +20,7 @@
 // through HBM for the common s >= 9 pairs): 1 = the inverse iteration, 2 = and the estimate;
 // 0 = the separate eigen_kernel / estimate_kernel, for A/B
 #ifndef ERP_FUSE_EIGEN
-#define ERP_FUSE_EIGEN 0
+#define ERP_FUSE_EIGEN 1
 #endif
 
 namespace {
