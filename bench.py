@@ -6,9 +6,11 @@ descriptors + keypoints (W x H = 5376 x 2688), exact k=2 + ratio-0.3 match -> ga
 eight_point::find with 10 000 initial_guess iterations (glibc-replay sampler, reference
 defaults otherwise).  A step = B such pairs resident in HBM, split into S independent
 sub-batches (own context + HIP stream each, so one sub-batch's latency-bound kernels overlap
-the other's); every step recomputes everything (no cached outputs).  Defaults B = 384, S = 3 (three
-sub-batches of 128 on three HIP streams: the latency-bound consensus / eigen kernels of one
-overlap the VALU- and MFMA-bound kernels of the others; 15.4k pairs/s at B = 128, S = 1).
+the other's); every step recomputes everything (no cached outputs).  Defaults B = 768, S = 4 (four
+sub-batches of 192 on four HIP streams: the latency-bound consensus / eigen kernels of one
+overlap the VALU- and MFMA-bound kernels of the others; r02m sweep on one MI355X, 10 steps each:
+384 x 3 31.9-32.0k pairs/s, 768 x 3 32.4-33.3k, 768 x 4 33.6k, 1536 x 3 33.5k,
+profiles/r02m_streamsweep.txt).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs B] [--streams S] [--iters I]
 
@@ -43,8 +45,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pairs", type=int, default=384, help="pairs per step per GPU")
-    ap.add_argument("--streams", type=int, default=3,
+    ap.add_argument("--pairs", type=int, default=768, help="pairs per step per GPU")
+    ap.add_argument("--streams", type=int, default=4,
                     help="independent sub-batches (own context + HIP stream) per step")
     ap.add_argument("--iters", type=int, default=10000)
     ap.add_argument("--kpts", type=int, default=4096)
