@@ -22,6 +22,10 @@
 #ifndef ERP_FUSE_EIGEN
 #define ERP_FUSE_EIGEN 1
 #endif
+// hypothesis records' E written only when the caller asked for the records (out->hyps)
+#ifndef ERP_SKIP_E
+#define ERP_SKIP_E 1
+#endif
 
 namespace {
 
@@ -444,7 +448,8 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
     {
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
         ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
-                                 cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN));
+                                 cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
+                                 ERP_SKIP_E ? (out && out->hyps) : true));
     }
     return ERP_OK;
 }

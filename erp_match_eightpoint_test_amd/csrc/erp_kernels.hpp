@@ -125,7 +125,9 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
 // then the estimate (rank-2 fix, decomposition, Euler angles, validity) -> hyps
 hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
                         double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
-                        hipStream_t st, int fused = 0);
+                        hipStream_t st, int fused = 0, bool want_e = true);
+// (want_e = false: estimate_kernel leaves the records' E unwritten -- the batch pipeline when the
+// caller did not ask for the hypothesis records; nothing downstream reads E)
 // R_vec_arr / T_vec_arr in push order + K + bounding-box scale; vchunk = scratch of
 // valid_chunk_bytes(sh) (per 1024-iteration chunk: count and bounding box)
 size_t valid_chunk_bytes(const BatchShape& sh);

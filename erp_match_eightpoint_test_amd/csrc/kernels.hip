@@ -580,7 +580,8 @@ __global__ __launch_bounds__(64) void sampler_kernel(
 // the estimate of one iteration from its selected vector e (rank-2 fix, decomposition, Euler
 // angles, validity) into its hypothesis record
 __device__ __forceinline__ void estimate_store(const double* e, double valid_abs,
-                                               erp_hypothesis* __restrict__ o) {
+                                               erp_hypothesis* __restrict__ o,
+                                               bool with_e = true) {
     Hyp hy;
     estimate_from_e(e, valid_abs, hy);
 #pragma unroll
@@ -591,6 +592,7 @@ __device__ __forceinline__ void estimate_store(const double* e, double valid_abs
     }
     o->R1_valid = hy.R1_valid;
     o->R2_valid = hy.R2_valid;
+    if (!with_e) return;  // E is only read when the caller asked for the records
 #pragma unroll
     for (int k = 0; k < 9; k++) o->E[k] = hy.E[k];
 }
@@ -1006,7 +1008,8 @@ __global__ __launch_bounds__(64) void eigen_fallback_kernel(const int32_t* __res
 __global__ __launch_bounds__(64) ERP_EST_ATTR void estimate_kernel(const int32_t* __restrict__ counts,
                                                       const double* __restrict__ evec, int iters,
                                                       double sample_frac, double valid_abs,
-                                                      erp_hypothesis* __restrict__ hyps) {
+                                                      erp_hypothesis* __restrict__ hyps,
+                                                      int with_e) {
     const int p = blockIdx.y;
     const int h = blockIdx.x * 64 + threadIdx.x;
     const int M = counts[p];
@@ -1016,7 +1019,7 @@ __global__ __launch_bounds__(64) ERP_EST_ATTR void estimate_kernel(const int32_t
     double e[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) e[k] = ei[(size_t)k * iters];
-    estimate_store(e, valid_abs, hyps + (size_t)p * iters + h);
+    estimate_store(e, valid_abs, hyps + (size_t)p * iters + h, with_e != 0);
 }
 
 // push R1 (if valid) then R2 (if valid) per iteration, in iteration order
@@ -2893,7 +2896,7 @@ hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream
 
 hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
                         double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
-                        hipStream_t st, int fused) {
+                        hipStream_t st, int fused, bool want_e) {
     dim3 grid((sh.iters + 63) / 64, sh.n_pairs);
     // fused >= 1: gram_mfma_kernel ran the inverse iteration (s >= 9) already; fused == 2: and
     // the estimate of its settled lanes, the fallback / thin kernels estimate their own lanes
@@ -2908,7 +2911,7 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
                        sample_frac, evec, own, valid_abs);
     if (fused != 2)
         hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
-                           sample_frac, valid_abs, hyps);
+                           sample_frac, valid_abs, hyps, (int)want_e);
     return hipGetLastError();
 }
 
