@@ -123,6 +123,9 @@ class feature_matcher:  # noqa: N801  (reference class name)
         im_left, im_right = _img_dev(im_left), _img_dev(im_right)
         if im_left.shape != im_right.shape:
             raise ValueError("draw_match: the two images differ in size")
+        if im_left.device != im_right.device or im_left.device.index != self.ctx.device:
+            raise ValueError(f"draw_match: images must be on the context's device "
+                             f"cuda:{self.ctx.device}")
         H, W = im_left.shape[:2]
         kl, kr = _keys_dev(key_left, im_left.device), _keys_dev(key_right, im_left.device)
         m = min(kl.shape[0], kr.shape[0])
@@ -250,10 +253,14 @@ class epipolar_tool:  # noqa: N801  (reference class name)
         self.im_width, self.im_height = int(im_width), int(im_height)
         self.epipole_mat_width, self.epipole_mat_height = int(output_width), int(output_height)
         self.seed, self.offset = int(seed), int(offset)
-        self.random_idx = np.zeros(max(self.n_key, 0), np.int32)
         if not (1 <= self.match_size and 0 <= self.n_key <= min(7, self.match_size)):
             raise ErpError(capi.ERP_INVALID_ARG,
                            "epipolar_tool: need 0 <= test_key_num <= min(7, match_size)")
+        # the constructor's choice (src/epipolar_tool.cpp:13-16), available before any draw
+        self.random_idx = np.zeros(self.n_key, np.int32)
+        check(self.ctx.L.erp_random_shuffle_prefix(self.seed, self.offset, self.match_size,
+                                                   self.n_key, _np_ptr(self.random_idx)),
+              "random_shuffle_prefix")
 
     def draw_epipole(self, test_E_mat):  # noqa: N803  (reference argument name)
         import torch

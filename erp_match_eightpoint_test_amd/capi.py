@@ -91,7 +91,8 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_vertical_rotate_dev", "erp_eular2rot", "erp_rot2eular", "erp_rot_from_vec",
             "erp_inv3", "erp_rectify_matrices", "erp_consensus_hyps_shard_dev",
             "erp_consensus_hyps_finish_dev", "erp_surf_params_default",
-            "erp_surf_detect_compute_dev", "erp_epipolar_draw_dev", "erp_draw_match_dev"]
+            "erp_surf_detect_compute_dev", "erp_epipolar_draw_dev", "erp_draw_match_dev",
+            "erp_random_shuffle_prefix"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
@@ -188,6 +189,7 @@ def load(build_if_missing: bool = False):
     L.erp_epipolar_draw_dev.argtypes = [P, P, P, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
                                         C.c_int32, C.c_int32, C.c_uint32, C.c_uint64, P, P, P, P]
     L.erp_draw_match_dev.argtypes = [P, P, P, C.c_int32, C.c_int32, P, P, C.c_int32, P, P]
+    L.erp_random_shuffle_prefix.argtypes = [C.c_uint32, C.c_uint64, C.c_int32, C.c_int32, P]
     L.erp_stage_name.argtypes = [C.c_int32]
     L.erp_stage_name.restype = C.c_char_p
     L.erp_ctx_stage_times.argtypes = [P, P, P]

@@ -165,6 +165,16 @@ struct CtxCall {
     CtxCall& operator=(const CtxCall&) = delete;
 };
 
+// The host-pointer entry points that write the shared scratch with blocking copies (null
+// stream): join the context's call order and wait on the host for the previous call's device
+// work first -- the null stream does not synchronise with non-blocking streams, so an earlier
+// *_dev call on such a stream may still be reading the buffers about to be overwritten.
+struct HostCtxCall : CtxCall {
+    explicit HostCtxCall(erp_ctx* c_) : CtxCall(c_, nullptr) {
+        if (c->pending) (void)hipEventSynchronize(c->done);
+    }
+};
+
 }  // namespace
 
 extern "C" {
@@ -195,9 +205,11 @@ void* erp_ctx_scratch_internal(erp_ctx* ctx, int which, size_t bytes) {
 void* erp_ctx_stamp_buffer_internal(erp_ctx* ctx, size_t bytes, uint32_t* epoch, bool* fresh) {
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DevBuf& b = ctx->extra[12];
-    void* before = b.p;
+    // growth is detected by the size: hipMalloc may hand the freed address back for the larger
+    // block, whose tail then holds stale stamps
+    const size_t n_before = b.n;
     if (!ensure(b, bytes)) return nullptr;
-    *fresh = b.p != before || ctx->viz_epoch == 0 || ctx->viz_epoch >= 0xFFFFu;
+    *fresh = b.n != n_before || ctx->viz_epoch == 0 || ctx->viz_epoch >= 0xFFFFu;
     ctx->viz_epoch = *fresh ? 1u : ctx->viz_epoch + 1u;
     *epoch = ctx->viz_epoch;
     return b.p;
@@ -878,8 +890,8 @@ erp_status erp_initial_guess(erp_ctx* ctx, const double* h_bl, const double* h_b
         return ERP_INVALID_ARG;
     erp_pair_result r;
     {
-        std::lock_guard<std::recursive_mutex> lk(ctx->mu);
         ERP_CK(hipSetDevice(ctx->device));
+        HostCtxCall call(ctx);
         const erp::BatchShape sh = make_shape(1, m, m, cfg->iters, cfg->sample_frac);
         erp_status es = ensure_estimator(ctx, sh, nullptr);
         if (es != ERP_OK) return es;
@@ -911,8 +923,8 @@ erp_status erp_eight_point_estimation(erp_ctx* ctx, const double* h_bl, const do
                                       int32_t m, erp_hypothesis* h_out) {
     if (!ctx || m < 0 || !h_out || (m > 0 && (!h_bl || !h_br))) return ERP_INVALID_ARG;
     if (m < 1) return ERP_TOO_FEW_POINTS;
-    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     ERP_CK(hipSetDevice(ctx->device));
+    HostCtxCall call(ctx);
     if (!ensure(ctx->in_d, (size_t)m * 48 + 36 * 8 * 2 + sizeof(erp_hypothesis) + 64))
         return ERP_OUT_OF_MEMORY;
     std::vector<double> pts((size_t)m * 6);

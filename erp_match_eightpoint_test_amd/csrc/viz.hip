@@ -161,12 +161,22 @@ __global__ __launch_bounds__(256) void match_lines_kernel(const erp_point2f* __r
                                                           uint32_t* __restrict__ win) {
     const int i = blockIdx.x;
     if (i >= m) return;
-    const int ax = round_even(kl[i].x), ay = round_even(kl[i].y);
-    const int bx = round_even(kr[i].x), by = round_even(kr[i].y);
+    // a non-finite keypoint draws nothing; coordinates are clamped to +-2^20 before the
+    // conversion (defined behaviour, no int overflow below), and the walk along the major axis
+    // to the canvas (pixels outside it are never written)
+    if (!isfinite(kl[i].x) || !isfinite(kl[i].y) || !isfinite(kr[i].x) || !isfinite(kr[i].y))
+        return;
+    const float kLim = 1048576.f;
+    const int ax = round_even(fminf(fmaxf(kl[i].x, -kLim), kLim));
+    const int ay = round_even(fminf(fmaxf(kl[i].y, -kLim), kLim));
+    const int bx = round_even(fminf(fmaxf(kr[i].x, -kLim), kLim));
+    const int by = round_even(fminf(fmaxf(kr[i].y, -kLim), kLim));
     const int dx = bx - ax, dy = by - ay;
     const bool xmaj = abs(dx) >= abs(dy);
-    const int a0 = xmaj ? min(ax, bx) - 3 : min(ay, by) - 3;
-    const int a1 = xmaj ? max(ax, bx) + 3 : max(ay, by) + 3;
+    const int ext = xmaj ? W : H;
+    const int a0 = max(xmaj ? min(ax, bx) - 3 : min(ay, by) - 3, -3);
+    const int a1 = min(xmaj ? max(ax, bx) + 3 : max(ay, by) + 3, ext + 2);
+    if (a0 > a1) return;
     const double len2 = (double)dx * dx + (double)dy * dy;
     const int steps = (a1 - a0 + 1) * 12;
     for (int s = threadIdx.x; s < steps; s += 256) {
@@ -272,20 +282,9 @@ struct CallGuard {
 
 extern "C" {
 
-erp_status erp_epipolar_draw_dev(erp_ctx* ctx, const erp_point2f* h_key_left,
-                                 const erp_point2f* h_key_right, int32_t m, int32_t im_width,
-                                 int32_t im_height, int32_t out_width, int32_t out_height,
-                                 int32_t n_key, uint32_t seed, uint64_t offset, const double E[9],
-                                 uint8_t* d_out, int32_t* h_random_idx, void* stream) {
-    using namespace erp;
-    if (!ctx || !E || !d_out || m < 1 || n_key < 0 || n_key > kEpiMaxKeys || n_key > m ||
-        im_width < 1 || im_height < 1 || out_width < 1 || out_height < 1 || !h_key_left ||
-        !h_key_right || (int64_t)out_width * out_height > ((int64_t)1 << 30))
-        return ERP_INVALID_ARG;
-    if (hipSetDevice(erp_ctx_device_internal(ctx)) != hipSuccess) return ERP_HIP_ERROR;
-    const hipStream_t st = (hipStream_t)stream;
-    CallGuard call(ctx, st);
-    // iota + std::random_shuffle on the glibc rand() stream (src/epipolar_tool.cpp:13-16)
+erp_status erp_random_shuffle_prefix(uint32_t seed, uint64_t offset, int32_t m, int32_t n,
+                                     int32_t* h_idx) {
+    if (m < 1 || n < 0 || n > m || (n > 0 && !h_idx)) return ERP_INVALID_ARG;
     uint32_t ring[31];
     host_glibc_window(seed, offset, ring);
     int pos = 0;  // ring[pos] = r[n-31]
@@ -301,6 +300,26 @@ erp_status erp_epipolar_draw_dev(erp_ctx* ctx, const erp_point2f* h_key_left,
         const int32_t j = (int32_t)((long)rnd() % ((long)i + 1));
         if (i != j) std::swap(idx[i], idx[j]);
     }
+    for (int32_t t = 0; t < n; t++) h_idx[t] = idx[t];
+    return ERP_OK;
+}
+
+erp_status erp_epipolar_draw_dev(erp_ctx* ctx, const erp_point2f* h_key_left,
+                                 const erp_point2f* h_key_right, int32_t m, int32_t im_width,
+                                 int32_t im_height, int32_t out_width, int32_t out_height,
+                                 int32_t n_key, uint32_t seed, uint64_t offset, const double E[9],
+                                 uint8_t* d_out, int32_t* h_random_idx, void* stream) {
+    using namespace erp;
+    if (!ctx || !E || !d_out || m < 1 || n_key < 0 || n_key > kEpiMaxKeys || n_key > m ||
+        im_width < 1 || im_height < 1 || out_width < 1 || out_height < 1 || !h_key_left ||
+        !h_key_right || (int64_t)out_width * out_height > ((int64_t)1 << 30))
+        return ERP_INVALID_ARG;
+    if (hipSetDevice(erp_ctx_device_internal(ctx)) != hipSuccess) return ERP_HIP_ERROR;
+    const hipStream_t st = (hipStream_t)stream;
+    CallGuard call(ctx, st);
+    // iota + std::random_shuffle on the glibc rand() stream (src/epipolar_tool.cpp:13-16)
+    int32_t idx[kEpiMaxKeys];
+    if (n_key > 0) (void)erp_random_shuffle_prefix(seed, offset, m, n_key, idx);
     EpiKeys k{};
     k.n = n_key;
     static const uint8_t colors[kEpiMaxKeys][3] = {{0, 0, 255}, {0, 127, 255}, {0, 255, 255},

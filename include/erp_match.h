@@ -347,6 +347,11 @@ erp_status erp_epipolar_draw_dev(erp_ctx* ctx, const erp_point2f* h_key_left,
                                  int32_t im_height, int32_t out_width, int32_t out_height,
                                  int32_t n_key, uint32_t seed, uint64_t offset, const double E[9],
                                  uint8_t* d_out, int32_t* h_random_idx, void* stream);
+/* epipolar_tool's constructor choice (src/epipolar_tool.cpp:13-16), host only: the first n of
+   std::random_shuffle(iota(m)) on the glibc rand() stream at (seed, offset) into h_idx (n <= m;
+   the shuffle consumes m - 1 rand() calls).  The same indices erp_epipolar_draw_dev draws. */
+erp_status erp_random_shuffle_prefix(uint32_t seed, uint64_t offset, int32_t m, int32_t n,
+                                     int32_t* h_idx);
 /* feature_matcher::draw_match (src/feature_matcher.cpp:61-86): d_out (W x H CV_8UC3) = the
    grey images of d_left / d_right (cvtColor CV_RGB2GRAY, as the reference calls it on its BGR
    images) in channels 0 / 1, 0 in channel 2, with a line of thickness 5 from key_left[i] to

@@ -61,3 +61,15 @@ def test_gfx950_code_object():
     from erp_match_eightpoint_test_amd import _build
     data = open(_build.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+@pytest.mark.parametrize("seed,offset,m,n", [(1, 0, 300, 7), (1, 80, 4000, 7), (7, 3, 9, 5),
+                                             (1, 0, 1, 1), (1, 0, 20, 0), (3, 12345, 2, 2)])
+def test_random_shuffle_prefix_matches_glibc(lib, oracle, seed, offset, m, n):
+    """epipolar_tool's constructor choice (src/epipolar_tool.cpp:13-16): host-only entry point,
+    against the oracle's glibc rand() + std::random_shuffle (pinned to the real libc)"""
+    import numpy as np
+    out = np.full(max(n, 1), -1, np.int32)
+    assert lib.erp_random_shuffle_prefix(seed, offset, m, n, out.ctypes.data) == 0
+    assert (out[:n] == oracle.GlibcRand(seed, offset).random_array(m)[:n]).all()
+    assert lib.erp_random_shuffle_prefix(seed, offset, m, m + 1, out.ctypes.data) == 1

@@ -57,3 +57,32 @@ def test_oracle_reproduces_batch_pair0(oracle):
                     oracle.make_cfg(iters=int(g["iters"])))
     assert r["K"] == g["K"][0] and r["min_idx"] == g["min_idx"][0]
     assert np.array_equal(r["R"], g["R"][0]) and np.array_equal(r["T"], g["T"][0])
+
+
+def test_manual100k_fixture_consistent(oracle):
+    """configs[4] fixture (tests/golden/gen_manual100k.py): the pinned input is the bench's
+    manual workload, K equals the stored validity bits, and the oracle reproduces the first
+    2048 iterations' sample sets and records (the same glibc stream prefix)."""
+    import gen_manual100k as GM
+    g = _npz("find_manual_100_it100k.npz")
+    man = json.load(open(os.path.join(GOLD, "MANIFEST.json")))
+    with open(os.path.join(GOLD, "find_manual_100_it100k.npz"), "rb") as f:
+        assert hashlib.sha256(f.read()).hexdigest() == man["find_manual_100_it100k.npz"]
+    c = synth.make_correspondences(int(g["seed"]), m=100, outlier_frac=0.6)
+    assert np.array_equal(c["kp_l"], g["kl"]) and np.array_equal(c["kp_r"], g["kr"])
+    iters = int(g["iters"])
+    bits = np.unpackbits(g["valid_bits"])[: 2 * iters]
+    assert int(bits.sum()) == int(g["K"])
+    assert int(g["best_rows"][0]) == int(g["min_idx"])
+    head = GM.HEAD
+    r = oracle.find(int(g["W"]), int(g["H"]), g["kl"], g["kr"], oracle.make_cfg(iters=head),
+                    detail=True)
+    assert np.array_equal(G.set_hashes(r["samples"]), g["head_hash"])
+    assert np.array_equal(GM.chunk_hashes(G.set_hashes(r["samples"]), int(g["chunk"]))[:2],
+                          g["chunk_hash"][:2])
+    v = np.stack([r["hyp"]["R1_valid"], r["hyp"]["R2_valid"]], 1).astype(np.uint8).reshape(-1)
+    assert np.array_equal(v, bits[: 2 * head])
+    sel = np.arange(0, head, int(g["stride"]))
+    he = g["hyp_every"][: sel.size]
+    assert np.abs(r["hyp"]["R1"][sel] - he["R1"]).max() == 0
+    assert np.abs(r["hyp"]["T"][sel] - he["T"]).max() == 0

@@ -7,7 +7,11 @@
 * configs[3]: one 16384 x 16384 match on both matcher methods, bit-exact
   (src/feature_matcher.cpp:42-59);
 * configs[2]: a 32-pair batch of 2048-keypoint pairs at 10 000 iterations, the 8 fixture pairs'
-  records and match lists equal to the oracle's.
+  records and match lists equal to the oracle's;
+* configs[4]: the bench's manual workload (100 correspondences, 60 % outliers) at 100 000
+  iterations (K ~ 89k valid rotations): every iteration's validity, every 25th iteration's
+  record, K / min_idx / R / T / the winner's trimmed mean -- unsharded and through the
+  row-sharded consensus of 2 and 8 emulated ranks (tests/golden/gen_manual100k.py).
 
 The inputs are regenerated from their seeds and pinned by sha256 before anything is compared.
 """
@@ -156,3 +160,47 @@ def test_batch_2048_configs2_fixture(ctx):
         assert np.abs(r["T"] - g["T"][k]).max() <= 2e-6
         mt = outs["matches"][i, :M].cpu().numpy()
         assert hashlib.sha256(mt.view(np.uint8).tobytes()).hexdigest() == str(g["match_sha"][k])
+
+
+@pytest.mark.parametrize("shards", [1, 2, 8])
+def test_manual_100k_fixture(ctx, shards):
+    """configs[4] at full size against the oracle (src/eight_point.cpp:87-150, I = 100 000)."""
+    import ctypes as C
+    import torch
+    from erp_match_eightpoint_test_amd import capi, dist as D, hyps_to_numpy, results_to_numpy
+    g = _npz("find_manual_100_it100k.npz")
+    W, H, iters, m = int(g["W"]), int(g["H"]), int(g["iters"]), len(g["kl"])
+    dkl = torch.from_numpy(np.ascontiguousarray(g["kl"], np.float32)).cuda()
+    dkr = torch.from_numpy(np.ascontiguousarray(g["kr"], np.float32)).cuda()
+    if shards == 1:
+        cfg = capi.default_cfg(iters=iters)
+        res = torch.zeros(capi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+        hyp = torch.zeros((iters, capi.HYP_DTYPE.itemsize), dtype=torch.uint8, device="cuda")
+        assert ctx.L.erp_eight_point_find_dev(ctx.h, W, H, dkl.data_ptr(), dkr.data_ptr(), m,
+                                              C.byref(cfg), res.data_ptr(), hyp.data_ptr(),
+                                              torch.cuda.current_stream().cuda_stream) == 0
+    else:
+        res, hyp = D.find_hypothesis_sharded_dev(ctx, W, H, dkl, dkr, m, iters,
+                                                 emulate_world=shards)
+        hyp = hyp[:iters]
+    torch.cuda.synchronize()
+    r = results_to_numpy(res.view(1, -1))[0]
+    gh = hyps_to_numpy(hyp.unsqueeze(0))[0]
+    bits = np.unpackbits(g["valid_bits"])[: 2 * iters].reshape(iters, 2)
+    got = np.stack([gh["R1_valid"], gh["R2_valid"]], 1) != 0
+    # R1 / R2 order inside an iteration follows a noise-level sign (DESIGN.md 3.2): validity as
+    # a count per iteration, the records as sets
+    bad = np.nonzero(got.sum(1) != bits.sum(1))[0]
+    assert bad.size == 0, f"{bad.size} iterations differ in validity, first {bad[:8]}"
+    sel = np.arange(0, iters, int(g["stride"]))
+    oh, hh = g["hyp_every"], gh[sel]
+    same = np.maximum(np.abs(hh["R1"] - oh["R1"]).max(1), np.abs(hh["R2"] - oh["R2"]).max(1))
+    swap = np.maximum(np.abs(hh["R1"] - oh["R2"]).max(1), np.abs(hh["R2"] - oh["R1"]).max(1))
+    assert np.minimum(same, swap).max() <= 2e-6
+    assert np.abs(hh["T"] - oh["T"]).max() <= 2e-6
+    e = np.minimum(np.abs(hh["E"] - oh["E"]).max(1), np.abs(hh["E"] + oh["E"]).max(1))
+    assert e.max() <= 1e-6
+    assert int(r["status"]) == 0 and int(r["K"]) == int(g["K"])
+    assert int(r["min_idx"]) == int(g["min_idx"]), (int(r["min_idx"]), int(g["min_idx"]))
+    assert np.abs(r["R"] - g["R"]).max() <= 2e-6 and np.abs(r["T"] - g["T"]).max() <= 2e-6
+    assert abs(float(r["min_dist"]) - float(g["min_dist"])) <= 1e-12 * abs(float(g["min_dist"]))

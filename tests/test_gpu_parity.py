@@ -221,6 +221,45 @@ def test_find_thin_svd_edges(ctx, m):
             assert min(np.abs(a["E"] - b["E"]).max(), np.abs(a["E"] + b["E"]).max()) <= 1e-6
 
 
+def test_host_call_after_side_stream_call(gpu_lib, oracle):
+    """a host-pointer call (initial_guess, eight_point_estimation) right after an
+    async *_dev call on a non-blocking side stream, on ONE context, must not overwrite the
+    scratch the side stream is still reading: both results equal their standalone runs"""
+    import ctypes as C
+    import torch
+    from erp_match_eightpoint_test_amd import Context, capi, eight_point
+    g = _npz("find_400_it80.npz")
+    W, H, iters = int(g["W"]), int(g["H"]), 20000
+    ctx = Context(0)
+    solo_st, solo, _ = _run_find_dev(ctx, g["kl"], g["kr"], W, H, iters)
+    c2 = synth.make_correspondences(11, m=120, outlier_frac=0.2, W=2048, H=1024)
+    bl = oracle.pixel_to_bearing(2048, 1024, c2["kp_l"])
+    br = oracle.pixel_to_bearing(2048, 1024, c2["kp_r"])
+    ep = eight_point(ctx=ctx, iters=80)
+    R_solo, T_solo = ep.initial_guess(2048, 1024, bl, br)
+    est_solo = ep.eight_point_estimation(2048, 1024, bl, br)
+    side = torch.cuda.Stream()
+    cfg = capi.default_cfg(iters=iters)
+    dkl = torch.from_numpy(np.ascontiguousarray(g["kl"], np.float32)).cuda()
+    dkr = torch.from_numpy(np.ascontiguousarray(g["kr"], np.float32)).cuda()
+    res = torch.zeros(capi.RESULT_DTYPE.itemsize, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    for _ in range(3):
+        res.zero_()
+        torch.cuda.synchronize()
+        assert ctx.L.erp_eight_point_find_dev(ctx.h, W, H, dkl.data_ptr(), dkr.data_ptr(),
+                                              len(g["kl"]), C.byref(cfg), res.data_ptr(), None,
+                                              side.cuda_stream) == 0
+        R, T = ep.initial_guess(2048, 1024, bl, br)  # no sync in between
+        est = ep.eight_point_estimation(2048, 1024, bl, br)
+        side.synchronize()
+        r = res.cpu().numpy().view(capi.RESULT_DTYPE)[0]
+        assert r["status"] == solo["status"] == 0 and r["K"] == solo["K"]
+        assert np.array_equal(r["R"], solo["R"]) and np.array_equal(r["T"], solo["T"])
+        assert np.array_equal(R, R_solo) and np.array_equal(T, T_solo)
+        assert all(np.array_equal(a, b) for a, b in zip(est, est_solo))
+
+
 def test_find_too_few_points(ctx):
     from erp_match_eightpoint_test_amd import ErpError, eight_point
     ep = eight_point(ctx=ctx)

@@ -69,10 +69,11 @@ def test_epipolar_draw_matches_oracle(ctx, oracle, W, H, ow, oh, m, n_key, scale
     kr[: min(m, 3)] = np.array([[0.5, 0.5], [W - 0.5, H - 0.5], [W - 1, 3]], np.float32)[: min(m, 3)]
     E = _essential(rng, scale)
     tool = epipolar_tool(kl, kr, W, H, ow, oh, n_key, seed=seed, offset=offset, ctx=ctx)
+    before = tool.random_idx.copy()  # filled by the constructor, as the reference's
     got = tool.draw_epipole(E).cpu().numpy()
     want, idx, margin = oracle.epipolar_draw(kl, kr, W, H, ow, oh, n_key, E, seed=seed,
                                              offset=offset)
-    assert (tool.random_idx == idx).all()
+    assert (tool.random_idx == idx).all() and (before == idx).all()
     n_bad = _certify(oracle, got, want, kl, idx, W, H, E)
     print(f"\nepipolar {ow}x{oh}: {int(want.any(-1).sum())} drawn pixels, threshold margin "
           f"{margin:.3g}, {n_bad} certified near-threshold differences")
@@ -139,6 +140,48 @@ def test_draw_match_stamps_do_not_leak(ctx, oracle):
     assert (fm.draw_match(ta, tb, k, k.flip(0))[..., 2] != 0).any()
     none = torch.zeros((0, 2), dtype=torch.float32, device="cuda")
     assert (fm.draw_match(ta, tb, none, none).cpu().numpy() == oracle.draw_match(a, b, [], [])).all()
+
+
+def test_draw_match_canvas_grows_between_calls(oracle):
+    """one context, a small canvas then larger ones: the grown stamp buffer (possibly at the
+    freed address) must be cleared -- stale stamps of the small call must not show as lines"""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, feature_matcher
+    fm = feature_matcher(ctx=Context(0))
+    rng = np.random.default_rng(21)
+    for H, W, m in ((60, 100, 80), (200, 300, 0), (240, 400, 5), (500, 900, 0)):
+        a, b, ta, tb = _images(rng, H, W)
+        kl = rng.uniform(0, [W, H], (m, 2)).astype(np.float32)
+        kr = rng.uniform(0, [W, H], (m, 2)).astype(np.float32)
+        got = fm.draw_match(ta, tb, torch.from_numpy(kl).cuda(), torch.from_numpy(kr).cuda())
+        want = oracle.draw_match(a, b, kl, kr)
+        assert (got.cpu().numpy() == want).all(), (H, W, m)
+
+
+def test_draw_match_nonfinite_and_far_keypoints(ctx, oracle):
+    """a NaN keypoint draws nothing (as a zero-length line far off the canvas); an endpoint
+    1e30 px away draws like one at the 2^20 clamp (the walk is clipped to the canvas, bounded)"""
+    import torch
+    from erp_match_eightpoint_test_amd import feature_matcher
+    rng = np.random.default_rng(22)
+    a, b, ta, tb = _images(rng, 64, 128)
+    kl = np.array([[10, 10], [np.nan, 5], [20, 30], [5, 5]], np.float32)
+    kr = np.array([[100, 50], [30, 30], [1e30, 30], [60, 40]], np.float32)
+    got = feature_matcher(ctx=ctx).draw_match(ta, tb, torch.from_numpy(kl).cuda(),
+                                              torch.from_numpy(kr).cuda()).cpu().numpy()
+    kl2, kr2 = kl.copy(), kr.copy()
+    kl2[1] = kr2[1] = (-5000, -5000)
+    kr2[2] = (1048576, 30)
+    assert (got == oracle.draw_match(a, b, kl2, kr2)).all()
+
+
+def test_device_mismatch_rejected(ctx):
+    import torch
+    from erp_match_eightpoint_test_amd import feature_matcher
+    a = torch.zeros((8, 8, 3), dtype=torch.uint8)
+    fm = feature_matcher(ctx=ctx)
+    with pytest.raises((ValueError, TypeError)):
+        fm.draw_match(a, a, np.zeros((0, 2), np.float32), np.zeros((0, 2), np.float32))
 
 
 def test_do_all_match_output(ctx):
