@@ -127,6 +127,13 @@ def stage_work(stage, B, kpts, iters, res):
         flops = float(np.sum(nb * K * 8.0))  # 3 sub, 3 mul, 2 add per squared distance
         return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", \
             "8 fp32 ops per binned squared distance (binned_rows x K)"
+    if stage == "sampler_gram":
+        # the fused kernel: bound by the replay's VALU issue; its int8 MFMA work is reported
+        # beside (roofline["mfma_frac"])
+        ops = float(np.sum((M - 1) * iters * 4.0))
+        return ops, "Top/s", PEAK_VALU_OPS, "valu", \
+            "4 int/fp64 lane-ops per rand() draw (floor) of the fused sampler+Gram kernel; " \
+            "peak = wave64 2-cycle VALU issue"
     if stage == "sampler":
         ops = float(np.sum((M - 1) * iters * 4.0))  # per draw: recurrence, shift, remainder, test
         return ops, "Top/s", PEAK_VALU_OPS, "valu", \
@@ -671,6 +678,12 @@ def main():
                 "avg_launch_ms": avg_s * 1e3, "work_per_launch": amount, "work_note": note}
         if peak == PEAK_VALU_OPS:
             roof["frac_vs_4cycle_issue"] = achieved / PEAK_VALU_OPS_4CYC
+        if dom == "sampler_gram":  # the MFMA half of the fused kernel against its own roof
+            g = stage_work("gram", args.pairs, args.kpts, args.iters, res)
+            gops = g[0] / stages[dom][1]
+            roof["mfma_achieved"] = gops / avg_s / 1e12
+            roof["mfma_peak"] = PEAK_I8_MFMA
+            roof["mfma_frac"] = roof["mfma_achieved"] / PEAK_I8_MFMA
     stage_roofs = {}
     for k in stages:
         w = stage_work(k, args.pairs, args.kpts, args.iters, res)
@@ -734,6 +747,45 @@ def main():
                 "binned_rows_mean": float(hres["binned_rows"].mean())}
     cpu = None
     parity = None
+    multi = None
+    if world > 1 and gathered is not None:
+        # rank 0's self-check of the timed step's RCCL-gathered records (outside the timed
+        # region): the first pair of every rank's block recomputed here alone, byte for byte,
+        # and against the oracle (the CPU baseline itself runs at N = 1 only)
+        import oracle as O
+        O.build()
+        threads, _ = host_cpu_share()
+        b1cache = {}
+
+        def first_pair(r):
+            if r not in b1cache:
+                b1cache[r] = make_batch(r, 1, args.kpts, args.seed, args.inlier_frac, args.sigma)[0]
+            return b1cache[r]
+
+        ctx_c = Context(local)
+        ctx_c.set_matcher(0 if args.matcher == "mfma" else 1)
+        run_c = PairBatchRunner(ctx=ctx_c, iters=args.iters)
+
+        def rerun(r):
+            b = to_device([first_pair(r)], dev)
+            o = run_c.run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"], b["off_r"],
+                          b["width"], b["height"], b["max_nq"], b["max_nt"])
+            torch.cuda.synchronize()
+            return o["results"][0].cpu().numpy()
+
+        def ora(r):
+            p = first_pair(r)
+            mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=threads)
+            o = O.find(p["W"], p["H"], p["kp_l"][mt["queryIdx"]], p["kp_r"][mt["trainIdx"]],
+                       O.make_cfg(iters=args.iters))
+            return dict(o, M=len(mt))
+        multi = D.check_gathered(gathered.cpu().numpy(), args.pairs, world, rerun, ora)
+        multi["gathered_rows"] = int(gathered.shape[0])
+        parity = {"pairs_checked": world, "all_equal": bool(multi["records_identical"] and
+                                                            multi["oracle_all_equal"]),
+                  "fields": "first pair of every rank's block: gathered record byte-identical "
+                            "to a rank-0 recomputation; status, M, K, min_idx equal and R, T "
+                            "within 2e-6 of the oracle"}
     if world == 1 and not args.no_cpu_baseline:
         cpu, ora = cpu_baseline(pairs, args.iters, args.cpu_seconds)
         # untimed pass of sub-batch 0 (the first pairs, the ones the oracle ran) with the match
@@ -776,7 +828,8 @@ def main():
                   "M_mean": float(res["M"].mean()), "K_mean": float(res["K"].mean()),
                   "consensus_survivors": res["survivors"].tolist(),
                   "near_ties": res["near_ties"].tolist(), "parity": parity,
-                  "gathered_records": None if gathered is None else int(gathered.shape[0])},
+                  "gathered_records": None if gathered is None else int(gathered.shape[0]),
+                  "multi_rank": multi},
     }
     print(json.dumps(line))
     if dist is not None:

@@ -96,7 +96,7 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
-          "consensus_refine", "knn2_exact"]
+          "consensus_refine", "knn2_exact", "sampler_gram"]
 MATCHER_MFMA_FILTER = 0  # erp_matcher_method
 MATCHER_VALU_EXACT = 1
 

@@ -105,6 +105,9 @@ struct erp_ctx {
     // zoomed central references before the pre-pruning (opt-in ERP_ZOOM_REFS=1: measured no
     // fewer binned rows)
     int zoom_refs = getenv("ERP_ZOOM_REFS") ? atoi(getenv("ERP_ZOOM_REFS")) : 0;  // 2: all refs
+    // the sampler and the Gram as one kernel (sampler_gram_kernel) when the bitmaps fit;
+    // ERP_FUSE_SAMPLER=0 runs the two standalone kernels (A/B knob)
+    bool fuse_sampler = !getenv("ERP_FUSE_SAMPLER") || atoi(getenv("ERP_FUSE_SAMPLER")) != 0;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -443,13 +446,25 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
                                    (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
                                    (uint32_t*)c->wins.p, (uint32_t*)c->idx.p, flags, st, 0));
     }
-    {
-        StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
-        ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
-                                   (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
-                                   (uint32_t*)c->wins.p, (uint32_t*)c->idx.p, flags, st, 1));
-    }
-    {
+    if (c->fuse_sampler && ERP_FUSE_EIGEN != 2 && erp::sampler_gram_fits(sh)) {
+        {
+            StageTimer _t(ctx, ERP_STAGE_GRAM, st);
+            ERP_CK(erp::launch_gram_limbs(counts, (double*)c->pts.p, sh, (int8_t*)c->limbs.p, st));
+        }
+        {
+            StageTimer _t(ctx, ERP_STAGE_SAMPLER_GRAM, st);
+            ERP_CK(erp::launch_sampler_gram(
+                counts, (uint32_t*)c->wins.p, (int8_t*)c->limbs.p, (double*)c->rtab.p, sh,
+                cfg->sample_frac, flags, (uint32_t*)c->idx.p, out ? out->samples : nullptr,
+                (double*)c->gram.p, ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr, st));
+        }
+    } else {
+        {
+            StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
+            ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
+                                       (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
+                                       (uint32_t*)c->wins.p, (uint32_t*)c->idx.p, flags, st, 1));
+        }
         StageTimer _t(ctx, ERP_STAGE_GRAM, st);
         ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
                                      cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
@@ -590,7 +605,7 @@ const char* erp_stage_name(int32_t stage) {
         "knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler",
         "eigen", "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
         "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
-        "consensus_refine", "knn2_exact"};
+        "consensus_refine", "knn2_exact", "sampler_gram"};
     return (stage >= 0 && stage < ERP_STAGE_COUNT) ? names[stage] : "unknown";
 }
 

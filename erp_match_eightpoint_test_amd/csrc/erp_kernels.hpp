@@ -116,6 +116,18 @@ hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st)
 // launch_eigen with fused = 1.  hyps != NULL as well: the settled lanes' estimates too (fused = 2:
 // the fallback and thin eigen kernels then write their own lanes' records, no estimate_kernel)
 size_t gram_limbs_bytes(const BatchShape& sh);
+// the sampler and the Gram fused into one kernel (sampler_gram_kernel: the replay's selection
+// words stay in LDS); usable when the batch's bitmaps fit beside the LDS rings (max_s below
+// ~4000).  Runs gram_limbs first, then the fused kernel; selw (may be NULL) receives the
+// selection words too (only the debug `samples` output reads them).  Same outputs as
+// launch_sampler(part 1) + launch_gram_mfma with hyps == NULL (evec: the fused eigen stage).
+bool sampler_gram_fits(const BatchShape& sh);
+hipError_t launch_gram_limbs(const int32_t* counts, const double* pts, const BatchShape& sh,
+                             int8_t* limbs, hipStream_t st);
+hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* wins, const int8_t* limbs,
+                               const double* rtab, const BatchShape& sh, double sample_frac,
+                               int32_t* flags, uint32_t* selw, int32_t* samples, double* gram,
+                               double* evec, hipStream_t st);
 hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint32_t* selw,
                             const BatchShape& sh, double sample_frac, int8_t* limbs,
                             double* gram, int32_t* samples, double* evec,

@@ -337,13 +337,18 @@ __device__ __forceinline__ uint32_t mod_rup_i24(uint32_t x, double r, int d) {
 // where gfx950 returns 0 and drops the write (scripts/dev/lds_oob.hip: measured up to 512 KB,
 // i.e. j < 65536 = the keypoint cap).  The LDS ops' results are consumed kReplayLag steps
 // after issue, so the traffic streams without waits.
-// (bm_lane = LDS byte address of the lane's word 0; words are 256 B apart: the address is one
-// v_lshl_add_u32 of j >> 5)
+// (bm_lane = LDS byte address of the lane's word 0; words are 2^RS B apart -- 256 B for the
+// standalone sampler's [word][lane], 1 KB for the fused kernel's [word][wave][lane]: the address
+// is one v_lshl_add_u32 of j >> 5)
+template <int RS>
 __device__ __forceinline__ uint32_t lds_word_addr(uint32_t bm_lane, uint32_t j) {
     uint32_t a;
-    asm("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(a) : "v"(j >> 5), "v"(bm_lane));
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(a) : "v"(j >> 5), "i"(RS), "v"(bm_lane));
     return a;
 }
+// uint32 index of word w of the lane's bitmap column
+template <int RS>
+__device__ __forceinline__ int bm_index(int w, int lane) { return (w << (RS - 2)) + lane; }
 
 // replay blocks consume a step's LDS return `kReplayLag` steps after issuing it (fewer live
 // registers than consuming all 31 after the block: occupancy)
@@ -371,7 +376,7 @@ __device__ __forceinline__ void lds_wait_step(uint32_t& o, int v) {
 }
 
 // steps i >= s: one LDS op per draw, no clamp, no validity select (~10 VALU per draw)
-template <bool I24>
+template <bool I24, int RS = 8>
 __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uint32_t* bm,
                                                        int lane, int i0,
                                                        const double* __restrict__ rtab) {
@@ -391,7 +396,7 @@ __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uin
             ring[slot] = rv - ring[(slot + 28) % 31];
             const uint32_t j = I24 ? mod_rup_i24(rv >> 1, rt[u], ii + 1)
                                    : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
-            olds[u] = lds_mskor_rtn(lds_word_addr(bm_lane, j), 1u << (j & 31), zero);
+            olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), 1u << (j & 31), zero);
             pos[u] = j;
         }
         const int v = u - kReplayLag;
@@ -407,7 +412,7 @@ __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uin
 // constant-position bit extract, the bit copy bm[j] := bm[i] is one masked OR (returning old
 // bm[j]), and a step that writes inside the window updates it with one bfi (out-of-window j
 // lands on the unused bit 31).  ~17 VALU + 1 DS per step.
-template <bool I24>
+template <bool I24, int RS = 8>
 __device__ __forceinline__ uint32_t replay_block_prefix(uint32_t (&ring)[31], uint32_t* bm,
                                                         int lane, int i0,
                                                         const double* __restrict__ rtab) {
@@ -417,7 +422,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix(uint32_t (&ring)[31], ui
     for (int u = 0; u < 31; u++) rt[u] = rtab[i0 - u + 1];
     const int base = i0 - 30;  // >= 1
     const int wA = i0 >> 5, wB = base >> 5;
-    const uint32_t hi = bm[wA * 64 + lane], lo = bm[wB * 64 + lane];
+    const uint32_t hi = bm[bm_index<RS>(wA, lane)], lo = bm[bm_index<RS>(wB, lane)];
     uint32_t win = wA == wB ? (lo >> (base & 31)) : __builtin_amdgcn_alignbit(hi, lo, base & 31);
     uint32_t olds[31], pos[31];
     uint32_t nw = 0;
@@ -432,7 +437,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix(uint32_t (&ring)[31], ui
                                    : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
             const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)win, 30 - u, 1);  // bm[i]
             const uint32_t bit = 1u << (j & 31);
-            olds[u] = lds_mskor_rtn(lds_word_addr(bm_lane, j), bit, bsp & bit);
+            olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), bit, bsp & bit);
             pos[u] = j;
             const uint32_t t = min(j - (uint32_t)base, 31u);
             const uint32_t m = 1u << t;
@@ -454,7 +459,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix(uint32_t (&ring)[31], ui
 #ifndef ERP_PREFIX_READ
 #define ERP_PREFIX_READ 1
 #endif
-template <bool I24>
+template <bool I24, int RS = 8>
 __device__ __forceinline__ uint32_t replay_block_prefix_rd(uint32_t (&ring)[31], uint32_t* bm,
                                                            int lane, int i0,
                                                            const double* __restrict__ rtab) {
@@ -472,7 +477,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix_rd(uint32_t (&ring)[31],
 #pragma unroll
             for (int k = u; k < (u == 0 ? 16 : 31); k++) rt[k] = rtab[i0 - k + 1];
         uint32_t rd;
-        const uint32_t ra = bm_lane + ((uint32_t)(ii >> 5) << 8);
+        const uint32_t ra = bm_lane + ((uint32_t)(ii >> 5) << RS);
         if (u == 0 || u == 16)  // the memory clobber holds the half's loads (merged) above it
             asm volatile("ds_read_b32 %0, %1" : "=v"(rd) : "v"(ra) : "memory");
         else
@@ -486,7 +491,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix_rd(uint32_t (&ring)[31],
         if (u > 0) nw |= __builtin_amdgcn_ubfe(prev, ppos, 1) << (u - 1);
         const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)rd, ii & 31, 1);  // bm[i]
         const uint32_t bit = 1u << (j & 31);
-        prev = lds_mskor_rtn(lds_word_addr(bm_lane, j), bit, bsp & bit);
+        prev = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), bit, bsp & bit);
         ppos = j;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(prev) : : "memory");
@@ -496,6 +501,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix_rd(uint32_t (&ring)[31],
 // the block that straddles s, and the last block that runs below step 1: at most two per
 // iteration, so each step is done on its own (compiler-tracked atomics; keeps the kernel's
 // register budget at the other blocks' level).  Steps below 1 do nothing.
+template <int RS = 8>
 __device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uint32_t* bm,
                                                        int lane, int i0, int s,
                                                        const double* __restrict__ rtab) {
@@ -510,13 +516,28 @@ __device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uin
         const double r = rtab[ii + 1];
         const uint32_t j = mod_rup(rv >> 1, r, (double)(ii + 1));
         // bm[i] (read before the clear: j = i keeps the bit)
-        const uint32_t bi = ii < s ? (bm[(ii >> 5) * 64 + lane] >> (ii & 31)) & 1u : 0u;
-        uint32_t* wp = &bm[(j >> 5) * 64 + lane];  // j >= s: a cleared or out-of-allocation word
+        const uint32_t bi = ii < s ? (bm[bm_index<RS>(ii >> 5, lane)] >> (ii & 31)) & 1u : 0u;
+        uint32_t* wp = &bm[bm_index<RS>((int)(j >> 5), lane)];  // j >= s: a cleared or out-of-allocation word
         const uint32_t old = atomicAnd(wp, ~(1u << (j & 31)));
         if (ii < s) atomicOr(wp, bi << (j & 31));
         word |= __builtin_amdgcn_ubfe(old, j, 1) << u;
     }
     return word;
+}
+
+// the 31 reverse steps i .. i-30 of one lane's replay, by block kind (uniform: i and s are)
+template <int RS>
+__device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t* bm, int lane,
+                                                 int i, int s, const double* __restrict__ rtab) {
+    if (i - 30 >= s && i - 30 >= 255) return replay_block_draws<true, RS>(ring, bm, lane, i, rtab);
+    if (i - 30 >= s) return replay_block_draws<false, RS>(ring, bm, lane, i, rtab);
+    if (i < s && i - 30 >= 255)
+        return ERP_PREFIX_READ ? replay_block_prefix_rd<true, RS>(ring, bm, lane, i, rtab)
+                               : replay_block_prefix<true, RS>(ring, bm, lane, i, rtab);
+    if (i < s && i - 30 >= 1)
+        return ERP_PREFIX_READ ? replay_block_prefix_rd<false, RS>(ring, bm, lane, i, rtab)
+                               : replay_block_prefix<false, RS>(ring, bm, lane, i, rtab);
+    return replay_block_mixed<RS>(ring, bm, lane, i, s, rtab);
 }
 
 // One lane = one iteration; writes the iteration's selection bitmap in block space:
@@ -550,19 +571,7 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     int i = M - 1, b = 0, emitted = 0;
     uint32_t lastw = 0;
     while (i >= 1) {
-        uint32_t word;
-        if (i - 30 >= s && i - 30 >= 255)
-            word = replay_block_draws<true>(ring, bm, lane, i, rtab);
-        else if (i - 30 >= s)
-            word = replay_block_draws<false>(ring, bm, lane, i, rtab);
-        else if (i < s && i - 30 >= 255)
-            word = ERP_PREFIX_READ ? replay_block_prefix_rd<true>(ring, bm, lane, i, rtab)
-                                   : replay_block_prefix<true>(ring, bm, lane, i, rtab);
-        else if (i < s && i - 30 >= 1)
-            word = ERP_PREFIX_READ ? replay_block_prefix_rd<false>(ring, bm, lane, i, rtab)
-                                   : replay_block_prefix<false>(ring, bm, lane, i, rtab);
-        else
-            word = replay_block_mixed(ring, bm, lane, i, s, rtab);
+        const uint32_t word = replay_block<8>(ring, bm, lane, i, s, rtab);
         emitted += __builtin_popcount(word);
         if (b == b0) lastw = word;
         else out[(size_t)b * 64] = word;
@@ -869,6 +878,218 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
         for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[t][k] << (8 * t);
         long long v2 = 0;
         const int x = acc[kGramLimbs][k];
+#pragma unroll
+        for (int t = 0; t < kGramLimbs; t++)
+            v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
+        if (h0 + row < iters) {
+            go[(size_t)r * iters + h0 + row] = (double)v * (1.0 / kGramScale);
+            if (r < 4) go[(size_t)(32 + r) * iters + h0 + row] = (double)v2 * (1.0 / kGramScale);
+        }
+    }
+}
+
+// ---- sampler -> Gram fusion ----------------------------------------------------------------
+// One workgroup = kFSw sampler waves (one iteration per lane, the replay of sampler_kernel) +
+// kFMw MFMA waves (32 iterations each, the K loop of gram_mfma_kernel), kFIters = 256
+// iterations of one pair.  The sampler waves emit selection words b = 2t, 2t+1 of step t into an
+// LDS ring while the MFMA waves consume step t-1's words with its limb images (LDS-DMA, issued
+// one step ahead), one barrier per step -- the K order both kernels already share
+// (src/eight_point.cpp:99-116: the sampled rows of each iteration's A^T A).  The selection words
+// never go to HBM (the standalone pair writes them and reads them back), and the VALU-bound
+// replay co-issues with the MFMA waves on every SIMD (MI355X_MICROARCH.md "Wave scheduling": an
+// MFMA-only and a VALU-only wave on one CU run concurrently).  12 waves per workgroup, one
+// workgroup per CU: each SIMD holds one sampler wave and two MFMA waves (<= 168 VGPRs).
+// LDS: [limb ring: 2 x 14 KB][selection ring: 2 x 2 KB] ... [bitmaps: rows x kFSw x 64 words]
+// with the bitmaps at the TOP of the allocation, so a draw position j >= s whose word lies past
+// the allocated rows reads 0 and its write is dropped (sampler_kernel's rule, same measured
+// gfx950 behaviour); rows between s and the allocated count are cleared by the prologue.  The
+// Gram epilogue (fused eigen) reuses the whole allocation as the [36][257] double stage.
+constexpr int kFSw = 4;
+constexpr int kFMw = 8;
+constexpr int kFIters = 64 * kFSw;
+constexpr int kFThreads = 64 * (kFSw + kFMw);
+constexpr int kFRowBytes = 64 * 4 * kFSw;                 // one bitmap word of every wave
+constexpr int kFRS = 10;                                  // log2(kFRowBytes)
+static_assert((1 << kFRS) == kFRowBytes, "row shift");
+constexpr int kFLimbSlot = kGramSelOff;                   // the step's two limb images (14 KB)
+constexpr int kFSelSlot = kGramWords * kFIters * 4;       // the step's selection words (2 KB)
+constexpr int kFSelOff = 2 * kFLimbSlot;
+constexpr int kFRingBytes = 2 * kFLimbSlot + 2 * kFSelSlot;
+constexpr int kFStg = kFIters + 1;                        // odd stride: conflict-free
+constexpr int kFStgBytes = 36 * kFStg * 8;
+constexpr int kFMaxLds = 160 * 1024;
+static_assert(kGramWords == 2, "two words per step");
+
+// limb pieces (1 KB each, 14 per step) moved by MFMA wave k: the first 14 % 8 move one more
+__device__ __forceinline__ int fused_piece0(int k) {
+    return k * (kGramPieces / kFMw) + min(k, kGramPieces % kFMw);
+}
+__device__ __forceinline__ int fused_pieces(int k) {
+    return kGramPieces / kFMw + (k < kGramPieces % kFMw ? 1 : 0);
+}
+
+__global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
+    const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins,
+    const int8_t* __restrict__ limbs, const double* __restrict__ rtab, int iters, int nwaves,
+    int nbw, double sample_frac, int rows, int bm_base, int32_t* __restrict__ flags,
+    uint32_t* __restrict__ selw, double* __restrict__ gram, int nhb, double* __restrict__ evec) {
+    extern __shared__ __align__(16) int8_t lds[];
+    // XCD-aware block order (gram_mfma_kernel): a pair's blocks on one XCD, whose L2 then
+    // serves the pair's limb images to all of them
+    const int NB = gridDim.x;
+    const int lbk = (NB & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (NB >> 3) + (blockIdx.x >> 3));
+    const int p = lbk / nhb, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || M < 2) return;  // uniform over the block
+    const int hb = (lbk % nhb) * kFIters;
+    if (hb >= iters) return;
+    const int b0 = (M - 1) / 31, u0 = (M - 1) % 31;  // word and bit of position 0
+    const int nb = b0 + 1;
+    const int nsteps = (nb + kGramWords - 1) / kGramWords;
+    uint32_t* selr = reinterpret_cast<uint32_t*>(lds + kFSelOff);  // [2][2][kFIters]
+    if (wv < kFSw) {
+        // ------------------------------------------------ sampler wave: 64 iterations
+        const int w = hb / 64 + wv;  // the standalone sampler's wave index (windows layout)
+        const bool live = w < nwaves;
+        asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\ts_nop 3" ::: "memory");
+        uint32_t* bm = reinterpret_cast<uint32_t*>(lds + bm_base) + wv * 64;  // this wave's column
+        for (int k = 0; k < rows + 2; k++)  // (rows past the allocation: dropped)
+            bm[bm_index<kFRS>(k, lane)] =
+                k < (s >> 5) ? ~0u : k == (s >> 5) ? (1u << (s & 31)) - 1u : 0u;
+        uint32_t ring[31];
+        if (live) {
+            const uint32_t* wi = wins + ((size_t)p * nwaves + w) * 31 * 64 + lane;
+#pragma unroll
+            for (int t = 0; t < 31; t++) ring[t] = wi[t * 64];
+        }
+        uint32_t* out = selw ? selw + ((size_t)p * nwaves + w) * (size_t)nbw * 64 + lane : nullptr;
+        int i = M - 1, emitted = 0;
+        for (int t = 0; t <= nsteps; t++) {
+            if (t < nsteps) {
+#pragma unroll 1
+                for (int q = 0; q < kGramWords; q++) {
+                    const int b = kGramWords * t + q;
+                    uint32_t word = 0;
+                    if (live && b < nb) {
+                        if (i >= 1) {
+                            word = replay_block<kFRS>(ring, bm, lane, i, s, rtab);
+                            i -= 31;
+                        }
+                        if (b == b0 && (bm[lane] & 1u))  // position 0 still unresolved
+                            word |= 1u << u0;
+                        emitted += __builtin_popcount(word);
+                        if (out) out[(size_t)b * 64] = word;
+                    }
+                    selr[((t & 1) * kGramWords + q) * kFIters + wv * 64 + lane] = word;
+                }
+            }
+            __syncthreads();
+        }
+        if (live && emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
+        if (evec && s >= 9) __syncthreads();  // the epilogue's staging barrier
+        return;
+    }
+    // ---------------------------------------------------- MFMA wave: 32 iterations
+    const int k = wv - kFSw;
+    i32x16 acc[kGramTiles];
+    {
+        const int r = lane & 31, hh = lane >> 5;
+        const int8_t* lg = limbs + (size_t)p * nbw * kGramWordBytes + lane * 16;
+        const int np = fused_pieces(k), pc0 = fused_piece0(k);
+        auto issue = [&](int step) {
+            int8_t* slot = lds + (step & 1) * kFLimbSlot;
+            const int8_t* src = lg + (size_t)step * kGramSelOff;
+            for (int q = 0; q < np; q++)
+                __builtin_amdgcn_global_load_lds((glb_vptr)(src + (pc0 + q) * 1024),
+                                                 (lds_vptr)(slot + (pc0 + q) * 1024), 16, 0, 0);
+        };
+#pragma unroll
+        for (int t = 0; t < kGramTiles; t++)
+#pragma unroll
+            for (int e = 0; e < 16; e++) acc[t][e] = 0;
+        const int boff = r * 32 + (((hh ^ (r >> 3)) & 1) << 4);
+        for (int t = 0; t <= nsteps; t++) {
+            if (t < nsteps) issue(t);  // into the slot every MFMA wave finished in step t - 2
+            if (t >= 1) {
+                const int st = t - 1;
+                const int8_t* slot = lds + (st & 1) * kFLimbSlot;
+                i32x4 bf[kGramWords][kGramTiles];
+#pragma unroll
+                for (int q = 0; q < kGramWords; q++)
+#pragma unroll
+                    for (int tt = 0; tt < kGramTiles; tt++)
+                        bf[q][tt] = *reinterpret_cast<const i32x4*>(slot + q * kGramWordBytes +
+                                                                    tt * 32 * 32 + boff);
+                uint32_t wsel[kGramWords];
+#pragma unroll
+                for (int q = 0; q < kGramWords; q++)
+                    wsel[q] = selr[((st & 1) * kGramWords + q) * kFIters + k * 32 + r];
+                i32x4 a[kGramWords];
+#pragma unroll
+                for (int q = 0; q < kGramWords; q++) {
+                    const uint32_t bits = (wsel[q] >> (16 * hh)) & 0xffffu;
+#pragma unroll
+                    for (int v = 0; v < 4; v++)
+                        a[q][v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
+                }
+#pragma unroll
+                for (int q = 0; q < kGramWords; q++)
+#pragma unroll
+                    for (int tt = 0; tt < kGramTiles; tt++)
+                        acc[tt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[q], bf[q][tt], acc[tt], 0, 0, 0);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs for step t landed
+            __syncthreads();
+        }
+    }
+    // ---------------------------------------------------- epilogue (MFMA waves hold the sums)
+    double* go = gram + (size_t)p * 36 * iters;
+    if (evec && s >= 9) {  // uniform over the block
+        double* stg = reinterpret_cast<double*>(lds);
+        {
+            const int r = lane & 31, hh = lane >> 5;
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+                const int row = k * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+                long long v = 0;
+#pragma unroll
+                for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[t][e] << (8 * t);
+                long long v2 = 0;
+                const int x = acc[kGramLimbs][e];
+#pragma unroll
+                for (int t = 0; t < kGramLimbs; t++)
+                    v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
+                stg[r * kFStg + row] = (double)v * (1.0 / kGramScale);
+                if (r < 4) stg[(32 + r) * kFStg + row] = (double)v2 * (1.0 / kGramScale);
+            }
+        }
+        __syncthreads();
+        if (k >= kFIters / 64) return;
+        const int hl = k * 64 + lane, h = hb + hl;
+        double e[9];
+        const bool ok = gram_min_eigvec9_inv(stg, kFStg, hl, e);
+        if (h >= iters) return;
+        if (!ok) {
+            e[0] = __builtin_nan("");
+#pragma unroll 4
+            for (int c = 0; c < 36; c++) go[(size_t)c * iters + h] = stg[c * kFStg + hl];
+        }
+        double* eo = evec + (size_t)p * 9 * iters + h;
+#pragma unroll
+        for (int c = 0; c < 9; c++) eo[(size_t)c * iters] = e[c];
+        return;
+    }
+    const int r = lane & 31, hh = lane >> 5;
+    const int h0 = hb + k * 32;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+        const int row = (e & 3) + 8 * (e >> 2) + 4 * hh;
+        long long v = 0;
+#pragma unroll
+        for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[t][e] << (8 * t);
+        long long v2 = 0;
+        const int x = acc[kGramLimbs][e];
 #pragma unroll
         for (int t = 0; t < kGramLimbs; t++)
             v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
@@ -2883,6 +3104,52 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
     hipLaunchKernelGGL(gram_mfma_kernel, dim3(nhb * sh.n_pairs), dim3(64 * kGramWaves), 0, st, counts, limbs,
                        selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb, evec, hyps,
                        valid_abs);
+    if (samples)
+        hipLaunchKernelGGL(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
+                           sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);
+    return hipGetLastError();
+}
+
+hipError_t launch_gram_limbs(const int32_t* counts, const double* pts, const BatchShape& sh,
+                             int8_t* limbs, hipStream_t st) {
+    hipLaunchKernelGGL(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
+                       pts, sh.max_nq, sh.sel_words, limbs);
+    return hipGetLastError();
+}
+
+// bitmap rows (one 32-position word of each sampler wave per row) and the allocation: rows cover
+// positions 0 .. max_s (sampler_kernel's rule), the total is a multiple of 5120 B (whole 1-KB
+// rows and whole 1280-B allocation granules) with the bitmaps at its top
+static void sampler_gram_lds(const BatchShape& sh, int* rows, int* bm_base, size_t* bytes) {
+    *rows = sh.max_s / 32 + 1;
+    size_t need = std::max<size_t>((size_t)kFRingBytes + (size_t)*rows * kFRowBytes,
+                                   (size_t)kFStgBytes);
+    need = (need + 5119) / 5120 * 5120;
+    *bytes = need;
+    *bm_base = (int)(need - (size_t)*rows * kFRowBytes);
+}
+
+bool sampler_gram_fits(const BatchShape& sh) {
+    int rows, base;
+    size_t bytes;
+    sampler_gram_lds(sh, &rows, &base, &bytes);
+    return bytes <= (size_t)kFMaxLds;
+}
+
+hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* wins, const int8_t* limbs,
+                               const double* rtab, const BatchShape& sh, double sample_frac,
+                               int32_t* flags, uint32_t* selw, int32_t* samples, double* gram,
+                               double* evec, hipStream_t st) {
+    int rows, bm_base;
+    size_t bytes;
+    sampler_gram_lds(sh, &rows, &bm_base, &bytes);
+    if (bytes > (size_t)kFMaxLds) return hipErrorInvalidValue;
+    const int nwaves = (sh.iters + 63) / 64;
+    const int nhb = (sh.iters + kFIters - 1) / kFIters;
+    uint32_t* sw = samples ? selw : nullptr;
+    hipLaunchKernelGGL(sampler_gram_kernel, dim3(nhb * sh.n_pairs), dim3(kFThreads), bytes, st,
+                       counts, wins, limbs, rtab, sh.iters, nwaves, sh.sel_words, sample_frac,
+                       rows, bm_base, flags, sw, gram, nhb, evec);
     if (samples)
         hipLaunchKernelGGL(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
                            sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);

@@ -226,6 +226,37 @@ def gather_records(local, group=None):
     return out
 
 
+def check_gathered(gathered, per_rank: int, world: int, rerun_fn, oracle_fn=None) -> dict:
+    """rank 0's self-check of the pair path's gathered records (outside the timed region):
+    for every rank r, the first pair of r's block is recomputed on rank 0 alone
+    (rerun_fn(r) -> 64-byte record as uint8[64]) and compared byte for byte with the record
+    rank r contributed (gathered[r * per_rank]); with oracle_fn(r) -> the oracle's find() of
+    that pair (dict with M, K, min_idx, R, T), the gathered record is also checked against the
+    CPU restatement (src/eight_point.cpp:152-192: K, min_idx equal, R / T within 2e-6)."""
+    from .capi import RESULT_DTYPE
+    g = np.ascontiguousarray(np.asarray(gathered, np.uint8)).reshape(-1, RESULT_DTYPE.itemsize)
+    bad_bytes, bad_oracle = [], []
+    for r in range(world):
+        rec = g[r * per_rank]
+        if not np.array_equal(np.asarray(rerun_fn(r), np.uint8).reshape(-1), rec):
+            bad_bytes.append(r)
+        if oracle_fn is not None:
+            o = oracle_fn(r)
+            x = rec.view(RESULT_DTYPE)[0]
+            ok = (int(x["status"]) == 0 and int(x["M"]) == int(o["M"]) and
+                  int(x["K"]) == int(o["K"]) and int(x["min_idx"]) == int(o["min_idx"]) and
+                  float(np.abs(x["R"] - o["R"]).max()) <= 2e-6 and
+                  float(np.abs(x["T"] - o["T"]).max()) <= 2e-6)
+            if not ok:
+                bad_oracle.append(r)
+    out = {"ranks_checked": world, "records_identical": not bad_bytes,
+           "mismatched_ranks": bad_bytes}
+    if oracle_fn is not None:
+        out["oracle_all_equal"] = not bad_oracle
+        out["oracle_mismatched_ranks"] = bad_oracle
+    return out
+
+
 def shard_pairs(n_pairs: int, group=None) -> range:
     import torch.distributed as dist
     a, b = block_range(n_pairs, dist.get_world_size(group), dist.get_rank(group))

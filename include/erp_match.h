@@ -182,7 +182,8 @@ typedef enum erp_stage {
     ERP_STAGE_KNN2_RESCORE = 14,    /* exact flann::L2 distances of the candidates */
     ERP_STAGE_CONSENSUS_REFINE = 15, /* tighter bounds for the survivors (sub-bins) */
     ERP_STAGE_KNN2_EXACT = 16,      /* exact sweep on packed FP32 VALU (ERP_MATCHER_VALU_EXACT) */
-    ERP_STAGE_COUNT = 17
+    ERP_STAGE_SAMPLER_GRAM = 17,    /* the sampler replay and the Gram MFMAs in one kernel */
+    ERP_STAGE_COUNT = 18
 } erp_stage;
 erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable);
 const char* erp_stage_name(int32_t stage);

@@ -24,6 +24,10 @@
   pipeline's 2048 x 1024 (resize_input, config_file.ini) with PIL's bilinear filter and
   stored as JPEG quality 95; ref_rectified_{left,right}_2.jpg: the reference's automatic
   output on that pair (output_20200423_2, re-encoded as JPEG quality 95).
+* tests/golden/real/ref_rectified_right.png, ref_rectified_{left,right}_2.png +
+  vertical_views.json: the other three rectified outputs (lossless) and their vertical views
+  pinned by the sha256 of the decoded BGR bytes (plus the one unwritten pixel's bytes), so all
+  four of the reference's vertical views are checked pixel for pixel.
 * tests/golden/real/MANIFEST.json: sha256 of every source and output file.
 """
 from __future__ import annotations
@@ -32,8 +36,11 @@ import hashlib
 import json
 import os
 import shutil
+import sys
 
 from PIL import Image
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 REF = "/root/reference/build"
 OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "real")
@@ -69,8 +76,35 @@ def main():
         Image.open(src).convert("RGB").save(os.path.join(OUT, f"ref_rectified_{side}_2.jpg"),
                                             quality=95, subsampling=0)
         man["sources"][f"output_20200423_2/rectified_{side}.png"] = sha(src)
+    # the other three vertical views (src/automatic.cpp:148-157): the rectified image as a
+    # lossless input, the reference's vertical view pinned by the sha256 of its decoded BGR
+    # bytes plus the bytes of the pixels the remap never writes (uninitialised there); the
+    # view itself (3 MB each) is not stored
+    vert = {}
+    for od, suffix in (("output_20200423", ""), ("output_20200423_2", "_2")):
+        for side in ("left", "right"):
+            src = os.path.join(REF, od, f"rectified_{side}.png")
+            name = f"ref_rectified_{side}{suffix}.png"
+            if not os.path.exists(os.path.join(OUT, name)):
+                shutil.copyfile(src, os.path.join(OUT, name))
+            man["sources"][f"{od}/rectified_{side}.png"] = sha(src)
+            vsrc = os.path.join(REF, od, f"rectified_{side}_vertical.png")
+            man["sources"][f"{od}/rectified_{side}_vertical.png"] = sha(vsrc)
+            import numpy as np
+            import oracle as O
+            O.build()
+            im = np.ascontiguousarray(np.asarray(Image.open(src).convert("RGB"))[..., ::-1])
+            want = np.ascontiguousarray(np.asarray(Image.open(vsrc).convert("RGB"))[..., ::-1])
+            a, b = O.vertical_rotate(im, fill=0), O.vertical_rotate(im, fill=255)
+            un = np.argwhere((a != b).any(-1))
+            vert[name] = {"reference_file": f"{od}/rectified_{side}_vertical.png",
+                          "shape": list(want.shape),
+                          "sha256_bgr": hashlib.sha256(want.tobytes()).hexdigest(),
+                          "unwritten": [[int(r), int(c), want[r, c].tolist()] for r, c in un]}
+    with open(os.path.join(OUT, "vertical_views.json"), "w") as f:
+        json.dump(vert, f, indent=1)
     for name in sorted(os.listdir(OUT)):
-        if name.endswith(".jpg") or name.endswith(".png"):
+        if name.endswith(".jpg") or name.endswith(".png") or name == "vertical_views.json":
             man["outputs"][name] = sha(os.path.join(OUT, name))
     with open(os.path.join(OUT, "MANIFEST.json"), "w") as f:
         json.dump(man, f, indent=1)

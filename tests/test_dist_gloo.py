@@ -265,9 +265,38 @@ def _gather_worker(rank, world, port, q):
     local = torch.from_numpy(rec.view(np.uint8).reshape(B, 64).copy())
     g = D.gather_records(local)
     if rank == 0:
-        q.put(g.numpy().copy())
+        # the bench's rank-0 self-check of the gathered records (first pair of every rank's
+        # block recomputed on rank 0, byte for byte, and against the oracle)
+        def rerun(r):
+            return local.numpy()[0] if r == 0 else _oracle_record(O, 700 + r * B)
+
+        def ora(r):
+            p = synth.make_pair(700 + r * B, n_kpts=192)
+            mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"])
+            o = O.find(p["W"], p["H"], p["kp_l"][mt["queryIdx"]], p["kp_r"][mt["trainIdx"]],
+                       O.make_cfg(iters=30))
+            return dict(o, M=len(mt))
+        chk = D.check_gathered(g.numpy(), B, world, rerun, ora)
+        # a corrupted record of rank 1 must be caught
+        bad = g.numpy().copy()
+        bad[B, 40] ^= 1
+        chk_bad = D.check_gathered(bad, B, world, rerun, None)
+        q.put((g.numpy().copy(), chk, chk_bad))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _oracle_record(O, seed):
+    """the 64-byte record _gather_worker builds for pair `seed`"""
+    from erp_match_eightpoint_test_amd.capi import RESULT_DTYPE
+    rec = np.zeros(1, RESULT_DTYPE)
+    p = synth.make_pair(seed, n_kpts=192)
+    mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"])
+    r = O.find(p["W"], p["H"], p["kp_l"][mt["queryIdx"]], p["kp_r"][mt["trainIdx"]],
+               O.make_cfg(iters=30))
+    rec[0]["R"], rec[0]["T"], rec[0]["M"], rec[0]["K"] = r["R"], r["T"], len(mt), r["K"]
+    rec[0]["min_idx"] = r["min_idx"]
+    return rec.view(np.uint8).reshape(64)
 
 
 def test_gather_records_gloo(oracle):
@@ -281,10 +310,12 @@ def test_gather_records_gloo(oracle):
     procs = [ctx.Process(target=_gather_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=180)
+    got, chk, chk_bad = q.get(timeout=180)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    assert chk["records_identical"] and chk["oracle_all_equal"] and chk["ranks_checked"] == 2
+    assert not chk_bad["records_identical"] and chk_bad["mismatched_ranks"] == [1]
     recs = got.reshape(-1).view(RESULT_DTYPE)
     assert len(recs) == 6
     for i, r in enumerate(recs):

@@ -107,6 +107,27 @@ def test_real_vertical_view_pixel_exact(api):
     assert len(bad) == 0, (len(bad), bad[:10])
 
 
+@pytest.mark.parametrize("name", ["ref_rectified_left.png", "ref_rectified_right.png",
+                                  "ref_rectified_left_2.png", "ref_rectified_right_2.png"])
+def test_real_vertical_views_all_four(api, name):
+    """all four of the reference's vertical views (src/automatic.cpp:148-157, both building
+    pairs): the device view of the reference's rectified image, with the remap's unwritten
+    pixels taken from the reference, has the sha256 of the reference's own decoded vertical
+    view (tests/golden/real/vertical_views.json) -- pixel-exact, without storing the views"""
+    import hashlib
+    ss, ep, er = api
+    meta = json.load(open(os.path.join(REAL, "vertical_views.json")))[name]
+    src = _dev(_bgr(os.path.join(REAL, name)))
+    a = er.vertical_rotate(src, fill=0).cpu().numpy()
+    b = er.vertical_rotate(src, fill=255).cpu().numpy()
+    un = np.argwhere((a != b).any(-1))
+    assert [[int(r), int(c)] for r, c in un] == [u[:2] for u in meta["unwritten"]]
+    for r, c, v in meta["unwritten"]:
+        a[r, c] = v
+    assert list(a.shape) == meta["shape"]
+    assert hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest() == meta["sha256_bgr"]
+
+
 def _kat(api, left_name, right_name, ref_l_name, ref_r_name, size=None):
     ss, ep, er = api
     W, H = 2048, 1024

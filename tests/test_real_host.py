@@ -15,6 +15,7 @@ from __future__ import annotations
 import os
 
 import numpy as np
+import pytest
 
 REAL = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "real")
 
@@ -33,3 +34,24 @@ def test_oracle_vertical_view_equals_reference_output(oracle):
     unwritten = (a != b).any(-1)
     assert int(unwritten.sum()) <= 4, int(unwritten.sum())
     assert np.array_equal(a[~unwritten], want[~unwritten])
+
+
+@pytest.mark.parametrize("name", ["ref_rectified_left.png", "ref_rectified_right.png",
+                                  "ref_rectified_left_2.png", "ref_rectified_right_2.png"])
+def test_oracle_vertical_views_all_four(oracle, name):
+    """all four of the reference's vertical views (both building pairs, left and right): the
+    oracle's view of the reference's rectified image, with the remap's unwritten pixels taken
+    from the reference, has the sha256 of the reference's own decoded vertical view
+    (tests/golden/real/vertical_views.json, tests/golden/gen_real.py)"""
+    import hashlib
+    import json
+    meta = json.load(open(os.path.join(REAL, "vertical_views.json")))[name]
+    src = _bgr(name)
+    a = oracle.vertical_rotate(src, fill=0)
+    b = oracle.vertical_rotate(src, fill=255)
+    un = np.argwhere((a != b).any(-1))
+    assert [[int(r), int(c)] for r, c in un] == [u[:2] for u in meta["unwritten"]]
+    for r, c, v in meta["unwritten"]:
+        a[r, c] = v
+    assert list(a.shape) == meta["shape"]
+    assert hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest() == meta["sha256_bgr"]
