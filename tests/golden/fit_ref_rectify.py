@@ -163,7 +163,10 @@ def fit_pair(name, method=Image.BILINEAR):
 
 
 def main():
-    out = {"method": __doc__.split("\n\n")[1].strip().split("\n")[0], "pairs": {}}
+    out = {"method": "least-squares fit of find()'s (rot, t) through the reference's rectify + "
+                     "rotate_image model to its own rectified_{left,right}.png "
+                     "(tests/golden/fit_ref_rectify.py); spread_deg = the fit on a PIL-box "
+                     "instead of PIL-bilinear resize of the input", "pairs": {}}
     for name in PAIRS:
         r = fit_pair(name, Image.BILINEAR)
         r2 = fit_pair(name, Image.BOX)
