@@ -174,6 +174,16 @@ def host_cpu_share():
                      "threads_basis": "min(sched_getaffinity, cgroup cpu.max quota)"}
 
 
+def oracle_pair(p, iters, nthreads):
+    """one pair through the oracle (exact k=2 match + find), with its match list"""
+    import oracle as O
+    mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=nthreads)
+    r = O.find(p["W"], p["H"], p["kp_l"][mt["queryIdx"]], p["kp_r"][mt["trainIdx"]],
+               O.make_cfg(iters=iters))
+    r["matches"] = mt
+    return r
+
+
 def cpu_baseline(pairs, iters, budget_s):
     """the oracle (CPU restatement, exact brute force + OpenCV-style SVD) on host cores: whole
     pairs of the same workload, as many as fit in ~budget_s (at least one), with OpenMP over
@@ -186,12 +196,7 @@ def cpu_baseline(pairs, iters, budget_s):
     os.environ["OMP_NUM_THREADS"] = str(threads)
 
     def one(p, nth):
-        mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=nth)
-        kl = p["kp_l"][mt["queryIdx"]]
-        kr = p["kp_r"][mt["trainIdx"]]
-        r = O.find(p["W"], p["H"], kl, kr, O.make_cfg(iters=iters))
-        r["matches"] = mt
-        return r
+        return oracle_pair(p, iters, nth)
 
     t0 = time.perf_counter()
     got = []
@@ -745,6 +750,19 @@ def main():
                 "survivors_mean": float(hres["survivors"].mean()),
                 "survivors_max": int(hres["survivors"].max()),
                 "binned_rows_mean": float(hres["binned_rows"].mean())}
+        if world == 1 and not args.no_cpu_baseline:
+            # the harder regime against the oracle too: the first pairs of the hard batch
+            # (30 % wrong matches exercise a different consensus regime), matches out
+            threads, _ = host_cpu_share()
+            n_h = 3
+            ora_h = [oracle_pair(p, args.iters, threads) for p in hpairs[:n_h]]
+            sb = subs[0]
+            b = hb[0]
+            o = sb["runner"].run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"],
+                                 b["off_r"], b["width"], b["height"], b["max_nq"], b["max_nt"],
+                                 want=("matches",))
+            torch.cuda.synchronize()
+            hard["parity"] = parity_check(hres, o["matches"][:n_h].cpu().numpy(), ora_h)
     cpu = None
     parity = None
     multi = None

@@ -525,6 +525,96 @@ __device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uin
     return word;
 }
 
+// ---- the same blocks with the 31 draw positions computed FIRST (ILP variants) ---------------
+// A block's 31 positions depend only on the ring words the previous block left (the backwards
+// recurrence writes values for the NEXT block), so they are 31 independent modulo chains: with
+// them ahead of the LDS ops the scheduler interleaves the chains instead of running each draw's
+// dependent fp64 sequence behind the previous draw's volatile LDS op.  This is what a wave that
+// is alone on its SIMD needs (the fused sampler_gram_kernel: one sampler wave per SIMD); the
+// standalone sampler hides the same latency with four waves per SIMD.
+template <bool I24>
+__device__ __forceinline__ void block_positions(uint32_t (&ring)[31], int i0,
+                                                const double* __restrict__ rtab,
+                                                uint32_t (&jj)[31]) {
+    double rt[31];
+#pragma unroll
+    for (int u = 0; u < 31; u++) rt[u] = rtab[i0 - u + 1];
+#pragma unroll
+    for (int u = 0; u < 31; u++) {
+        const int ii = i0 - u;
+        const int slot = 30 - u;
+        const uint32_t rv = ring[slot];
+        ring[slot] = rv - ring[(slot + 28) % 31];
+        jj[u] = I24 ? mod_rup_i24(rv >> 1, rt[u], ii + 1) : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
+    }
+}
+
+template <bool I24, int RS>
+__device__ __forceinline__ uint32_t replay_block_draws_ilp(uint32_t (&ring)[31], uint32_t* bm,
+                                                           int lane, int i0,
+                                                           const double* __restrict__ rtab) {
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
+    uint32_t jj[31];
+    block_positions<I24>(ring, i0, rtab, jj);
+    const uint32_t zero = 0;
+    uint32_t olds[31];
+    uint32_t nw = 0;
+#pragma unroll
+    for (int u = 0; u < 31 + kReplayLag; u++) {
+        if (u < 31)
+            olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, jj[u]), 1u << (jj[u] & 31), zero);
+        const int v = u - kReplayLag;
+        if (v >= 0) {
+            lds_wait_step(olds[v], v);
+            nw |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
+        }
+    }
+    return nw;
+}
+
+template <bool I24, int RS>
+__device__ __forceinline__ uint32_t replay_block_prefix_ilp(uint32_t (&ring)[31], uint32_t* bm,
+                                                            int lane, int i0,
+                                                            const double* __restrict__ rtab) {
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
+    uint32_t jj[31];
+    block_positions<I24>(ring, i0, rtab, jj);
+    const int base = i0 - 30;  // >= 1
+    const int wA = i0 >> 5, wB = base >> 5;
+    const uint32_t hi = bm[bm_index<RS>(wA, lane)], lo = bm[bm_index<RS>(wB, lane)];
+    uint32_t win = wA == wB ? (lo >> (base & 31)) : __builtin_amdgcn_alignbit(hi, lo, base & 31);
+    uint32_t olds[31];
+    uint32_t nw = 0;
+#pragma unroll
+    for (int u = 0; u < 31 + kReplayLag; u++) {
+        if (u < 31) {
+            const uint32_t j = jj[u];
+            const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)win, 30 - u, 1);  // bm[i]
+            const uint32_t bit = 1u << (j & 31);
+            olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), bit, bsp & bit);
+            const uint32_t t = min(j - (uint32_t)base, 31u);
+            const uint32_t m = 1u << t;
+            win = (win & ~m) | (bsp & m);
+        }
+        const int v = u - kReplayLag;
+        if (v >= 0) {
+            lds_wait_step(olds[v], v);
+            nw |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
+        }
+    }
+    return nw;
+}
+
+template <int RS>
+__device__ __forceinline__ uint32_t replay_block_ilp(uint32_t (&ring)[31], uint32_t* bm, int lane,
+                                                     int i, int s, const double* __restrict__ rtab) {
+    if (i - 30 >= s && i - 30 >= 255) return replay_block_draws_ilp<true, RS>(ring, bm, lane, i, rtab);
+    if (i - 30 >= s) return replay_block_draws_ilp<false, RS>(ring, bm, lane, i, rtab);
+    if (i < s && i - 30 >= 255) return replay_block_prefix_ilp<true, RS>(ring, bm, lane, i, rtab);
+    if (i < s && i - 30 >= 1) return replay_block_prefix_ilp<false, RS>(ring, bm, lane, i, rtab);
+    return replay_block_mixed<RS>(ring, bm, lane, i, s, rtab);
+}
+
 // the 31 reverse steps i .. i-30 of one lane's replay, by block kind (uniform: i and s are)
 template <int RS>
 __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t* bm, int lane,
@@ -912,9 +1002,10 @@ constexpr int kFRowBytes = 64 * 4 * kFSw;                 // one bitmap word of 
 constexpr int kFRS = 10;                                  // log2(kFRowBytes)
 static_assert((1 << kFRS) == kFRowBytes, "row shift");
 constexpr int kFLimbSlot = kGramSelOff;                   // the step's two limb images (14 KB)
+constexpr int kFRing = 3;                                 // limb slots: DMAs 2 steps ahead
 constexpr int kFSelSlot = kGramWords * kFIters * 4;       // the step's selection words (2 KB)
-constexpr int kFSelOff = 2 * kFLimbSlot;
-constexpr int kFRingBytes = 2 * kFLimbSlot + 2 * kFSelSlot;
+constexpr int kFSelOff = kFRing * kFLimbSlot;
+constexpr int kFRingBytes = kFRing * kFLimbSlot + 2 * kFSelSlot;
 constexpr int kFStg = kFIters + 1;                        // odd stride: conflict-free
 constexpr int kFStgBytes = 36 * kFStg * 8;
 constexpr int kFMaxLds = 160 * 1024;
@@ -973,7 +1064,7 @@ __global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
                     uint32_t word = 0;
                     if (live && b < nb) {
                         if (i >= 1) {
-                            word = replay_block<kFRS>(ring, bm, lane, i, s, rtab);
+                            word = replay_block_ilp<kFRS>(ring, bm, lane, i, s, rtab);
                             i -= 31;
                         }
                         if (b == b0 && (bm[lane] & 1u))  // position 0 still unresolved
@@ -998,7 +1089,7 @@ __global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
         const int8_t* lg = limbs + (size_t)p * nbw * kGramWordBytes + lane * 16;
         const int np = fused_pieces(k), pc0 = fused_piece0(k);
         auto issue = [&](int step) {
-            int8_t* slot = lds + (step & 1) * kFLimbSlot;
+            int8_t* slot = lds + (step % kFRing) * kFLimbSlot;
             const int8_t* src = lg + (size_t)step * kGramSelOff;
             for (int q = 0; q < np; q++)
                 __builtin_amdgcn_global_load_lds((glb_vptr)(src + (pc0 + q) * 1024),
@@ -1009,11 +1100,16 @@ __global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
 #pragma unroll
             for (int e = 0; e < 16; e++) acc[t][e] = 0;
         const int boff = r * 32 + (((hh ^ (r >> 3)) & 1) << 4);
+        // step st's limbs are DMA'd at iteration st + 2 - kFRing (two steps ahead), into the slot
+        // the MFMA waves last read at iteration st + 1 - kFRing (finished before that barrier);
+        // iteration t waits for the DMA it issued kFRing - 2 iterations earlier
+        static_assert(kFRing == 3, "lookahead");
+        issue(0);
         for (int t = 0; t <= nsteps; t++) {
-            if (t < nsteps) issue(t);  // into the slot every MFMA wave finished in step t - 2
+            if (t + 1 < nsteps) issue(t + 1);
             if (t >= 1) {
                 const int st = t - 1;
-                const int8_t* slot = lds + (st & 1) * kFLimbSlot;
+                const int8_t* slot = lds + (st % kFRing) * kFLimbSlot;
                 i32x4 bf[kGramWords][kGramTiles];
 #pragma unroll
                 for (int q = 0; q < kGramWords; q++)
@@ -1039,7 +1135,13 @@ __global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
                     for (int tt = 0; tt < kGramTiles; tt++)
                         acc[tt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[q], bf[q][tt], acc[tt], 0, 0, 0);
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMAs for step t landed
+            // step t's DMAs (issued in the previous iteration) have landed; step t + 1's may fly
+            if (t + 1 < nsteps) {
+                if (np == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             __syncthreads();
         }
     }

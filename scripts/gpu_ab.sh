@@ -1,0 +1,17 @@
+#!/bin/bash
+# A/B of an environment knob on one box: optional GPU test subset (TEST_K), then the default
+# bench (no CPU baseline) once per value of KNOB in VALUES; prints value, step, stages.
+#   TAG=r03b KNOB=ERP_FUSE_SAMPLER VALUES="0 1" TEST_K="fused" bash scripts/gpu_ab.sh
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+TAG=${TAG:-ab}
+if [ -n "${TEST_K:-}" ]; then
+  echo "== gpu tests -k $TEST_K" && timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -k "$TEST_K" > gpurun_out/pytest_${TAG}.log 2>&1 || { tail -30 gpurun_out/pytest_${TAG}.log; exit 1; }
+  tail -2 gpurun_out/pytest_${TAG}.log
+fi
+for V in ${VALUES:-0 1}; do
+  echo "== bench $KNOB=$V" && env $KNOB=$V timeout -k 10 400 python bench.py --no-cpu-baseline --steps ${STEPS:-10} --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench_${TAG}_$V.json 2> gpurun_out/bench_${TAG}_$V.err || { tail -20 gpurun_out/bench_${TAG}_$V.err; exit 1; }
+  python scripts/bench_summary.py gpurun_out/bench_${TAG}_$V.json 2>/dev/null || python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_$V.json'));print(d['value'], d['ms_per_step'], {k:round(v,2) for k,v in d['stages_ms_serial_step'].items() if v>0.3})"
+done

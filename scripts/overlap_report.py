@@ -23,7 +23,8 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
-    n = re.sub(r"\(.*", "", name)
+    n = name.replace("(anonymous namespace)", "anon")
+    n = re.sub(r"\(.*", "", n)
     n = re.sub(r"<.*", "", n)
     n = n.split("::")[-1]
     return n.replace("_kernel", "")

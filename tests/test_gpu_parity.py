@@ -368,6 +368,38 @@ def test_batch_pipeline_valu_matcher_equals_mfma(gpu_lib):
         assert M > 0 and np.array_equal(ma[i, :M], mb[i, :M])
 
 
+@pytest.mark.parametrize("sizes,iters", [([512, 700, 300, 1024], 300), ([4096, 2048], 1000),
+                                         ([9000], 300)])
+def test_sampler_gram_fused_equals_standalone(gpu_lib, sizes, iters):
+    """the fused sampler->Gram kernel (default) and the standalone sampler + Gram kernels
+    (ERP_FUSE_SAMPLER=0) give byte-identical records, hypotheses and sample sets: ragged pair
+    sizes, partial 256-iteration blocks, M = 9000 (s = 2250: 71 bitmap rows, the fused LDS
+    near its largest)"""
+    import os as _os
+
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
+    pairs = [synth.make_pair(4100 + i, n_kpts=n) for i, n in enumerate(sizes)]
+    args = _batch(pairs)
+    outs = {}
+    for fuse in ("1", "0"):
+        _os.environ["ERP_FUSE_SAMPLER"] = fuse
+        try:
+            c = Context(0)
+        finally:
+            del _os.environ["ERP_FUSE_SAMPLER"]
+        o = PairBatchRunner(ctx=c, iters=iters).run(*args, want=("hyps", "samples"))
+        torch.cuda.synchronize()
+        outs[fuse] = (results_to_numpy(o["results"]).view(np.uint8).copy(),
+                      o["hyps"].cpu().numpy(), o["samples"].cpu().numpy())
+    ra, ha, sa = outs["1"]
+    rb, hb, sb = outs["0"]
+    assert np.array_equal(ra, rb)
+    assert np.array_equal(ha, hb)
+    assert np.array_equal(sa, sb)
+    assert np.all(results_to_numpy(o["results"])["status"] == 0)
+
+
 def test_batch_full_size_properties(ctx, oracle):
     """configs[1] shape: 4096 x 4096 keypoints, 10k iterations.  Size-independent checks:
     matches bit-exact vs the oracle, sampled sets of a spread of iterations vs the oracle's
