@@ -105,9 +105,11 @@ struct erp_ctx {
     // zoomed central references before the pre-pruning (opt-in ERP_ZOOM_REFS=1: measured no
     // fewer binned rows)
     int zoom_refs = getenv("ERP_ZOOM_REFS") ? atoi(getenv("ERP_ZOOM_REFS")) : 0;  // 2: all refs
-    // the sampler and the Gram as one kernel (sampler_gram_kernel) when the bitmaps fit;
-    // ERP_FUSE_SAMPLER=0 runs the two standalone kernels (A/B knob)
-    bool fuse_sampler = !getenv("ERP_FUSE_SAMPLER") || atoi(getenv("ERP_FUSE_SAMPLER")) != 0;
+    // the sampler and the Gram as one kernel (sampler_gram_kernel, opt-in ERP_FUSE_SAMPLER=1):
+    // measured 1.6x SLOWER than the two standalone kernels (the Gram's int32
+    // accumulators leave room for one sampler wave per SIMD, and one wave alone issues VALU at
+    // about a third of the rate four waves reach), so the default is the standalone pair
+    bool fuse_sampler = getenv("ERP_FUSE_SAMPLER") && atoi(getenv("ERP_FUSE_SAMPLER")) != 0;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;

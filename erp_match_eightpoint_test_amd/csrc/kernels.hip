@@ -525,6 +525,25 @@ __device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uin
     return word;
 }
 
+// wait until at most n LDS ops are in flight, carrying o as an operand (n is a constant after
+// unrolling: the switch folds to one s_waitcnt)
+template <int N>
+__device__ __forceinline__ void lds_wait_imm(uint32_t& o) {
+    asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(o) : "n"(N) : "memory");
+}
+__device__ __forceinline__ void lds_wait_n(uint32_t& o, int n) {
+    switch (n) {
+#define ERP_W(k) case k: lds_wait_imm<k>(o); break;
+        ERP_W(0) ERP_W(1) ERP_W(2) ERP_W(3) ERP_W(4) ERP_W(5) ERP_W(6) ERP_W(7)
+        ERP_W(8) ERP_W(9) ERP_W(10) ERP_W(11) ERP_W(12) ERP_W(13) ERP_W(14)
+#undef ERP_W
+        default: lds_wait_imm<15>(o); break;
+    }
+}
+// a wave alone on its SIMD has nothing else to cover the masked-OR latency: the ILP variants keep
+// up to 15 in flight (the lgkmcnt limit) instead of kReplayLag
+constexpr int kIlpLag = 15;
+
 // ---- the same blocks with the 31 draw positions computed FIRST (ILP variants) ---------------
 // A block's 31 positions depend only on the ring words the previous block left (the backwards
 // recurrence writes values for the NEXT block), so they are 31 independent modulo chains: with
@@ -558,18 +577,18 @@ __device__ __forceinline__ uint32_t replay_block_draws_ilp(uint32_t (&ring)[31],
     block_positions<I24>(ring, i0, rtab, jj);
     const uint32_t zero = 0;
     uint32_t olds[31];
-    uint32_t nw = 0;
+    uint32_t nw[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int u = 0; u < 31 + kReplayLag; u++) {
+    for (int u = 0; u < 31 + kIlpLag; u++) {
         if (u < 31)
             olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, jj[u]), 1u << (jj[u] & 31), zero);
-        const int v = u - kReplayLag;
+        const int v = u - kIlpLag;
         if (v >= 0) {
-            lds_wait_step(olds[v], v);
-            nw |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
+            lds_wait_n(olds[v], 30 - v < kIlpLag ? 30 - v : kIlpLag);
+            nw[v & 3] |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
         }
     }
-    return nw;
+    return (nw[0] | nw[1]) | (nw[2] | nw[3]);  // four partial words: no serial OR chain
 }
 
 template <bool I24, int RS>
@@ -584,9 +603,9 @@ __device__ __forceinline__ uint32_t replay_block_prefix_ilp(uint32_t (&ring)[31]
     const uint32_t hi = bm[bm_index<RS>(wA, lane)], lo = bm[bm_index<RS>(wB, lane)];
     uint32_t win = wA == wB ? (lo >> (base & 31)) : __builtin_amdgcn_alignbit(hi, lo, base & 31);
     uint32_t olds[31];
-    uint32_t nw = 0;
+    uint32_t nw[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int u = 0; u < 31 + kReplayLag; u++) {
+    for (int u = 0; u < 31 + kIlpLag; u++) {
         if (u < 31) {
             const uint32_t j = jj[u];
             const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)win, 30 - u, 1);  // bm[i]
@@ -596,13 +615,13 @@ __device__ __forceinline__ uint32_t replay_block_prefix_ilp(uint32_t (&ring)[31]
             const uint32_t m = 1u << t;
             win = (win & ~m) | (bsp & m);
         }
-        const int v = u - kReplayLag;
+        const int v = u - kIlpLag;
         if (v >= 0) {
-            lds_wait_step(olds[v], v);
-            nw |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
+            lds_wait_n(olds[v], 30 - v < kIlpLag ? 30 - v : kIlpLag);
+            nw[v & 3] |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
         }
     }
-    return nw;
+    return (nw[0] | nw[1]) | (nw[2] | nw[3]);  // four partial words: no serial OR chain
 }
 
 template <int RS>
@@ -632,6 +651,7 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
 
 // One lane = one iteration; writes the iteration's selection bitmap in block space:
 // sel[p][w][b][lane] bit u <-> index i = M-1-31b-u (b = 0 .. (M-1)/31), exactly s bits set.
+template <bool ILP>
 __global__ __launch_bounds__(64) void sampler_kernel(
     const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins, int nwaves, int nbw,
     double sample_frac, const double* __restrict__ rtab, uint32_t* __restrict__ selw,
@@ -661,7 +681,8 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     int i = M - 1, b = 0, emitted = 0;
     uint32_t lastw = 0;
     while (i >= 1) {
-        const uint32_t word = replay_block<8>(ring, bm, lane, i, s, rtab);
+        const uint32_t word = ILP ? replay_block_ilp<8>(ring, bm, lane, i, s, rtab)
+                                  : replay_block<8>(ring, bm, lane, i, s, rtab);
         emitted += __builtin_popcount(word);
         if (b == b0) lastw = word;
         else out[(size_t)b * 64] = word;
@@ -1023,7 +1044,8 @@ __global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
     const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins,
     const int8_t* __restrict__ limbs, const double* __restrict__ rtab, int iters, int nwaves,
     int nbw, double sample_frac, int rows, int bm_base, int32_t* __restrict__ flags,
-    uint32_t* __restrict__ selw, double* __restrict__ gram, int nhb, double* __restrict__ evec) {
+    uint32_t* __restrict__ selw, double* __restrict__ gram, int nhb, double* __restrict__ evec,
+    int diag) {
     extern __shared__ __align__(16) int8_t lds[];
     // XCD-aware block order (gram_mfma_kernel): a pair's blocks on one XCD, whose L2 then
     // serves the pair's limb images to all of them
@@ -1062,7 +1084,7 @@ __global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
                 for (int q = 0; q < kGramWords; q++) {
                     const int b = kGramWords * t + q;
                     uint32_t word = 0;
-                    if (live && b < nb) {
+                    if (live && b < nb && !(diag & 2)) {
                         if (i >= 1) {
                             word = replay_block_ilp<kFRS>(ring, bm, lane, i, s, rtab);
                             i -= 31;
@@ -1104,10 +1126,10 @@ __global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
         // the MFMA waves last read at iteration st + 1 - kFRing (finished before that barrier);
         // iteration t waits for the DMA it issued kFRing - 2 iterations earlier
         static_assert(kFRing == 3, "lookahead");
-        issue(0);
+        if (!(diag & 1)) issue(0);
         for (int t = 0; t <= nsteps; t++) {
-            if (t + 1 < nsteps) issue(t + 1);
-            if (t >= 1) {
+            if (t + 1 < nsteps && !(diag & 1)) issue(t + 1);
+            if (t >= 1 && !(diag & 1)) {
                 const int st = t - 1;
                 const int8_t* slot = lds + (st % kFRing) * kFLimbSlot;
                 i32x4 bf[kGramWords][kGramTiles];
@@ -1136,7 +1158,7 @@ __global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
                         acc[tt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[q], bf[q][tt], acc[tt], 0, 0, 0);
             }
             // step t's DMAs (issued in the previous iteration) have landed; step t + 1's may fly
-            if (t + 1 < nsteps) {
+            if (t + 1 < nsteps && !(diag & 1)) {
                 if (np == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
                 else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
             } else {
@@ -3180,8 +3202,16 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         // gfx950, scripts/dev/lds_oob.hip) so that no word of the allocation goes uncleared
         const int nwords = (sh.max_s / 32 + 1 + 4) / 5 * 5;
         const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
-        hipLaunchKernelGGL(sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
-                           wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags, nwords);
+        // ERP_SAMPLER_ILP=1: the blocks with their 31 positions computed first (A/B knob)
+        static const bool ilp = getenv("ERP_SAMPLER_ILP") && atoi(getenv("ERP_SAMPLER_ILP")) != 0;
+        if (ilp)
+            hipLaunchKernelGGL(sampler_kernel<true>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st,
+                               counts, wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags,
+                               nwords);
+        else
+            hipLaunchKernelGGL(sampler_kernel<false>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st,
+                               counts, wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags,
+                               nwords);
     }
     return hipGetLastError();
 }
@@ -3231,6 +3261,13 @@ static void sampler_gram_lds(const BatchShape& sh, int* rows, int* bm_base, size
     *bm_base = (int)(need - (size_t)*rows * kFRowBytes);
 }
 
+// ERP_FUSED_DIAG (development): bit 0 = the MFMA waves skip their DMAs and MFMAs, bit 1 = the
+// sampler waves skip the replay (results are then wrong: timing decomposition only)
+static int fused_diag() {
+    static const int d = getenv("ERP_FUSED_DIAG") ? atoi(getenv("ERP_FUSED_DIAG")) : 0;
+    return d;
+}
+
 bool sampler_gram_fits(const BatchShape& sh) {
     int rows, base;
     size_t bytes;
@@ -3251,7 +3288,7 @@ hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* wins, cons
     uint32_t* sw = samples ? selw : nullptr;
     hipLaunchKernelGGL(sampler_gram_kernel, dim3(nhb * sh.n_pairs), dim3(kFThreads), bytes, st,
                        counts, wins, limbs, rtab, sh.iters, nwaves, sh.sel_words, sample_frac,
-                       rows, bm_base, flags, sw, gram, nhb, evec);
+                       rows, bm_base, flags, sw, gram, nhb, evec, fused_diag());
     if (samples)
         hipLaunchKernelGGL(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
                            sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);

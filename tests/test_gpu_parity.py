@@ -371,8 +371,8 @@ def test_batch_pipeline_valu_matcher_equals_mfma(gpu_lib):
 @pytest.mark.parametrize("sizes,iters", [([512, 700, 300, 1024], 300), ([4096, 2048], 1000),
                                          ([9000], 300)])
 def test_sampler_gram_fused_equals_standalone(gpu_lib, sizes, iters):
-    """the fused sampler->Gram kernel (default) and the standalone sampler + Gram kernels
-    (ERP_FUSE_SAMPLER=0) give byte-identical records, hypotheses and sample sets: ragged pair
+    """the fused sampler->Gram kernel (opt-in ERP_FUSE_SAMPLER=1) and the standalone sampler +
+    Gram kernels (default) give byte-identical records, hypotheses and sample sets: ragged pair
     sizes, partial 256-iteration blocks, M = 9000 (s = 2250: 71 bitmap rows, the fused LDS
     near its largest)"""
     import os as _os
