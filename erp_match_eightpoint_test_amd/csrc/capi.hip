@@ -94,7 +94,7 @@ struct erp_ctx {
     DevBuf zsel;              // consensus zoom: the survivors' rank-window bins (level 1 grid)
     DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
-        rtab, limbs, tsplit, ovf, remap_scr, vchunk;
+        rtab, limbs, tsplit, ovf, remap_scr, vchunk, lipref;
     DevBuf extra[13];         // erp_ctx_scratch_internal slots (1-11 SURF, 12 viz)
     uint64_t surf_key = 0;    // (W, H, params) of the SURF layer table in extra[1]
     uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
@@ -105,6 +105,9 @@ struct erp_ctx {
     // zoomed central references before the pre-pruning (opt-in ERP_ZOOM_REFS=1: measured no
     // fewer binned rows)
     int zoom_refs = getenv("ERP_ZOOM_REFS") ? atoi(getenv("ERP_ZOOM_REFS")) : 0;  // 2: all refs
+    // second pre-pruning stage: every 4th first-stage survivor on the fine grid as a reference
+    // for the others (kernels.hip consensus_lipschitz2_kernel; ERP_LIP2=0 for A/B)
+    int lip2 = getenv("ERP_LIP2") ? atoi(getenv("ERP_LIP2")) : 1;
     // the sampler and the Gram as one kernel (sampler_gram_kernel, opt-in ERP_FUSE_SAMPLER=1):
     // measured 1.6x SLOWER than the two standalone kernels (the Gram's int32
     // accumulators leave room for one sampler wave per SIMD, and one wave alone issues VALU at
@@ -274,7 +277,8 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->kcount, &ctx->tmean, &ctx->sortbuf, &ctx->w0, &ctx->off, &ctx->wh,
                      &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
                      &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins,
-                     &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf, &ctx->remap_scr, &ctx->vchunk};
+                     &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf, &ctx->remap_scr, &ctx->vchunk,
+                     &ctx->lipref};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (DevBuf& b : ctx->extra)
@@ -392,8 +396,9 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->w0, 31 * 4) && ensure(c->results, P * sizeof(erp_pair_result)) &&
               ensure(c->dscale, P * 4) && ensure(c->lb, P * 2 * sh.iters * 8) &&
               ensure(c->ub, P * 2 * sh.iters * 8) && ensure(c->surv, P * 2 * sh.iters * 4) &&
-              ensure(c->bsel, P * 2 * sh.iters * 8) && ensure(c->zsel, P * 2 * sh.iters * 8) && ensure(c->edges, erp::consensus_edges_bytes((int)P)) &&
-              ensure(c->nsurv, P * 16 + 4) && ensure(c->vchunk, erp::valid_chunk_bytes(sh));
+              ensure(c->bsel, P * 2 * sh.iters * 8) && ensure(c->zsel, P * 2 * sh.iters * 8) &&
+              ensure(c->lipref, erp::lipref_bytes((int)P, 2 * sh.iters)) && ensure(c->edges, erp::consensus_edges_bytes((int)P)) &&
+              ensure(c->nsurv, P * 20 + 8) && ensure(c->vchunk, erp::valid_chunk_bytes(sh));
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
     if (ok && !(out && out->dist)) ok = ensure(c->tmean, P * 2 * sh.iters * 8);
@@ -515,7 +520,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             cfg->trim_lo, cfg->trim_hi, lbp, ubp, bselp, shard,
                                             nshards, (int32_t*)c->surv.p,
                                             (int32_t*)c->nsurv.p + sh.n_pairs,
-                                            (int32_t*)c->zsel.p, c->zoom_refs, st));
+                                            (int32_t*)c->zsel.p, c->zoom_refs, c->lip2,
+                                            (int32_t*)c->sortbuf.p, c->lipref.p, st));
     }
     if (phase == 1) return ERP_OK;
     if (phase == 2)  // the bounds ran per shard (binned rows not combined): report -1
@@ -548,7 +554,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
                                             bselp, lbp,
-                                            ubp, (int32_t*)c->sortbuf.p, st));
+                                            ubp, (int32_t*)c->sortbuf.p, c->lipref.p, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);

@@ -2024,116 +2024,238 @@ constexpr int kLipStep = ERP_LIP_STEP;  // every 16th row is a reference row
 #endif
 constexpr int kRefStep = ERP_REF_STEP;  // every 16th survivor is refined first (refine pass)
 constexpr int kLipMinK = 1024;  // smaller sets: no pre-pruning (every non-reference row listed)
-constexpr int kLipChunk = 1024; // reference rows staged in LDS per chunk
+#ifndef ERP_LIP2_STEP
+#define ERP_LIP2_STEP 4
+#endif
+constexpr int kLip2Step = ERP_LIP2_STEP;  // every 4th L1 row is a second-stage reference
 
-__global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
+// The references of a pruning pass, staged ONCE per pair (consensus_lip_refs_kernel) into
+// lref[p][0 .. lcnt[p]) as (x, y, z, squared pruning radius), with U = their smallest UB in
+// lU[p] (+inf: no pruning for the pair).  Every pruning block then reads them with coalesced
+// loads: when each block gathered its references' LB and coordinates itself (dependent
+// gathers, ~20 per block of 512 rows) the kernels spent ~80 % of their wave cycles waiting
+// (SQ_WAIT_ANY, profiles/r03_sq_lipschitz.txt).
+constexpr int kLipChunk2 = 512;  // references per LDS chunk
+int lipref_cap(int stride) { return stride / kLip2Step + 64; }  // >= refs of any mode
+
+// one block per pair.  Modes: stage 1 (slist == nullptr, zb == nullptr): rows ra + c lstep of
+// the shard (pairs with K >= kLipMinK); list mode (slist, zb == nullptr): survivor-list
+// positions c lstep (pairs with > kRefineMin survivors, before the refine pass); stage 2 (slist =
+// L1, zb): L1 positions c lstep of the pairs with a second stage, U also <= the stage-1 U
+// already in lU[p].  Only references with LB_c > U (1 + 1e-5) can prune; their radius is
+// thr_c = (LB_c (1 - 1e-5) - U (1 + 1e-5))^2 (1 - 1e-5) in squared f32 distance (the header
+// of consensus_lipschitz_kernel has the margins).
+__global__ __launch_bounds__(256) void consensus_lip_refs_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride, double trim_lo,
-    double trim_hi, double* __restrict__ lb, double* __restrict__ ub,
-    const int32_t* __restrict__ slist, const int32_t* __restrict__ scount,
-    int32_t* __restrict__ rlist, int olstride, int32_t* __restrict__ rcount, int shard,
-    int nshards, int lstep) {
-    // slist == nullptr: the rows [ra, rb) of row shard `shard` of `nshards` (all K rows when
-    // unsharded) before the histogram pass, against that shard's own reference rows ra, ra + 16,
-    // ... (configs[4]'s row-sharded consensus: U is then the shard's smallest reference UB, still
-    // >= the global minimum of T, so every pruning stays rigorous); else the per-pair survivor
-    // list slist[p][0 .. scount[p]) after the first select (before the refine pass, whose
-    // reference survivors, every 16th, are already refined)
-    __shared__ float4 refs[kLipChunk];
+    double trim_hi, const double* __restrict__ lb, const double* __restrict__ ub,
+    const int32_t* __restrict__ slist, const int32_t* __restrict__ scount, int lstep, int shard,
+    int nshards, const int32_t* __restrict__ zb, float4* __restrict__ lref,
+    double* __restrict__ lU, int32_t* __restrict__ lcnt, int cap) {
     __shared__ double red[4];
     __shared__ int nlive;
+    const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
+    const int K = kcount[p];
+    const int ra = slist ? 0 : (int)((int64_t)K * shard / nshards);
+    const int n = slist ? scount[p] : (int)((int64_t)K * (shard + 1) / nshards) - ra;
+    const int32_t* SL = slist ? slist + (size_t)p * stride : nullptr;
+    auto rowpos = [&](int k) { return SL ? (int)SL[k] : ra + k; };
+    const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
+    const int nref = n > 0 ? (n + lstep - 1) / lstep : 0;
+    bool on = hi > lo && (zb ? zb[p] >= 0 : (SL ? n > kRefineMin : K >= kLipMinK));
+    const double Uprev = zb ? lU[p] : __builtin_huge_val();
+    double U = __builtin_huge_val();
+    if (on) {  // (uniform)
+        for (int c = tid; c < nref; c += 256) U = fmin(U, ub[(size_t)p * stride + rowpos(c * lstep)]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) U = fmin(U, __shfl_xor(U, o, 64));
+        if (lane == 0) red[tid >> 6] = U;
+        if (tid == 0) nlive = 0;
+        __syncthreads();
+        U = fmin(fmin(fmin(red[0], red[1]), fmin(red[2], red[3])), Uprev);
+        on = U > 0.0 && U < __builtin_huge_val();
+    }
+    if (!on) {
+        if (tid == 0) {
+            lU[p] = __builtin_huge_val();
+            lcnt[p] = 0;
+        }
+        return;
+    }
+    const double Um = U * (1.0 + 1e-5);
+    const float* X = rv + (size_t)p * 3 * stride;
+    float4* R = lref + (size_t)p * cap;
+    for (int c = tid; c < nref; c += 256) {
+        const int row = rowpos(c * lstep);
+        const double a = lb[(size_t)p * stride + row] * (1.0 - 1e-5) - Um;
+        if (a > 0.0) {
+            const float thr = (float)(a * a * (1.0 - 1e-5));
+            R[atomicAdd(&nlive, 1)] = make_float4(X[row], X[stride + row], X[2 * stride + row], thr);
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        lU[p] = U;
+        lcnt[p] = nlive;
+    }
+}
+
+// The candidate rows of a pruning block (up to 512; x, y, z and the row index as bits in act)
+// against the pair's staged references R[0 .. m), kLipChunk2 at a time through LDS.  After
+// every kLipBatch references the rows still unpruned are compacted (in place, densely; thread t
+// takes slots 2t, 2t + 1 as one packed pair), so the live rows fill the first ceil(na / 128)
+// waves and the others skip: on a configs[1] pair ~84 % of the rows are pruned, most by one
+// of the first ~100 references in any order (a numpy model of the fixture pair: ~2.5x fewer
+// tests than every row against every reference).  prune(row) is called once per pruned row;
+// the survivors are left in act[0 .. return value).  Counters cnt[t & 3] of batch t are reset
+// two batches ahead, between barriers.
+constexpr int kLipBatch = 64;
+struct LipShared {
+    float4 act[512];
+    float4 refs[kLipChunk2];
+    double red[4];
+    int cnt[4];
+};
+template <class Prune>
+__device__ int lip_prune_rows(LipShared& sh, int na, const float4* __restrict__ R, int m,
+                              Prune prune) {
+    const int tid = threadIdx.x, lane = wave_lane();
+    int t = 0;
+    for (int c0 = 0; c0 < m && na > 0; c0 += kLipChunk2) {
+        const int nc = min(kLipChunk2, m - c0);
+        __syncthreads();  // the previous chunk's readers are done
+        for (int c = tid; c < nc; c += 256) sh.refs[c] = R[c0 + c];
+        __syncthreads();
+        for (int q0 = 0; q0 < nc && na > 0; q0 += kLipBatch, t++) {
+            const int q1 = min(nc, q0 + kLipBatch);
+            const bool v0 = 2 * tid < na, v1 = 2 * tid + 1 < na;
+            const float4 a0 = sh.act[v0 ? 2 * tid : 0];
+            const float4 a1 = sh.act[v1 ? 2 * tid + 1 : 0];
+            const f32x2 xi = {a0.x, a1.x}, yi = {a0.y, a1.y}, zi = {a0.z, a1.z};
+            uint32_t neg0 = 0u, neg1 = 0u;
+            if (v0) {  // (a wave whose slots are all empty skips the tests)
+                for (int q = q0; q < q1; q++) {
+                    const float4 r = sh.refs[q];
+                    const f32x2 dx = xi - r.x, dy = yi - r.y, dz = zi - r.z;
+                    f32x2 s2 = dx * dx;
+                    s2 = __builtin_elementwise_fma(dy, dy, s2);
+                    s2 = __builtin_elementwise_fma(dz, dz, s2);
+                    const f32x2 d = s2 - r.w;
+                    neg0 |= __float_as_uint(d[0]);
+                    neg1 |= __float_as_uint(d[1]);
+                }
+            }
+            const bool p0 = v0 && (neg0 >> 31), p1 = v1 && (neg1 >> 31);
+            if (p0) prune(__float_as_int(a0.w));
+            if (p1) prune(__float_as_int(a1.w));
+            const bool k0 = v0 && !p0, k1 = v1 && !p1;
+            const uint64_t b0 = __builtin_amdgcn_ballot_w64(k0), b1 = __builtin_amdgcn_ballot_w64(k1);
+            int base = 0;
+            if (lane == 0 && (b0 | b1))
+                base = atomicAdd(&sh.cnt[t & 3], __builtin_popcountll(b0) + __builtin_popcountll(b1));
+            base = __shfl(base, 0, 64);
+            __syncthreads();  // every slot of this batch is read: compact in place
+            const uint64_t below = (1ull << lane) - 1ull;
+            if (k0) sh.act[base + __builtin_popcountll(b0 & below)] = a0;
+            if (k1) sh.act[base + __builtin_popcountll(b0) + __builtin_popcountll(b1 & below)] = a1;
+            __syncthreads();
+            na = sh.cnt[t & 3];
+            if (tid == 0) sh.cnt[(t + 2) & 3] = 0;
+        }
+    }
+    return na;
+}
+
+// append act[0 .. na) (the rows left) to a per-pair list
+__device__ void lip_append(const LipShared& sh, int na, int32_t* __restrict__ list,
+                           int32_t* __restrict__ count) {
+    const int tid = threadIdx.x, lane = wave_lane();
+    for (int a = tid; a - tid < na; a += 256) {
+        const bool keep = a < na;
+        const int i = keep ? __float_as_int(sh.act[a].w) : 0;
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
+        int base = 0;
+        if (lane == 0 && bal) base = atomicAdd(count, __builtin_popcountll(bal));
+        base = __shfl(base, 0, 64);
+        if (keep) list[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = i;
+    }
+}
+
+// Lipschitz pre-pruning (before the full bounds pass).  The trimmed mean T(x) of the distances
+// from x to the set is 1-Lipschitz in x (every distance is, so are the order statistics and
+// their mean): T(i) >= T(c) - d(i, c).  The bounds kernel first runs on the reference rows
+// c = 0, kLipStep, 2 kLipStep, ... (1/16 of the rows); with U = their smallest UB, a row i with
+// d(i, c) < LB(c) - U for some reference c has T(i) > U >= the final min UB, so it cannot be the
+// argmin and skips the K-column histogram pass.  The test runs in squared f32 distances against
+// per-reference thresholds thr_c = (LB_c (1 - 1e-5) - U (1 + 1e-5))^2 (1 - 1e-5): the 1e-5
+// margins cover the f32 rounding of s (<= 5u), the reference's own f32 distances and fp64 sum
+// (<= 4u relative) and the rounding of thr, so a pruned row's LB = U (1 + 5e-6) is rigorous and
+// strictly above every UB that select compares against.  Pruned rows get [LB, +inf) and no
+// boundary bins (select drops them); the others are appended (any order) to the per-pair list
+// that the second bounds pass reads.  Synthetic configs[1] pairs (one cluster of ~1e4 valid
+// rotations): ~84 % of the rows are pruned.
+//   slist == nullptr: the rows [ra, rb) of row shard `shard` of `nshards` (all K rows when
+// unsharded), against that shard's own reference rows ra, ra + 16, ... (configs[4]'s
+// row-sharded consensus: U is then the shard's smallest reference UB, still >= the global
+// minimum of T, so every pruning stays rigorous); else the per-pair survivor list
+// slist[p][0 .. scount[p]) after the first select (before the refine pass, whose reference
+// survivors, every 16th, are already refined).  The references: consensus_lip_refs_kernel.
+__global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride,
+    double* __restrict__ lb, double* __restrict__ ub, const int32_t* __restrict__ slist,
+    const int32_t* __restrict__ scount, int32_t* __restrict__ rlist, int olstride,
+    int32_t* __restrict__ rcount, int shard, int nshards, int lstep,
+    const float4* __restrict__ lref, const double* __restrict__ lU,
+    const int32_t* __restrict__ lcnt, int cap) {
+    __shared__ LipShared sh;
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
     const int ra = slist ? 0 : (int)((int64_t)K * shard / nshards);
     const int n = slist ? scount[p] : (int)((int64_t)K * (shard + 1) / nshards) - ra;
-    const int i0 = blockIdx.x * 512;  // two positions per thread: i0 + tid and i0 + 256 + tid
+    const int i0 = blockIdx.x * 512;  // positions i0 .. i0 + 511
     if (i0 >= n) return;
     if (slist && n <= kRefineMin) return;  // few survivors: no refine pass, nothing to list
     const int32_t* SL = slist ? slist + (size_t)p * stride : nullptr;
-    auto rowpos = [&](int k) { return SL ? (int)SL[k] : ra + k; };
     const float* X = rv + (size_t)p * 3 * stride;
-    const float* Y = X + stride;
-    const float* Z = Y + stride;
     double* LBp = lb + (size_t)p * stride;
     double* UBp = ub + (size_t)p * stride;
-    const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
-    const int nref = (n + lstep - 1) / lstep;  // every lstep-th position is a reference
-    bool prune_on = (SL ? n > kRefineMin : K >= kLipMinK) && hi > lo;
-    double U = __builtin_huge_val();
-    if (prune_on) {
-        for (int c = tid; c < nref; c += 256) U = fmin(U, UBp[rowpos(c * lstep)]);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) U = fmin(U, __shfl_xor(U, o, 64));
-        if (lane == 0) red[tid >> 6] = U;
-        __syncthreads();
-        U = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
-        prune_on = U > 0.0 && U < __builtin_huge_val();
-    }
-    int ii[2];
-    bool active[2];
-    f32x2 xi, yi, zi;
+    const double U = lU[p];
+    const int m = lcnt[p];
+    const bool prune_on = U < __builtin_huge_val();
+    // the block's candidate rows, compacted into act; in list mode a survivor whose own
+    // (first-pass) LB already exceeds the refined U cannot be the argmin either (T_i >= LB_i >
+    // U >= min T: not even a tie): pruned at once, no refine needed
+    if (tid < 4) sh.cnt[tid] = 0;
+    __syncthreads();
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const int k = i0 + 256 * h + tid;
-        active[h] = k < n && (k % lstep) != 0;
-        ii[h] = active[h] ? rowpos(k) : 0;
-        xi[h] = active[h] ? X[ii[h]] : 0.f;
-        yi[h] = active[h] ? Y[ii[h]] : 0.f;
-        zi[h] = active[h] ? Z[ii[h]] : 0.f;
-    }
-    // sign bits of s - thr over the references: negative for some c = pruned
-    uint32_t neg0 = 0u, neg1 = 0u;
-    if (prune_on) {
-        const double Um = U * (1.0 + 1e-5);
-        for (int c0 = 0; c0 < nref; c0 += kLipChunk) {
-            const int nc = min(kLipChunk, nref - c0);
-            __syncthreads();  // the previous chunk's readers are done
-            if (tid == 0) nlive = 0;
-            __syncthreads();
-            // only references with LB_c > U (1 + 1e-5) can prune: compacted (any order)
-            for (int c = tid; c < nc; c += 256) {
-                const int row = rowpos((c0 + c) * lstep);
-                const double a = LBp[row] * (1.0 - 1e-5) - Um;
-                if (a > 0.0) {
-                    const float thr = (float)(a * a * (1.0 - 1e-5));
-                    refs[atomicAdd(&nlive, 1)] = make_float4(X[row], Y[row], Z[row], thr);
-                }
-            }
-            __syncthreads();
-            const int m = nlive;
-            for (int q = 0; q < m; q++) {
-                const float4 r = refs[q];
-                const f32x2 dx = xi - r.x, dy = yi - r.y, dz = zi - r.z;
-                f32x2 s = dx * dx;
-                s = __builtin_elementwise_fma(dy, dy, s);
-                s = __builtin_elementwise_fma(dz, dz, s);
-                const f32x2 t = s - r.w;
-                neg0 |= __float_as_uint(t[0]);
-                neg1 |= __float_as_uint(t[1]);
-            }
+        bool act = k < n && (k % lstep) != 0;
+        const int i = act ? (SL ? (int)SL[k] : ra + k) : 0;
+        if (act && SL && prune_on && LBp[i] > U * (1.0 + 1e-5)) {
+            LBp[i] = fmax(LBp[i], U * (1.0 + 5e-6));
+            UBp[i] = __builtin_huge_val();
+            act = false;
         }
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(act);
+        int base = 0;
+        if (lane == 0 && bal) base = atomicAdd(&sh.cnt[3], __builtin_popcountll(bal));
+        base = __shfl(base, 0, 64);
+        if (act)
+            sh.act[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] =
+                make_float4(X[i], X[stride + i], X[2 * stride + i], __int_as_float(i));
     }
-    const bool pr[2] = {(neg0 >> 31) != 0u, (neg1 >> 31) != 0u};
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const int i = ii[h];
-        // list mode: a survivor whose own (first-pass) LB already exceeds the refined U cannot
-        // be the argmin either (T_i >= LB_i > U >= min T: not even a tie) -- no refine needed
-        const bool above = SL && prune_on && active[h] && LBp[i] > U * (1.0 + 1e-5);
-        const bool pruned = active[h] && (pr[h] || above);
-        if (pruned) {
+    __syncthreads();
+    int na = sh.cnt[3];
+    __syncthreads();
+    if (tid == 3) sh.cnt[3] = 0;  // (batch counters 0 .. 3 start at zero)
+    if (prune_on && m > 0) {
+        auto prune = [&](int i) {
             LBp[i] = SL ? fmax(LBp[i], U * (1.0 + 5e-6)) : U * (1.0 + 5e-6);
             UBp[i] = __builtin_huge_val();
-        }
-        const bool keep = active[h] && !pr[h];
-        const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
-        if (bal) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(&rcount[p], __builtin_popcountll(bal));
-            base = __shfl(base, 0, 64);
-            if (keep)
-                rlist[(size_t)p * olstride + base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = i;
-        }
+        };
+        na = lip_prune_rows(sh, na, lref + (size_t)p * cap, m, prune);
     }
+    lip_append(sh, na, rlist + (size_t)p * olstride, &rcount[p]);
 }
 
 // Tighter bounds for the surviving rows (4 per block, lanes rotating over the rows as in the
@@ -2396,6 +2518,19 @@ constexpr int kZoomMin = ERP_ZOOM_MIN;         // survivors per pair below which
 #endif
 constexpr int kZoomMax = ERP_ZOOM_MAX;         // ... and above which none either
 
+// d-space edges of the zoom grid whose first bin is z (absolute, in units of key >> (23 - MANT)):
+// bin b holds the keys of [z + b, z + b + 1) << (23 - MANT), so the reference's d = sqrtf(s)
+// lies in [sqrtf(lower key), sqrtf(upper key)]; the edge bins also hold the clamped keys
+template <int MANT>
+__device__ __forceinline__ void zoom_grid_edges(int z, float* __restrict__ ed) {
+    constexpr int kShift = 23 - MANT;
+    for (int b = threadIdx.x; b < kNB; b += blockDim.x) {
+        const uint32_t key = (uint32_t)(z + b) << kShift;
+        ed[b] = b == 0 ? 0.f : __builtin_sqrtf(__uint_as_float(key));
+        ed[kNB + b] = b == kNB - 1 ? kInf : __builtin_sqrtf(__uint_as_float(key + (1u << kShift)));
+    }
+}
+
 // per pair: the zoom grid's first bin zbase[p] (absolute, in units of key >> (23 - MANT); -1:
 // no zoom) from the span of the survivors' rank-window bins of the previous grid (SRC_MANT bins
 // per binade, absolute), and its d-space edges
@@ -2405,7 +2540,6 @@ __global__ __launch_bounds__(256) void consensus_zoom_prep_kernel(
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
     const int32_t* __restrict__ wsel, int wsel_base_coarse, int stride, double trim_lo,
     double trim_hi, int32_t* __restrict__ zbase, float* __restrict__ edz) {
-    constexpr int kShift = 23 - MANT;
     static_assert(MANT >= SRC_MANT, "finer grid");
     __shared__ int red[2][4];
     const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
@@ -2420,8 +2554,12 @@ __global__ __launch_bounds__(256) void consensus_zoom_prep_kernel(
     int amin = 1 << 30, bmax = -1;
     for (int k = tid; k < n; k += 256) {
         const int row = surv[(size_t)p * stride + k];
-        amin = min(amin, wsel[((size_t)p * stride + row) * 2]);
-        bmax = max(bmax, wsel[((size_t)p * stride + row) * 2 + 1]);
+        const int a = wsel[((size_t)p * stride + row) * 2];
+        const int b = wsel[((size_t)p * stride + row) * 2 + 1];
+        if (a >= 0 && b >= 0) {  // (-1: a second-stage reference whose window left the fine grid)
+            amin = min(amin, a);
+            bmax = max(bmax, b);
+        }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -2435,6 +2573,10 @@ __global__ __launch_bounds__(256) void consensus_zoom_prep_kernel(
     __syncthreads();
     amin = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
     bmax = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+    if (bmax < 0) {
+        if (tid == 0) zbase[p] = -1;
+        return;
+    }
     // the first pass's bins are relative to the pair's grid (bsel + (elo << kMantBits));
     // the zoom passes write absolute bins
     const int off = wsel_base_coarse ? (bounds_elo(dscale[p]) << kMantBits) : 0;
@@ -2442,12 +2584,7 @@ __global__ __launch_bounds__(256) void consensus_zoom_prep_kernel(
     const int ulo = (amin + off) << up, uhi = ((bmax + off + 1) << up) - 1;  // in this grid's bins
     const int z = max(max(ulo, uhi - (kNB - 1)), 1 << MANT);                 // top-aligned
     if (tid == 0) zbase[p] = z;
-    float* ed = edz + (size_t)p * 2 * kNB;
-    for (int b = tid; b < kNB; b += 256) {
-        const uint32_t key = (uint32_t)(z + b) << kShift;
-        ed[b] = b == 0 ? 0.f : __builtin_sqrtf(__uint_as_float(key));
-        ed[kNB + b] = b == kNB - 1 ? kInf : __builtin_sqrtf(__uint_as_float(key + (1u << kShift)));
-    }
+    zoom_grid_edges<MANT>(z, edz + (size_t)p * 2 * kNB);
 }
 
 // one unit (kBoundRows survivors of one pair) per block; items flattened over the pairs; writes
@@ -2459,7 +2596,7 @@ __device__ __forceinline__ void consensus_zoom_unit(
     double trim_hi, double* __restrict__ lb, double* __restrict__ ub,
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
     const int32_t* __restrict__ uoff, int n_pairs, int32_t* __restrict__ zsel, int g,
-    uint32_t* hist) {
+    uint32_t* hist, int step, const float* __restrict__ dscale, int32_t* __restrict__ bsel_out) {
     constexpr int kShift = 23 - MANT;
     constexpr int R = kBoundRows;
     constexpr int NS = 256 / R;
@@ -2473,10 +2610,11 @@ __device__ __forceinline__ void consensus_zoom_unit(
         if (uoff[m] <= g) p = m; else b = m;
     }
     const int tid = threadIdx.x, lane = wave_lane();
-    const int K = kcount[p], nloc = nsurv[p], zbase = zbase_p[p];
+    const int K = kcount[p], nloc = (nsurv[p] + step - 1) / step, zbase = zbase_p[p];
     const int l0 = (g - uoff[p]) * R;
     if (zbase < 0 || l0 >= nloc) return;  // (uniform)
     const int32_t* RL = surv + (size_t)p * stride;
+    auto rowat = [&](int l) { return (int)RL[(size_t)l * step]; };
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
@@ -2487,7 +2625,7 @@ __device__ __forceinline__ void consensus_zoom_unit(
 #pragma unroll
     for (int t = 0; t < R; t++) {
         const int r = (lane + t) & (R - 1);
-        const int row = RL[min(l0 + r, nloc - 1)];
+        const int row = rowat(min(l0 + r, nloc - 1));
         xi[t >> 1][t & 1] = X[row];
         yi[t >> 1][t & 1] = Y[row];
         zi[t >> 1][t & 1] = Z[row];
@@ -2562,7 +2700,7 @@ __device__ __forceinline__ void consensus_zoom_unit(
     int cum = 0;
     for (int q = 0; q < sl; q++) cum += part[q][r];
     const bool rvalid = l0 + r < nloc;
-    const int row = rvalid ? RL[l0 + r] : 0;
+    const int row = rvalid ? rowat(l0 + r) : 0;
     float L = 0.f, U = 0.f;
     int sel_a = -1, sel_b = -1;  // bins of ranks lo and hi-1 on this grid
     if (cum < hi && cum + c > lo) {
@@ -2583,6 +2721,23 @@ __device__ __forceinline__ void consensus_zoom_unit(
     if (rvalid) {
         if (sel_a >= 0) zsel[((size_t)p * stride + row) * 2] = zbase + sel_a;
         if (sel_b >= 0) zsel[((size_t)p * stride + row) * 2 + 1] = zbase + sel_b;
+        if (bsel_out) {
+            // rows with no first-pass histogram (the second-stage references of the
+            // pre-pruning): their rank-window bins on the coarse grid, which refine and the
+            // exact pass start from, are the fine bins' coarse parents -- except in a clamped
+            // edge bin, where they are unknown (-1: those passes then keep the old bounds /
+            // take the radix path)
+            static_assert(MANT >= kMantBits, "fine grid");
+            const int cb = bounds_elo(dscale[p]) << kMantBits;
+            auto coarse = [&](int sel) {
+                if (sel <= 0 || sel >= kNB - 1) return -1;
+                const int c = ((zbase + sel) >> (MANT - kMantBits)) - cb;
+                return (c > 0 && c < kNB - 1) ? c : -1;
+            };
+            // (written by the slice that holds the rank: exactly one per rank when hi > lo)
+            if (sel_a >= 0) bsel_out[((size_t)p * stride + row) * 2] = coarse(sel_a);
+            if (sel_b >= 0) bsel_out[((size_t)p * stride + row) * 2 + 1] = coarse(sel_b);
+        }
     }
     partL[sl][r] = L;
     partU[sl][r] = U;
@@ -2597,8 +2752,15 @@ __device__ __forceinline__ void consensus_zoom_unit(
         // sequential sum (as in the first pass)
         double* lp = lb + (size_t)p * stride + row;
         double* up = ub + (size_t)p * stride + row;
-        *lp = fmax(*lp, ((double)L / w) * (1.0 - 2e-4));
-        *up = fmin(*up, ((double)U / w) * (1.0 + 2e-4));
+        const double nl = hi > lo ? ((double)L / w) * (1.0 - 2e-4) : 0.0;
+        const double nu = hi > lo ? ((double)U / w) * (1.0 + 2e-4) : 0.0;
+        if (bsel_out) {  // no earlier bounds for these rows: overwrite
+            *lp = nl;
+            *up = nu;
+        } else {
+            *lp = fmax(*lp, nl);
+            *up = fmin(*up, nu);
+        }
     }
 }
 
@@ -2609,11 +2771,13 @@ __global__ __launch_bounds__(256) void consensus_zoom_kernel(
     const float* __restrict__ edz, const int32_t* __restrict__ zbase_p, int stride, double trim_lo,
     double trim_hi, double* __restrict__ lb, double* __restrict__ ub,
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
-    const int32_t* __restrict__ uoff, int n_pairs, int32_t* __restrict__ zsel) {
+    const int32_t* __restrict__ uoff, int n_pairs, int32_t* __restrict__ zsel, int step,
+    const float* __restrict__ dscale, int32_t* __restrict__ bsel_out) {
     __shared__ __align__(16) uint32_t hist[kNB * kBoundRows];  // [bin][row]
     if ((int)blockIdx.x >= uoff[n_pairs]) return;
     consensus_zoom_unit<MANT>(kcount, rv, edz, zbase_p, stride, trim_lo, trim_hi, lb, ub, surv,
-                              nsurv, uoff, n_pairs, zsel, blockIdx.x, hist);
+                              nsurv, uoff, n_pairs, zsel, blockIdx.x, hist, step, dscale,
+                              bsel_out);
 }
 
 // Before the Lipschitz pre-pruning: the reference rows whose first-pass UB is within 3 % of the
@@ -2648,6 +2812,156 @@ __global__ __launch_bounds__(256) void consensus_pick_central_kernel(
     }
     __syncthreads();
     if (tid == 0) count[p] = min(n_s, cap);
+}
+
+// ---- second pre-pruning stage (ERP_LIP2, default on) ------------------------------------
+// After the first stage a configs[1] pair still lists ~16 % of its rows (L1): the rows near
+// the minimum, where T is flat and the references every 16th row, with bounds 2^-5 wide, stop
+// pruning.  Every m-th L1 row (the second-stage references) is bounded on the fine zoom grid
+// (64 bins per binade of s, ~2^-7 wide, consensus_zoom_unit with a list step), and the other
+// L1 rows are tested against them exactly as against the first-stage references (T is
+// 1-Lipschitz): with U2 = min(U1, min UB over the second-stage references), any UB >= min T, a
+// row with d(i, c) < LB(c) - U2 has T(i) > U2, so its LB = U2 (1 + 5e-6) is rigorous.  Only
+// the rows that survive (L2) get the coarse K-column histogram.  On the fixture pair of
+// configs[1] (tests/golden/find_4096_it10k.npz) this bins 408 fine + ~620 coarse rows instead
+// of ~1630 coarse rows after the 625 first-stage references (a numpy model of the two tests).
+constexpr int kLip2Min = 64;              // smaller L1 lists: no second stage
+
+// per pair: whether the second stage runs (zb[p] = the fine grid's first bin, else -1) and the
+// fine grid's edges, placed on the rank windows (first-pass bsel) of the central first-stage
+// references (UB within 1/16 of the smallest): the L1 rows lie near them, and T's order
+// statistics are 1-Lipschitz too, so their windows lie near those
+__global__ __launch_bounds__(256) void consensus_ref2_prep_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ dscale,
+    const double* __restrict__ ub, const int32_t* __restrict__ bsel,
+    const int32_t* __restrict__ n1c, int stride, double trim_lo, double trim_hi, int shard,
+    int nshards, int32_t* __restrict__ zb, float* __restrict__ edz) {
+    constexpr int MANT = 6;
+    __shared__ double redd[4];
+    __shared__ int red[2][4];
+    const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
+    const int K = kcount[p], n1 = n1c[p];
+    const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
+    if (n1 < kLip2Min || K < kLipMinK || hi <= lo) {
+        if (tid == 0) zb[p] = -1;
+        return;
+    }
+    const int ra = (int)((int64_t)K * shard / nshards), rb = (int)((int64_t)K * (shard + 1) / nshards);
+    const int nref = rb > ra ? (rb - ra + kLipStep - 1) / kLipStep : 0;
+    const double* U = ub + (size_t)p * stride;
+    double m = __builtin_huge_val();
+    for (int c = tid; c < nref; c += 256) m = fmin(m, U[ra + c * kLipStep]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o, 64));
+    if (lane == 0) redd[tid >> 6] = m;
+    __syncthreads();
+    m = fmin(fmin(redd[0], redd[1]), fmin(redd[2], redd[3]));
+    const double lim = m * (1.0 + 0.0625);
+    int amin = 1 << 30, bmax = -1;
+    for (int c = tid; c < nref && m < __builtin_huge_val(); c += 256) {
+        const int row = ra + c * kLipStep;
+        if (U[row] <= lim) {
+            amin = min(amin, bsel[((size_t)p * stride + row) * 2]);
+            bmax = max(bmax, bsel[((size_t)p * stride + row) * 2 + 1]);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        amin = min(amin, __shfl_xor(amin, o, 64));
+        bmax = max(bmax, __shfl_xor(bmax, o, 64));
+    }
+    if (lane == 0) {
+        red[0][tid >> 6] = amin;
+        red[1][tid >> 6] = bmax;
+    }
+    __syncthreads();
+    amin = min(min(red[0][0], red[0][1]), min(red[0][2], red[0][3]));
+    bmax = max(max(red[1][0], red[1][1]), max(red[1][2], red[1][3]));
+    if (bmax < 0 || amin > bmax) {
+        if (tid == 0) zb[p] = -1;
+        return;
+    }
+    const int off = bounds_elo(dscale[p]) << kMantBits;
+    constexpr int up = MANT - kMantBits;
+    const int ulo = (amin + off) << up, uhi = ((bmax + off + 1) << up) - 1;
+    // margins: an L1 row's window reaches below the central references' (its rank-lo distance
+    // is >= theirs - d(i, c) only) by more than it reaches above: 2 binades of s below ulo, 1
+    // above uhi when the span allows, else the top kept
+    const int z = max(max(ulo - 2 * (1 << MANT), uhi + (1 << MANT) - (kNB - 1)), 1 << MANT);
+    if (tid == 0) zb[p] = z;
+    zoom_grid_edges<MANT>(z, edz + (size_t)p * 2 * kNB);
+}
+
+// the test itself: positions k of L1 (l1[p][0 .. n1c[p])), k % m == 0 the references (bounded
+// by the zoom pass); the rows that survive are appended to l2 / n2c.  A pair without a second
+// stage (zb < 0) passes every L1 row through.
+__global__ __launch_bounds__(256) void consensus_lipschitz2_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride,
+    double* __restrict__ lb, double* __restrict__ ub, const int32_t* __restrict__ l1,
+    const int32_t* __restrict__ n1c, const int32_t* __restrict__ zb, int m,
+    const int32_t* __restrict__ bsel, int32_t* __restrict__ l2, int32_t* __restrict__ n2c,
+    int32_t* __restrict__ nfb, const float4* __restrict__ lref, const double* __restrict__ lU,
+    const int32_t* __restrict__ lcnt, int cap) {
+    __shared__ LipShared sh;
+    const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
+    const int n = n1c[p];
+    const int i0 = blockIdx.x * 512;  // positions i0 .. i0 + 511 of L1
+    if (i0 >= n) return;
+    const bool on = zb[p] >= 0;  // (uniform)
+    const int32_t* L = l1 + (size_t)p * stride;
+    const float* X = rv + (size_t)p * 3 * stride;
+    double* LBp = lb + (size_t)p * stride;
+    double* UBp = ub + (size_t)p * stride;
+    const double U = on ? lU[p] : __builtin_huge_val();  // min(U1, the references' UBs)
+    const int nref = on ? lcnt[p] : 0;
+    // candidates: the L1 rows that are not second-stage references, and the references whose
+    // rank window left the fine grid (coarse window bins unknown, fine bounds loose: the coarse
+    // pass re-bins them, overwriting their bounds and window bins)
+    if (tid < 4) sh.cnt[tid] = 0;
+    __syncthreads();
+    int fb = 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int k = i0 + 256 * h + tid;
+        bool act = k < n;
+        const int i = act ? (int)L[k] : 0;
+        if (act && on && k % m == 0) {
+            act = bsel[((size_t)p * stride + i) * 2] < 0 || bsel[((size_t)p * stride + i) * 2 + 1] < 0;
+            fb += act;
+        }
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(act);
+        int base = 0;
+        if (lane == 0 && bal) base = atomicAdd(&sh.cnt[3], __builtin_popcountll(bal));
+        base = __shfl(base, 0, 64);
+        if (act)
+            sh.act[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] =
+                make_float4(X[i], X[stride + i], X[2 * stride + i], __int_as_float(i));
+    }
+    if (fb) atomicAdd(&nfb[p], fb);  // (rare: binned twice, counted once)
+    __syncthreads();
+    int na = sh.cnt[3];
+    __syncthreads();
+    if (tid == 3) sh.cnt[3] = 0;
+    if (U < __builtin_huge_val() && nref > 0) {
+        // (a pruned row's LB = U (1 + 5e-6) is rigorous for a reference row too)
+        auto prune = [&](int i) {
+            LBp[i] = U * (1.0 + 5e-6);
+            UBp[i] = __builtin_huge_val();
+        };
+        na = lip_prune_rows(sh, na, lref + (size_t)p * cap, nref, prune);
+    }
+    lip_append(sh, na, l2 + (size_t)p * stride, &n2c[p]);
+}
+
+// binned rows beyond the first-stage references (erp_pair_result.binned_rows): the second-stage
+// references plus L2
+__global__ void consensus_ref2_count_kernel(int n_pairs, const int32_t* __restrict__ zb, int m,
+                                            const int32_t* __restrict__ n2c,
+                                            const int32_t* __restrict__ nfb,
+                                            int32_t* __restrict__ n1c) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pairs) return;
+    n1c[p] = (zb[p] >= 0 ? (n1c[p] + m - 1) / m : 0) + n2c[p] - nfb[p];
 }
 
 __global__ __launch_bounds__(256) void consensus_refine_kernel(
@@ -3373,19 +3687,41 @@ hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const f
     if (level == 1)
         hipLaunchKernelGGL(consensus_zoom_kernel<6>, dim3(max_units), dim3(256), 0, st, kcount, rv,
                            (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb,
-                           ub, surv, (const int32_t*)nsurv, (const int32_t*)uoff, P, zsel);
+                           ub, surv, (const int32_t*)nsurv, (const int32_t*)uoff, P, zsel, 1,
+                           dscale, (int32_t*)nullptr);
     else
         hipLaunchKernelGGL(consensus_zoom_kernel<8>, dim3(max_units), dim3(256), 0, st, kcount, rv,
                            (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb,
-                           ub, surv, (const int32_t*)nsurv, (const int32_t*)uoff, P, zsel);
+                           ub, surv, (const int32_t*)nsurv, (const int32_t*)uoff, P, zsel, 1,
+                           dscale, (int32_t*)nullptr);
     return hipGetLastError();
+}
+
+// the pruning references' scratch: [P][cap] float4, then lU [P] doubles, then lcnt [P] ints
+size_t lipref_bytes(int n_pairs, int stride) {
+    return (size_t)n_pairs * lipref_cap(stride) * sizeof(float4) + (size_t)n_pairs * 12 + 64;
+}
+struct LipRefViews {
+    float4* ref;
+    double* U;
+    int32_t* cnt;
+    int cap;
+};
+static LipRefViews lipref_views(void* base, int n_pairs, int stride) {
+    LipRefViews v;
+    v.cap = lipref_cap(stride);
+    v.ref = reinterpret_cast<float4*>(base);
+    v.U = reinterpret_cast<double*>(v.ref + (size_t)n_pairs * v.cap);
+    v.cnt = reinterpret_cast<int32_t*>(v.U + n_pairs);
+    return v;
 }
 
 hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const float* dscale,
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
-                                   int32_t* zsel, int zoom_refs, hipStream_t st) {
+                                   int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
+                                   void* lipref, hipStream_t st) {
     hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     const int stride = 2 * sh.iters;
     if (!rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
@@ -3415,22 +3751,63 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                                     trim_hi, lb, ub, bsel, rlist, cnt, zsel, 1, st);
         if (ze != hipSuccess) return ze;
     }
-    const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * sh.n_pairs, st);
+    const int P = sh.n_pairs;
+    const LipRefViews lr = lipref_views(lipref, P, stride);
+    const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * P, st);
     if (me != hipSuccess) return me;
-    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((srows + 511) / 512, sh.n_pairs),
-                       dim3(256), 0, st, kcount, rv, stride, trim_lo, trim_hi, lb, ub,
-                       (const int32_t*)nullptr, (const int32_t*)nullptr, rlist, stride, rcount,
-                       shard, nshards, kLipStep);
-    int32_t* uoff = rcount + sh.n_pairs;  // [n_pairs + 1] after the counts
-    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)rcount,
-                       sh.n_pairs, kBoundRows, 0, uoff);
+    hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
+                       trim_lo, trim_hi, (const double*)lb, (const double*)ub,
+                       (const int32_t*)nullptr, (const int32_t*)nullptr, kLipStep, shard, nshards,
+                       (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap);
+    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
+                       st, kcount, rv, stride, lb, ub, (const int32_t*)nullptr,
+                       (const int32_t*)nullptr, rlist, stride, rcount, shard, nshards, kLipStep,
+                       (const float4*)lr.ref, (const double*)lr.U, (const int32_t*)lr.cnt,
+                       lr.cap);
+    int32_t* uoff = rcount + P;  // [n_pairs + 1] after the counts
+    const int32_t* blist = rlist;
+    const int32_t* bcount = rcount;
+    if (lip2 && list2) {
+        // second stage: every kLip2Step-th L1 row on the fine grid, the other L1 rows tested
+        // against them; the survivors (list2, counts after the unit prefix) get the coarse pass
+        float* edz = edges + (size_t)P * 2 * kNB;
+        int32_t* zb = reinterpret_cast<int32_t*>(edges + (size_t)P * 4 * kNB);
+        int32_t* n2 = uoff + P + 1;
+        hipLaunchKernelGGL(consensus_ref2_prep_kernel, dim3(P), dim3(256), 0, st, kcount, dscale,
+                           (const double*)ub, (const int32_t*)bsel, (const int32_t*)rcount, stride,
+                           trim_lo, trim_hi, shard, nshards, zb, edz);
+        hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)rcount,
+                           P, kBoundRows * kLip2Step, kLip2Min - 1, uoff);
+        const int units2 = P * ((stride + kBoundRows * kLip2Step - 1) / (kBoundRows * kLip2Step));
+        hipLaunchKernelGGL(consensus_zoom_kernel<6>, dim3(units2), dim3(256), 0, st, kcount, rv,
+                           (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb, ub,
+                           (const int32_t*)rlist, (const int32_t*)rcount, (const int32_t*)uoff, P,
+                           zsel, kLip2Step, dscale, bsel);
+        const hipError_t m2 = hipMemsetAsync(n2, 0, sizeof(int32_t) * 2 * P, st);  // + nfb
+        if (m2 != hipSuccess) return m2;
+        hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv,
+                           stride, trim_lo, trim_hi, (const double*)lb, (const double*)ub,
+                           (const int32_t*)rlist, (const int32_t*)rcount, kLip2Step, shard,
+                           nshards, (const int32_t*)zb, lr.ref, lr.U, lr.cnt, lr.cap);
+        hipLaunchKernelGGL(consensus_lipschitz2_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
+                           st, kcount, rv, stride, lb, ub, (const int32_t*)rlist,
+                           (const int32_t*)rcount, (const int32_t*)zb, kLip2Step,
+                           (const int32_t*)bsel, list2, n2, n2 + P, (const float4*)lr.ref,
+                           (const double*)lr.U, (const int32_t*)lr.cnt, lr.cap);
+        hipLaunchKernelGGL(consensus_ref2_count_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P,
+                           (const int32_t*)zb, kLip2Step, (const int32_t*)n2,
+                           (const int32_t*)(n2 + P), rcount);
+        blist = list2;
+        bcount = n2;
+    }
+    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, bcount, P, kBoundRows, 0,
+                       uoff);
     // one block per unit of the longest possible lists: the live units come first in dispatch
     // order, the trailing blocks exit after one load
-    const int max_units = sh.n_pairs * ((stride + kBoundRows - 1) / kBoundRows);
+    const int max_units = P * ((stride + kBoundRows - 1) / kBoundRows);
     hipLaunchKernelGGL(consensus_bounds_list_kernel, dim3(max_units), dim3(256), 0, st,
-                       kcount, rv, dscale, edges, stride, trim_lo, trim_hi, lb, ub, bsel,
-                       (const int32_t*)rlist, (const int32_t*)rcount, (const int32_t*)uoff,
-                       sh.n_pairs);
+                       kcount, rv, dscale, edges, stride, trim_lo, trim_hi, lb, ub, bsel, blist,
+                       bcount, (const int32_t*)uoff, P);
     return hipGetLastError();
 }
 
@@ -3446,7 +3823,8 @@ hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, cons
 hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const float* dscale,
                                    const BatchShape& sh, double trim_lo, double trim_hi,
                                    const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
-                                   double* lb, double* ub, int32_t* list2, hipStream_t st) {
+                                   double* lb, double* ub, int32_t* list2, void* lipref,
+                                   hipStream_t st) {
     // scratch after nsurv[n_pairs] and the bounds-list counts[n_pairs]: the unit prefix
     // [n_pairs + 1], then the counts of list2 [n_pairs]
     const int P = sh.n_pairs, stride = 2 * sh.iters, l2stride = sortbuf_len(sh.iters);
@@ -3461,9 +3839,14 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
     // (B) Lipschitz pruning of the other survivors against the refined references
     const hipError_t me = hipMemsetAsync(n2, 0, sizeof(int32_t) * P, st);
     if (me != hipSuccess) return me;
+    const LipRefViews lr = lipref_views(lipref, P, stride);
+    hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
+                       trim_lo, trim_hi, (const double*)lb, (const double*)ub, surv, nsurv,
+                       kRefStep, 0, 1, (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap);
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, P), dim3(256), 0, st,
-                       kcount, rv, stride, trim_lo, trim_hi, lb, ub, surv, nsurv, list2, l2stride,
-                       n2, 0, 1, kRefStep);
+                       kcount, rv, stride, lb, ub, surv, nsurv, list2, l2stride, n2, 0, 1,
+                       kRefStep, (const float4*)lr.ref, (const double*)lr.U,
+                       (const int32_t*)lr.cnt, lr.cap);
     // (C) the survivors the references did not prune
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)n2, P,
                        kRefineRows, 0, uoff);
