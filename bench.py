@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--sigma", type=float, default=0.03,
                     help="pairs workload: descriptor noise of the true partners")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--worst-steps", type=int, default=3,
+                    help="pairs workload: timed steps of the worst-case batch (every pair a "
+                         "two-cluster consensus pair -- R1 and R2 both valid, K ~ 2 x iters -- "
+                         "at inlier fraction 0.98, so M ~ 4k; scripts/twin_seeds.json)")
     ap.add_argument("--hard-steps", type=int, default=3,
                     help="pairs workload: timed steps of a second, harder batch (half the left "
                          "keypoints without a partner, descriptor noise 0.035, 30%% of the true "
@@ -763,6 +767,48 @@ def main():
                                  want=("matches",))
             torch.cuda.synchronize()
             hard["parity"] = parity_check(hres, o["matches"][:n_h].cpu().numpy(), ora_h)
+    # the worst case beside it: every pair a two-cluster consensus pair (the pose makes R1 and
+    # R2 both valid, src/eight_point.cpp:71-85: K ~ 2 x iters, every trimmed mean within ~1 % of
+    # the minimum) at inlier fraction 0.98 (M ~ 4k: the most sampler / Gram work per pair)
+    worst = None
+    if args.steps > 0 and args.worst_steps > 0:
+        seeds = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                            "scripts", "twin_seeds.json")))["seeds"]
+        from erp_match_eightpoint_test_amd import synth
+        wpairs = [synth.make_pair(seeds[(rank * args.pairs + i) % len(seeds)], n_kpts=args.kpts,
+                                  inlier_frac=0.98, sigma=args.sigma) for i in range(args.pairs)]
+        wparts = [wpairs[i * args.pairs // S:(i + 1) * args.pairs // S] for i in range(S)]
+        wb = [to_device(part, dev) for part in wparts]
+        for sb, b in zip(subs, wb):
+            sb["runner"].reserve(len(b["width"]), b["max_nq"], b["max_nt"])
+        call(wb)
+        torch.cuda.synchronize()
+        tw0 = time.perf_counter()
+        for _ in range(args.worst_steps):
+            wout = call(wb)
+        torch.cuda.synchronize()
+        tw = (time.perf_counter() - tw0) / args.worst_steps
+        wres = results_to_numpy(wout)
+        worst = {"value": args.pairs / tw, "unit": "pairs/s", "ms_per_step": tw * 1e3,
+                 "steps": args.worst_steps, "inlier_frac": 0.98, "sigma": args.sigma,
+                 "seeds": "scripts/twin_seeds.json (R1 and R2 both valid)",
+                 "all_status_ok": bool(np.all(wres["status"] == 0)),
+                 "M_mean": float(wres["M"].mean()), "M_max": int(wres["M"].max()),
+                 "K_mean": float(wres["K"].mean()), "K_min": int(wres["K"].min()),
+                 "survivors_mean": float(wres["survivors"].mean()),
+                 "survivors_max": int(wres["survivors"].max()),
+                 "binned_rows_mean": float(wres["binned_rows"].mean())}
+        if world == 1 and not args.no_cpu_baseline:
+            threads, _ = host_cpu_share()
+            n_w = 1
+            ora_w = [oracle_pair(p, args.iters, threads) for p in wpairs[:n_w]]
+            sb = subs[0]
+            b = wb[0]
+            o = sb["runner"].run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"],
+                                 b["off_r"], b["width"], b["height"], b["max_nq"], b["max_nt"],
+                                 want=("matches",))
+            torch.cuda.synchronize()
+            worst["parity"] = parity_check(wres, o["matches"][:n_w].cpu().numpy(), ora_w)
     cpu = None
     parity = None
     multi = None
@@ -837,6 +883,7 @@ def main():
         "cpu_baseline": cpu,
         "latency": lat,
         "hard_data": hard,
+        "worst_case": worst,
         "stages_ms_serial_step": {k: v[0] for k, v in stages.items()},
         # the streams' overlap: the step's kernels run one after another (HIP events, serial
         # pass) against the timed, 4-stream step

@@ -2123,25 +2123,34 @@ __device__ int lip_prune_rows(LipShared& sh, int na, const float4* __restrict__ 
     for (int c0 = 0; c0 < m && na > 0; c0 += kLipChunk2) {
         const int nc = min(kLipChunk2, m - c0);
         __syncthreads();  // the previous chunk's readers are done
-        for (int c = tid; c < nc; c += 256) sh.refs[c] = R[c0 + c];
+        // (padded to whole batches with references that prune nothing: radius^2 = -1)
+        const int ncp = (nc + kLipBatch - 1) / kLipBatch * kLipBatch;
+        for (int c = tid; c < ncp; c += 256)
+            sh.refs[c] = c < nc ? R[c0 + c] : make_float4(0.f, 0.f, 0.f, -1.f);
         __syncthreads();
         for (int q0 = 0; q0 < nc && na > 0; q0 += kLipBatch, t++) {
-            const int q1 = min(nc, q0 + kLipBatch);
             const bool v0 = 2 * tid < na, v1 = 2 * tid + 1 < na;
             const float4 a0 = sh.act[v0 ? 2 * tid : 0];
             const float4 a1 = sh.act[v1 ? 2 * tid + 1 : 0];
             const f32x2 xi = {a0.x, a1.x}, yi = {a0.y, a1.y}, zi = {a0.z, a1.z};
             uint32_t neg0 = 0u, neg1 = 0u;
             if (v0) {  // (a wave whose slots are all empty skips the tests)
-                for (int q = q0; q < q1; q++) {
-                    const float4 r = sh.refs[q];
-                    const f32x2 dx = xi - r.x, dy = yi - r.y, dz = zi - r.z;
-                    f32x2 s2 = dx * dx;
-                    s2 = __builtin_elementwise_fma(dy, dy, s2);
-                    s2 = __builtin_elementwise_fma(dz, dz, s2);
-                    const f32x2 d = s2 - r.w;
-                    neg0 |= __float_as_uint(d[0]);
-                    neg1 |= __float_as_uint(d[1]);
+                // eight references' LDS reads ahead of their tests: one LDS latency per eight
+                // (one per reference measured the kernel latency-bound, SQ_WAIT_ANY 73 %)
+                for (int q = q0; q < q0 + kLipBatch; q += 8) {
+                    float4 r[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) r[u] = sh.refs[q + u];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) {
+                        const f32x2 dx = xi - r[u].x, dy = yi - r[u].y, dz = zi - r[u].z;
+                        f32x2 s2 = dx * dx;
+                        s2 = __builtin_elementwise_fma(dy, dy, s2);
+                        s2 = __builtin_elementwise_fma(dz, dz, s2);
+                        const f32x2 d = s2 - r[u].w;
+                        neg0 |= __float_as_uint(d[0]);
+                        neg1 |= __float_as_uint(d[1]);
+                    }
                 }
             }
             const bool p0 = v0 && (neg0 >> 31), p1 = v1 && (neg1 >> 31);
@@ -2521,13 +2530,20 @@ constexpr int kZoomMax = ERP_ZOOM_MAX;         // ... and above which none eithe
 // d-space edges of the zoom grid whose first bin is z (absolute, in units of key >> (23 - MANT)):
 // bin b holds the keys of [z + b, z + b + 1) << (23 - MANT), so the reference's d = sqrtf(s)
 // lies in [sqrtf(lower key), sqrtf(upper key)]; the edge bins also hold the clamped keys
+// The zoom bins s' = fma(dz, dz, fma(dy, dy, dx dx)) (two roundings fewer than the reference's
+// s = dx dx + dy dy + dz dz; both within 2^-22.4 of the exact sum of the exact squares of the
+// same dx, dy, dz), so the reference's s of a key in [E_b, E_b+1) lies in [E_b (1 - 2^-21),
+// E_b+1 (1 + 2^-21)] and its d = sqrtf(s) in [sqrtf(E_b) (1 - 2^-20), sqrtf(E_b+1) (1 + 2^-20)]
+// (the factors also cover sqrtf's own rounding and the f32 products).
 template <int MANT>
 __device__ __forceinline__ void zoom_grid_edges(int z, float* __restrict__ ed) {
     constexpr int kShift = 23 - MANT;
     for (int b = threadIdx.x; b < kNB; b += blockDim.x) {
         const uint32_t key = (uint32_t)(z + b) << kShift;
-        ed[b] = b == 0 ? 0.f : __builtin_sqrtf(__uint_as_float(key));
-        ed[kNB + b] = b == kNB - 1 ? kInf : __builtin_sqrtf(__uint_as_float(key + (1u << kShift)));
+        ed[b] = b == 0 ? 0.f : __builtin_sqrtf(__uint_as_float(key)) * (1.0f - 0x1p-20f);
+        ed[kNB + b] = b == kNB - 1
+                          ? kInf
+                          : __builtin_sqrtf(__uint_as_float(key + (1u << kShift))) * (1.0f + 0x1p-20f);
     }
 }
 
@@ -2629,8 +2645,10 @@ __device__ __forceinline__ void consensus_zoom_unit(
         xi[t >> 1][t & 1] = X[row];
         yi[t >> 1][t & 1] = Y[row];
         zi[t >> 1][t & 1] = Z[row];
-        hoff[t] = hist_addr + 4u * (uint32_t)r;
+        // (absolute keys: bin 0 of the grid is key zbase)
+        hoff[t] = hist_addr + 4u * (uint32_t)r - 64u * (uint32_t)zbase;
     }
+    const uint32_t zlo = (uint32_t)zbase, zhi = (uint32_t)zbase + (uint32_t)(kNB - 1);
     for (int k = tid; k < kNB * R / 4; k += 256)
         reinterpret_cast<uint4*>(hist)[k] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
@@ -2661,14 +2679,18 @@ __device__ __forceinline__ void consensus_zoom_unit(
                 const float xj = cx[c], yj = cy[c], zj = cz[c];
 #pragma unroll
                 for (int t = 0; t < kPairs; t++) {
-                    // rdist2's operations and order, two rows per packed instruction
+                    // s' (zoom_grid_edges), two rows per packed instruction
                     const f32x2 dx = xi[t] - xj, dy = yi[t] - yj, dz = zi[t] - zj;
-                    const f32x2 s = (dx * dx + dy * dy) + dz * dz;
+                    f32x2 s = dx * dx;
+                    s = __builtin_elementwise_fma(dy, dy, s);
+                    s = __builtin_elementwise_fma(dz, dz, s);
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
-                        const int bz = min(max((int)(__float_as_uint(s[h]) >> kShift) - zbase, 0),
-                                           kNB - 1);  // (one v_med3_i32)
-                        lds_inc(lshl6_add((uint32_t)bz, hoff[2 * t + h]));
+                        // keys outside the grid clamp into its edge bins (one v_med3_u32)
+                        uint32_t key;
+                        asm("v_med3_u32 %0, %1, %2, %3"
+                            : "=v"(key) : "v"(__float_as_uint(s[h]) >> kShift), "s"(zlo), "v"(zhi));
+                        lds_inc(lshl6_add(key, hoff[2 * t + h]));
                     }
                 }
             }

@@ -142,6 +142,68 @@ __global__ __launch_bounds__(256) void probe_mfma(const half8* __restrict__ A, i
     out[blockIdx.x * 256 + tid] = s;
 }
 
+// variant 7: 16 rows per block (the B operand: row = lane & 15), 16 stream columns per
+// v_mfma_f32_16x16x4_f32 (A = column i = lane & 15, component lane >> 4), D = n_i + n_j - 2 u.v
+// with C = n_j (per lane); 4 distances per lane per MFMA -> key, address, ds_add_u32 into the
+// [bin][16 rows] histogram of the VALU kernel (41 KB, 3 blocks per CU)
+typedef float float4v __attribute__((ext_vector_type(4)));
+template <int UNR>
+__global__ __launch_bounds__(256) void probe_mfma16(const float4* __restrict__ col, int K, int base,
+                                                    uint32_t* __restrict__ out, uint64_t* clk) {
+    __shared__ __align__(16) uint32_t hist[(kGuard + kNB) * R];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t ha = (uint32_t)(size_t)(lds_u32*)hist;
+    const int j = lane & 15, k = lane >> 4;
+    const uint32_t hoff = ha + 4u * (uint32_t)j - 64u * (uint32_t)(base - kGuard);
+    for (int q = tid; q < (kGuard + kNB) * R; q += 256) hist[q] = 0;
+    const float4 rj = col[blockIdx.x * 16 + j];
+    const float b = k == 0 ? rj.x : k == 1 ? rj.y : k == 2 ? rj.z : 1.0f;
+    const float nj = rj.x * rj.x + rj.y * rj.y + rj.z * rj.z + 1e-12f;
+    const float4v c = {nj, nj, nj, nj};
+    __syncthreads();
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    const int ntiles = (K + 15) / 16;
+    const float* cf = reinterpret_cast<const float*>(col);
+    float a = cf[(size_t)((w * 16 + j) % K) * 4 + k];
+    if (UNR == 1) {
+        for (int t = w; t < ntiles; t += 4) {
+            const int tn = t + 4 < ntiles ? t + 4 : t;
+            const float an = cf[(size_t)(tn * 16 + j) * 4 + k];
+            const float4v d = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+#pragma unroll
+            for (int q = 0; q < 4; q++) lds_inc(lshl6_add(__float_as_uint(d[q]) >> kBinShift, hoff));
+            a = an;
+        }
+    } else {
+        // UNR tiles per step: their MFMAs issued together, the next step's operands loaded ahead
+        float av[UNR], an[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; u++) av[u] = cf[(size_t)(((w * UNR + u) * 16 + j) % K) * 4 + k];
+        for (int t = w * UNR; t < ntiles; t += 4 * UNR) {
+#pragma unroll
+            for (int u = 0; u < UNR; u++) {
+                const int tn = min(t + 4 * UNR + u, ntiles - 1);
+                an[u] = cf[(size_t)(tn * 16 + j) * 4 + k];
+            }
+            float4v d[UNR];
+#pragma unroll
+            for (int u = 0; u < UNR; u++) d[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], b, c, 0, 0, 0);
+#pragma unroll
+            for (int u = 0; u < UNR; u++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) lds_inc(lshl6_add(__float_as_uint(d[u][q]) >> kBinShift, hoff));
+#pragma unroll
+            for (int u = 0; u < UNR; u++) av[u] = an[u];
+        }
+    }
+    __syncthreads();
+    const uint64_t t1 = __builtin_amdgcn_s_memtime();
+    if (tid == 0 && blockIdx.x == 0) *clk = t1 - t0;
+    uint32_t s = 0;
+    for (int q = tid; q < (kGuard + kNB) * R; q += 256) s += hist[q] * (uint32_t)q;
+    out[blockIdx.x * 256 + tid] = s;
+}
+
 template <int V>
 float run(const float* X, const float* Y, const float* Z, int K, int rows, int base, uint32_t* out,
           uint64_t* clk, uint64_t* hclk) {
@@ -223,6 +285,37 @@ int main() {
         hipMemcpy(&hc, clk, 8, hipMemcpyDeviceToHost);
         printf("variant 4 (mfma, 32 rows/block, %zu B LDS): %.3f ms  %.1f cycles per wave-distance per SIMD  memtime %llu  err %s\n",
                shm, ms, ms * 1e-3 * 2.4e9 * 1024.0 / wd, (unsigned long long)hc, hipGetErrorString(hipGetLastError()));
+    }
+    {
+        // variant 7: columns as float4 (x', y', z', |x'|^2 as -2x' ... timing only): centered,
+        // A = -2 u, n; B = u, 1
+        std::vector<float4> hc(rows);
+        for (int i = 0; i < rows; i++) {
+            const float x = h[i % K] - 0.1f, y = h[K + i % K] - 0.2f, z = h[2 * K + i % K] - 0.3f;
+            hc[i] = make_float4(-2.f * x, -2.f * y, -2.f * z, x * x + y * y + z * z);
+        }
+        float4* dc;
+        hipMalloc(&dc, rows * 16);
+        hipMemcpy(dc, hc.data(), rows * 16, hipMemcpyHostToDevice);
+        const int b16 = (int)(__builtin_bit_cast(uint32_t, 1e-12f) >> kBinShift) - 16;
+        hipEvent_t e0, e1;
+        hipEventCreate(&e0);
+        hipEventCreate(&e1);
+        auto go = [&](auto kern, const char* name) {
+            kern<<<rows / 16, 256>>>(dc, K, b16, out, clk);
+            hipEventRecord(e0);
+            for (int r = 0; r < 5; r++) kern<<<rows / 16, 256>>>(dc, K, b16, out, clk);
+            hipEventRecord(e1);
+            hipEventSynchronize(e1);
+            float ms;
+            hipEventElapsedTime(&ms, e0, e1);
+            ms /= 5;
+            printf("variant 7 (%s): %.3f ms  %.1f cycles per wave-distance per SIMD  err %s\n",
+                   name, ms, ms * 1e-3 * 2.4e9 * 1024.0 / wd, hipGetErrorString(hipGetLastError()));
+        };
+        go(probe_mfma16<1>, "mfma 16x16x4 f32, 16 rows/block");
+        go(probe_mfma16<2>, "same, 2 tiles per step");
+        go(probe_mfma16<4>, "same, 4 tiles per step");
     }
     return 0;
 }
