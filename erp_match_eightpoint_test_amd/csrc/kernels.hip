@@ -2027,7 +2027,8 @@ constexpr int kLipMinK = 1024;  // smaller sets: no pre-pruning (every non-refer
 #ifndef ERP_LIP2_STEP
 #define ERP_LIP2_STEP 4
 #endif
-constexpr int kLip2Step = ERP_LIP2_STEP;  // every 4th L1 row is a second-stage reference
+constexpr int kLip2Step = ERP_LIP2_STEP;  // 1 in 4 L1 rows is a second-stage reference
+static_assert((kLip2Step & (kLip2Step - 1)) == 0, "power of two (is_ref2)");
 
 // The references of a pruning pass, staged ONCE per pair (consensus_lip_refs_kernel) into
 // lref[p][0 .. lcnt[p]) as (x, y, z, squared pruning radius), with U = their smallest UB in
@@ -2175,9 +2176,13 @@ __device__ int lip_prune_rows(LipShared& sh, int na, const float4* __restrict__ 
 }
 
 // append act[0 .. na) (the rows left) to a per-pair list
+// (and, when list2 is given, the rows that are second-stage references, is_ref2, to list2 too)
+__device__ __forceinline__ bool is_ref2(int row) { return (row & (kLip2Step - 1)) == 1; }
 __device__ void lip_append(const LipShared& sh, int na, int32_t* __restrict__ list,
-                           int32_t* __restrict__ count) {
+                           int32_t* __restrict__ count, int32_t* __restrict__ list2 = nullptr,
+                           int32_t* __restrict__ count2 = nullptr) {
     const int tid = threadIdx.x, lane = wave_lane();
+    const uint64_t below = (1ull << lane) - 1ull;
     for (int a = tid; a - tid < na; a += 256) {
         const bool keep = a < na;
         const int i = keep ? __float_as_int(sh.act[a].w) : 0;
@@ -2185,7 +2190,15 @@ __device__ void lip_append(const LipShared& sh, int na, int32_t* __restrict__ li
         int base = 0;
         if (lane == 0 && bal) base = atomicAdd(count, __builtin_popcountll(bal));
         base = __shfl(base, 0, 64);
-        if (keep) list[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = i;
+        if (keep) list[base + __builtin_popcountll(bal & below)] = i;
+        if (list2) {
+            const bool k2 = keep && is_ref2(i);
+            const uint64_t b2 = __builtin_amdgcn_ballot_w64(k2);
+            int base2 = 0;
+            if (lane == 0 && b2) base2 = atomicAdd(count2, __builtin_popcountll(b2));
+            base2 = __shfl(base2, 0, 64);
+            if (k2) list2[base2 + __builtin_popcountll(b2 & below)] = i;
+        }
     }
 }
 
@@ -2214,7 +2227,8 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     const int32_t* __restrict__ scount, int32_t* __restrict__ rlist, int olstride,
     int32_t* __restrict__ rcount, int shard, int nshards, int lstep,
     const float4* __restrict__ lref, const double* __restrict__ lU,
-    const int32_t* __restrict__ lcnt, int cap) {
+    const int32_t* __restrict__ lcnt, int cap, int32_t* __restrict__ r2list,
+    int32_t* __restrict__ r2cnt) {
     __shared__ LipShared sh;
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
@@ -2264,7 +2278,8 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
         };
         na = lip_prune_rows(sh, na, lref + (size_t)p * cap, m, prune);
     }
-    lip_append(sh, na, rlist + (size_t)p * olstride, &rcount[p]);
+    lip_append(sh, na, rlist + (size_t)p * olstride, &rcount[p],
+               r2list ? r2list + (size_t)p * stride : nullptr, r2list ? &r2cnt[p] : nullptr);
 }
 
 // Tighter bounds for the surviving rows (4 per block, lanes rotating over the rows as in the
@@ -2914,13 +2929,15 @@ __global__ __launch_bounds__(256) void consensus_ref2_prep_kernel(
     zoom_grid_edges<MANT>(z, edz + (size_t)p * 2 * kNB);
 }
 
-// the test itself: positions k of L1 (l1[p][0 .. n1c[p])), k % m == 0 the references (bounded
-// by the zoom pass); the rows that survive are appended to l2 / n2c.  A pair without a second
-// stage (zb < 0) passes every L1 row through.
+// the test itself: the rows of L1 (l1[p][0 .. n1c[p])); those with is_ref2(row) are the
+// references (bounded by the zoom pass; a function of the row index, not of the list position,
+// so the reference set does not depend on the order the first stage appended L1 in: every
+// record, binned_rows included, is the same on every run); the rows that survive are appended to
+// l2 / n2c.  A pair without a second stage (zb < 0) passes every L1 row through.
 __global__ __launch_bounds__(256) void consensus_lipschitz2_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride,
     double* __restrict__ lb, double* __restrict__ ub, const int32_t* __restrict__ l1,
-    const int32_t* __restrict__ n1c, const int32_t* __restrict__ zb, int m,
+    const int32_t* __restrict__ n1c, const int32_t* __restrict__ zb,
     const int32_t* __restrict__ bsel, int32_t* __restrict__ l2, int32_t* __restrict__ n2c,
     int32_t* __restrict__ nfb, const float4* __restrict__ lref, const double* __restrict__ lU,
     const int32_t* __restrict__ lcnt, int cap) {
@@ -2947,7 +2964,7 @@ __global__ __launch_bounds__(256) void consensus_lipschitz2_kernel(
         const int k = i0 + 256 * h + tid;
         bool act = k < n;
         const int i = act ? (int)L[k] : 0;
-        if (act && on && k % m == 0) {
+        if (act && on && is_ref2(i)) {
             act = bsel[((size_t)p * stride + i) * 2] < 0 || bsel[((size_t)p * stride + i) * 2 + 1] < 0;
             fb += act;
         }
@@ -2977,13 +2994,14 @@ __global__ __launch_bounds__(256) void consensus_lipschitz2_kernel(
 
 // binned rows beyond the first-stage references (erp_pair_result.binned_rows): the second-stage
 // references plus L2
-__global__ void consensus_ref2_count_kernel(int n_pairs, const int32_t* __restrict__ zb, int m,
+__global__ void consensus_ref2_count_kernel(int n_pairs, const int32_t* __restrict__ zb,
+                                            const int32_t* __restrict__ r2c,
                                             const int32_t* __restrict__ n2c,
                                             const int32_t* __restrict__ nfb,
                                             int32_t* __restrict__ n1c) {
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= n_pairs) return;
-    n1c[p] = (zb[p] >= 0 ? (n1c[p] + m - 1) / m : 0) + n2c[p] - nfb[p];
+    n1c[p] = (zb[p] >= 0 ? r2c[p] : 0) + n2c[p] - nfb[p];
 }
 
 __global__ __launch_bounds__(256) void consensus_refine_kernel(
@@ -3719,14 +3737,18 @@ hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const f
     return hipGetLastError();
 }
 
-// the pruning references' scratch: [P][cap] float4, then lU [P] doubles, then lcnt [P] ints
+// the pruning references' scratch: [P][cap] float4, lU [P] doubles, lcnt [P] ints, then the
+// second-stage reference list [P][stride] ints and its counts [P]
 size_t lipref_bytes(int n_pairs, int stride) {
-    return (size_t)n_pairs * lipref_cap(stride) * sizeof(float4) + (size_t)n_pairs * 12 + 64;
+    return (size_t)n_pairs * lipref_cap(stride) * sizeof(float4) + (size_t)n_pairs * 16 +
+           (size_t)n_pairs * stride * 4 + 64;
 }
 struct LipRefViews {
     float4* ref;
     double* U;
     int32_t* cnt;
+    int32_t* r2cnt;
+    int32_t* r2list;
     int cap;
 };
 static LipRefViews lipref_views(void* base, int n_pairs, int stride) {
@@ -3735,6 +3757,8 @@ static LipRefViews lipref_views(void* base, int n_pairs, int stride) {
     v.ref = reinterpret_cast<float4*>(base);
     v.U = reinterpret_cast<double*>(v.ref + (size_t)n_pairs * v.cap);
     v.cnt = reinterpret_cast<int32_t*>(v.U + n_pairs);
+    v.r2cnt = v.cnt + n_pairs;
+    v.r2list = v.r2cnt + n_pairs;
     return v;
 }
 
@@ -3777,6 +3801,11 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
     const LipRefViews lr = lipref_views(lipref, P, stride);
     const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * P, st);
     if (me != hipSuccess) return me;
+    const bool two = lip2 && list2;  // second pre-pruning stage
+    if (two) {
+        const hipError_t m1 = hipMemsetAsync(lr.r2cnt, 0, sizeof(int32_t) * P, st);
+        if (m1 != hipSuccess) return m1;
+    }
     hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
                        trim_lo, trim_hi, (const double*)lb, (const double*)ub,
                        (const int32_t*)nullptr, (const int32_t*)nullptr, kLipStep, shard, nshards,
@@ -3785,39 +3814,40 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                        st, kcount, rv, stride, lb, ub, (const int32_t*)nullptr,
                        (const int32_t*)nullptr, rlist, stride, rcount, shard, nshards, kLipStep,
                        (const float4*)lr.ref, (const double*)lr.U, (const int32_t*)lr.cnt,
-                       lr.cap);
+                       lr.cap, two ? lr.r2list : nullptr, two ? lr.r2cnt : nullptr);
     int32_t* uoff = rcount + P;  // [n_pairs + 1] after the counts
     const int32_t* blist = rlist;
     const int32_t* bcount = rcount;
-    if (lip2 && list2) {
-        // second stage: every kLip2Step-th L1 row on the fine grid, the other L1 rows tested
-        // against them; the survivors (list2, counts after the unit prefix) get the coarse pass
+    if (two) {
+        // second stage: the L1 rows with is_ref2 (listed apart by the first stage) on the fine
+        // grid, the other L1 rows tested against them; the survivors (list2, counts after the
+        // unit prefix) get the coarse pass
         float* edz = edges + (size_t)P * 2 * kNB;
         int32_t* zb = reinterpret_cast<int32_t*>(edges + (size_t)P * 4 * kNB);
         int32_t* n2 = uoff + P + 1;
         hipLaunchKernelGGL(consensus_ref2_prep_kernel, dim3(P), dim3(256), 0, st, kcount, dscale,
                            (const double*)ub, (const int32_t*)bsel, (const int32_t*)rcount, stride,
                            trim_lo, trim_hi, shard, nshards, zb, edz);
-        hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)rcount,
-                           P, kBoundRows * kLip2Step, kLip2Min - 1, uoff);
-        const int units2 = P * ((stride + kBoundRows * kLip2Step - 1) / (kBoundRows * kLip2Step));
+        hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st,
+                           (const int32_t*)lr.r2cnt, P, kBoundRows, 0, uoff);
+        const int units2 = P * ((stride / kLip2Step + 1 + kBoundRows - 1) / kBoundRows);
         hipLaunchKernelGGL(consensus_zoom_kernel<6>, dim3(units2), dim3(256), 0, st, kcount, rv,
                            (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb, ub,
-                           (const int32_t*)rlist, (const int32_t*)rcount, (const int32_t*)uoff, P,
-                           zsel, kLip2Step, dscale, bsel);
+                           (const int32_t*)lr.r2list, (const int32_t*)lr.r2cnt,
+                           (const int32_t*)uoff, P, zsel, 1, dscale, bsel);
         const hipError_t m2 = hipMemsetAsync(n2, 0, sizeof(int32_t) * 2 * P, st);  // + nfb
         if (m2 != hipSuccess) return m2;
         hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv,
                            stride, trim_lo, trim_hi, (const double*)lb, (const double*)ub,
-                           (const int32_t*)rlist, (const int32_t*)rcount, kLip2Step, shard,
+                           (const int32_t*)lr.r2list, (const int32_t*)lr.r2cnt, 1, shard,
                            nshards, (const int32_t*)zb, lr.ref, lr.U, lr.cnt, lr.cap);
         hipLaunchKernelGGL(consensus_lipschitz2_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
                            st, kcount, rv, stride, lb, ub, (const int32_t*)rlist,
-                           (const int32_t*)rcount, (const int32_t*)zb, kLip2Step,
-                           (const int32_t*)bsel, list2, n2, n2 + P, (const float4*)lr.ref,
-                           (const double*)lr.U, (const int32_t*)lr.cnt, lr.cap);
+                           (const int32_t*)rcount, (const int32_t*)zb, (const int32_t*)bsel, list2,
+                           n2, n2 + P, (const float4*)lr.ref, (const double*)lr.U,
+                           (const int32_t*)lr.cnt, lr.cap);
         hipLaunchKernelGGL(consensus_ref2_count_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P,
-                           (const int32_t*)zb, kLip2Step, (const int32_t*)n2,
+                           (const int32_t*)zb, (const int32_t*)lr.r2cnt, (const int32_t*)n2,
                            (const int32_t*)(n2 + P), rcount);
         blist = list2;
         bcount = n2;
@@ -3868,7 +3898,7 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, P), dim3(256), 0, st,
                        kcount, rv, stride, lb, ub, surv, nsurv, list2, l2stride, n2, 0, 1,
                        kRefStep, (const float4*)lr.ref, (const double*)lr.U,
-                       (const int32_t*)lr.cnt, lr.cap);
+                       (const int32_t*)lr.cnt, lr.cap, (int32_t*)nullptr, (int32_t*)nullptr);
     // (C) the survivors the references did not prune
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)n2, P,
                        kRefineRows, 0, uoff);
