@@ -32,7 +32,7 @@ STAGE_KERNEL = {
     "knn2_filter": "knn2_filter_kernel",
     "knn2_rescore": "knn2_rescore_kernel", "knn2_merge": "knn2_merge_kernel",
     "bearings": "bearings_from_matches_kernel", "jump_prep": "jump_prep_kernel",
-    "windows": "sampler_window_kernel", "sampler": "sampler_kernel", "gram": "gram_mfma_kernel",
+    "windows": "sampler_window_kernel", "sampler": "sampler_kernel<false>", "gram": "gram_mfma_kernel",
     "eigen": "eigen_kernel<false>", "valid_compact": "valid_compact_kernel",
     "consensus_bounds": "consensus_bounds_kernel", "consensus_select": "consensus_select_kernel",
     "consensus_refine": "consensus_refine_kernel", "consensus_rows": "consensus_rows_kernel",
@@ -130,9 +130,9 @@ def main():
             n = len(disp[k])
             lines.append(f"{k:36s} dispatches={n:3d} " +
                          " ".join(f"{c}={x / n:.4g}" for c, x in sorted(v.items())))
-        smp = acc.get("sampler_kernel")
+        smp = acc.get("sampler_kernel<false>")
         if smp and a.draws > 0:
-            n = len(disp["sampler_kernel"])
+            n = len(disp["sampler_kernel<false>"])
             wd = a.draws / 64.0  # wave-level draws per launch
             lines.append(f"# sampler: {a.draws:.4g} draws per launch -> "
                          f"{smp['SQ_INSTS_VALU'] / n / wd:.2f} VALU and "
