@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--sigma", type=float, default=0.03,
                     help="pairs workload: descriptor noise of the true partners")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--main-batch", choices=["default", "worst"], default="default",
+                    help="pairs workload: 'worst' makes the timed batch itself the worst-case "
+                         "batch (for stage profiles of it; not the headline)")
     ap.add_argument("--worst-steps", type=int, default=3,
                     help="pairs workload: timed steps of the worst-case batch (every pair a "
                          "two-cluster consensus pair -- R1 and R2 both valid, K ~ 2 x iters -- "
@@ -92,6 +95,15 @@ def make_batch(rank: int, B: int, kpts: int, seed: int, inlier_frac: float = 0.8
     pairs = [synth.make_pair(seed + 1000 * rank + i, n_kpts=kpts, inlier_frac=inlier_frac,
                              sigma=sigma, mismatch_frac=mismatch_frac) for i in range(B)]
     return pairs
+
+
+def make_worst_batch(rank: int, B: int, kpts: int, sigma: float):
+    """the worst-case batch: two-cluster consensus pairs (scripts/twin_seeds.json: R1 and R2
+    both valid) at inlier fraction 0.98"""
+    from erp_match_eightpoint_test_amd import synth
+    seeds = json.load(open(os.path.join(ROOT, "scripts", "twin_seeds.json")))["seeds"]
+    return [synth.make_pair(seeds[(rank * B + i) % len(seeds)], n_kpts=kpts, inlier_frac=0.98,
+                            sigma=sigma) for i in range(B)]
 
 
 def to_device(pairs, dev):
@@ -587,7 +599,10 @@ def main():
 
     from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
     from erp_match_eightpoint_test_amd import dist as D
-    pairs = make_batch(rank, args.pairs, args.kpts, args.seed, args.inlier_frac, args.sigma)
+    if args.main_batch == "worst":
+        pairs = make_worst_batch(rank, args.pairs, args.kpts, args.sigma)
+    else:
+        pairs = make_batch(rank, args.pairs, args.kpts, args.seed, args.inlier_frac, args.sigma)
     S = max(1, min(args.streams, args.pairs))
     parts = [pairs[i * args.pairs // S:(i + 1) * args.pairs // S] for i in range(S)]
     subs = []
@@ -772,11 +787,7 @@ def main():
     # the minimum) at inlier fraction 0.98 (M ~ 4k: the most sampler / Gram work per pair)
     worst = None
     if args.steps > 0 and args.worst_steps > 0:
-        seeds = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                            "scripts", "twin_seeds.json")))["seeds"]
-        from erp_match_eightpoint_test_amd import synth
-        wpairs = [synth.make_pair(seeds[(rank * args.pairs + i) % len(seeds)], n_kpts=args.kpts,
-                                  inlier_frac=0.98, sigma=args.sigma) for i in range(args.pairs)]
+        wpairs = make_worst_batch(rank, args.pairs, args.kpts, args.sigma)
         wparts = [wpairs[i * args.pairs // S:(i + 1) * args.pairs // S] for i in range(S)]
         wb = [to_device(part, dev) for part in wparts]
         for sb, b in zip(subs, wb):

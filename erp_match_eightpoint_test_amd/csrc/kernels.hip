@@ -2282,6 +2282,42 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
                r2list ? r2list + (size_t)p * stride : nullptr, r2list ? &r2cnt[p] : nullptr);
 }
 
+// f(x_j, y_j, z_j) for the columns j = tid, tid + 256, ... of a block of 256: batches of
+// kRowsCB columns per thread with the next batch loaded before this one is processed
+constexpr int kRowsCB = 8;
+template <class F>
+__device__ __forceinline__ void for_columns(const float* __restrict__ X, const float* __restrict__ Y,
+                                            const float* __restrict__ Z, int K, F f) {
+    const int tid = threadIdx.x;
+    float cx[kRowsCB], cy[kRowsCB], cz[kRowsCB], nx[kRowsCB], ny[kRowsCB], nz[kRowsCB];
+    const int kmax = K - 1;
+#pragma unroll
+    for (int c = 0; c < kRowsCB; c++) {
+        const int j = min(c * 256 + tid, kmax);
+        cx[c] = X[j];
+        cy[c] = Y[j];
+        cz[c] = Z[j];
+    }
+    for (int j0 = 0; j0 < K; j0 += kRowsCB * 256) {
+#pragma unroll
+        for (int c = 0; c < kRowsCB; c++) {
+            const int j = min(j0 + kRowsCB * 256 + c * 256 + tid, kmax);
+            nx[c] = X[j];
+            ny[c] = Y[j];
+            nz[c] = Z[j];
+        }
+#pragma unroll
+        for (int c = 0; c < kRowsCB; c++)
+            if (j0 + c * 256 + tid < K) f(cx[c], cy[c], cz[c]);
+#pragma unroll
+        for (int c = 0; c < kRowsCB; c++) {
+            cx[c] = nx[c];
+            cy[c] = ny[c];
+            cz[c] = nz[c];
+        }
+    }
+}
+
 // Tighter bounds for the surviving rows (4 per block, lanes rotating over the rows as in the
 // bounds kernel).  For each row: the exact s of every column (the reference's expression),
 // an fp64 sum of sqrt(s) (raw v_sqrt_f32, bracketed by its 2^-22 error bound) over the bins
@@ -2346,8 +2382,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
         below[tid][1] = 0;
     }
     __syncthreads();
-    for (int j = tid; j < K; j += 256) {
-        const float xj = X[j], yj = Y[j], zj = Z[j];
+    for_columns(X, Y, Z, K, [&](float xj, float yj, float zj) {
 #pragma unroll
         for (int t = 0; t < kRefineRows; t++) {
             const float s = rdist2(xi[t], yi[t], zi[t], xj, yj, zj);
@@ -2363,7 +2398,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
                 atomicAdd(&sub[r][e == ba[t] ? 0 : 1][(key >> kLowBits) & (kNS - 1u)], 1u);
             }
         }
-    }
+    });
 #pragma unroll
     for (int t = 0; t < kRefineRows; t++) {
         const int r = (lane + t) & (kRefineRows - 1);
@@ -3023,14 +3058,20 @@ __global__ __launch_bounds__(256) void consensus_refine_kernel(
 
 // Trimmed mean of a surviving row i, ranks [lo, hi), lo = (long)(K*0.2), hi = (long)(K*0.8).
 // The bounds kernel already located the (s'-)bins b_a, b_b holding ranks lo and hi-1; here
-//   pass 1: exact s = dx*dx + dy*dy + dz*dz for every column; fp64 sum of sqrtf(s) over the
-//           bins strictly between b_a and b_b, exact counts below them, and for the two bins
-//           1024-way sub-histograms (key bits 18..9) with their fp64 sums of sqrtf(s);
-//   pass 2: 512-way histograms of the two sub-bins holding the ranks (key bits 8..0, i.e.
-//           exact values) -> the exact keys va, vb at ranks lo and hi-1 and their
+//   pass 1: exact s = dx*dx + dy*dy + dz*dz for every column; exact counts below b_a and b_b
+//           and 1024-way sub-histograms (key bits 18..9) of the two bins -> the sub-bins holding
+//           the ranks;
+//   pass 2: the fp64 sum of sqrtf(s) over every key strictly between those two sub-bins (a
+//           register sum per thread), and 512-way histograms of the two sub-bins (key bits
+//           8..0, i.e. exact values) -> the exact keys va, vb at ranks lo and hi-1 and their
 //           multiplicities.
-// Sum = sum over keys strictly between va and vb (assembled from the levels) + the boundary
+// Sum = the pass-2 sum + the exact values inside the rank sub-bins + the boundary
 // multiplicities.  (The sort order of the distances is the order of s: sqrtf is monotone.)
+// No fp64 LDS atomics (the sub-bins' sums used to be LDS fp64 atomics in pass 1), and the
+// columns stream with kRowsCB loads in flight per thread (for_columns): one row per block reads
+// all K columns twice, and with 4 loads in flight it waited on L2 for most of its time (on the
+// worst-case batch, 1 700 survivors per two-cluster pair: 116 -> 75 ms per step; a
+// wave-combined form of the sub-bin counts measured slower: its ballots run on every column).
 // When a bin edge moved an element between the s' and s binnings across a rank, or a rank
 // sits in the under/overflow bin, the row takes the 4-pass radix path instead.  The sum is
 // not the reference's sorted sequential one in the last bits; consensus_final re-scores near
@@ -3043,7 +3084,6 @@ __device__ void consensus_rows_block(const int32_t* __restrict__ kcount,
                                      const int32_t* __restrict__ bsel,
                                      double* __restrict__ tmean, int p, int vb) {
     __shared__ uint32_t histA[2048], histB[2048];  // radix fallback; level counts alias it
-    __shared__ double sA[kNS], sB[kNS];
     __shared__ int ws[8];
     __shared__ int res[2];
     __shared__ double red[8];
@@ -3074,42 +3114,28 @@ __device__ void consensus_rows_block(const int32_t* __restrict__ kcount,
         for (int k = tid; k < kNS; k += 256) {
             cA[k] = 0;
             cB[k] = 0;
-            sA[k] = 0.0;
-            sB[k] = 0.0;
         }
         for (int k = tid; k < NL; k += 256) {
             tA[k] = 0;
             tB[k] = 0;
         }
         __syncthreads();
-        double acc = 0.0;
         long belowA = 0, belowB = 0;
-#pragma unroll 4
-        for (int j = tid; j < K; j += 256) {
-            const float s = rdist2(xi, yi, zi, X[j], Y[j], Z[j]);
+        // columns in batches of kRowsCB per thread, the next batch's loads in flight while this
+        // one is binned (one row per block streams all K columns twice: with 4 loads in flight
+        // the kernel waited on L2 for most of its time)
+        for_columns(X, Y, Z, K, [&](float xj, float yj, float zj) {
+            const float s = rdist2(xi, yi, zi, xj, yj, zj);
             const uint32_t key = __float_as_uint(s);
             const int e = min(max((int)(key >> kBinShift) - base, 0), kNB - 1);
             belowA += e < ba;
             belowB += e < bb;
-            if (e > ba && e < bb) {
-                acc += (double)__builtin_sqrtf(s);
-            } else if (e == ba || e == bb) {
-                const int sub = (int)((key >> kLowBits) & (kNS - 1u));
-                const double d = (double)__builtin_sqrtf(s);
-                if (e == ba) {
-                    atomicAdd(&cA[sub], 1u);
-                    atomicAdd(&sA[sub], d);
-                } else {
-                    atomicAdd(&cB[sub], 1u);
-                    atomicAdd(&sB[sub], d);
-                }
-            }
-        }
-        const double inner = block_sum_f64(acc, red);
+            if (e == ba || e == bb)
+                atomicAdd(&histA[(e == ba ? 0 : kNS) + (int)((key >> kLowBits) & (kNS - 1u))], 1u);
+        });
         const long cumA = block_sum_i64(belowA, red);
         const long cumB = block_sum_i64(belowB, red);
         const uint32_t* cX = (ba == bb) ? cA : cB;
-        const double* sX = (ba == bb) ? sA : sB;
         long befA, befB;
         const int sa = find_bin<kNS>(cA, lo - cumA, &befA, ws, res);
         const int sb = find_bin<kNS>(cX, hi - 1 - cumB, &befB, ws, res);
@@ -3117,30 +3143,26 @@ __device__ void consensus_rows_block(const int32_t* __restrict__ kcount,
         if (fast) {
             const uint32_t prefA = ((uint32_t)(base + ba) << kSubBits) | (uint32_t)sa;  // key >> kLowBits
             const uint32_t prefB = ((uint32_t)(base + bb) << kSubBits) | (uint32_t)sb;
-#pragma unroll 4
-            for (int j = tid; j < K; j += 256) {
-                const uint32_t key = __float_as_uint(rdist2(xi, yi, zi, X[j], Y[j], Z[j]));
-                if ((key >> kLowBits) == prefA) atomicAdd(&tA[key & (NL - 1u)], 1u);
-                if ((key >> kLowBits) == prefB) atomicAdd(&tB[key & (NL - 1u)], 1u);
-            }
+            double between = 0.0;  // keys in sub-bins strictly between prefA and prefB
+            for_columns(X, Y, Z, K, [&](float xj, float yj, float zj) {
+                const float s = rdist2(xi, yi, zi, xj, yj, zj);
+                const uint32_t key = __float_as_uint(s);
+                const uint32_t kp = key >> kLowBits;
+                if (kp > prefA && kp < prefB) between += (double)__builtin_sqrtf(s);
+                if (kp == prefA) atomicAdd(&tA[key & (NL - 1u)], 1u);
+                else if (kp == prefB) atomicAdd(&tB[key & (NL - 1u)], 1u);
+            });
             __syncthreads();
+            // (prefA == prefB: both ranks in one sub-bin, counted in tA)
+            const uint32_t* tX = prefA == prefB ? tA : tB;
             long befA3, befB3;
             const int ta = find_bin<NL>(tA, lo - cumA - befA, &befA3, ws, res);
-            const int tb = find_bin<NL>(tB, hi - 1 - cumB - befB, &befB3, ws, res);
+            const int tb = find_bin<NL>(tX, hi - 1 - cumB - befB, &befB3, ws, res);
             const uint32_t va = (prefA << kLowBits) | (uint32_t)ta;
             const uint32_t vb = (prefB << kLowBits) | (uint32_t)tb;
             const long le_a = cumA + befA + befA3 + tA[ta];  // #keys <= va
             const long lt_b = cumB + befB + befB3;           // #keys <  vb
-            // keys strictly between va and vb
-            double part = 0.0;
-            for (int k = tid; k < kNS; k += 256) {  // whole sub-bins
-                if (ba != bb) {
-                    if (k > sa) part += sA[k];
-                    if (k < sb) part += sX[k];
-                } else if (sa != sb) {
-                    if (k > sa && k < sb) part += sA[k];
-                }
-            }
+            double part = between;
             for (int k = tid; k < NL; k += 256) {  // exact values inside the rank sub-bins
                 const double dA = (double)__builtin_sqrtf(__uint_as_float((prefA << kLowBits) | k));
                 const double dB = (double)__builtin_sqrtf(__uint_as_float((prefB << kLowBits) | k));
@@ -3155,8 +3177,7 @@ __device__ void consensus_rows_block(const int32_t* __restrict__ kcount,
             if (va == vb)
                 sum = (double)(hi - lo) * (double)__builtin_sqrtf(__uint_as_float(va));
             else
-                sum = inner + mid +
-                      (double)(le_a - lo) * (double)__builtin_sqrtf(__uint_as_float(va)) +
+                sum = mid + (double)(le_a - lo) * (double)__builtin_sqrtf(__uint_as_float(va)) +
                       (double)(hi - lt_b) * (double)__builtin_sqrtf(__uint_as_float(vb));
         }
         __syncthreads();
