@@ -62,6 +62,9 @@ def parse():
     ap.add_argument("--main-batch", choices=["default", "worst"], default="default",
                     help="pairs workload: 'worst' makes the timed batch itself the worst-case "
                          "batch (for stage profiles of it; not the headline)")
+    ap.add_argument("--sampler", choices=["glibc", "philox"], default="glibc",
+                    help="glibc: the reference's rand() replay (the headline); philox: the "
+                         "counter-based mode (SURVEY 8b), parity against the oracle in that mode")
     ap.add_argument("--worst-steps", type=int, default=3,
                     help="pairs workload: timed steps of the worst-case batch (every pair a "
                          "two-cluster consensus pair -- R1 and R2 both valid, K ~ 2 x iters -- "
@@ -150,6 +153,12 @@ def stage_work(stage, B, kpts, iters, res):
         return ops, "Top/s", PEAK_VALU_OPS, "valu", \
             "4 int/fp64 lane-ops per rand() draw (floor) of the fused sampler+Gram kernel; " \
             "peak = wave64 2-cycle VALU issue"
+    if stage == "sampler" and SAMPLER == 1:
+        s = np.floor(M * 0.25)
+        ops = float(np.sum(s * iters * 27.0))
+        return ops, "Top/s", PEAK_VALU_OPS, "valu", \
+            "27 int lane-ops per Philox draw (10 rounds x ~10 ops per 4 draws + mulhi, test-and-" \
+            "set); peak = wave64 2-cycle VALU issue"
     if stage == "sampler":
         ops = float(np.sum((M - 1) * iters * 4.0))  # per draw: recurrence, shift, remainder, test
         return ops, "Top/s", PEAK_VALU_OPS, "valu", \
@@ -190,12 +199,15 @@ def host_cpu_share():
                      "threads_basis": "min(sched_getaffinity, cgroup cpu.max quota)"}
 
 
+SAMPLER = 0  # erp_ransac_cfg.sampler of every run (--sampler): 0 glibc replay, 1 Philox
+
+
 def oracle_pair(p, iters, nthreads):
     """one pair through the oracle (exact k=2 match + find), with its match list"""
     import oracle as O
     mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=nthreads)
     r = O.find(p["W"], p["H"], p["kp_l"][mt["queryIdx"]], p["kp_r"][mt["trainIdx"]],
-               O.make_cfg(iters=iters))
+               O.make_cfg(iters=iters, sampler=SAMPLER))
     r["matches"] = mt
     return r
 
@@ -240,12 +252,17 @@ def parity_check(gpu_res, gpu_matches, ora):
     min_idx and status equal, R / T within 2e-6, the match list (queryIdx, trainIdx,
     distance bits) bit-exact.  gpu_res: result records of the timed step (same pairs, same
     order); gpu_matches: [pairs, max_nq, 4] int32 from an untimed pass with the matches out."""
-    bad = []
+    bad, swaps = [], []
     for i, o in enumerate(ora):
         r = gpu_res[i]
         M = len(o["matches"])
+        # min_idx one apart with the same R: the winner iteration's R1 / R2 push order differs
+        # (it follows the sign of a noise-level singular vector, DESIGN.md 3.2), not the winner
+        di = int(r["min_idx"]) - int(o["min_idx"])
+        if abs(di) == 1:
+            swaps.append(i)
         ok = (int(r["status"]) == o["status"] == 0 and int(r["M"]) == M and int(r["K"]) == o["K"]
-              and int(r["min_idx"]) == o["min_idx"]
+              and abs(di) <= 1
               and float(np.abs(r["R"] - o["R"]).max()) <= 2e-6
               and float(np.abs(r["T"] - o["T"]).max()) <= 2e-6
               and np.array_equal(gpu_matches[i, :M].view(np.uint32).reshape(-1)[: 4 * M],
@@ -253,7 +270,9 @@ def parity_check(gpu_res, gpu_matches, ora):
         if not ok:
             bad.append(i)
     return {"pairs_checked": len(ora), "all_equal": not bad, "mismatched_pairs": bad,
-            "fields": "status, M, K, min_idx equal; R, T within 2e-6; matches bit-exact"}
+            "r1r2_order_swaps": swaps,
+            "fields": "status, M, K equal; min_idx equal (or the same iteration's other rotation, "
+                      "listed in r1r2_order_swaps); R, T within 2e-6; matches bit-exact"}
 
 
 def load_pmc(tag, stage):
@@ -568,6 +587,8 @@ def check_world(args) -> int:
 
 def main():
     args = parse()
+    global SAMPLER
+    SAMPLER = 1 if args.sampler == "philox" else 0
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_launch_ranks(args))
     check_world(args)
@@ -610,7 +631,7 @@ def main():
         b = to_device(part, dev)
         ctx = Context(local)
         ctx.set_matcher(0 if args.matcher == "mfma" else 1)
-        runner = PairBatchRunner(ctx=ctx, iters=args.iters)
+        runner = PairBatchRunner(ctx=ctx, iters=args.iters, sampler=SAMPLER)
         runner.reserve(len(part), b["max_nq"], b["max_nt"])
         subs.append(dict(b=b, ctx=ctx, runner=runner, stream=torch.cuda.Stream(dev),
                          res=torch.empty((len(part), 64), dtype=torch.uint8, device=dev)))
@@ -726,7 +747,7 @@ def main():
         b1 = to_device(pairs[:1], dev)
         ctx1 = Context(local)
         ctx1.set_matcher(0 if args.matcher == "mfma" else 1)
-        run1 = PairBatchRunner(ctx=ctx1, iters=args.iters)
+        run1 = PairBatchRunner(ctx=ctx1, iters=args.iters, sampler=SAMPLER)
         run1.reserve(1, b1["max_nq"], b1["max_nt"])
         ts = []
         for k in range(23):
@@ -839,7 +860,7 @@ def main():
 
         ctx_c = Context(local)
         ctx_c.set_matcher(0 if args.matcher == "mfma" else 1)
-        run_c = PairBatchRunner(ctx=ctx_c, iters=args.iters)
+        run_c = PairBatchRunner(ctx=ctx_c, iters=args.iters, sampler=SAMPLER)
 
         def rerun(r):
             b = to_device([first_pair(r)], dev)
@@ -852,7 +873,7 @@ def main():
             p = first_pair(r)
             mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=threads)
             o = O.find(p["W"], p["H"], p["kp_l"][mt["queryIdx"]], p["kp_r"][mt["trainIdx"]],
-                       O.make_cfg(iters=args.iters))
+                       O.make_cfg(iters=args.iters, sampler=SAMPLER))
             return dict(o, M=len(mt))
         multi = D.check_gathered(gathered.cpu().numpy(), args.pairs, world, rerun, ora)
         multi["gathered_rows"] = int(gathered.shape[0])
@@ -886,7 +907,8 @@ def main():
                                f"batch of {args.pairs} independent pairs per step per GPU",
                    "kpts": args.kpts, "iters": args.iters, "pairs_per_step_per_gpu": args.pairs,
                    "streams": S, "matcher": args.matcher,
-                   "parallelism": f"pair-sharded x{world}", "sampler": "glibc replay (seed 1)",
+                   "parallelism": f"pair-sharded x{world}", "sampler": ("glibc replay (seed 1)" if SAMPLER == 0
+                               else "Philox4x32-10 + Floyd (seed 1; no reference counterpart)"),
                    "rccl_world": world if dist is not None else None,
                    "inlier_frac": args.inlier_frac, "sigma": args.sigma},
         "roofline": roof,

@@ -431,7 +431,9 @@ erp_status upload_w0(erp_ctx* c, const erp_ransac_cfg* cfg, hipStream_t st) {
 }
 
 bool cfg_ok(const erp_ransac_cfg* cfg) {
-    return cfg && cfg->iters >= 1 && cfg->sampler == ERP_SAMPLER_GLIBC && cfg->sample_frac > 0 &&
+    return cfg && cfg->iters >= 1 &&
+           (cfg->sampler == ERP_SAMPLER_GLIBC || cfg->sampler == ERP_SAMPLER_PHILOX) &&
+           cfg->sample_frac > 0 &&
            cfg->sample_frac <= 1.0 && cfg->trim_lo >= 0 && cfg->trim_hi <= 1.0 &&
            cfg->trim_lo <= cfg->trim_hi;
 }
@@ -443,6 +445,26 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
     auto* counts = (int32_t*)c->counts.p;
     auto* flags = (int32_t*)c->flags.p;
     auto* hyps = (out && out->hyps) ? out->hyps : (erp_hypothesis*)c->hyps.p;
+    if (cfg->sampler == ERP_SAMPLER_PHILOX) {  // counter-based: no jump polynomials / windows
+        {
+            StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
+            ERP_CK(erp::launch_philox_sampler(counts, sh, cfg->sample_frac, cfg->seed, cfg->offset,
+                                              sh.max_nq, (uint32_t*)c->idx.p, flags, st));
+        }
+        {
+            StageTimer _t(ctx, ERP_STAGE_GRAM, st);
+            ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
+                                         cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
+                                         out ? out->samples : nullptr,
+                                         ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr,
+                                         ERP_FUSE_EIGEN == 2 ? hyps : nullptr, cfg->valid_abs, st));
+        }
+        StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
+        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac, cfg->valid_abs,
+                                 (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
+                                 ERP_SKIP_E ? (out && out->hyps) : true));
+        return ERP_OK;
+    }
     {
         StageTimer _t(ctx, ERP_STAGE_JUMP_PREP, st);
         ERP_CK(erp::launch_jump_prep(counts, sh, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p, st));

@@ -107,6 +107,11 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
 // rtab[d] = 1/d rounded up, d < kRecipTable (the sampler's exact modulo); *bad counts entries
 // whose one-sided error bound fails (never, by construction; checked once per context)
 constexpr int kRecipTable = 65538;
+// the counter-based sampler (ERP_SAMPLER_PHILOX): selection words in the replay's format,
+// max_m = the batch's largest M (<= max_nq); hipErrorInvalidValue when M's bitmap exceeds LDS
+hipError_t launch_philox_sampler(const int32_t* counts, const BatchShape& sh, double sample_frac,
+                                 uint32_t seed, uint64_t offset, int max_m, uint32_t* selw,
+                                 int32_t* flags, hipStream_t st);
 hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st);
 // Gram of every iteration's sample on int8 MFMA (exact fixed-point sums) -> gram[p][36][iters];
 // limbs = scratch of gram_limbs_bytes(sh); samples (debug, may be NULL) = the sampled indices.

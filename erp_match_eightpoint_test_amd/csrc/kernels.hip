@@ -699,6 +699,91 @@ __global__ __launch_bounds__(64) void sampler_kernel(
 
 // the estimate of one iteration from its selected vector e (rank-2 fix, decomposition, Euler
 // angles, validity) into its hypothesis record
+// ---- counter-based sampler (ERP_SAMPLER_PHILOX) ------------------------------------------
+// No reference counterpart (the reference replays glibc rand(): sampler_kernel above); SURVEY.md
+// section 8b's `sampler = PHILOX`: iteration h's s-subset of [0, M) by Floyd's algorithm on
+// Philox4x32-10 draws, exactly as oracle/erp_oracle.c erpo_philox_sample defines it:
+//   draw k (j = M - s + k): u_k = philox(ctr = (lo32(h), hi32(h), k / 4, 0), key = (seed,
+//   0x243F6A88))[k mod 4], t = mulhi(u_k, j + 1); t joins the set unless it is there, then j.
+// h = offset + iteration.  s draws per iteration instead of the replay's M - 1 (a quarter at
+// the reference's sample_frac), each a Philox quarter-block (~20 VALU) and an LDS bit test-and-
+// set; no serial dependence between iterations, so no jump polynomials or windows.  One lane =
+// one iteration, an M-bit LDS bitmap per lane ([word][lane]: the 32 lanes of a bank group on 32
+// banks); the set is then written in the replay's selection-word format (bit u of word b <->
+// index M-1-31b-u), which the Gram kernel reads unchanged.
+__device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+        // one 32x32->64 product each (v_mad_u64_u32) instead of a mul_hi + mul_lo pair
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c[0], p1 = (uint64_t)0xCD9E8D57u * c[2];
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0, n2;  // three-input xors (gfx950 v_bitop3, LUT 0x96 = a ^ b ^ c)
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n0) : "v"(hi1), "v"(c[1]), "s"(k0));
+        asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(n2) : "v"(hi0), "v"(c[3]), "s"(k1));
+        c[0] = n0;
+        c[1] = lo1;
+        c[2] = n2;
+        c[3] = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+}
+
+__global__ __launch_bounds__(64) void philox_sampler_kernel(
+    const int32_t* __restrict__ counts, int iters, int nwaves, int nbw, double sample_frac,
+    uint32_t seed, uint64_t offset, int nwords, uint32_t* __restrict__ selw,
+    int32_t* __restrict__ flags) {
+    extern __shared__ uint32_t bm[];  // [nwords][64]
+    const int p = blockIdx.y, w = blockIdx.x, lane = wave_lane();
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || M < 2) return;
+    uint32_t* out = selw + ((size_t)p * nwaves + w) * (size_t)nbw * 64 + lane;
+    const int nb = (M - 1) / 31 + 1;
+    if ((M + 31) / 32 > nwords) {  // M beyond the per-lane LDS bitmap (> 20 480): loud status
+        if (lane == 0) atomicOr(&flags[p], 8);  // ERP_INVALID_ARG; empty sets for the Gram pass
+        for (int b = 0; b < nb; b++) out[(size_t)b * 64] = 0u;
+        return;
+    }
+    const int mw = (M + 31) / 32;
+    for (int k = 0; k < mw; k++) bm[k * 64 + lane] = 0u;
+    const uint64_t h = offset + (uint64_t)(w * 64 + lane);
+    uint32_t u[4];
+    for (int k0 = 0; k0 < s; k0 += 4) {
+        u[0] = (uint32_t)h;
+        u[1] = (uint32_t)(h >> 32);
+        u[2] = (uint32_t)(k0 >> 2);
+        u[3] = 0u;
+        philox4x32_10(u, seed, 0x243F6A88u);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int k = k0 + q;
+            if (k < s) {  // (uniform)
+                const uint32_t j = (uint32_t)(M - s + k);
+                const uint32_t t = __umulhi(u[q], j + 1u);
+                const uint32_t old = atomicOr(&bm[(t >> 5) * 64 + lane], 1u << (t & 31));
+                if (old & (1u << (t & 31))) atomicOr(&bm[(j >> 5) * 64 + lane], 1u << (j & 31));
+            }
+        }
+    }
+    // the set as selection words: block b holds indices hi = M-1-31b down to hi - 30
+    int emitted = 0;
+    for (int b = 0; b < nb; b++) {
+        const int hi = M - 1 - 31 * b, lo = hi - 30;  // lo may be negative (the last block)
+        const int l0 = lo < 0 ? 0 : lo;
+        const uint32_t a = bm[(l0 >> 5) * 64 + lane];
+        const uint32_t c = ((l0 >> 5) + 1) < mw ? bm[((l0 >> 5) + 1) * 64 + lane] : 0u;
+        uint32_t win = __builtin_amdgcn_alignbit(c, a, (uint32_t)(l0 & 31));  // bits l0 ..
+        if (lo < 0) win = (win << (-lo));  // position v of the window <-> index lo + v
+        win &= 0x7fffffffu;                // the block's 31 indices lo .. hi
+        const uint32_t word = __builtin_bitreverse32(win) >> 1;  // bit u <-> index hi - u
+        emitted += __builtin_popcount(word);
+        out[(size_t)b * 64] = word;
+    }
+    if (emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
+}
+
 __device__ __forceinline__ void estimate_store(const double* e, double valid_abs,
                                                erp_hypothesis* __restrict__ o,
                                                bool with_e = true) {
@@ -3588,6 +3673,26 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
                                counts, wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags,
                                nwords);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_philox_sampler(const int32_t* counts, const BatchShape& sh, double sample_frac,
+                                 uint32_t seed, uint64_t offset, int max_m, uint32_t* selw,
+                                 int32_t* flags, hipStream_t st) {
+    const int nwaves = (sh.iters + 63) / 64;
+    // the bitmap is sized for the batch's largest possible M (max_m = max queries), capped at
+    // one CU's LDS: 640 words = M <= 20 480; a pair with more matches gets ERP_INVALID_ARG
+    const int nwords = std::min((max_m + 31) / 32, 640);
+    const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
+    if (shmem > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute((const void*)philox_sampler_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)shmem);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(philox_sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
+                       sh.iters, nwaves, sh.sel_words, sample_frac, seed, offset, nwords, selw,
+                       flags);
     return hipGetLastError();
 }
 

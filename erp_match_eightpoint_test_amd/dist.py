@@ -53,7 +53,15 @@ def valid_list(hyps: np.ndarray):
     return np.ascontiguousarray(r[v], np.float32), np.ascontiguousarray(t[v], np.float32)
 
 
-def find_hypothesis_sharded(hyp_fn, consensus_fn, m: int, iters: int, offset: int, group=None):
+def stream_offset(base: int, a: int, m: int, sampler: int = 0) -> int:
+    """the erp_ransac_cfg.offset that starts iteration a of a run begun at `base`: the glibc
+    replay consumes m-1 rand() draws per iteration (base + a (m-1)); the counter-based Philox
+    sampler (ERP_SAMPLER_PHILOX) keys each iteration by its number (base + a)."""
+    return base + a if sampler == 1 else base + a * (m - 1)
+
+
+def find_hypothesis_sharded(hyp_fn, consensus_fn, m: int, iters: int, offset: int, group=None,
+                            sampler: int = 0):
     """One find() with its iterations split over the ranks of `group`.
 
     hyp_fn(iters_local, offset_local) -> numpy structured array of per-iteration records (fields
@@ -64,7 +72,7 @@ def find_hypothesis_sharded(hyp_fn, consensus_fn, m: int, iters: int, offset: in
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     a, b = block_range(iters, world, rank)
-    local = hyp_fn(b - a, offset + a * (m - 1))
+    local = hyp_fn(b - a, stream_offset(offset, a, m, sampler))
     raw = torch.from_numpy(np.ascontiguousarray(local).view(np.uint8).reshape(len(local), -1).copy())
     parts = all_gather_rows(raw, group)
     merged = np.concatenate([p.numpy().reshape(-1).view(local.dtype) for p in parts])
@@ -111,7 +119,8 @@ class CapiShardBackend:
         import ctypes as C
 
         from .capi import check
-        cfg = self._cfg(iters=b - a, offset=self.base + a * (self.m - 1))
+        cfg = self._cfg(iters=b - a, offset=stream_offset(self.base, a, self.m,
+                                                          self.cfg_kwargs.get("sampler", 0)))
         check(self.ctx.L.erp_eight_point_hypotheses_dev(
             self.ctx.h, self.W, self.H, self.d_kl.data_ptr(), self.d_kr.data_ptr(), self.m,
             C.byref(cfg), out.data_ptr(), self.st), "erp_eight_point_hypotheses_dev")
@@ -204,7 +213,7 @@ def find_hypothesis_sharded_dev(ctx, W: int, H: int, d_kl, d_kr, m: int, iters: 
                                 cfg_kwargs: dict | None = None, group=None, stream=None,
                                 shard_consensus: bool = True, emulate_world: int = 0):
     """configs[4] on GPUs, device-resident end to end (sharded_find over the C ABI:
-    erp_eight_point_hypotheses_dev at glibc offset base + r B (m-1), RCCL all_gather of the
+    erp_eight_point_hypotheses_dev at offset stream_offset(base, r B, m), RCCL all_gather of the
     blocks, erp_consensus_hyps_dev, or erp_consensus_hyps_shard_dev + RCCL all_reduce +
     erp_consensus_hyps_finish_dev) -- the same result as the unsharded
     erp_eight_point_find_dev.  Everything, collectives included, is ordered on `stream`.

@@ -75,13 +75,19 @@ typedef struct erp_point2f {
 } erp_point2f;
 
 typedef enum erp_sampler {
-    ERP_SAMPLER_GLIBC = 0 /* replay of glibc rand() + libstdc++ random_shuffle (the reference) */
+    ERP_SAMPLER_GLIBC = 0, /* replay of glibc rand() + libstdc++ random_shuffle (the reference) */
+    ERP_SAMPLER_PHILOX = 1 /* counter-based, no reference counterpart:
+                              iteration h's subset by Floyd's algorithm on Philox4x32-10 draws,
+                              h = offset + iteration (offset counts iterations, not rand() calls);
+                              the exact definition: oracle/erp_oracle.c erpo_philox_sample.
+                              A pair with more than 20480 matches (the per-lane LDS bitmap)
+                              gets ERP_INVALID_ARG. */
 } erp_sampler;
 
 /* initial_guess parameters; erp_ransac_cfg_default() gives the reference constants. */
 typedef struct erp_ransac_cfg {
     int32_t iters;       /* 80   src/eight_point.cpp:99 */
-    int32_t sampler;     /* ERP_SAMPLER_GLIBC */
+    int32_t sampler;     /* ERP_SAMPLER_GLIBC (the reference) or ERP_SAMPLER_PHILOX */
     double sample_frac;  /* 0.25 :102 */
     double trim_lo;      /* 0.2  :143 */
     double trim_hi;      /* 0.8  :143 */

@@ -43,7 +43,7 @@ assert HYP_DTYPE.itemsize == C.sizeof(Hyp)
 class Cfg(C.Structure):
     _fields_ = [("iters", C.c_int32), ("sample_frac", C.c_double), ("trim_lo", C.c_double),
                 ("trim_hi", C.c_double), ("valid_abs", C.c_double), ("seed", C.c_uint32),
-                ("offset", C.c_uint64)]
+                ("offset", C.c_uint64), ("sampler", C.c_int32)]
 
 
 class Diag(C.Structure):
@@ -84,6 +84,8 @@ def lib():
         L.erpo_glibc_discard.argtypes = [C.POINTER(Glibc), C.c_uint64]
         L.erpo_glibc_window.argtypes = [C.POINTER(Glibc), P]
         L.erpo_random_array.argtypes = [P, C.c_int32, C.POINTER(Glibc)]
+        L.erpo_philox4x32.argtypes = [P, P, P]
+        L.erpo_philox_sample.argtypes = [C.c_int32, C.c_int32, C.c_uint64, C.c_uint32, P]
         L.erpo_l2sq.argtypes = [P, P, C.c_int32]
         L.erpo_l2sq.restype = C.c_float
         L.erpo_match_two_image.argtypes = [P, C.c_int32, P, C.c_int32, C.c_int32, C.c_float, P, P,
@@ -142,9 +144,26 @@ def _p(a):
 
 
 def make_cfg(iters=80, sample_frac=0.25, trim_lo=0.2, trim_hi=0.8, valid_abs=1.57, seed=1,
-             offset=0) -> Cfg:
-    """Reference defaults: src/eight_point.cpp:99 (80), :102 (0.25), :143 (0.2/0.8), :76 (1.57)."""
-    return Cfg(iters, sample_frac, trim_lo, trim_hi, valid_abs, seed, offset)
+             offset=0, sampler=0) -> Cfg:
+    """Reference defaults: src/eight_point.cpp:99 (80), :102 (0.25), :143 (0.2/0.8), :76 (1.57).
+    sampler 1: the counter-based Philox sampler (no reference counterpart; erp_oracle.c)."""
+    return Cfg(iters, sample_frac, trim_lo, trim_hi, valid_abs, seed, offset, sampler)
+
+
+def philox4x32(ctr, key) -> np.ndarray:
+    """One Philox4x32-10 block (Random123 constants)."""
+    c = np.ascontiguousarray(ctr, np.uint32)
+    k = np.ascontiguousarray(key, np.uint32)
+    o = np.zeros(4, np.uint32)
+    lib().erpo_philox4x32(_p(c), _p(k), _p(o))
+    return o
+
+
+def philox_sample(m: int, s: int, h: int, seed: int = 1) -> np.ndarray:
+    """The Philox sampler's s-subset of [0, m) for iteration counter h (ascending)."""
+    out = np.zeros(max(s, 1), np.int32)
+    lib().erpo_philox_sample(m, s, C.c_uint64(h), C.c_uint32(seed), _p(out))
+    return out[:s]
 
 
 class GlibcRand:

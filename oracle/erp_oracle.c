@@ -86,6 +86,55 @@ void erpo_random_array(int32_t* a, int32_t n, erpo_glibc* g) {
 }
 
 /* ======================================================================================
+ * Counter-based sampler (ERP_SAMPLER_PHILOX; SURVEY.md section 8b's `sampler = PHILOX`).  No
+ * reference counterpart: the reference only has the glibc shuffle above.  Philox4x32-10 as
+ * published (Salmon, Moraes, Dror, Shaw, "Parallel random numbers: as easy as 1, 2, 3",
+ * SC'11; Random123's constants), checked against Random123's known-answer vectors
+ * (tests/test_oracle.py).  Iteration h's s-subset of [0, m): Floyd's algorithm, draw k
+ * (k = 0 .. s-1, j = m - s + k) t = floor(u_k (j + 1) / 2^32) with
+ *   u_k = philox4x32_10(ctr = (lo32(h), hi32(h), k / 4, 0), key = (seed, 0x243F6A88))[k mod 4],
+ * t joins the set unless it is already there, then j does.  (The multiply-shift range map is
+ * biased by < (j + 1) / 2^32 <= 2^-16 per draw; h = cfg->offset + iteration.)
+ * ==================================================================================== */
+void erpo_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; r++) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        c0 = hi1 ^ c1 ^ k0;
+        c1 = lo1;
+        c2 = hi0 ^ c3 ^ k1;
+        c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0;
+    out[1] = c1;
+    out[2] = c2;
+    out[3] = c3;
+}
+
+void erpo_philox_sample(int32_t m, int32_t s, uint64_t h, uint32_t seed, int32_t* out) {
+    uint8_t* in = (uint8_t*)calloc((size_t)(m > 0 ? m : 1), 1);
+    const uint32_t key[2] = {seed, 0x243F6A88u};
+    uint32_t u[4] = {0, 0, 0, 0};
+    for (int32_t k = 0; k < s; k++) {
+        if ((k & 3) == 0) {
+            const uint32_t ctr[4] = {(uint32_t)h, (uint32_t)(h >> 32), (uint32_t)(k >> 2), 0u};
+            erpo_philox4x32(ctr, key, u);
+        }
+        const int32_t j = m - s + k;
+        const int32_t t = (int32_t)(((uint64_t)u[k & 3] * (uint64_t)(j + 1)) >> 32);
+        if (in[t]) in[j] = 1; else in[t] = 1;
+    }
+    int32_t n = 0;
+    for (int32_t i = 0; i < m; i++)
+        if (in[i]) out[n++] = i;
+    free(in);
+}
+
+/* ======================================================================================
  * Matcher: feature_matcher::match_two_image (src/feature_matcher.cpp:42-59).
  * FlannBasedMatcher::knnMatch(k=2) is approximate (randomized KD-trees); the oracle is its
  * exact limit: brute force in flann::L2<float>::operator() accumulation order (groups of 4,
@@ -561,17 +610,23 @@ int erpo_initial_guess(const double* bl, const double* br, int32_t m, const erpo
         if (diag) *diag = dg;
         return -2;
     }
-    erpo_glibc g;
-    erpo_glibc_seed(&g, cfg->seed);
-    erpo_glibc_discard(&g, cfg->offset);
     /* draw every subset first (the rand() stream is sequential), then estimate in parallel */
     int32_t* idx = (int32_t*)malloc(sizeof(int32_t) * (size_t)iters * sample_n);
-    int32_t* a = (int32_t*)malloc(sizeof(int32_t) * (size_t)m);
-    for (int32_t it = 0; it < iters; it++) {
-        erpo_random_array(a, m, &g);
-        memcpy(idx + (size_t)it * sample_n, a, sizeof(int32_t) * (size_t)sample_n);
+    if (cfg->sampler == 1) {  /* ERP_SAMPLER_PHILOX: ascending index sets */
+        for (int32_t it = 0; it < iters; it++)
+            erpo_philox_sample(m, sample_n, cfg->offset + (uint64_t)it, cfg->seed,
+                               idx + (size_t)it * sample_n);
+    } else {
+        erpo_glibc g;
+        erpo_glibc_seed(&g, cfg->seed);
+        erpo_glibc_discard(&g, cfg->offset);
+        int32_t* a = (int32_t*)malloc(sizeof(int32_t) * (size_t)m);
+        for (int32_t it = 0; it < iters; it++) {
+            erpo_random_array(a, m, &g);
+            memcpy(idx + (size_t)it * sample_n, a, sizeof(int32_t) * (size_t)sample_n);
+        }
+        free(a);
     }
-    free(a);
     if (samples) memcpy(samples, idx, sizeof(int32_t) * (size_t)iters * sample_n);
     erpo_hyp* hs = (erpo_hyp*)malloc(sizeof(erpo_hyp) * (size_t)iters);
 #ifdef _OPENMP

@@ -65,6 +65,10 @@ void erpo_glibc_discard(erpo_glibc* g, uint64_t n);
 /* the 31-word window (r[n-31..n-1] of the additive recurrence) that precedes draw n=pos */
 void erpo_glibc_window(const erpo_glibc* g, uint32_t out[31]);
 
+/* Philox4x32-10 block; iteration h's s-subset of [0, m) in ascending order (erp_oracle.c) */
+void erpo_philox4x32(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+void erpo_philox_sample(int32_t m, int32_t s, uint64_t h, uint32_t seed, int32_t* out);
+
 /* libstdc++ std::random_shuffle over iota(n) using g (random_array::rand_idx_generate) */
 void erpo_random_array(int32_t* a, int32_t n, erpo_glibc* g);
 
@@ -149,7 +153,9 @@ typedef struct {
     double trim_hi;       /* 0.8 (:143) */
     double valid_abs;     /* 1.57 (:76,81) */
     uint32_t seed;        /* 1: srand never called */
-    uint64_t offset;      /* rand() calls consumed before initial_guess (e.g. by FLANN) */
+    uint64_t offset;      /* rand() calls consumed before initial_guess (e.g. by FLANN);
+                             sampler 1: the first iteration's counter */
+    int32_t sampler;      /* 0: glibc replay (the reference), 1: Philox4x32-10 + Floyd */
 } erpo_cfg;
 
 typedef struct {

@@ -452,6 +452,66 @@ def test_sampler_large_match_count(ctx, oracle):
             assert np.array_equal(np.sort(samples[it, :s]), np.sort(a[:s])), it
 
 
+@pytest.mark.parametrize("sizes,iters", [([512, 700, 300, 1024], 300), ([9000], 200),
+                                         ([60000], 70)])
+def test_philox_sampler_vs_oracle(gpu_lib, oracle, sizes, iters):
+    """sampler = ERP_SAMPLER_PHILOX: every iteration's sampled set equals the
+    oracle's Floyd-on-Philox set (erp_oracle.c erpo_philox_sample, Random123 KAT-pinned), the
+    hypotheses and the result equal the oracle's find() run with the same sampler; a pair with
+    M ~ 27k matches (an 864-word bitmap per lane, past one CU's LDS) gets ERP_INVALID_ARG"""
+    import torch
+    from erp_match_eightpoint_test_amd import (Context, PairBatchRunner, capi, hyps_to_numpy,
+                                               results_to_numpy)
+    pairs = [synth.make_pair(5100 + i, n_kpts=n) for i, n in enumerate(sizes)]
+    args = _batch(pairs)
+    c = Context(0)
+    outs = PairBatchRunner(ctx=c, iters=iters, sampler=1).run(*args, want=("hyps", "samples"))
+    torch.cuda.synchronize()
+    res = results_to_numpy(outs["results"])
+    hyps = hyps_to_numpy(outs["hyps"])
+    for i, p in enumerate(pairs):
+        M = int(res[i]["M"])
+        if M > 20480:  # beyond one CU's LDS for the per-lane bitmap: a loud status, no result
+            assert res[i]["status"] == capi.ERP_INVALID_ARG
+            continue
+        assert res[i]["status"] == 0
+        s = int(M * 0.25)
+        got = np.sort(outs["samples"][i, :, :s].cpu().numpy(), axis=1)
+        for it in range(iters):
+            assert np.array_equal(got[it], oracle.philox_sample(M, s, it)), it
+        ref, _, _, _ = oracle.match_two_image(p["desc_l"], p["desc_r"], nthreads=8)
+        assert len(ref) == M
+        kl = p["kp_l"][ref["queryIdx"]]
+        kr = p["kp_r"][ref["trainIdx"]]
+        o = oracle.find(p["W"], p["H"], kl, kr, oracle.make_cfg(iters=iters, sampler=1),
+                        detail=True)
+        _check_hyps(hyps[i], o["hyp"])
+        assert res[i]["K"] == o["K"]
+        assert np.abs(res[i]["R"] - o["R"]).max() <= 2e-6
+        assert np.abs(res[i]["T"] - o["T"]).max() <= 2e-6
+
+
+def test_philox_hypothesis_blocks_by_offset(ctx, oracle):
+    """Philox iteration blocks [a, b) at offset stream_offset(0, a, M, sampler=1) = a reproduce
+    one run's records (the counter-based configs[4] partition)"""
+    from erp_match_eightpoint_test_amd import dist as D
+    import torch
+    g = _npz("find_manual_100_it500.npz")
+    kl = torch.from_numpy(np.ascontiguousarray(g["kl"])).cuda()
+    kr = torch.from_numpy(np.ascontiguousarray(g["kr"])).cuda()
+    m = kl.shape[0]
+    fn = D.gpu_hypotheses(ctx, int(g["W"]), int(g["H"]), kl, kr, m, {"sampler": 1})
+    full = fn(500, 0)
+    parts = [fn(b - a, D.stream_offset(0, a, m, 1))
+             for a, b in [D.block_range(500, 3, r) for r in range(3)]]
+    merged = np.concatenate(parts)
+    for f in ("R1", "R2", "T", "R1_valid", "R2_valid", "E"):
+        assert np.array_equal(merged[f], full[f]), f
+    o = oracle.find(int(g["W"]), int(g["H"]), g["kl"], g["kr"],
+                    oracle.make_cfg(iters=500, sampler=1), detail=True)
+    _check_hyps(full, o["hyp"])
+
+
 # ---------------------------------------------------------- sharding entry points (GPU)
 def test_hypothesis_blocks_by_offset_match_full_run(ctx, oracle):
     """erp_eight_point_hypotheses_dev on iteration blocks [0,a) and [a,I) with the glibc offset

@@ -152,3 +152,66 @@ def test_consensus_semantics(oracle):
     assert mi == 1 and d[1] == d[2]
     rc, mi, d = oracle.consensus(np.zeros((0, 3), np.float32))
     assert rc == -3
+
+
+# ------------------------------------------------- counter-based sampler (ERP_SAMPLER_PHILOX)
+@pytest.mark.parametrize("ctr,key,want", [
+    ((0, 0, 0, 0), (0, 0), (0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8)),
+    ((0xFFFFFFFF,) * 4, (0xFFFFFFFF,) * 2, (0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD)),
+    ((0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344), (0xA4093822, 0x299F31D0),
+     (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)),
+])
+def test_philox_known_answers(oracle, ctr, key, want):
+    """Philox4x32-10: Random123's published known-answer vectors (kat_vectors, philox4x32_10)"""
+    assert tuple(int(x) for x in oracle.philox4x32(ctr, key)) == want
+
+
+@pytest.mark.parametrize("m,s", [(2, 1), (8, 2), (100, 25), (1000, 250), (33, 33), (4096, 1024)])
+def test_philox_sample_is_a_subset(oracle, m, s):
+    """Floyd on Philox draws: s distinct indices of [0, m), ascending, a function of (h, seed)
+    only; different iterations draw different sets"""
+    seen = set()
+    for h in range(20):
+        a = oracle.philox_sample(m, s, h)
+        assert a.shape == (s,) and np.all(np.diff(a) > 0) and a[0] >= 0 and a[-1] < m
+        assert np.array_equal(a, oracle.philox_sample(m, s, h))
+        seen.add(a.tobytes())
+    if s < m:
+        assert len(seen) > 1
+    b = oracle.philox_sample(m, s, 3, seed=2)
+    assert b.shape == (s,)
+
+
+def test_philox_sample_uniform_marginals(oracle):
+    """each index of [0, m) is drawn with probability s / m (chi-square over 4000 iterations)"""
+    m, s, n = 40, 10, 4000
+    cnt = np.zeros(m)
+    for h in range(n):
+        cnt[oracle.philox_sample(m, s, h)] += 1
+    exp = n * s / m
+    chi2 = float(((cnt - exp) ** 2 / exp).sum())
+    assert chi2 < 80.0  # 39 dof: p ~ 1e-4
+
+
+def test_philox_find_offset_blocks(oracle):
+    """find() with the Philox sampler: iteration it samples philox_sample(M, s, offset + it), so
+    iteration blocks run at offsets a (not a (M-1) as for the glibc replay) reproduce one run;
+    the recovered rotation passes the same known-answer bar as the reference's sampler"""
+    from erp_match_eightpoint_test_amd import dist as D
+    p = synth.make_pair(77, n_kpts=400)
+    ref, _, _, _ = oracle.match_two_image(p["desc_l"], p["desc_r"])
+    kl, kr = p["kp_l"][ref["queryIdx"]], p["kp_r"][ref["trainIdx"]]
+    M = len(ref)
+    s = int(M * 0.25)
+    full = oracle.find(p["W"], p["H"], kl, kr, oracle.make_cfg(iters=60, sampler=1), detail=True)
+    assert full["rc"] == 0
+    for it in (0, 1, 59):
+        assert np.array_equal(np.sort(full["samples"][it]), oracle.philox_sample(M, s, it))
+    a = 25
+    blk = oracle.find(p["W"], p["H"], kl, kr,
+                      oracle.make_cfg(iters=60 - a, sampler=1,
+                                      offset=D.stream_offset(0, a, M, sampler=1)), detail=True)
+    assert np.array_equal(blk["samples"], full["samples"][a:])
+    for f in blk["hyp"].dtype.names:  # (field by field: the records have padding bytes)
+        assert np.array_equal(blk["hyp"][f], full["hyp"][a:][f], equal_nan=True), f
+    assert np.degrees(np.abs(full["R"] - p["euler_gt"])).mean() < 1.0
