@@ -16,6 +16,7 @@
 
 #include <math.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -176,6 +177,37 @@ __device__ __forceinline__ float second4(float a0, float a1, float b0, float b1)
     return fminf(fmaxf(m1, o1), fminf(m2, o2));
 }
 
+// A candidate slot is one 32-B record: the tile's 16 bounds as bf16, with the tile's index
+// (tile0 / 32 < 2048: rows < 65536, chunk lengths are multiples of 32) in the 16 mantissa LSBs
+// (bit 2 d of the index in dword d's low half, bit 2 d + 1 in its high half).  The knn2_rescore
+// side widens each value by 2^-6 |v| instead of 2^-8 |v| (round to nearest: 1/2 ulp, the
+// replaced LSB: 1 ulp, so |v - u'| <= 3 2^-8 |v|).  Before round 3 the tile index went to a
+// separate int32 array: a scattered 4-B store per slot that HBM wrote as a whole sector (the
+// filter's slot writes 0.72 GB per 192-pair launch against 0.35 GB of bounds; ERP_CAND_TILE_ARRAY=1
+// keeps that layout for A/B).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8 cand_embed_tile(bf16x8 b, int g, int tile0) {
+    const uint32_t ti = (uint32_t)tile0 >> 5;
+    u32x4 w = __builtin_bit_cast(u32x4, b);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int d = 4 * g + k;
+        const uint32_t bits = ((ti >> (2 * d)) & 1u) | (((ti >> (2 * d + 1)) & 1u) << 16);
+        w[k] = (w[k] & 0xfffefffeu) | bits;
+    }
+    return __builtin_bit_cast(bf16x8, w);
+}
+__device__ __forceinline__ int cand_tile(bf16x8 v0, bf16x8 v1) {
+    const u32x4 a = __builtin_bit_cast(u32x4, v0), b = __builtin_bit_cast(u32x4, v1);
+    uint32_t ti = 0;
+#pragma unroll
+    for (int d = 0; d < 8; d++) {
+        const uint32_t w = d < 4 ? a[d] : b[d - 4];
+        ti |= ((w & 1u) << (2 * d)) | (((w >> 16) & 1u) << (2 * d + 1));
+    }
+    return (int)(ti << 5);
+}
+
 __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restrict__ dq,
                                                           const bf16x8* __restrict__ thi,
                                                           const float* __restrict__ tn,
@@ -189,7 +221,8 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
                                                           int32_t* __restrict__ ctile,
                                                           bf16x8* __restrict__ cval,
                                                           const bf16x8* __restrict__ sent_hi,
-                                                          const float* __restrict__ sent_tu) {
+                                                          const float* __restrict__ sent_tu,
+                                                          int tile_array) {
     __shared__ __align__(16) char sm[2 * kFStageB];
     // XCD-aware block order: workgroups are dealt to the 8 XCDs round-robin by linear id, so
     // XCD x gets the contiguous logical range [x NB/8, (x+1) NB/8) (query blocks fastest, then
@@ -322,13 +355,13 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
                     const int sl = ncand[j]++;
                     if (sl < kCandSlots) {
                         const size_t slot = (size_t)cl[j] * kCandSlots + sl;
-                        ctile[slot] = tile0;
+                        if (tile_array) ctile[slot] = tile0;
 #pragma unroll
                         for (int g = 0; g < 2; g++) {
                             bf16x8 b;
 #pragma unroll
                             for (int i = 0; i < 8; i++) b[i] = (__bf16)acc[j][8 * g + i];
-                            cval[slot * 2 + g] = b;
+                            cval[slot * 2 + g] = tile_array ? b : cand_embed_tile(b, g, tile0);
                         }
                     }
                 }
@@ -436,7 +469,7 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                                                            const bf16x8* __restrict__ cval,
                                                            Top2* __restrict__ part,
                                                            int32_t* __restrict__ ovf, int qblocks,
-                                                           float ratio) {
+                                                           float ratio, int tile_array) {
     __shared__ int32_t plist[kPassList * 256];
     __shared__ float plb[kPassList * 256];
     // XCD-aware block order as in knn2_filter (a pair's blocks on one XCD: its f32 train rows,
@@ -487,7 +520,10 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
         const float lq = (__builtin_fmaf(qq, -kFEps, qq) - kFTiny) - teM;
         // u* = v + 2^-8 |v| + |q|^2 (1 + eps) >= u' + |q|^2 (1 + eps) = u >= e (the filter's
         // upper bound; the f32 roundings here are far inside its 2.1e-4 S slack)
-        const float uq = __builtin_fmaf(qq, kFEps, qq);
+        const float uq = __builtin_fmaf(qq, kFEps, qq) + kFTiny;
+        // the stored value's widening: round to nearest (2^-8 |v|), +1 ulp with the tile index
+        // in the LSB (3 2^-8 |v|, taken as 2^-6)
+        const float wv = tile_array ? 0x1p-8f : 0x1p-6f;
         int npass = 0;
         float l1 = kInf, l2 = kInf, umin = kInf;  // two smallest l*, smallest u*
         int r1 = -1, ra = -1;                     // their rows
@@ -495,13 +531,13 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
             const int n = h ? n1 : n0;
             for (int k = 0; k < n; k++) {
                 const size_t slot = (l0 + h) * kCandSlots + k;
-                const int tile0 = ctile[slot];
                 const bf16x8 v0 = cval[slot * 2], v1 = cval[slot * 2 + 1];
+                const int tile0 = tile_array ? ctile[slot] : cand_tile(v0, v1);
 #pragma unroll
                 for (int e = 0; e < 16; e++) {
                     // bf16 round to nearest: |v - u'| <= 2^-9 |u'|, so v - 2^-8 |v| <= u'
                     const float x = (float)(e < 8 ? v0[e] : v1[e - 8]);
-                    const float lo = __builtin_fmaf(-0x1p-8f, fabsf(x), x) + lq;
+                    const float lo = __builtin_fmaf(-wv, fabsf(x), x) + lq;
                     const int row = tile0 + (e & 3) + 8 * (e >> 2) + 4 * h;
                     if (lo <= U2 && row < nt) {
                         if (npass < kPassList) {
@@ -509,7 +545,7 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                             plb[npass * 256 + threadIdx.x] = lo;
                         }
                         npass++;
-                        const float hi = __builtin_fmaf(0x1p-8f, fabsf(x), x) + uq;
+                        const float hi = __builtin_fmaf(wv, fabsf(x), x) + uq;
                         if (lo < l1) {
                             l2 = l1;
                             l1 = lo;
@@ -919,6 +955,13 @@ __global__ void set_i32_kernel(int32_t* p, int32_t v) { *p = v; }
 }  // namespace
 
 // ====================================================================== launchers =======
+// ERP_CAND_TILE_ARRAY=1: the tile index of a candidate slot in its own int32 array (the
+// layout before round 3, an A/B knob); default: inside the slot's bf16 bounds
+static bool cand_tile_array() {
+    static const bool v = getenv("ERP_CAND_TILE_ARRAY") && atoi(getenv("ERP_CAND_TILE_ARRAY")) != 0;
+    return v;
+}
+
 size_t knn2_cand_bytes(const BatchShape& sh) {
     return (size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 * kCandSlots * (2 * sizeof(bf16x8) + 4);
 }
@@ -964,7 +1007,7 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
     hipLaunchKernelGGL(knn2_filter_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
                        st, desc_q, thi, tn, tmax, off_q, off_t, sh.fchunk_len, sh.fchunks,
                        sh.max_nq, sh.max_nt, qblocks, pu, ccount, ctile, cval,
-                       (const bf16x8*)sent, (const float*)(sent + 128));
+                       (const bf16x8*)sent, (const float*)(sent + 128), (int)cand_tile_array());
     return hipGetLastError();
 }
 
@@ -980,7 +1023,8 @@ hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const i
     hipLaunchKernelGGL(knn2_rescore_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
                        st, desc_q, desc_t, off_q, off_t, sh.max_nq, sh.fchunk_len, sh.fchunks,
                        split_tmax(sh, split), pu, ccount, ctile, cval, part, ovf, qblocks,
-                       sh.fchunks == 1 ? ratio : -1.f);  // (bound decisions need one chunk)
+                       sh.fchunks == 1 ? ratio : -1.f,  // (bound decisions need one chunk)
+                       (int)cand_tile_array());
     hipLaunchKernelGGL(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
                        sh.max_nq, sh.fchunk_len, sh.fchunks, ovf, part);
     return hipGetLastError();
