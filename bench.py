@@ -74,7 +74,7 @@ def parse():
                          "keypoints without a partner, descriptor noise 0.035, 30%% of the true "
                          "matches at wrong positions) reported beside the headline; 0 = off")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--profile-tag", default="r03c",
+    ap.add_argument("--profile-tag", default="r03e",
                     help="profiles/<tag>_pmc_<stage>.json: HBM bytes per launch (roofline.traffic)")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
@@ -903,8 +903,10 @@ def main():
         "warmup": args.warmup, "ms_per_step": elapsed / max(args.steps, 1) * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32+f64",
         "data": "synthetic (seeded SURF-like descriptors + ERP keypoints, synth.make_pair)",
-        "config": {"workload": "configs[1] shape: 4096x4096 kpts/pair, 10k initial_guess iters, "
-                               f"batch of {args.pairs} independent pairs per step per GPU",
+        "config": {"workload": (("configs[1] shape" if args.kpts == 4096 else
+                                 "configs[2] shape" if args.kpts == 2048 else "custom shape") +
+                                f": {args.kpts}x{args.kpts} kpts/pair, {args.iters} initial_guess "
+                                f"iters, batch of {args.pairs} independent pairs per step per GPU"),
                    "kpts": args.kpts, "iters": args.iters, "pairs_per_step_per_gpu": args.pairs,
                    "streams": S, "matcher": args.matcher,
                    "parallelism": f"pair-sharded x{world}", "sampler": ("glibc replay (seed 1)" if SAMPLER == 0

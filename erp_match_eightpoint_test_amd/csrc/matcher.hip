@@ -346,9 +346,10 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
             tmin[j] = min2f(ta, tb);
         }
         if (extract) {
-            // a lane whose 16 rows of the tile may hold a candidate stores them whole (tile,
-            // 16 bounds as bf16: two 16-B stores); knn2_rescore picks the rows under the final
-            // bound (widening each stored value by its bf16 rounding)
+            // a lane whose 16 rows of the tile may hold a candidate stores them whole (16
+            // bounds as bf16 carrying the tile index: two 16-B stores); knn2_rescore picks the
+            // rows under the final bound (widening each stored value by its bf16 rounding and
+            // the replaced LSB)
 #pragma unroll
             for (int j = 0; j < 2; j++) {
                 if (tmin[j] <= thr[j]) {
