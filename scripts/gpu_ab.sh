@@ -11,7 +11,10 @@ if [ -n "${TEST_K:-}" ]; then
   echo "== gpu tests -k $TEST_K" && timeout -k 10 600 python -u -m pytest tests -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -k "$TEST_K" > gpurun_out/pytest_${TAG}.log 2>&1 || { tail -30 gpurun_out/pytest_${TAG}.log; exit 1; }
   tail -2 gpurun_out/pytest_${TAG}.log
 fi
+N=0
 for V in ${VALUES:-0 1}; do
-  echo "== bench $KNOB=$V" && env $KNOB=$V timeout -k 10 400 python bench.py --no-cpu-baseline --steps ${STEPS:-10} --warmup 2 ${BENCH_ARGS:-} > gpurun_out/bench_${TAG}_$V.json 2> gpurun_out/bench_${TAG}_$V.err || { tail -20 gpurun_out/bench_${TAG}_$V.err; exit 1; }
-  python scripts/bench_summary.py gpurun_out/bench_${TAG}_$V.json 2>/dev/null || python -c "import json;d=json.load(open('gpurun_out/bench_${TAG}_$V.json'));print(d['value'], d['ms_per_step'], {k:round(v,2) for k,v in d['stages_ms_serial_step'].items() if v>0.3})"
+  N=$((N + 1))
+  F=gpurun_out/bench_${TAG}_${N}_$(echo "$V" | tr '/' '_')
+  echo "== bench $KNOB=$V" && env $KNOB=$V timeout -k 10 400 python bench.py --no-cpu-baseline --steps ${STEPS:-10} --warmup 2 ${BENCH_ARGS:-} > $F.json 2> $F.err || { tail -20 $F.err; exit 1; }
+  python scripts/bench_summary.py $F.json 2>/dev/null || python -c "import json;d=json.load(open('$F.json'));print(d['value'], d['ms_per_step'], {k:round(v,2) for k,v in d['stages_ms_serial_step'].items() if v>0.3})"
 done
