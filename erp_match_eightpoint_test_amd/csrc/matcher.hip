@@ -114,6 +114,13 @@ constexpr float kFMargin = 0x1p-20f;
 constexpr int kFRowB = 128;
 constexpr int kFHiB = kFST * kFT * kFRowB;        // 16384
 constexpr int kFStageB = kFHiB + kFST * kFT * 4;  // + 512
+// Tile schedule (profiles/r03g_filter_chains_ab.txt, same-box A/B per 768-pair step): 0 = the
+// two query blocks' MFMA chains interleaved, both min trees after the last MFMA (2.68 ms);
+// 1 = chain 0 whole, then chain 1 with chain 0's min tree between its MFMAs (2.57 ms);
+// 2 = as 1, and chain 1's min tree deferred past the next tile's MFMAs (2.55 ms, 158 VGPRs).
+#ifndef ERP_FILTER_CHAINS
+#define ERP_FILTER_CHAINS 2
+#endif
 
 __device__ __forceinline__ bf16x8 round8(const float4 a, const float4 b, float s) {
     const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -306,8 +313,12 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     for (int c = 0; c < 4; c++) rd_hi[c] = r * kFRowB + (((2 * c + h) ^ ((r >> 1) & 7)) << 4);
     const int rd_tu = kFHiB + 16 * h;
     // one tile: the A fragments and C operand from LDS, two 4-MFMA chains (the wave's two query
-    // blocks), the epilogue (group minima; with `extract`, the candidate test and slot stores)
-    auto tile = [&](const char* sb, int u, int tile0, bool extract) {
+    // blocks); then the epilogue of each chain (group minima; with `extract`, the candidate test
+    // and slot stores)
+    struct Acc2 {
+        f32x16 a0, a1;
+    };
+    auto tile_mma = [&](const char* sb, int u) __attribute__((always_inline)) -> Acc2 {
         bf16x8 ah[4];
 #pragma unroll
         for (int c = 0; c < 4; c++)
@@ -321,53 +332,73 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
             ci[4 * g + 2] = t4.z;
             ci[4 * g + 3] = t4.w;
         }
-        f32x16 acc[2];
+        Acc2 r;
+        r.a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[0], qh[0][0], ci, 0, 0, 0);
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[0], qh[j][0], ci, 0, 0, 0);
+        for (int c = 1; c < 4; c++)
+            r.a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[c], qh[0][c], r.a0, 0, 0, 0);
+#if ERP_FILTER_CHAINS
+        // chain 0 whole before chain 1: its min tree then issues between chain 1's MFMAs instead
+        // of after both (the interleaved order exposes the last MFMA's drain)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        r.a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[0], qh[1][0], ci, 0, 0, 0);
 #pragma unroll
-            for (int c = 1; c < 4; c++)
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[c], qh[j][c], acc[j], 0, 0, 0);
-        }
-        float tmin[2];
+        for (int c = 1; c < 4; c++)
+            r.a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[c], qh[1][c], r.a1, 0, 0, 0);
+        return r;
+    };
+    auto tile_epi = [&](int j, f32x16 e, int tile0, bool extract) __attribute__((always_inline)) {
+        float ta = min3f(e[0], e[1], e[2]);
+        ta = min3f(ta, e[3], e[4]);
+        ta = min3f(ta, e[5], e[6]);
+        ta = min2f(ta, e[7]);
+        float tb = min3f(e[8], e[9], e[10]);
+        tb = min3f(tb, e[11], e[12]);
+        tb = min3f(tb, e[13], e[14]);
+        tb = min2f(tb, e[15]);
+        gm[j][0] = min2f(gm[j][0], ta);
+        gm[j][1] = min2f(gm[j][1], tb);
+        // a lane whose 16 rows of the tile may hold a candidate stores them whole (16 bounds
+        // as bf16 carrying the tile index: two 16-B stores); knn2_rescore picks the rows under
+        // the final bound (widening each stored value by its bf16 rounding and the replaced LSB)
+        if (extract && min2f(ta, tb) <= thr[j]) {
+            const int sl = ncand[j]++;
+            if (sl < kCandSlots) {
+                const size_t slot = (size_t)cl[j] * kCandSlots + sl;
+                if (tile_array) ctile[slot] = tile0;
 #pragma unroll
-        for (int j = 0; j < 2; j++) {
-            const f32x16 e = acc[j];
-            float ta = min3f(e[0], e[1], e[2]);
-            ta = min3f(ta, e[3], e[4]);
-            ta = min3f(ta, e[5], e[6]);
-            ta = min2f(ta, e[7]);
-            float tb = min3f(e[8], e[9], e[10]);
-            tb = min3f(tb, e[11], e[12]);
-            tb = min3f(tb, e[13], e[14]);
-            tb = min2f(tb, e[15]);
-            gm[j][0] = min2f(gm[j][0], ta);
-            gm[j][1] = min2f(gm[j][1], tb);
-            tmin[j] = min2f(ta, tb);
-        }
-        if (extract) {
-            // a lane whose 16 rows of the tile may hold a candidate stores them whole (16
-            // bounds as bf16 carrying the tile index: two 16-B stores); knn2_rescore picks the
-            // rows under the final bound (widening each stored value by its bf16 rounding and
-            // the replaced LSB)
+                for (int g = 0; g < 2; g++) {
+                    bf16x8 b;
 #pragma unroll
-            for (int j = 0; j < 2; j++) {
-                if (tmin[j] <= thr[j]) {
-                    const int sl = ncand[j]++;
-                    if (sl < kCandSlots) {
-                        const size_t slot = (size_t)cl[j] * kCandSlots + sl;
-                        if (tile_array) ctile[slot] = tile0;
-#pragma unroll
-                        for (int g = 0; g < 2; g++) {
-                            bf16x8 b;
-#pragma unroll
-                            for (int i = 0; i < 8; i++) b[i] = (__bf16)acc[j][8 * g + i];
-                            cval[slot * 2 + g] = tile_array ? b : cand_embed_tile(b, g, tile0);
-                        }
-                    }
+                    for (int i = 0; i < 8; i++) b[i] = (__bf16)e[8 * g + i];
+                    cval[slot * 2 + g] = tile_array ? b : cand_embed_tile(b, g, tile0);
                 }
             }
         }
+    };
+    // the stage's 4 tiles.  ERP_FILTER_CHAINS == 2: software-pipelined by one chain -- tile u's
+    // second chain is reduced after tile u + 1's MFMAs are issued, so neither chain's drain is
+    // waited on (+16 live VGPRs)
+    auto tiles = [&](const char* sb, int tb0, bool extract) __attribute__((always_inline)) {
+#if ERP_FILTER_CHAINS == 2
+        f32x16 prev;
+#pragma unroll
+        for (int u = 0; u < kFST; u++) {
+            const Acc2 acc = tile_mma(sb, u);
+            tile_epi(0, acc.a0, tb0 + u * kFT, extract);
+            if (u > 0) tile_epi(1, prev, tb0 + (u - 1) * kFT, extract);
+            prev = acc.a1;
+        }
+        tile_epi(1, prev, tb0 + (kFST - 1) * kFT, extract);
+#else
+#pragma unroll
+        for (int u = 0; u < kFST; u++) {
+            const Acc2 acc = tile_mma(sb, u);
+            tile_epi(0, acc.a0, tb0 + u * kFT, extract);
+            tile_epi(1, acc.a1, tb0 + u * kFT, extract);
+        }
+#endif
     };
     // one stage: wait for its DMAs (issued during the previous stage), barrier, the next
     // stage's DMAs into the other buffer (whose reads finished before this barrier), 4 tiles,
@@ -379,8 +410,7 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (it < nstages) dma(sm + (1 - BUF) * kFStageB, it + 1 == nstages ? 0 : it + 1);
-#pragma unroll
-        for (int u = 0; u < kFST; u++) tile(sb, u, t0 + (st * kFST + u) * kFT, it > 0);
+        tiles(sb, t0 + st * kFST * kFT, it > 0);
         if (it < nstages) {
 #pragma unroll
             for (int j = 0; j < 2; j++) {
