@@ -3124,7 +3124,13 @@ __global__ void consensus_ref2_count_kernel(int n_pairs, const int32_t* __restri
     n1c[p] = (zb[p] >= 0 ? r2c[p] : 0) + n2c[p] - nfb[p];
 }
 
-__global__ __launch_bounds__(256) void consensus_refine_kernel(
+// ERP_REFINE_MINB (r03k): 4 blocks per CU bound the kernel to 128 VGPRs (153 unbounded, no
+// spills either way; its 32 KB of LDS already allows 4): 4 waves per SIMD instead of 3
+// (profiles/r03k_ab.txt: refine 0.626 -> 0.605 ms per 768-pair step)
+#ifndef ERP_REFINE_MINB
+#define ERP_REFINE_MINB 4
+#endif
+__global__ __launch_bounds__(256, ERP_REFINE_MINB) void consensus_refine_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv,
     const float* __restrict__ dscale, int stride, double trim_lo, double trim_hi,
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
