@@ -74,7 +74,7 @@ def parse():
                          "keypoints without a partner, descriptor noise 0.035, 30%% of the true "
                          "matches at wrong positions) reported beside the headline; 0 = off")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--profile-tag", default="r03h",
+    ap.add_argument("--profile-tag", default="r03l",
                     help="profiles/<tag>_pmc_<stage>.json: HBM bytes per launch (roofline.traffic)")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")

@@ -1,8 +1,10 @@
 #!/bin/bash
-# one-off GPU call: round artifacts (tests, bench, rocprof stats, FETCH/WRITE PMC) of the
-# current code under TAG
+# one-off GPU call: smoke(), then the round artifacts (tests, bench, rocprof stats, FETCH/WRITE
+# PMC) of the current code under TAG
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${TAG:-r03h} bash scripts/gpu_round_artifacts.sh || exit 1
+echo "== smoke" && timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG:-r03l}.log 2>&1 || { tail -20 gpurun_out/smoke_${TAG:-r03l}.log; exit 1; }
+tail -1 gpurun_out/smoke_${TAG:-r03l}.log
+TAG=${TAG:-r03l} bash scripts/gpu_round_artifacts.sh || exit 1
