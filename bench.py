@@ -6,11 +6,12 @@ descriptors + keypoints (W x H = 5376 x 2688), exact k=2 + ratio-0.3 match -> ga
 eight_point::find with 10 000 initial_guess iterations (glibc-replay sampler, reference
 defaults otherwise).  A step = B such pairs resident in HBM, split into S independent
 sub-batches (own context + HIP stream each, so one sub-batch's latency-bound kernels overlap
-the other's); every step recomputes everything (no cached outputs).  Defaults B = 768, S = 4 (four
-sub-batches of 192 on four HIP streams: the latency-bound consensus / eigen kernels of one
-overlap the VALU- and MFMA-bound kernels of the others; r02m sweep on one MI355X, 10 steps each:
-384 x 3 31.9-32.0k pairs/s, 768 x 3 32.4-33.3k, 768 x 4 33.6k, 1536 x 3 33.5k,
-profiles/r02m_streamsweep.txt).
+the other's); every step recomputes everything (no cached outputs).  Defaults B = 768, S = 6 (six
+sub-batches of 128 on six HIP streams: the latency-bound consensus / eigen kernels of one
+overlap the VALU- and MFMA-bound kernels of the others; r03 sweep on one MI355X, 8 steps each,
+profiles/r03n_step_sweep.txt: 768 x 4 34.8-35.0k pairs/s, 768 x 6 35.7-36.5k, 768 x 8
+34.9-35.2k, 1024 x 4 35.1k, 1536 x 4 34.6k, 1536 x 6 35.6k; the r02m sweep had 768 x 4 ahead of
+768 x 3 and 384 x 3, profiles/r02m_streamsweep.txt).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--pairs B] [--streams S] [--iters I]
 
@@ -49,7 +50,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--pairs", type=int, default=768, help="pairs per step per GPU")
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=6,
                     help="independent sub-batches (own context + HIP stream) per step")
     ap.add_argument("--iters", type=int, default=10000)
     ap.add_argument("--kpts", type=int, default=4096)
@@ -74,7 +75,7 @@ def parse():
                          "keypoints without a partner, descriptor noise 0.035, 30%% of the true "
                          "matches at wrong positions) reported beside the headline; 0 = off")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--profile-tag", default="r03l",
+    ap.add_argument("--profile-tag", default="r03n",
                     help="profiles/<tag>_pmc_<stage>.json: HBM bytes per launch (roofline.traffic)")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
