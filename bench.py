@@ -42,6 +42,9 @@ PEAK_I8_MFMA = 2 * PEAK_BF16_MFMA   # TOP/s dense (32x32x32 i8 = the cycles of 3
 # over 2 cycles on a SIMD-32, i.e. 32 lanes / cycle / SIMD): 256 CU x 4 SIMD x 32 x 2.4 GHz
 PEAK_VALU_OPS = 256 * 4 * 32 * 2.4e9 / 1e12          # 78.6 T lane-ops/s
 PEAK_VALU_OPS_4CYC = PEAK_VALU_OPS / 2                # secondary: every op at 4 cycles (39.3)
+# profiles/<tag>_pmc_<stage>.json of the shipped step (768 pairs, 6 sub-batches = 128-pair
+# launches): the HBM bytes per launch that roofline.traffic reports
+PROFILE_TAG = "r04a"
 
 
 def parse():
@@ -75,7 +78,7 @@ def parse():
                          "keypoints without a partner, descriptor noise 0.035, 30%% of the true "
                          "matches at wrong positions) reported beside the headline; 0 = off")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--profile-tag", default="r03n",
+    ap.add_argument("--profile-tag", default=PROFILE_TAG,
                     help="profiles/<tag>_pmc_<stage>.json: HBM bytes per launch (roofline.traffic)")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
@@ -204,12 +207,16 @@ SAMPLER = 0  # erp_ransac_cfg.sampler of every run (--sampler): 0 glibc replay, 
 
 
 def oracle_pair(p, iters, nthreads):
-    """one pair through the oracle (exact k=2 match + find), with its match list"""
+    """one pair through the oracle (exact k=2 match + find), with its match list and the
+    per-iteration validity flags (for the R1 / R2 order rule of parity_check)"""
     import oracle as O
     mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=nthreads)
     r = O.find(p["W"], p["H"], p["kp_l"][mt["queryIdx"]], p["kp_r"][mt["trainIdx"]],
-               O.make_cfg(iters=iters, sampler=SAMPLER))
+               O.make_cfg(iters=iters, sampler=SAMPLER), detail=True)
     r["matches"] = mt
+    r["hyp"] = {"R1_valid": r["hyp"]["R1_valid"].copy(), "R2_valid": r["hyp"]["R2_valid"].copy()}
+    for k in ("samples", "rvec", "tvec", "dist"):
+        r.pop(k, None)
     return r
 
 
@@ -249,21 +256,25 @@ def cpu_baseline(pairs, iters, budget_s):
 
 
 def parity_check(gpu_res, gpu_matches, ora):
-    """the timed workload against the oracle, pair by pair (the pairs cpu_baseline ran): M, K,
-    min_idx and status equal, R / T within 2e-6, the match list (queryIdx, trainIdx,
-    distance bits) bit-exact.  gpu_res: result records of the timed step (same pairs, same
-    order); gpu_matches: [pairs, max_nq, 4] int32 from an untimed pass with the matches out."""
+    """the timed workload against the oracle, pair by pair (the pairs cpu_baseline ran): M, K
+    and status equal, min_idx equal (dist.min_idx_agrees: one apart only when both rows are the
+    R1 / R2 of ONE iteration, from the oracle's validity flags), R / T within 2e-6, the match list
+    (queryIdx, trainIdx, distance bits) bit-exact.  gpu_res: result records of the timed step
+    (same pairs, same order); gpu_matches: [pairs, max_nq, 4] int32 from an untimed pass with the
+    matches out."""
+    from erp_match_eightpoint_test_amd.dist import min_idx_agrees
     bad, swaps = [], []
     for i, o in enumerate(ora):
         r = gpu_res[i]
         M = len(o["matches"])
-        # min_idx one apart with the same R: the winner iteration's R1 / R2 push order differs
-        # (it follows the sign of a noise-level singular vector, DESIGN.md 3.2), not the winner
-        di = int(r["min_idx"]) - int(o["min_idx"])
-        if abs(di) == 1:
+        hy = o.get("hyp")
+        agree, swap = min_idx_agrees(r["min_idx"], o["min_idx"],
+                                     None if hy is None else hy["R1_valid"],
+                                     None if hy is None else hy["R2_valid"])
+        if swap:
             swaps.append(i)
         ok = (int(r["status"]) == o["status"] == 0 and int(r["M"]) == M and int(r["K"]) == o["K"]
-              and abs(di) <= 1
+              and agree
               and float(np.abs(r["R"] - o["R"]).max()) <= 2e-6
               and float(np.abs(r["T"] - o["T"]).max()) <= 2e-6
               and np.array_equal(gpu_matches[i, :M].view(np.uint32).reshape(-1)[: 4 * M],
@@ -272,16 +283,23 @@ def parity_check(gpu_res, gpu_matches, ora):
             bad.append(i)
     return {"pairs_checked": len(ora), "all_equal": not bad, "mismatched_pairs": bad,
             "r1r2_order_swaps": swaps,
-            "fields": "status, M, K equal; min_idx equal (or the same iteration's other rotation, "
-                      "listed in r1r2_order_swaps); R, T within 2e-6; matches bit-exact"}
+            "fields": "status, M, K equal; min_idx equal (or, listed in r1r2_order_swaps, the "
+                      "other rotation of the SAME iteration with the same R); R, T within 2e-6; "
+                      "matches bit-exact"}
 
 
 def load_pmc(tag, stage):
+    """(HBM bytes per launch of `stage` from profiles/<tag>_pmc_<stage>.json, that path).  A
+    missing file is reported loudly (stderr) and in the line (roofline.traffic_missing), never
+    as a silent null."""
     path = os.path.join(ROOT, "profiles", f"{tag}_pmc_{stage}.json")
     if os.path.exists(path):
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
-    return None
+            return json.load(f).get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    print(f"bench.py: WARNING: no PMC traffic file {os.path.relpath(path, ROOT)} for the "
+          f"dominant kernel '{stage}' (--profile-tag {tag}); roofline.traffic is null",
+          file=sys.stderr)
+    return None, None
 
 
 def run_dense(args):
@@ -672,6 +690,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    out = None
     for _ in range(args.steps):
         out = call()
         if dist is not None:
@@ -680,6 +699,7 @@ def main():
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
+    timed_out = out  # the last timed step's records (torch.cat: a tensor of its own)
     # per-kernel durations: one more step AFTER the timed region, its sub-batches run one after
     # the other with HIP events around every kernel (standalone kernel times; inside the timed
     # region the sub-batches overlap, so events there would also count queueing behind the
@@ -695,7 +715,10 @@ def main():
             stages[k] = (a[0] + ms, a[1] + n)
         sb["ctx"].set_profiling(False)
     elapsed = t1 - t0
-    out = torch.cat([sb["res"] for sb in subs])  # (the serial pass recomputed the same step)
+    serial_out = torch.cat([sb["res"] for sb in subs])  # the serial pass recomputed the step
+    out = timed_out if timed_out is not None else serial_out
+    timed_identical = (None if timed_out is None else
+                       bool(torch.equal(timed_out.cpu(), serial_out.cpu())))
     if dist is not None:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -719,9 +742,14 @@ def main():
         amount /= stages[dom][1]  # the step's work over its launches (one per sub-batch)
         avg_s = stages[dom][0] / stages[dom][1] / 1e3
         achieved = amount / avg_s / 1e12
+        traffic, tsrc = load_pmc(args.profile_tag, dom)
         roof = {"bound": bound, "kernel": dom, "achieved": achieved, "peak": peak, "unit": unit,
-                "frac": achieved / peak, "traffic": load_pmc(args.profile_tag, dom),
-                "avg_launch_ms": avg_s * 1e3, "work_per_launch": amount, "work_note": note}
+                "frac": achieved / peak, "traffic": traffic,
+                "traffic_source": tsrc if tsrc else None,
+                "avg_launch_ms": avg_s * 1e3, "work_per_launch": amount, "work_note": note,
+                "launch_pairs": args.pairs // S}
+        if tsrc is None:
+            roof["traffic_missing"] = f"profiles/{args.profile_tag}_pmc_{dom}.json"
         if peak == PEAK_VALU_OPS:
             roof["frac_vs_4cycle_issue"] = achieved / PEAK_VALU_OPS_4CYC
         if dom == "sampler_gram":  # the MFMA half of the fused kernel against its own roof
@@ -760,7 +788,8 @@ def main():
             if k >= 3:
                 ts.append(time.perf_counter() - ta)
         lat = {"single_pair_ms": float(np.median(ts)) * 1e3,
-               "note": "one 4096x4096 pair, 10k iterations, batch of 1, host-timed, median of 20"}
+               "note": f"one {args.kpts}x{args.kpts} pair, {args.iters} iterations, batch of 1, "
+                       "host-timed, median of 20"}
     # a harder batch through the same contexts and streams (beside the headline, not `value`):
     # half the left keypoints without a true partner, more descriptor noise (0.035: much more
     # and the 0.3 ratio test rejects the true partners too), 30 % of the true matches at wrong
@@ -874,7 +903,7 @@ def main():
             p = first_pair(r)
             mt, _, _, _ = O.match_two_image(p["desc_l"], p["desc_r"], nthreads=threads)
             o = O.find(p["W"], p["H"], p["kp_l"][mt["queryIdx"]], p["kp_r"][mt["trainIdx"]],
-                       O.make_cfg(iters=args.iters, sampler=SAMPLER))
+                       O.make_cfg(iters=args.iters, sampler=SAMPLER), detail=True)
             return dict(o, M=len(mt))
         multi = D.check_gathered(gathered.cpu().numpy(), args.pairs, world, rerun, ora)
         multi["gathered_rows"] = int(gathered.shape[0])
@@ -898,6 +927,9 @@ def main():
         parity = parity_check(res, o["matches"][:n0].cpu().numpy(), ora)
         parity["rerun_records_identical"] = bool(
             np.array_equal(rerun.view(np.uint8), res[:len(rerun)].view(np.uint8)))
+        # the parity-checked records ARE the timed step's; the serial profile pass after the
+        # timed region must reproduce them byte for byte
+        parity["timed_records_identical"] = timed_identical
     line = {
         "metric": "ERP image-pairs/sec (4k x 4k kpts, 10k RANSAC iters); match-set bit-exact",
         "value": value, "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
@@ -913,6 +945,7 @@ def main():
                    "parallelism": f"pair-sharded x{world}", "sampler": ("glibc replay (seed 1)" if SAMPLER == 0
                                else "Philox4x32-10 + Floyd (seed 1; no reference counterpart)"),
                    "rccl_world": world if dist is not None else None,
+                   "profile_tag": args.profile_tag,
                    "inlier_frac": args.inlier_frac, "sigma": args.sigma},
         "roofline": roof,
         "roofline_stages": stage_roofs,
@@ -927,8 +960,12 @@ def main():
                     "step_ms": elapsed / max(args.steps, 1) * 1e3},
         "check": {"all_status_ok": ok, "mean_abs_euler_err_deg_max": max(err_deg),
                   "M_mean": float(res["M"].mean()), "K_mean": float(res["K"].mean()),
-                  "consensus_survivors": res["survivors"].tolist(),
-                  "near_ties": res["near_ties"].tolist(), "parity": parity,
+                  "consensus_survivors": {"mean": float(res["survivors"].mean()),
+                                          "max": int(res["survivors"].max()),
+                                          "pairs_over_8": np.nonzero(res["survivors"] > 8)[0].tolist()},
+                  "near_ties": {"total": int(res["near_ties"].sum()),
+                                "pairs": np.nonzero(res["near_ties"])[0].tolist()},
+                  "parity": parity,
                   "gathered_records": None if gathered is None else int(gathered.shape[0]),
                   "multi_rank": multi},
     }

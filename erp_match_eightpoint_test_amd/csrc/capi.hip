@@ -438,6 +438,14 @@ bool cfg_ok(const erp_ransac_cfg* cfg) {
            cfg->trim_lo <= cfg->trim_hi;
 }
 
+// the Philox sampler's per-lane LDS bitmap holds M <= 20480 positions (kernels.hip
+// launch_philox_sampler); entry points that know m on the host refuse larger pairs up front (the
+// batch pipeline, where M is only known on the device, flags the pair instead)
+constexpr int32_t kPhiloxMaxM = 20480;
+bool sampler_m_ok(const erp_ransac_cfg* cfg, int32_t m) {
+    return cfg->sampler != ERP_SAMPLER_PHILOX || m <= kPhiloxMaxM;
+}
+
 // estimator stages after counts/pts are in place
 erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
                           const erp_batch_outputs* out, hipStream_t st) {
@@ -763,7 +771,8 @@ erp_status erp_eight_point_find_dev(erp_ctx* ctx, int32_t W, int32_t H, const er
                                     const erp_point2f* d_kr, int32_t m, const erp_ransac_cfg* cfg,
                                     erp_pair_result* d_result, erp_hypothesis* d_hyps,
                                     void* stream) {
-    if (!ctx || W <= 0 || H <= 0 || m < 0 || m > 65535 || !d_result || !cfg_ok(cfg))
+    if (!ctx || W <= 0 || H <= 0 || m < 0 || m > 65535 || !d_result || !cfg_ok(cfg) ||
+        !sampler_m_ok(cfg, m))
         return ERP_INVALID_ARG;
     if (m > 0 && (!d_kl || !d_kr)) return ERP_INVALID_ARG;
     ERP_CK(hipSetDevice(ctx->device));
@@ -790,7 +799,8 @@ erp_status erp_eight_point_hypotheses_dev(erp_ctx* ctx, int32_t W, int32_t H,
                                           const erp_point2f* d_kl, const erp_point2f* d_kr,
                                           int32_t m, const erp_ransac_cfg* cfg,
                                           erp_hypothesis* d_hyps, void* stream) {
-    if (!ctx || W <= 0 || H <= 0 || m < 0 || m > 65535 || !d_hyps || !cfg_ok(cfg))
+    if (!ctx || W <= 0 || H <= 0 || m < 0 || m > 65535 || !d_hyps || !cfg_ok(cfg) ||
+        !sampler_m_ok(cfg, m))
         return ERP_INVALID_ARG;
     if (m > 0 && (!d_kl || !d_kr)) return ERP_INVALID_ARG;
     if ((int32_t)(m * cfg->sample_frac) < 1) return ERP_TOO_FEW_POINTS;
@@ -931,7 +941,8 @@ erp_status erp_eight_point_find(erp_ctx* ctx, int32_t W, int32_t H, const erp_po
 erp_status erp_initial_guess(erp_ctx* ctx, const double* h_bl, const double* h_br, int32_t m,
                              const erp_ransac_cfg* cfg, float R_out[3], float T_out[3],
                              erp_pair_result* h_result) {
-    if (!ctx || m < 0 || m > 65535 || (m > 0 && (!h_bl || !h_br)) || !cfg_ok(cfg))
+    if (!ctx || m < 0 || m > 65535 || (m > 0 && (!h_bl || !h_br)) || !cfg_ok(cfg) ||
+        !sampler_m_ok(cfg, m))
         return ERP_INVALID_ARG;
     erp_pair_result r;
     {

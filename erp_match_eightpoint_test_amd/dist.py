@@ -235,16 +235,43 @@ def gather_records(local, group=None):
     return out
 
 
+def min_idx_agrees(got: int, want: int, r1_valid=None, r2_valid=None) -> tuple[bool, bool]:
+    """(agrees, is_swap) for a consensus winner index `got` against the oracle's `want` in
+    R_vec_arr order (src/eight_point.cpp:113-126: R1 then R2 per iteration).  Equal indices
+    agree.  Indices one apart agree ONLY when both rows are the two rotations of one iteration
+    (R1 and R2 both valid there): the R1 / R2 order follows the sign of a noise-level singular
+    vector inside decomposeEssentialMat, so the push order of that iteration may
+    differ while the winning rotation is the same.  r1_valid / r2_valid: the oracle's
+    per-iteration validity flags (needed to map rows to iterations; without them a +-1 is a
+    mismatch)."""
+    got, want = int(got), int(want)
+    if got == want:
+        return True, False
+    if abs(got - want) != 1 or r1_valid is None or r2_valid is None:
+        return False, False
+    v1 = np.asarray(r1_valid).astype(bool)
+    v2 = np.asarray(r2_valid).astype(bool)
+    # row k belongs to the iteration whose [start, start + count) covers k
+    cnt = v1.astype(np.int64) + v2.astype(np.int64)
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]])
+    lo = min(got, want)
+    it = int(np.searchsorted(start, lo, side="right")) - 1
+    same = 0 <= it < len(cnt) and cnt[it] == 2 and start[it] == lo
+    return bool(same), bool(same)
+
+
 def check_gathered(gathered, per_rank: int, world: int, rerun_fn, oracle_fn=None) -> dict:
     """rank 0's self-check of the pair path's gathered records (outside the timed region):
     for every rank r, the first pair of r's block is recomputed on rank 0 alone
     (rerun_fn(r) -> 64-byte record as uint8[64]) and compared byte for byte with the record
     rank r contributed (gathered[r * per_rank]); with oracle_fn(r) -> the oracle's find() of
     that pair (dict with M, K, min_idx, R, T), the gathered record is also checked against the
-    CPU restatement (src/eight_point.cpp:152-192: K, min_idx equal, R / T within 2e-6)."""
+    CPU restatement (src/eight_point.cpp:152-192: K equal, min_idx equal by min_idx_agrees --
+    given the oracle's per-iteration validity flags o["hyp"] when present -- and R / T within
+    2e-6)."""
     from .capi import RESULT_DTYPE
     g = np.ascontiguousarray(np.asarray(gathered, np.uint8)).reshape(-1, RESULT_DTYPE.itemsize)
-    bad_bytes, bad_oracle = [], []
+    bad_bytes, bad_oracle, swaps = [], [], []
     for r in range(world):
         rec = g[r * per_rank]
         if not np.array_equal(np.asarray(rerun_fn(r), np.uint8).reshape(-1), rec):
@@ -252,8 +279,14 @@ def check_gathered(gathered, per_rank: int, world: int, rerun_fn, oracle_fn=None
         if oracle_fn is not None:
             o = oracle_fn(r)
             x = rec.view(RESULT_DTYPE)[0]
+            hy = o.get("hyp")
+            agree, swap = min_idx_agrees(x["min_idx"], o["min_idx"],
+                                         None if hy is None else hy["R1_valid"],
+                                         None if hy is None else hy["R2_valid"])
+            if swap:
+                swaps.append(r)
             ok = (int(x["status"]) == 0 and int(x["M"]) == int(o["M"]) and
-                  int(x["K"]) == int(o["K"]) and int(x["min_idx"]) == int(o["min_idx"]) and
+                  int(x["K"]) == int(o["K"]) and agree and
                   float(np.abs(x["R"] - o["R"]).max()) <= 2e-6 and
                   float(np.abs(x["T"] - o["T"]).max()) <= 2e-6)
             if not ok:
@@ -263,6 +296,7 @@ def check_gathered(gathered, per_rank: int, world: int, rerun_fn, oracle_fn=None
     if oracle_fn is not None:
         out["oracle_all_equal"] = not bad_oracle
         out["oracle_mismatched_ranks"] = bad_oracle
+        out["r1r2_order_swaps"] = swaps
     return out
 
 

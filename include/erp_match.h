@@ -117,7 +117,11 @@ typedef struct erp_pair_result {
     int32_t min_idx;     /* consensus winner in R_vec_arr order */
     int32_t sample_n;    /* (int)(M * sample_frac) */
     int32_t near_ties;   /* rows re-scored exactly by the near-tie resolver */
-    int32_t survivors;   /* rows whose trimmed-mean bounds did not exclude them */
+    int32_t survivors;   /* rows whose trimmed-mean bounds did not exclude them (a diagnostic:
+                            it depends on which pruning references ran, so a row-sharded
+                            consensus -- erp_consensus_hyps_shard/finish_dev -- may report a
+                            different count than the unsharded one; 1 <= survivors <= K, and
+                            <= binned_rows when that is reported) */
     int32_t binned_rows; /* rows whose K-column distance histogram was built (K, or the
                             reference rows + the rows Lipschitz pre-pruning kept) */
     double min_dist;     /* trimmed-mean distance of the winner */

@@ -512,6 +512,36 @@ def test_philox_hypothesis_blocks_by_offset(ctx, oracle):
     _check_hyps(full, o["hyp"])
 
 
+@pytest.mark.parametrize("m", [20480, 20481, 30000])
+def test_philox_match_cap_is_invalid_arg(ctx, m):
+    """the Philox sampler's per-lane bitmap holds M <= 20480: every host-m entry point refuses a
+    larger pair with ERP_INVALID_ARG up front (hypotheses_dev, find_dev, initial_guess) instead of
+    returning hypotheses built from empty samples; M = 20480 itself runs"""
+    import ctypes as C
+
+    import torch
+    from erp_match_eightpoint_test_amd import HYP_DTYPE, capi
+    rng = np.random.default_rng(m)
+    kl = torch.from_numpy(rng.uniform(0, 2000, (m, 2)).astype(np.float32)).cuda()
+    kr = torch.from_numpy(rng.uniform(0, 2000, (m, 2)).astype(np.float32)).cuda()
+    cfg = capi.default_cfg(iters=2, sampler=1)
+    hyps = torch.zeros((2, HYP_DTYPE.itemsize), dtype=torch.uint8, device="cuda")
+    res = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    want = capi.ERP_OK if m <= 20480 else capi.ERP_INVALID_ARG
+    assert ctx.L.erp_eight_point_hypotheses_dev(ctx.h, 2048, 1024, kl.data_ptr(), kr.data_ptr(),
+                                                m, C.byref(cfg), hyps.data_ptr(), st) == want
+    assert ctx.L.erp_eight_point_find_dev(ctx.h, 2048, 1024, kl.data_ptr(), kr.data_ptr(), m,
+                                          C.byref(cfg), res.data_ptr(), None, st) == want
+    torch.cuda.synchronize()
+    if m > 20480:
+        bl = np.zeros((m, 3))
+        bl[:, 2] = 1.0
+        out = capi.PairResult()
+        assert ctx.L.erp_initial_guess(ctx.h, bl.ctypes.data, bl.ctypes.data, m, C.byref(cfg),
+                                       None, None, C.byref(out)) == capi.ERP_INVALID_ARG
+
+
 # ---------------------------------------------------------- sharding entry points (GPU)
 def test_hypothesis_blocks_by_offset_match_full_run(ctx, oracle):
     """erp_eight_point_hypotheses_dev on iteration blocks [0,a) and [a,I) with the glibc offset
@@ -606,8 +636,12 @@ def test_consensus_row_shards_equal_unsharded(ctx, world, iters):
     for f in ("status", "K", "min_idx", "near_ties"):
         assert r[f] == ref[f], (f, r[f], ref[f])
     # (how many rows survive the selections depends on which references each shard prunes
-    # with -- a diagnostic, not part of the result)
-    assert r["survivors"] >= 1 and ref["survivors"] >= 1
+    # with -- a diagnostic, not part of the result; include/erp_match.h says so).  Bounded:
+    # a survivor is a binned row (pruned rows get LB > every UB), so 1 <= survivors <= binned
+    # rows <= K unsharded, and <= K sharded (binned_rows is -1 there: not combined over shards)
+    assert 1 <= ref["survivors"] <= ref["binned_rows"] <= ref["K"]
+    assert 1 <= r["survivors"] <= r["K"]
+    assert r["binned_rows"] == (-1 if world > 1 else ref["binned_rows"])
     assert np.array_equal(r["R"], R) and np.array_equal(r["T"], T)
     assert r["min_dist"] == ref["min_dist"]
 

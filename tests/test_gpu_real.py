@@ -180,6 +180,11 @@ def test_real_building2_matches_reference_output(api):
     assert rel < 1.5, rel
 
 
+# (rotation, T) gap bars in degrees against the reference's recovered estimate: the measured
+# gaps of this deterministic pipeline (profiles/r04_real_gaps.json) plus a stated margin
+GAP_BARS = {"building": (1.5, 20.0), "building2": (1.5, 20.0)}
+
+
 @pytest.mark.parametrize("pair,left,right", [
     ("building", "left_building.jpg", "right_building.jpg"),
     ("building2", "left_building2_2048.jpg", "right_building2_2048.jpg")])
@@ -199,7 +204,17 @@ def test_real_estimate_vs_recovered_reference(api, pair, left, right):
     print(f"\n{pair}: ours R={np.degrees(R)} deg T={T}; reference (recovered) "
           f"R={np.degrees(ref['R_vec'])} deg T={np.asarray(ref['T_vec'])}; rotation gap "
           f"{dR:.3f} deg, T gap {dT:.2f} deg (M={M})")
-    assert dR < 1.5, dR
+    out = os.environ.get("ERP_REAL_GAPS_OUT")
+    if out:  # the round's artifact run records the gaps (profiles/r04_real_gaps.json)
+        rec = json.load(open(out)) if os.path.exists(out) else {}
+        rec[pair] = {"rotation_gap_deg": dR, "T_gap_deg": dT, "M": int(M),
+                     "K": int(ep.last_result["K"]), "R_ours": [float(x) for x in R],
+                     "T_ours": [float(x) for x in T], "R_ref": list(map(float, ref["R_vec"])),
+                     "T_ref": list(map(float, ref["T_vec"])),
+                     "bar_rotation_deg": GAP_BARS[pair][0], "bar_T_deg": GAP_BARS[pair][1]}
+        json.dump(rec, open(out, "w"), indent=1)
+    assert dR < GAP_BARS[pair][0], dR
+    assert dT < GAP_BARS[pair][1], dT
 
 
 def test_real_building_matches_reference_output(api):
