@@ -40,12 +40,13 @@ class Point2f(C.Structure):
 class RansacCfg(C.Structure):
     _fields_ = [("iters", C.c_int32), ("sampler", C.c_int32), ("sample_frac", C.c_double),
                 ("trim_lo", C.c_double), ("trim_hi", C.c_double), ("valid_abs", C.c_double),
-                ("seed", C.c_uint32), ("reserved", C.c_uint32), ("offset", C.c_uint64)]
+                ("seed", C.c_uint32), ("inlier_thr", C.c_float), ("offset", C.c_uint64)]
 
 
 class Hypothesis(C.Structure):
     _fields_ = [("R1", C.c_float * 3), ("R2", C.c_float * 3), ("T", C.c_float * 3),
-                ("R1_valid", C.c_int32), ("R2_valid", C.c_int32), ("E", C.c_double * 9)]
+                ("R1_valid", C.c_int32), ("R2_valid", C.c_int32), ("inliers", C.c_int32),
+                ("E", C.c_double * 9)]
 
 
 class PairResult(C.Structure):
@@ -69,7 +70,7 @@ class BatchOutputs(C.Structure):
 DMATCH_DTYPE = np.dtype([("queryIdx", "<i4"), ("trainIdx", "<i4"), ("imgIdx", "<i4"),
                          ("distance", "<f4")])
 HYP_DTYPE = np.dtype([("R1", "<f4", 3), ("R2", "<f4", 3), ("T", "<f4", 3), ("R1_valid", "<i4"),
-                      ("R2_valid", "<i4"), ("E", "<f8", 9)], align=True)
+                      ("R2_valid", "<i4"), ("inliers", "<i4"), ("E", "<f8", 9)], align=True)
 RESULT_DTYPE = np.dtype([("R", "<f4", 3), ("T", "<f4", 3), ("status", "<i4"), ("M", "<i4"),
                          ("K", "<i4"), ("min_idx", "<i4"), ("sample_n", "<i4"),
                          ("near_ties", "<i4"), ("survivors", "<i4"), ("binned_rows", "<i4"),
@@ -96,7 +97,7 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
-          "consensus_refine", "knn2_exact", "sampler_gram"]
+          "consensus_refine", "knn2_exact", "sampler_gram", "inliers"]
 MATCHER_MFMA_FILTER = 0  # erp_matcher_method
 MATCHER_VALU_EXACT = 1
 

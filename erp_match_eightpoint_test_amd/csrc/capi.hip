@@ -94,7 +94,7 @@ struct erp_ctx {
     DevBuf zsel;              // consensus zoom: the survivors' rank-window bins (level 1 grid)
     DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
-        rtab, limbs, tsplit, ovf, remap_scr, vchunk, lipref;
+        rtab, limbs, tsplit, ovf, remap_scr, vchunk, lipref, inl;
     DevBuf extra[13];         // erp_ctx_scratch_internal slots (1-11 SURF, 12 viz)
     uint64_t surf_key = 0;    // (W, H, params) of the SURF layer table in extra[1]
     uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
@@ -278,7 +278,7 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
                      &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins,
                      &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf, &ctx->remap_scr, &ctx->vchunk,
-                     &ctx->lipref};
+                     &ctx->lipref, &ctx->inl};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (DevBuf& b : ctx->extra)
@@ -435,7 +435,7 @@ bool cfg_ok(const erp_ransac_cfg* cfg) {
            (cfg->sampler == ERP_SAMPLER_GLIBC || cfg->sampler == ERP_SAMPLER_PHILOX) &&
            cfg->sample_frac > 0 &&
            cfg->sample_frac <= 1.0 && cfg->trim_lo >= 0 && cfg->trim_hi <= 1.0 &&
-           cfg->trim_lo <= cfg->trim_hi;
+           cfg->trim_lo <= cfg->trim_hi && cfg->inlier_thr >= 0.0f && cfg->inlier_thr < 1e30f;
 }
 
 // the Philox sampler's per-lane LDS bitmap holds M <= 20480 positions (kernels.hip
@@ -444,6 +444,22 @@ bool cfg_ok(const erp_ransac_cfg* cfg) {
 constexpr int32_t kPhiloxMaxM = 20480;
 bool sampler_m_ok(const erp_ransac_cfg* cfg, int32_t m) {
     return cfg->sampler != ERP_SAMPLER_PHILOX || m <= kPhiloxMaxM;
+}
+
+// the records' E: written when the caller asked for the records or the inlier count reads it
+bool want_e(const erp_ransac_cfg* cfg, const erp_batch_outputs* out) {
+    return !ERP_SKIP_E || (out && out->hyps) || cfg->inlier_thr > 0.0f;
+}
+
+// the opt-in inlier count after the estimate (cfg->inlier_thr > 0; nothing runs otherwise)
+erp_status run_inliers(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
+                       erp_hypothesis* hyps, hipStream_t st) {
+    if (!(cfg->inlier_thr > 0.0f)) return ERP_OK;
+    if (!ensure(c->inl, erp::inlier_scratch_bytes(sh))) return ERP_OUT_OF_MEMORY;
+    StageTimer _t(c, ERP_STAGE_INLIERS, st);
+    ERP_CK(erp::launch_inliers((int32_t*)c->counts.p, (double*)c->pts.p, sh, cfg->sample_frac,
+                               cfg->inlier_thr, c->inl.p, hyps, st));
+    return ERP_OK;
 }
 
 // estimator stages after counts/pts are in place
@@ -467,11 +483,13 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
                                          ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr,
                                          ERP_FUSE_EIGEN == 2 ? hyps : nullptr, cfg->valid_abs, st));
         }
-        StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
-        ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac, cfg->valid_abs,
-                                 (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
-                                 ERP_SKIP_E ? (out && out->hyps) : true));
-        return ERP_OK;
+        {
+            StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
+            ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
+                                     cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
+                                     want_e(cfg, out)));
+        }
+        return run_inliers(c, sh, cfg, hyps, st);
     }
     {
         StageTimer _t(ctx, ERP_STAGE_JUMP_PREP, st);
@@ -513,9 +531,9 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
         ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
                                  cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
-                                 ERP_SKIP_E ? (out && out->hyps) : true));
+                                 want_e(cfg, out)));
     }
-    return ERP_OK;
+    return run_inliers(c, sh, cfg, hyps, st);
 }
 
 // consensus stages after the hypothesis records are in place (counts may be null when the
@@ -643,7 +661,7 @@ const char* erp_stage_name(int32_t stage) {
         "knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler",
         "eigen", "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
         "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
-        "consensus_refine", "knn2_exact", "sampler_gram"};
+        "consensus_refine", "knn2_exact", "sampler_gram", "inliers"};
     return (stage >= 0 && stage < ERP_STAGE_COUNT) ? names[stage] : "unknown";
 }
 

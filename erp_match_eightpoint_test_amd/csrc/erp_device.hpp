@@ -459,14 +459,31 @@ ERP_HD ERP_INLINE double max_vec(const float* v) {
 // Rank-2 correction, decomposition, Euler conversion and validity
 // (src/eight_point.cpp:42-84).  e: 9-vector (E row-major, sign irrelevant: every step below is
 // odd in E and decomposeEssentialMat's det fixes cancel the sign exactly).
-ERP_HD inline void estimate_from_e(const double* e, double valid_abs, Hyp& h) {
+// E_mat_correct (src/eight_point.cpp:45-50): SVDecomp of the 3x3 E, w_f[2] = 0,
+// u_f * diag(w_f) * vt_f
+ERP_HD inline void rank2_correct(const double* e, double* Ec) {
     double wf[3], uf[9], vtf[9];
     svd3_opencv(e, wf, uf, vtf);
     wf[2] = 0.0;
     const double wd[9] = {wf[0], 0, 0, 0, wf[1], 0, 0, 0, wf[2]};
-    double tmp[9], Ec[9];
+    double tmp[9];
     gemm33(uf, wd, tmp);
     gemm33(tmp, vtf, Ec);
+}
+
+// The opt-in inlier residual (erp_ransac_cfg.inlier_thr; no reference counterpart):
+// res = l^T Ec r in a fixed fp64 order, u_k = l_i r_j (k = 3i + j), res = Ec_0 u_0, then
+// res = fma(Ec_k, u_k, res), k = 1..8 (oracle/erp_oracle.c erpo_inlier_count: the same order)
+ERP_HD ERP_INLINE double inlier_residual(const double* Ec, const double* l, const double* r) {
+    double res = Ec[0] * (l[0] * r[0]);
+#pragma unroll
+    for (int k = 1; k < 9; k++) res = fma(Ec[k], l[k / 3] * r[k % 3], res);
+    return res;
+}
+
+ERP_HD inline void estimate_from_e(const double* e, double valid_abs, Hyp& h) {
+    double Ec[9];
+    rank2_correct(e, Ec);
     double R1[9], R2[9], t[3];
     decompose_e(Ec, R1, R2, t);
     double e1[3], e2[3];

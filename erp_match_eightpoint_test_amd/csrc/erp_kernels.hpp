@@ -145,6 +145,13 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
                         hipStream_t st, int fused = 0, bool want_e = true);
 // (want_e = false: estimate_kernel leaves the records' E unwritten -- the batch pipeline when the
 // caller did not ask for the hypothesis records; nothing downstream reads E)
+// the opt-in inlier count (cfg.inlier_thr > 0): every iteration's matches with
+// |l^T E' r| < thr into hyps[p][iters].inliers (the records' E must be written); scratch of
+// inlier_scratch_bytes(sh)
+size_t inlier_scratch_bytes(const BatchShape& sh);
+hipError_t launch_inliers(const int32_t* counts, const double* pts, const BatchShape& sh,
+                          double sample_frac, float thr, void* scratch, erp_hypothesis* hyps,
+                          hipStream_t st);
 // R_vec_arr / T_vec_arr in push order + K + bounding-box scale; vchunk = scratch of
 // valid_chunk_bytes(sh) (per 1024-iteration chunk: count and bounding box)
 size_t valid_chunk_bytes(const BatchShape& sh);

@@ -797,6 +797,7 @@ __device__ __forceinline__ void estimate_store(const double* e, double valid_abs
     }
     o->R1_valid = hy.R1_valid;
     o->R2_valid = hy.R2_valid;
+    o->inliers = 0;  // (the opt-in inlier_count_kernel overwrites it)
     if (!with_e) return;  // E is only read when the caller asked for the records
 #pragma unroll
     for (int k = 0; k < 9; k++) o->E[k] = hy.E[k];
@@ -1582,6 +1583,125 @@ __global__ __launch_bounds__(1024) void valid_scatter_kernel(const int32_t* __re
         }
         pos++;
     }
+}
+
+// ============================================== opt-in inlier count (cfg.inlier_thr > 0) ===
+// No reference counterpart (src/eight_point.cpp:99-127 keeps no score): for every
+// iteration, the matches among ALL M with |l^T E' r| < thr, E' = E_mat_correct of that
+// iteration (:45-50), fp64 in the fixed order of inlier_residual (erp_device.hpp).  Work per
+// pair: M x iters residuals (~2.7e7 at configs[1]), so the count runs in f32 and only the band
+// the f32 evaluation cannot decide is redone exactly:
+//   |res32 - res64| <= (9 + 4 + 1) 2^-24 sum_k |E'_k| |u_k| <= 14 2^-24 ||E'||_F |l| |r|
+//                   ~= 8.4e-7   (9 roundings of the FMA chain, 3 of u = fl(fl(l) fl(r)), 1 of
+//                                fl(E'); ||E'||_F <= ||e|| = 1 and |l| = |r| = 1 up to ulps),
+// so with d = 2^-19 (~1.9e-6, twice that plus the rounding of thr -+ d to f32) |res32| < thr - d
+// is an inlier, |res32| >= thr + d is not, and the rest is recomputed in fp64.
+constexpr float kInlierBand = 0x1p-19f;
+constexpr int kInlierChunk = 256;  // matches per pass of a wave (4 per lane)
+
+// E' of every iteration from its record's e (rank2_correct: the estimate's own operations) ->
+// ec64 [p][iters][9] (the exact path) and its f32 image ec32 [p][iters][16]
+__global__ __launch_bounds__(64) void inlier_prep_kernel(const int32_t* __restrict__ counts,
+                                                         const erp_hypothesis* __restrict__ hyps,
+                                                         int iters, double sample_frac,
+                                                         double* __restrict__ ec64,
+                                                         float* __restrict__ ec32) {
+    const int p = blockIdx.y, h = blockIdx.x * 64 + threadIdx.x;
+    if ((int)(counts[p] * sample_frac) < 1 || h >= iters) return;
+    const erp_hypothesis* hy = hyps + (size_t)p * iters + h;
+    double e[9], Ec[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) e[k] = hy->E[k];
+    rank2_correct(e, Ec);
+    double* o = ec64 + ((size_t)p * iters + h) * 9;
+    float* f = ec32 + ((size_t)p * iters + h) * 16;
+#pragma unroll
+    for (int k = 0; k < 9; k++) {
+        o[k] = Ec[k];
+        f[k] = (float)Ec[k];
+    }
+}
+
+// u = fl(l) (x) fl(r) per match as f32, SoA [p][9][mpad]; rows >= M are NaN (never counted)
+__global__ __launch_bounds__(256) void inlier_points_kernel(const int32_t* __restrict__ counts,
+                                                            const double* __restrict__ pts,
+                                                            int max_nq, int mpad,
+                                                            float* __restrict__ u32) {
+    const int p = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= mpad) return;
+    float* o = u32 + (size_t)p * 9 * mpad + i;
+    if (i >= counts[p]) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) o[(size_t)k * mpad] = __builtin_nanf("");
+        return;
+    }
+    const double* q = pts + ((size_t)p * (max_nq + 1) + i) * 6;
+    const float l[3] = {(float)q[0], (float)q[1], (float)q[2]};
+    const float r[3] = {(float)q[3], (float)q[4], (float)q[5]};
+#pragma unroll
+    for (int k = 0; k < 9; k++) o[(size_t)k * mpad] = l[k / 3] * r[k % 3];
+}
+
+// One wave per 64 iterations of a pair.  The wave holds 256 matches in VGPRs (u: 4 per lane)
+// and runs its iterations over them with E' wave-uniform (scalar loads): 9 f32 FMAs per
+// (match, iteration), the wave-reduced count popcount(ballot(|res| < thr - d)) on the SALU, the
+// band [thr - d, thr + d) recomputed in fp64 by its lanes.  Iteration h's count accumulates in
+// lane h of `acc`, written into the record once at the end.
+__global__ __launch_bounds__(64) void inlier_count_kernel(
+    const int32_t* __restrict__ counts, const float* __restrict__ u32,
+    const float* __restrict__ ec32, const double* __restrict__ ec64,
+    const double* __restrict__ pts, int max_nq, int mpad, int iters, double sample_frac,
+    float thr_lo, float thr_hi, double thr, erp_hypothesis* __restrict__ hyps) {
+    const int p = blockIdx.y, lane = threadIdx.x, h0 = blockIdx.x * 64;
+    const int M = counts[p];
+    if ((int)(M * sample_frac) < 1) return;
+    const int nh = min(64, iters - h0);
+    const float* U = u32 + (size_t)p * 9 * mpad;
+    const float* E32 = ec32 + ((size_t)p * iters + h0) * 16;
+    int acc = 0;
+    for (int c0 = 0; c0 < M; c0 += kInlierChunk) {
+        float u[4][9];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int k = 0; k < 9; k++) u[q][k] = U[(size_t)k * mpad + c0 + q * 64 + lane];
+        for (int h = 0; h < nh; h++) {
+            const float* e = E32 + h * 16;
+            float ev[9];
+#pragma unroll
+            for (int k = 0; k < 9; k++) ev[k] = e[k];
+            int cnt = 0;
+            uint64_t amb_any = 0;
+            bool amb[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                float res = ev[0] * u[q][0];
+#pragma unroll
+                for (int k = 1; k < 9; k++) res = fmaf(ev[k], u[q][k], res);
+                const float a = fabsf(res);
+                const uint64_t in = __ballot(a < thr_lo);
+                const uint64_t below_hi = __ballot(a < thr_hi);
+                cnt += __popcll(in);
+                amb[q] = ((below_hi & ~in) >> lane) & 1;
+                amb_any |= below_hi & ~in;
+            }
+            if (amb_any) {  // rare: the matches the f32 value cannot decide, exactly
+                const double* E64 = ec64 + ((size_t)p * iters + h0 + h) * 9;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    bool ex = false;
+                    if (amb[q]) {
+                        const double* b =
+                            pts + ((size_t)p * (max_nq + 1) + c0 + q * 64 + lane) * 6;
+                        ex = fabs(inlier_residual(E64, b, b + 3)) < thr;
+                    }
+                    cnt += __popcll(__ballot(ex));
+                }
+            }
+            acc = lane == h ? acc + cnt : acc;
+        }
+    }
+    if (lane < nh) hyps[(size_t)p * iters + h0 + lane].inliers = acc;
 }
 
 // ================================================================= consensus ============
@@ -3804,6 +3924,34 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
     if (fused != 2)
         hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
                            sample_frac, valid_abs, hyps, (int)want_e);
+    return hipGetLastError();
+}
+
+size_t inlier_scratch_bytes(const BatchShape& sh) {
+    const size_t P = sh.n_pairs, I = sh.iters;
+    const size_t mpad = (size_t)(sh.max_nq + kInlierChunk - 1) / kInlierChunk * kInlierChunk;
+    return P * I * 9 * 8 + P * I * 16 * 4 + P * 9 * mpad * 4;
+}
+
+hipError_t launch_inliers(const int32_t* counts, const double* pts, const BatchShape& sh,
+                          double sample_frac, float thr, void* scratch, erp_hypothesis* hyps,
+                          hipStream_t st) {
+    const size_t P = sh.n_pairs, I = sh.iters;
+    const int mpad = (sh.max_nq + kInlierChunk - 1) / kInlierChunk * kInlierChunk;
+    double* ec64 = (double*)scratch;
+    float* ec32 = (float*)(ec64 + P * I * 9);
+    float* u32 = ec32 + P * I * 16;
+    const double t = (double)thr, d = (double)kInlierBand;
+    const float lo = t > d ? (float)(t - d) : 0.0f;  // (|res32| < 0 never holds)
+    const float hi = (float)(t + d);
+    const dim3 g((sh.iters + 63) / 64, sh.n_pairs);
+    hipLaunchKernelGGL(inlier_prep_kernel, g, dim3(64), 0, st, counts, (const erp_hypothesis*)hyps,
+                       sh.iters, sample_frac, ec64, ec32);
+    hipLaunchKernelGGL(inlier_points_kernel, dim3(mpad / 256, sh.n_pairs), dim3(256), 0, st, counts,
+                       pts, sh.max_nq, mpad, u32);
+    hipLaunchKernelGGL(inlier_count_kernel, g, dim3(64), 0, st, counts, (const float*)u32,
+                       (const float*)ec32, (const double*)ec64, pts, sh.max_nq, mpad, sh.iters,
+                       sample_frac, lo, hi, t, hyps);
     return hipGetLastError();
 }
 

@@ -93,7 +93,17 @@ typedef struct erp_ransac_cfg {
     double trim_hi;      /* 0.8  :143 */
     double valid_abs;    /* 1.57 :76,81 */
     uint32_t seed;       /* 1: the reference never calls srand() */
-    uint32_t reserved;
+    float inlier_thr;    /* 0 (default) = off: nothing below changes.  > 0: every iteration also
+                            counts its inliers, the correspondences with |l^T E' r| < inlier_thr
+                            (l, r the unit bearings of a match, E' = E_mat_correct of that
+                            iteration, src/eight_point.cpp:46-50: the rank-2 correction of the
+                            unit-norm solved e), into erp_hypothesis.inliers (the winner's count:
+                            the record of the iteration that pushed row min_idx).  No reference
+                            counterpart (its loop, :99-127, keeps no score): the opt-in
+                            "inlier count" of SURVEY.md F2.  Exact definition (fp64, fixed
+                            order): u_k = l_i * r_j (k = 3i + j), res = E'_0 u_0, then
+                            res = fma(E'_k, u_k, res) for k = 1..8; inlier iff |res| < thr
+                            (oracle/erp_oracle.c erpo_inlier_count). */
     uint64_t offset;     /* rand() calls consumed before initial_guess (e.g. by FLANN) */
 } erp_ransac_cfg;
 
@@ -104,6 +114,7 @@ typedef struct erp_hypothesis {
     float T[3];
     int32_t R1_valid;
     int32_t R2_valid;
+    int32_t inliers;     /* matches with |l^T E' r| < cfg.inlier_thr (erp_ransac_cfg); 0 when off */
     double E[9];
 } erp_hypothesis;
 
@@ -193,7 +204,8 @@ typedef enum erp_stage {
     ERP_STAGE_CONSENSUS_REFINE = 15, /* tighter bounds for the survivors (sub-bins) */
     ERP_STAGE_KNN2_EXACT = 16,      /* exact sweep on packed FP32 VALU (ERP_MATCHER_VALU_EXACT) */
     ERP_STAGE_SAMPLER_GRAM = 17,    /* the sampler replay and the Gram MFMAs in one kernel */
-    ERP_STAGE_COUNT = 18
+    ERP_STAGE_INLIERS = 18,         /* opt-in per-iteration inlier count (cfg.inlier_thr > 0) */
+    ERP_STAGE_COUNT = 19
 } erp_stage;
 erp_status erp_ctx_set_profiling(erp_ctx* ctx, int32_t enable);
 const char* erp_stage_name(int32_t stage);

@@ -31,19 +31,20 @@ class Glibc(C.Structure):
 
 class Hyp(C.Structure):
     _fields_ = [("R1", C.c_float * 3), ("R2", C.c_float * 3), ("T", C.c_float * 3),
-                ("R1_valid", C.c_int32), ("R2_valid", C.c_int32), ("E", C.c_double * 9),
-                ("E_corr", C.c_double * 9)]
+                ("R1_valid", C.c_int32), ("R2_valid", C.c_int32), ("inliers", C.c_int32),
+                ("E", C.c_double * 9), ("E_corr", C.c_double * 9)]
 
 
 HYP_DTYPE = np.dtype([("R1", "<f4", 3), ("R2", "<f4", 3), ("T", "<f4", 3), ("R1_valid", "<i4"),
-                      ("R2_valid", "<i4"), ("E", "<f8", 9), ("E_corr", "<f8", 9)], align=True)
+                      ("R2_valid", "<i4"), ("inliers", "<i4"), ("E", "<f8", 9),
+                      ("E_corr", "<f8", 9)], align=True)
 assert HYP_DTYPE.itemsize == C.sizeof(Hyp)
 
 
 class Cfg(C.Structure):
     _fields_ = [("iters", C.c_int32), ("sample_frac", C.c_double), ("trim_lo", C.c_double),
                 ("trim_hi", C.c_double), ("valid_abs", C.c_double), ("seed", C.c_uint32),
-                ("offset", C.c_uint64), ("sampler", C.c_int32)]
+                ("offset", C.c_uint64), ("sampler", C.c_int32), ("inlier_thr", C.c_double)]
 
 
 class Diag(C.Structure):
@@ -96,6 +97,11 @@ def lib():
         L.erpo_pixel_to_bearing.argtypes = [C.c_int32, C.c_int32, C.c_float, C.c_float, P]
         L.erpo_svdecomp.argtypes = [P, C.c_int32, C.c_int32, P, P, P]
         L.erpo_svdecomp.restype = C.c_int
+        L.erpo_rank2.argtypes = [P, P]
+        L.erpo_rank2.restype = None
+        L.erpo_inlier_count.argtypes = [P, P, C.c_int32, P, C.c_double, C.c_double,
+                                        C.POINTER(C.c_int32)]
+        L.erpo_inlier_count.restype = C.c_int32
         L.erpo_eight_point_estimation.argtypes = [P, P, C.c_int32, C.POINTER(Hyp)]
         L.erpo_eight_point_estimation.restype = C.c_int
         L.erpo_consensus.argtypes = [P, C.c_int32, C.c_double, C.c_double, C.POINTER(C.c_int32), P]
@@ -144,10 +150,32 @@ def _p(a):
 
 
 def make_cfg(iters=80, sample_frac=0.25, trim_lo=0.2, trim_hi=0.8, valid_abs=1.57, seed=1,
-             offset=0, sampler=0) -> Cfg:
+             offset=0, sampler=0, inlier_thr=0.0) -> Cfg:
     """Reference defaults: src/eight_point.cpp:99 (80), :102 (0.25), :143 (0.2/0.8), :76 (1.57).
-    sampler 1: the counter-based Philox sampler (no reference counterpart; erp_oracle.c)."""
-    return Cfg(iters, sample_frac, trim_lo, trim_hi, valid_abs, seed, offset, sampler)
+    sampler 1: the counter-based Philox sampler (no reference counterpart; erp_oracle.c);
+    inlier_thr > 0: every iteration's inlier count into hyp["inliers"] (no counterpart)."""
+    return Cfg(iters, sample_frac, trim_lo, trim_hi, valid_abs, seed, offset, sampler,
+               float(inlier_thr))
+
+
+def rank2(e) -> np.ndarray:
+    """E_mat_correct of a solved 9-vector (src/eight_point.cpp:45-50) -> 9 doubles"""
+    e = np.ascontiguousarray(e, np.float64).reshape(9)
+    Ec = np.zeros(9, np.float64)
+    lib().erpo_rank2(_p(e), _p(Ec))
+    return Ec
+
+
+def inlier_count(bl, br, Ec, thr: float, band: float = 0.0):
+    """(count of |l^T Ec r| < thr in erp_match.h's fixed fp64 order, matches within `band` of
+    the threshold)"""
+    bl = np.ascontiguousarray(bl, np.float64).reshape(-1, 3)
+    br = np.ascontiguousarray(br, np.float64).reshape(-1, 3)
+    Ec = np.ascontiguousarray(Ec, np.float64).reshape(9)
+    nb = C.c_int32(0)
+    n = lib().erpo_inlier_count(_p(bl), _p(br), bl.shape[0], _p(Ec), float(thr), float(band),
+                                C.byref(nb))
+    return int(n), int(nb.value)
 
 
 def philox4x32(ctr, key) -> np.ndarray:

@@ -492,6 +492,33 @@ static double max_vec(const float* v) {
         return v[2];
 }
 
+void erpo_rank2(const double e[9], double Ec[9]) {
+    double wf[3], uf[9], vtf[9];
+    erpo_svdecomp(e, 3, 3, wf, uf, vtf); /* (:46) */
+    wf[2] = 0.0;                          /* w_f.at<double>(0,2) = 0 (:47) */
+    const double wd[9] = {wf[0], 0, 0, 0, wf[1], 0, 0, 0, wf[2]};
+    double tmp[9];
+    gemm33(uf, wd, tmp);
+    gemm33(tmp, vtf, Ec); /* E_mat_correct = u_f * w_f_diag * vt_f (:50) */
+}
+
+/* the opt-in inlier count (no reference counterpart; erp_match.h erp_ransac_cfg.inlier_thr) */
+int32_t erpo_inlier_count(const double* bl, const double* br, int32_t m, const double Ec[9],
+                          double thr, double band, int32_t* n_band) {
+    int32_t n = 0, nb = 0;
+    for (int32_t i = 0; i < m; i++) {
+        const double* l = bl + (size_t)i * 3;
+        const double* r = br + (size_t)i * 3;
+        double res = Ec[0] * (l[0] * r[0]);
+        for (int k = 1; k < 9; k++) res = fma(Ec[k], l[k / 3] * r[k % 3], res);
+        const double a = fabs(res);
+        n += a < thr;
+        nb += fabs(a - thr) <= band;
+    }
+    if (n_band) *n_band = nb;
+    return n;
+}
+
 static int eight_point_estimation_impl(const double* bl, const double* br, int32_t m, double valid_abs,
                                        erpo_hyp* h) {
     if (m < 1) return -2;
@@ -522,13 +549,8 @@ static int eight_point_estimation_impl(const double* bl, const double* br, int32
     free(vt);
     free(u);
 
-    double wf[3], uf[9], vtf[9];
-    erpo_svdecomp(E, 3, 3, wf, uf, vtf); /* (:46) */
-    wf[2] = 0.0;                          /* w_f.at<double>(0,2) = 0 (:47) */
-    const double wd[9] = {wf[0], 0, 0, 0, wf[1], 0, 0, 0, wf[2]};
-    double tmp[9], Ec[9];
-    gemm33(uf, wd, tmp);
-    gemm33(tmp, vtf, Ec); /* E_mat_correct = u_f * w_f_diag * vt_f (:50) */
+    double Ec[9];
+    erpo_rank2(E, Ec);
 
     double R1[9], R2[9], t[3];
     decompose_essential(Ec, R1, R2, t); /* (:54) */
@@ -645,6 +667,10 @@ int erpo_initial_guess(const double* bl, const double* br, int32_t m, const erpo
                 memcpy(sr + (size_t)k * 3, br + (size_t)p * 3, 3 * sizeof(double));
             }
             eight_point_estimation_impl(sl, sr, sample_n, cfg->valid_abs, &hs[it]);
+            hs[it].inliers = cfg->inlier_thr > 0
+                                 ? erpo_inlier_count(bl, br, m, hs[it].E_corr, cfg->inlier_thr,
+                                                     0.0, NULL)
+                                 : 0;
         }
         free(sl);
         free(sr);

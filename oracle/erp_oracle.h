@@ -138,6 +138,7 @@ int erpo_svdecomp(const double* src, int32_t m, int32_t n, double* w, double* u,
 typedef struct {
     float R1[3], R2[3], T[3];
     int32_t R1_valid, R2_valid;
+    int32_t inliers;    /* erpo_inlier_count of E_corr at cfg->inlier_thr (0 when off) */
     double E[9];        /* e = last row of vt, reshaped row-major */
     double E_corr[9];   /* u * diag(w0,w1,0) * vt */
 } erpo_hyp;
@@ -156,7 +157,18 @@ typedef struct {
     uint64_t offset;      /* rand() calls consumed before initial_guess (e.g. by FLANN);
                              sampler 1: the first iteration's counter */
     int32_t sampler;      /* 0: glibc replay (the reference), 1: Philox4x32-10 + Floyd */
+    double inlier_thr;    /* > 0: every iteration's erpo_inlier_count (no reference counterpart) */
 } erpo_cfg;
+
+/* E_mat_correct (src/eight_point.cpp:45-50) of a solved 9-vector e: SVDecomp of the 3x3,
+ * w_f[2] = 0, u_f * diag(w_f) * vt_f */
+void erpo_rank2(const double e[9], double Ec[9]);
+/* The opt-in inlier count (erp_ransac_cfg.inlier_thr; no reference counterpart): matches i
+ * with |res_i| < thr, res_i = Ec_0 u_0 then fma(Ec_k, u_k, res) for k = 1..8, u_k = l_i*r_j
+ * (k = 3i + j) in fp64.  *n_band (optional): matches with ||res_i| - thr| <= band (the ones a
+ * differently rounded Ec could flip). */
+int32_t erpo_inlier_count(const double* bl, const double* br, int32_t m, const double Ec[9],
+                          double thr, double band, int32_t* n_band);
 
 typedef struct {
     int32_t K;            /* valid R vectors */

@@ -542,6 +542,58 @@ def test_philox_match_cap_is_invalid_arg(ctx, m):
                                        None, None, C.byref(out)) == capi.ERP_INVALID_ARG
 
 
+# ------------------------------------------------- opt-in inlier count (cfg.inlier_thr > 0)
+@pytest.mark.parametrize("sizes,iters,thr,sampler", [([512, 700, 300], 80, 1e-3, 0),
+                                                     ([512, 700, 300], 80, 2e-2, 0),
+                                                     ([4096], 10000, 5e-3, 0),
+                                                     ([1024, 900], 500, 5e-3, 1)])
+def test_inlier_count_vs_oracle(gpu_lib, oracle, sizes, iters, thr, sampler):
+    """erp_ransac_cfg.inlier_thr > 0 (no reference counterpart): every iteration's
+    count of |l^T E' r| < thr over ALL M matches equals the oracle's fp64 count evaluated on the
+    GPU record's own E (erpo_rank2 + erpo_inlier_count: exact, up to the matches within 1e-12 of
+    the threshold), and the oracle find's own count within the matches a 1e-9 change of E' could
+    flip (80 / 500 iterations); the result records equal the run with the count off, whose
+    records carry 0 (the default path is unchanged)."""
+    import torch
+    from erp_match_eightpoint_test_amd import (Context, PairBatchRunner, hyps_to_numpy,
+                                               results_to_numpy)
+    pairs = [synth.make_pair(7300 + i, n_kpts=n) for i, n in enumerate(sizes)]
+    args = _batch(pairs)
+    c = Context(0)
+    on = PairBatchRunner(ctx=c, iters=iters, sampler=sampler, inlier_thr=thr).run(
+        *args, want=("matches", "hyps"))
+    off = PairBatchRunner(ctx=c, iters=iters, sampler=sampler).run(*args, want=("hyps",))
+    torch.cuda.synchronize()
+    r_on, r_off = results_to_numpy(on["results"]), results_to_numpy(off["results"])
+    assert np.array_equal(r_on.view(np.uint8), r_off.view(np.uint8))
+    h_on, h_off = hyps_to_numpy(on["hyps"]), hyps_to_numpy(off["hyps"])
+    assert (h_off["inliers"] == 0).all()
+    for f in ("R1", "R2", "T", "R1_valid", "R2_valid", "E"):
+        assert np.array_equal(h_on[f], h_off[f]), f
+    for i, p in enumerate(pairs):
+        assert r_on[i]["status"] == 0
+        M = int(r_on[i]["M"])
+        mt = on["matches"][i, :M].cpu().numpy()
+        bl = oracle.pixel_to_bearing(p["W"], p["H"], p["kp_l"][mt[:, 0]])
+        br = oracle.pixel_to_bearing(p["W"], p["H"], p["kp_r"][mt[:, 1]])
+        got = h_on[i]["inliers"]
+        assert got.max() > 0 and (got <= M).all()
+        for it in range(iters):
+            n, nb = oracle.inlier_count(bl, br, oracle.rank2(h_on[i][it]["E"]), thr, 1e-12)
+            assert abs(int(got[it]) - n) <= nb, (i, it, int(got[it]), n, nb)
+        if iters <= 500:
+            o = oracle.find(p["W"], p["H"], p["kp_l"][mt[:, 0]], p["kp_r"][mt[:, 1]],
+                            oracle.make_cfg(iters=iters, sampler=sampler, inlier_thr=thr),
+                            detail=True)
+            for it in range(iters):
+                _, nb = oracle.inlier_count(bl, br, o["hyp"][it]["E_corr"], thr, 1e-9)
+                assert abs(int(got[it]) - int(o["hyp"][it]["inliers"])) <= nb, (i, it)
+            # the consensus winner's count: the iteration that pushed row min_idx
+            v = h_on[i]["R1_valid"].astype(int) + h_on[i]["R2_valid"].astype(int)
+            w_it = int(np.searchsorted(np.cumsum(v), int(r_on[i]["min_idx"]), side="right"))
+            assert got[w_it] >= np.median(got), (got[w_it], np.median(got))
+
+
 # ---------------------------------------------------------- sharding entry points (GPU)
 def test_hypothesis_blocks_by_offset_match_full_run(ctx, oracle):
     """erp_eight_point_hypotheses_dev on iteration blocks [0,a) and [a,I) with the glibc offset

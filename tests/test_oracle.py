@@ -215,3 +215,33 @@ def test_philox_find_offset_blocks(oracle):
     for f in blk["hyp"].dtype.names:  # (field by field: the records have padding bytes)
         assert np.array_equal(blk["hyp"][f], full["hyp"][a:][f], equal_nan=True), f
     assert np.degrees(np.abs(full["R"] - p["euler_gt"])).mean() < 1.0
+
+
+def test_inlier_count_restatement(oracle):
+    """the opt-in inlier count (erp_match.h erp_ransac_cfg.inlier_thr; no reference counterpart):
+    erpo_rank2 is E_mat_correct (rank 2, unit-norm e -> ||E'|| <= 1, singular values = e's top
+    two), the count agrees with an independent numpy evaluation of l^T E' r up to the matches
+    within 1e-12 of the threshold, and find(detail) fills every iteration's count from its
+    E_corr (0 when off)."""
+    from erp_match_eightpoint_test_amd import synth
+    rng = np.random.default_rng(5)
+    e = rng.standard_normal(9)
+    e /= np.linalg.norm(e)
+    Ec = oracle.rank2(e)
+    s_e = np.linalg.svd(e.reshape(3, 3), compute_uv=False)
+    s_c = np.linalg.svd(Ec.reshape(3, 3), compute_uv=False)
+    assert np.allclose(s_c[:2], s_e[:2], atol=1e-13) and s_c[2] < 1e-13
+    c = synth.make_correspondences(11, m=300, outlier_frac=0.5)
+    bl = oracle.pixel_to_bearing(c["W"], c["H"], c["kp_l"])
+    br = oracle.pixel_to_bearing(c["W"], c["H"], c["kp_r"])
+    res = np.abs(np.einsum("ni,ij,nj->n", bl, Ec.reshape(3, 3), br))
+    for thr in (1e-3, 1e-2, 0.1, 0.5):
+        n, nb = oracle.inlier_count(bl, br, Ec, thr, 1e-12)
+        assert abs(n - int((res < thr).sum())) <= nb
+    o = oracle.find(c["W"], c["H"], c["kp_l"], c["kp_r"], oracle.make_cfg(iters=40, inlier_thr=0.01),
+                    detail=True)
+    for h in o["hyp"]:
+        assert h["inliers"] == oracle.inlier_count(bl, br, h["E_corr"], 0.01)[0]
+    off = oracle.find(c["W"], c["H"], c["kp_l"], c["kp_r"], oracle.make_cfg(iters=40), detail=True)
+    assert (off["hyp"]["inliers"] == 0).all()
+    assert off["min_idx"] == o["min_idx"] and np.array_equal(off["R"], o["R"])
