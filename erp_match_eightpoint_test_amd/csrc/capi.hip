@@ -108,6 +108,11 @@ struct erp_ctx {
     // second pre-pruning stage: every 4th first-stage survivor on the fine grid as a reference
     // for the others (kernels.hip consensus_lipschitz2_kernel; ERP_LIP2=0 for A/B)
     int lip2 = getenv("ERP_LIP2") ? atoi(getenv("ERP_LIP2")) : 1;
+    // convexity-augmented pruning: the central first-stage references' distance gradient G
+    // (kernels.hip consensus_grad_kernel; ERP_LIPG=0 for A/B), for references with
+    // UB <= U * ERP_LIPG_FAC
+    int lipg = getenv("ERP_LIPG") ? atoi(getenv("ERP_LIPG")) : 1;
+    float lipg_fac = getenv("ERP_LIPG_FAC") ? (float)atof(getenv("ERP_LIPG_FAC")) : 1.1f;
     // the sampler and the Gram as one kernel (sampler_gram_kernel, opt-in ERP_FUSE_SAMPLER=1):
     // measured 1.6x SLOWER than the two standalone kernels (the Gram's int32
     // accumulators leave room for one sampler wave per SIMD, and one wave alone issues VALU at
@@ -569,7 +574,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             nshards, (int32_t*)c->surv.p,
                                             (int32_t*)c->nsurv.p + sh.n_pairs,
                                             (int32_t*)c->zsel.p, c->zoom_refs, c->lip2,
-                                            (int32_t*)c->sortbuf.p, c->lipref.p, st));
+                                            (int32_t*)c->sortbuf.p, c->lipref.p, c->lipg,
+                                            c->lipg_fac, st));
     }
     if (phase == 1) return ERP_OK;
     if (phase == 2)  // the bounds ran per shard (binned rows not combined): report -1

@@ -175,7 +175,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
                                    int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
-                                   void* lipref, hipStream_t st);
+                                   void* lipref, int lipg, float gfac, hipStream_t st);
 size_t lipref_bytes(int n_pairs, int stride);
 // survivors = rows with LB <= min UB (again = 1: only pairs the refine pass touched)
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,

@@ -2380,6 +2380,68 @@ __device__ int lip_prune_rows(LipShared& sh, int na, const float4* __restrict__ 
     return na;
 }
 
+// the rows act[0 .. na) against the gradient references GR[0 .. m) (two float4 each, staged
+// through LDS 256 at a time); same compaction as lip_prune_rows
+template <class Prune>
+__device__ int lip_prune_grad(LipShared& sh, int na, const float4* __restrict__ GR, int m,
+                              double U, Prune prune) {
+    constexpr int kChunk = kLipChunk2 / 2, kBatch = 32;
+    const int tid = threadIdx.x, lane = wave_lane();
+    const float Um = (float)(U * (1.0 + 1.1e-5));  // >= U (1 + 1e-5) after rounding
+    // the batch counters restart at zero (lip_prune_rows leaves its last two batches' counts)
+    __syncthreads();
+    if (tid < 4) sh.cnt[tid] = 0;
+    int t = 0;
+    for (int c0 = 0; c0 < m && na > 0; c0 += kChunk) {
+        const int nc = min(kChunk, m - c0);
+        __syncthreads();
+        const int ncp = (nc + kBatch - 1) / kBatch * kBatch;  // padding prunes nothing
+        for (int c = tid; c < 2 * ncp; c += 256)
+            sh.refs[c] = c < 2 * nc ? GR[2 * c0 + c]
+                                    : make_float4(0.f, 0.f, 0.f, (c & 1) ? 0.f : -kInf);
+        __syncthreads();
+        for (int q0 = 0; q0 < nc && na > 0; q0 += kBatch, t++) {
+            const bool v0 = 2 * tid < na, v1 = 2 * tid + 1 < na;
+            const float4 a0 = sh.act[v0 ? 2 * tid : 0];
+            const float4 a1 = sh.act[v1 ? 2 * tid + 1 : 0];
+            bool p0 = false, p1 = false;
+            if (v0) {
+                for (int q = q0; q < q0 + kBatch; q++) {
+                    const float4 A = sh.refs[2 * q], B = sh.refs[2 * q + 1];
+                    const float dx0 = a0.x - A.x, dy0 = a0.y - A.y, dz0 = a0.z - A.z;
+                    const float dx1 = a1.x - A.x, dy1 = a1.y - A.y, dz1 = a1.z - A.z;
+                    const float n0 = __builtin_amdgcn_sqrtf(
+                        __builtin_fmaf(dz0, dz0, __builtin_fmaf(dy0, dy0, dx0 * dx0)));
+                    const float n1 = __builtin_amdgcn_sqrtf(
+                        __builtin_fmaf(dz1, dz1, __builtin_fmaf(dy1, dy1, dx1 * dx1)));
+                    const float g0 = __builtin_fmaf(B.z, dz0, __builtin_fmaf(B.y, dy0, B.x * dx0));
+                    const float g1 = __builtin_fmaf(B.z, dz1, __builtin_fmaf(B.y, dy1, B.x * dx1));
+                    p0 |= __builtin_fmaf(-B.w, n0, A.w + g0) > Um;
+                    p1 |= __builtin_fmaf(-B.w, n1, A.w + g1) > Um;
+                }
+            }
+            p0 = v0 && p0;
+            p1 = v1 && p1;
+            if (p0) prune(__float_as_int(a0.w));
+            if (p1) prune(__float_as_int(a1.w));
+            const bool k0 = v0 && !p0, k1 = v1 && !p1;
+            const uint64_t b0 = __builtin_amdgcn_ballot_w64(k0), b1 = __builtin_amdgcn_ballot_w64(k1);
+            int base = 0;
+            if (lane == 0 && (b0 | b1))
+                base = atomicAdd(&sh.cnt[t & 3], __builtin_popcountll(b0) + __builtin_popcountll(b1));
+            base = __shfl(base, 0, 64);
+            __syncthreads();
+            const uint64_t below = (1ull << lane) - 1ull;
+            if (k0) sh.act[base + __builtin_popcountll(b0 & below)] = a0;
+            if (k1) sh.act[base + __builtin_popcountll(b0) + __builtin_popcountll(b1 & below)] = a1;
+            __syncthreads();
+            na = sh.cnt[t & 3];
+            if (tid == 0) sh.cnt[(t + 2) & 3] = 0;
+        }
+    }
+    return na;
+}
+
 // append act[0 .. na) (the rows left) to a per-pair list
 // (and, when list2 is given, the rows that are second-stage references, is_ref2, to list2 too)
 __device__ __forceinline__ bool is_ref2(int row) { return (row & (kLip2Step - 1)) == 1; }
@@ -2433,7 +2495,8 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     int32_t* __restrict__ rcount, int shard, int nshards, int lstep,
     const float4* __restrict__ lref, const double* __restrict__ lU,
     const int32_t* __restrict__ lcnt, int cap, int32_t* __restrict__ r2list,
-    int32_t* __restrict__ r2cnt) {
+    int32_t* __restrict__ r2cnt, const float4* __restrict__ gref, const int32_t* __restrict__ gcnt,
+    int gcap) {
     __shared__ LipShared sh;
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
@@ -2482,6 +2545,13 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
             UBp[i] = __builtin_huge_val();
         };
         na = lip_prune_rows(sh, na, lref + (size_t)p * cap, m, prune);
+    }
+    if (prune_on && gref && gcnt[p] > 0) {  // the rows left against the central references' G
+        auto prune = [&](int i) {
+            LBp[i] = U * (1.0 + 5e-6);
+            UBp[i] = __builtin_huge_val();
+        };
+        na = lip_prune_grad(sh, na, gref + (size_t)p * gcap * 2, gcnt[p], U, prune);
     }
     lip_append(sh, na, rlist + (size_t)p * olstride, &rcount[p],
                r2list ? r2list + (size_t)p * stride : nullptr, r2list ? &r2cnt[p] : nullptr);
@@ -2740,6 +2810,136 @@ __global__ __launch_bounds__(1024) void list_prefix_kernel(const int32_t* __rest
         __syncthreads();
     }
     if (tid == 0) uoff[n_pairs] = carry;
+}
+
+// ---- convexity-augmented pruning (round 4; ctx knob ERP_LIPG, default on) ----------------
+// Beyond 1-Lipschitz, every distance is CONVEX in x: d(x, x_j) >= a_j + <u_j, x - c> with
+// a_j = d(c, x_j) and u_j = (c - x_j) / a_j (u_j = 0 when a_j = 0: d(x, x_j) = |x - c| >= 0).
+// With delta = x - c, b_j = <u_j, delta> (|b_j| <= |delta|) and W(v) = the sum of the order
+// statistics lo .. hi-1 of v (monotone in every element), F_m(v) = the sum of its m smallest:
+//   W(d(x, .)) >= W(a + b) = F_hi(a + b) - F_lo(a + b)
+//              >= [F_hi(a) + F_hi(b)] - [F_lo(a) + sum_{S_lo(a)} b]
+//              >= W(a) + sum_j b_j - (K - hi) |delta| - <g_S', delta> - (lo - |S'|) |delta|
+// (F_hi(a + b) >= F_hi(a) + F_hi(b) over its minimising set; F_lo(a + b) <= the sum over S_lo(a);
+// F_hi(b) = sum_j b_j minus its K - hi largest, each <= |delta|; S' = the columns whose key lies
+// two or more bins below the bin of rank lo -- strictly below every column from that bin on,
+// so inside S_lo(a) whatever the rounding -- and the lo - |S'| other members of S_lo(a) add
+// <= |delta| each).  Hence
+//   T(x) >= T(c) + <G, delta> - pen |delta|,  G = (g_all - g_S') / w,
+//   pen = ((K - hi) + (lo - |S'|)) / w  (~1/3 at the reference's 0.2 / 0.8 trim, against the
+// Lipschitz bound's 1).  Near the minimum, where T is flat and Lipschitz pruning stops, this
+// prunes ~half of the rows the first stage leaves (a numpy model of the configs[1] fixture
+// pair: L1 1631 -> 853 rows with G on the 77 central references of 625).  G costs one more
+// K-column pass per reference (unit vectors: one rsq), so only the central references get it:
+// those that can prune (LB_c > U) with UB_c <= U gfac.
+// Rigor: G is summed in f32 per thread (<= ceil(K/256) unit vectors of norm <= 1 + 2^-21 each)
+// and in fp64 over the block, so |G~ - G| w <= K 2^-20 + 256 n^2 2^-23 (n = ceil(K/256)); that
+// and the f32 evaluation of the test (delta, the dot product, |delta| by v_sqrt_f32: each
+// <= ~1e-6 of (|G| + pen) |delta|) are covered by pen += eps_G + 1e-5 (|G| + pen + 1); the
+// reference's own f32 distances and fp64 sum (T_ref = T (1 +- 4u)) by LB_c (1 - 1e-5) and
+// U (1 + 1.1e-5), as in the Lipschitz test: a pruned row's LB = U (1 + 5e-6) stays rigorous.
+
+// the references of pair p that get G (stage-1 reference rows ra + c lstep of the shard): can
+// prune (LB_c (1 - 1e-5) > U (1 + 1e-5)), central (UB_c <= U gfac), window bin of rank lo >= 2
+__global__ __launch_bounds__(256) void consensus_grad_select_kernel(
+    const int32_t* __restrict__ kcount, int stride, const double* __restrict__ lb,
+    const double* __restrict__ ub, const int32_t* __restrict__ bsel, int lstep, int shard,
+    int nshards, const double* __restrict__ lU, float gfac, int32_t* __restrict__ gsel,
+    int32_t* __restrict__ gcnt, int gcap) {
+    __shared__ int n;
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int K = kcount[p];
+    const double U = lU[p];
+    if (tid == 0) n = 0;
+    __syncthreads();
+    if (U < __builtin_huge_val()) {
+        const int ra = (int)((int64_t)K * shard / nshards);
+        const int nr = (int)((int64_t)K * (shard + 1) / nshards) - ra;
+        const int nref = nr > 0 ? (nr + lstep - 1) / lstep : 0;
+        const double Um = U * (1.0 + 1e-5), Uc = U * (double)gfac;
+        for (int c = tid; c < nref; c += 256) {
+            const int row = ra + c * lstep;
+            const size_t o = (size_t)p * stride + row;
+            if (lb[o] * (1.0 - 1e-5) > Um && ub[o] <= Uc && bsel[o * 2] >= 2) {
+                const int k = atomicAdd(&n, 1);
+                if (k < gcap) gsel[(size_t)p * gcap + k] = row;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) gcnt[p] = min(n, gcap);
+}
+
+// G and pen of every selected reference (items = (pair, reference) flattened by goff): one block
+// per item, the K columns in the bounds pass's own key computation (S' membership) -> gref
+// [p][k][2] = {(c, LB_c (1 - 1e-5)), (G, pen)}
+__global__ __launch_bounds__(256) void consensus_grad_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv,
+    const float* __restrict__ dscale, int stride, double trim_lo, double trim_hi,
+    const double* __restrict__ lb, const int32_t* __restrict__ bsel,
+    const int32_t* __restrict__ gsel, const int32_t* __restrict__ goff, int n_pairs, int gcap,
+    float4* __restrict__ gref) {
+    __shared__ double red[7][4];
+    const int tid = threadIdx.x, lane = wave_lane(), wv = tid >> 6;
+    const int total = goff[n_pairs];
+    for (int g = blockIdx.x; g < total; g += gridDim.x) {
+        int p, k;
+        pair_of_item(goff, n_pairs, g, &p, &k);
+        const int c = gsel[(size_t)p * gcap + k];
+        const int K = kcount[p];
+        const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
+        const float* X = rv + (size_t)p * 3 * stride;
+        const float* Y = X + stride;
+        const float* Z = Y + stride;
+        const int elo = bounds_elo(dscale[p]);
+        const uint32_t kmax = (uint32_t)((elo << kMantBits) + bsel[((size_t)p * stride + c) * 2] - 2);
+        const float e0 = bounds_bias(elo);
+        const float xc = X[c], yc = Y[c], zc = Z[c];
+        float ga[3] = {0.f, 0.f, 0.f}, gs[3] = {0.f, 0.f, 0.f};
+        int ns = 0;
+        for (int j = tid; j < K; j += 256) {
+            const float dx = xc - X[j], dy = yc - Y[j], dz = zc - Z[j];
+            // the bounds pass's biased key (rows minus columns there: the squares are equal)
+            const float sb = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, __builtin_fmaf(dx, dx, e0)));
+            const float s = __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+            const float r = s > 0.f ? __builtin_amdgcn_rsqf(s) : 0.f;
+            const float ux = dx * r, uy = dy * r, uz = dz * r;
+            ga[0] += ux;
+            ga[1] += uy;
+            ga[2] += uz;
+            if ((__float_as_uint(sb) >> kBinShift) <= kmax) {
+                gs[0] += ux;
+                gs[1] += uy;
+                gs[2] += uz;
+                ns++;
+            }
+        }
+        double v[7] = {ga[0], ga[1], ga[2], gs[0], gs[1], gs[2], (double)ns};
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) v[q] += __shfl_xor(v[q], o, 64);
+            if (lane == 0) red[q][wv] = v[q];
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double t[7];
+#pragma unroll
+            for (int q = 0; q < 7; q++) t[q] = (red[q][0] + red[q][1]) + (red[q][2] + red[q][3]);
+            const double w = (double)(hi - lo);
+            const double G0 = (t[0] - t[3]) / w, G1 = (t[1] - t[4]) / w, G2 = (t[2] - t[5]) / w;
+            const double nth = (double)((K + 255) / 256);
+            const double epsG = ((double)K * 0x1p-20 + 256.0 * nth * nth * 0x1p-23) / w;
+            double pen = ((double)(K - hi) + (double)(lo - (int)t[6])) / w + epsG;
+            const double gn = sqrt(G0 * G0 + G1 * G1 + G2 * G2);
+            pen += 1e-5 * (gn + pen + 1.0);
+            float4* o = gref + ((size_t)p * gcap + k) * 2;
+            o[0] = make_float4(xc, yc, zc, (float)(lb[(size_t)p * stride + c] * (1.0 - 1e-5)));
+            // (G rounded to f32: its error, 2^-24 |G| |delta|, is inside the 1e-5 |G| term)
+            o[1] = make_float4((float)G0, (float)G1, (float)G2, (float)(pen * (1.0 + 1e-6)));
+        }
+        __syncthreads();
+    }
 }
 
 __global__ __launch_bounds__(256) void consensus_bounds_list_kernel(
@@ -4019,9 +4219,13 @@ hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const f
 
 // the pruning references' scratch: [P][cap] float4, lU [P] doubles, lcnt [P] ints, then the
 // second-stage reference list [P][stride] ints and its counts [P]
+// then the gradient references: gref [P][gcap][2] float4, gsel [P][gcap], gcnt [P], goff [P + 1]
+static int grad_cap(int stride) { return stride / kLipStep + 64; }  // >= stage-1 references
 size_t lipref_bytes(int n_pairs, int stride) {
+    const size_t gcap = grad_cap(stride);
     return (size_t)n_pairs * lipref_cap(stride) * sizeof(float4) + (size_t)n_pairs * 16 +
-           (size_t)n_pairs * stride * 4 + 64;
+           (size_t)n_pairs * stride * 4 + 64 + (size_t)n_pairs * gcap * 2 * sizeof(float4) +
+           (size_t)n_pairs * gcap * 4 + (size_t)n_pairs * 8 + 128;
 }
 struct LipRefViews {
     float4* ref;
@@ -4030,6 +4234,11 @@ struct LipRefViews {
     int32_t* r2cnt;
     int32_t* r2list;
     int cap;
+    float4* gref;
+    int32_t* gsel;
+    int32_t* gcnt;
+    int32_t* goff;
+    int gcap;
 };
 static LipRefViews lipref_views(void* base, int n_pairs, int stride) {
     LipRefViews v;
@@ -4039,6 +4248,13 @@ static LipRefViews lipref_views(void* base, int n_pairs, int stride) {
     v.cnt = reinterpret_cast<int32_t*>(v.U + n_pairs);
     v.r2cnt = v.cnt + n_pairs;
     v.r2list = v.r2cnt + n_pairs;
+    v.gcap = grad_cap(stride);
+    uintptr_t gb = reinterpret_cast<uintptr_t>(v.r2list + (size_t)n_pairs * stride) + 64;
+    gb = (gb + 15) & ~(uintptr_t)15;
+    v.gref = reinterpret_cast<float4*>(gb);
+    v.gsel = reinterpret_cast<int32_t*>(v.gref + (size_t)n_pairs * v.gcap * 2);
+    v.gcnt = v.gsel + (size_t)n_pairs * v.gcap;
+    v.goff = v.gcnt + n_pairs;
     return v;
 }
 
@@ -4047,7 +4263,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
                                    int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
-                                   void* lipref, hipStream_t st) {
+                                   void* lipref, int lipg, float gfac, hipStream_t st) {
     hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     const int stride = 2 * sh.iters;
     if (!rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
@@ -4090,11 +4306,23 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                        trim_lo, trim_hi, (const double*)lb, (const double*)ub,
                        (const int32_t*)nullptr, (const int32_t*)nullptr, kLipStep, shard, nshards,
                        (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap);
+    if (lipg) {  // the central references' G (convexity-augmented pruning)
+        hipLaunchKernelGGL(consensus_grad_select_kernel, dim3(P), dim3(256), 0, st, kcount, stride,
+                           (const double*)lb, (const double*)ub, (const int32_t*)bsel, kLipStep,
+                           shard, nshards, (const double*)lr.U, gfac, lr.gsel, lr.gcnt, lr.gcap);
+        hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)lr.gcnt,
+                           P, 1, 0, lr.goff);
+        hipLaunchKernelGGL(consensus_grad_kernel, dim3(std::min(P * 64, 2048)), dim3(256), 0, st,
+                           kcount, rv, dscale, stride, trim_lo, trim_hi, (const double*)lb,
+                           (const int32_t*)bsel, (const int32_t*)lr.gsel, (const int32_t*)lr.goff,
+                           P, lr.gcap, lr.gref);
+    }
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
                        st, kcount, rv, stride, lb, ub, (const int32_t*)nullptr,
                        (const int32_t*)nullptr, rlist, stride, rcount, shard, nshards, kLipStep,
                        (const float4*)lr.ref, (const double*)lr.U, (const int32_t*)lr.cnt,
-                       lr.cap, two ? lr.r2list : nullptr, two ? lr.r2cnt : nullptr);
+                       lr.cap, two ? lr.r2list : nullptr, two ? lr.r2cnt : nullptr,
+                       lipg ? (const float4*)lr.gref : nullptr, (const int32_t*)lr.gcnt, lr.gcap);
     int32_t* uoff = rcount + P;  // [n_pairs + 1] after the counts
     const int32_t* blist = rlist;
     const int32_t* bcount = rcount;
@@ -4178,7 +4406,8 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
     hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, P), dim3(256), 0, st,
                        kcount, rv, stride, lb, ub, surv, nsurv, list2, l2stride, n2, 0, 1,
                        kRefStep, (const float4*)lr.ref, (const double*)lr.U,
-                       (const int32_t*)lr.cnt, lr.cap, (int32_t*)nullptr, (int32_t*)nullptr);
+                       (const int32_t*)lr.cnt, lr.cap, (int32_t*)nullptr, (int32_t*)nullptr,
+                       (const float4*)nullptr, (const int32_t*)nullptr, 0);
     // (C) the survivors the references did not prune
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)n2, P,
                        kRefineRows, 0, uoff);

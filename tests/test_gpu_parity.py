@@ -846,6 +846,68 @@ def test_consensus_lipschitz_prepruning(ctx, oracle, case):
         assert res["binned_rows"] < K // 2, res["binned_rows"]
 
 
+@pytest.mark.parametrize("case", ["cluster", "cluster_outliers", "shell", "two_clusters",
+                                  "bench_pairs"])
+def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case):
+    """the convexity-augmented pruning (central references' distance gradient G, ERP_LIPG) keeps
+    every result field the Lipschitz-only run gives (status, K, min_idx, R, T, min_dist,
+    near_ties), is deterministic run to run (every byte, binned_rows included), and bins no more
+    rows than Lipschitz alone -- on synthetic clouds against the oracle and on configs[1]-shaped
+    pairs through the batch pipeline"""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
+    from erp_match_eightpoint_test_amd import dist as D
+
+    def ctx_with(v):
+        monkeypatch.setenv("ERP_LIPG", v)
+        return Context(0)
+
+    if case == "bench_pairs":
+        pairs = [synth.make_pair(20200423 + i, n_kpts=2048) for i in range(6)]
+        args = _batch(pairs)
+        recs = {}
+        for v in ("0", "1", "1"):
+            out = PairBatchRunner(ctx=ctx_with(v), iters=10000).run(*args)
+            torch.cuda.synchronize()
+            recs.setdefault(v, []).append(results_to_numpy(out["results"]))
+        a, b = recs["0"][0], recs["1"][0]
+        assert np.array_equal(recs["1"][0].view(np.uint8), recs["1"][1].view(np.uint8))
+        for f in ("status", "M", "K", "min_idx", "R", "T", "min_dist", "near_ties"):
+            assert np.array_equal(a[f], b[f]), f
+        # (a second-stage reference the gradient prunes no longer prunes for stage 2: a few
+        # rows may move to the coarse list, so the bound is on the total, not per row)
+        assert b["binned_rows"].sum() <= a["binned_rows"].sum()
+        print(f"binned rows lipschitz {a['binned_rows'].tolist()} -> grad {b['binned_rows'].tolist()}")
+        return
+    rng = np.random.default_rng({"cluster": 21, "cluster_outliers": 22, "shell": 23,
+                                 "two_clusters": 25}[case])
+    K = 8000
+    if case == "cluster":
+        rv = rng.standard_normal((K, 3)) * 6e-5 + np.array([0.09, 0.24, 0.26])
+    elif case == "cluster_outliers":
+        rv = rng.standard_normal((K, 3)) * 6e-5 + np.array([0.09, 0.24, 0.26])
+        far = rng.choice(K, 400, replace=False)
+        rv[far] = rng.uniform(-1.5, 1.5, (400, 3))
+    elif case == "shell":
+        v = rng.standard_normal((K, 3))
+        rv = 0.01 * v / np.linalg.norm(v, axis=1, keepdims=True) + 0.2
+    else:
+        a = rng.standard_normal((K // 2, 3)) * 6e-5 + np.array([0.1, 0.2, 0.3])
+        b = rng.standard_normal((K - K // 2, 3)) * 6e-5 + np.array([-1.2, 0.9, 0.4])
+        rv = np.concatenate([a, b])[rng.permutation(K)]
+    rv = rv.astype(np.float32)
+    tv = rng.standard_normal((K, 3)).astype(np.float32)
+    _, mi, dref = oracle.consensus(rv)
+    r0 = D.gpu_consensus(ctx_with("0"), "cuda")(rv, tv)
+    r1 = D.gpu_consensus(ctx_with("1"), "cuda")(rv, tv)
+    r2 = D.gpu_consensus(ctx_with("1"), "cuda")(rv, tv)
+    assert np.array_equal(np.asarray(r1).view(np.uint8), np.asarray(r2).view(np.uint8))
+    for r in (r0, r1):
+        assert r["status"] == 0 and r["min_idx"] == mi
+        assert abs(r["min_dist"] - dref[mi]) <= 1e-12 * abs(dref[mi])
+    assert r1["binned_rows"] <= r0["binned_rows"] + 64, (r1["binned_rows"], r0["binned_rows"])
+
+
 def test_consensus_small_set_bins_every_row(ctx, oracle):
     """below 1024 rows there is no pre-pruning: every row is binned."""
     from erp_match_eightpoint_test_amd import dist as D
