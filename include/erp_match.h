@@ -134,7 +134,8 @@ typedef struct erp_pair_result {
                             different count than the unsharded one; 1 <= survivors <= K, and
                             <= binned_rows when that is reported) */
     int32_t binned_rows; /* rows whose K-column distance histogram was built (K, or the
-                            reference rows + the rows Lipschitz pre-pruning kept) */
+                            reference rows + the rows Lipschitz pre-pruning kept; K on the
+                            row-sharded path, whose shards do not combine it) */
     double min_dist;     /* trimmed-mean distance of the winner */
 } erp_pair_result;
 

@@ -690,10 +690,9 @@ def test_consensus_row_shards_equal_unsharded(ctx, world, iters):
     # (how many rows survive the selections depends on which references each shard prunes
     # with -- a diagnostic, not part of the result; include/erp_match.h says so).  Bounded:
     # a survivor is a binned row (pruned rows get LB > every UB), so 1 <= survivors <= binned
-    # rows <= K unsharded, and <= K sharded (binned_rows is -1 there: not combined over shards)
+    # rows <= K (the row-sharded path reports binned_rows = K: not combined over the shards)
     assert 1 <= ref["survivors"] <= ref["binned_rows"] <= ref["K"]
-    assert 1 <= r["survivors"] <= r["K"]
-    assert r["binned_rows"] == (-1 if world > 1 else ref["binned_rows"])
+    assert 1 <= r["survivors"] <= r["binned_rows"] == r["K"]
     assert np.array_equal(r["R"], R) and np.array_equal(r["T"], T)
     assert r["min_dist"] == ref["min_dist"]
 
