@@ -410,8 +410,14 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
     if (!ok) return ERP_OUT_OF_MEMORY;
     if (!c->rtab_valid) {  // once per context: the reciprocal table, verified exactly
         constexpr int n = erp::kRecipTable;
-        if (!ensure(c->rtab, (size_t)n * 8 + 8)) return ERP_OUT_OF_MEMORY;
-        int32_t* d_bad = (int32_t*)((char*)c->rtab.p + (size_t)n * 8);
+        if (!ensure(c->rtab, erp::kRecipTableBytes)) return ERP_OUT_OF_MEMORY;
+        {  // the magic-number table after it (the sampler's d >= 256 quotients)
+            std::vector<uint64_t> mt(n);
+            if (!erp::build_magic_table(mt.data(), n)) return ERP_INTERNAL;
+            ERP_CK(hipMemcpy((double*)c->rtab.p + n, mt.data(), (size_t)n * 8,
+                             hipMemcpyHostToDevice));
+        }
+        int32_t* d_bad = (int32_t*)((char*)c->rtab.p + (size_t)n * 16);
         ERP_CK(hipMemset(d_bad, 0, 4));
         ERP_CK(erp::launch_recip_table(n, (double*)c->rtab.p, d_bad, nullptr));
         int32_t bad = 0;

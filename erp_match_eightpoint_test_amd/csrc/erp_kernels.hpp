@@ -107,6 +107,12 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
 // rtab[d] = 1/d rounded up, d < kRecipTable (the sampler's exact modulo); *bad counts entries
 // whose one-sided error bound fails (never, by construction; checked once per context)
 constexpr int kRecipTable = 65538;
+// the sampler's table allocation: rtab [kRecipTable] doubles, then the magic-number table
+// [kRecipTable] uint64 (ERP_SAMPLER_MAGIC), then the check counter
+constexpr size_t kRecipTableBytes = (size_t)kRecipTable * 16 + 8;
+// host: mtab[d] = m_d | (l_d - 1) << 32 (kernels.hip mod_magic_i24); false if a divisor fails
+// the exact Granlund-Montgomery condition (never, by construction)
+bool build_magic_table(uint64_t* mtab, int n);
 // the counter-based sampler (ERP_SAMPLER_PHILOX): selection words in the replay's format,
 // max_m = the batch's largest M (<= max_nq); hipErrorInvalidValue when M's bitmap exceeds LDS
 hipError_t launch_philox_sampler(const int32_t* counts, const BatchShape& sh, double sample_frac,

@@ -325,6 +325,36 @@ __device__ __forceinline__ uint32_t mod_rup_i24(uint32_t x, double r, int d) {
 }
 
 
+// ERP_SAMPLER_MAGIC (round 4): the d >= 256 steps' quotient by a 32-bit multiply-high instead of
+// the fp64 reciprocal: floor(x / d) = mulhi(x, m_d) >> (l_d - 1) for every x < 2^31 with
+// l_d = ceil(log2 d) and m_d = ceil(2^(31 + l_d) / d) < 2^32 (Granlund & Montgomery,
+// "Division by invariant integers using multiplication", PLDI 1994, Thm 4.2: 2^(31+l) <= m d <=
+// 2^(31+l) + 2^l; checked exactly for every d when the host builds the table).  v_mul_hi_u32 +
+// one shift by a scalar (2 VALU, 6 cycles) replaces v_cvt_f64_u32 + v_fma_f64 (8 cycles); the
+// remainder stays one v_mad_i32_i24.  The table mtab[d] = m_d | (l_d - 1) << 32 sits right after
+// the reciprocal table (rtab + kRecipTable), read by scalar loads like it.
+#ifndef ERP_SAMPLER_MAGIC
+#define ERP_SAMPLER_MAGIC 0
+#endif
+__device__ __forceinline__ uint32_t mod_magic_i24(uint32_t x, uint64_t mt, int d) {
+    const uint32_t q = __umulhi(x, (uint32_t)mt) >> (uint32_t)(mt >> 32);
+    int j;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(j) : "v"(q), "s"(-d), "v"(x));
+    return (uint32_t)j;
+}
+// the per-step divisor constant of a d >= 256 step: the magic pair or the reciprocal
+#if ERP_SAMPLER_MAGIC
+typedef uint64_t StepDiv;
+__device__ __forceinline__ StepDiv step_div(const double* rtab, int d) {
+    return reinterpret_cast<const uint64_t*>(rtab + kRecipTable)[d];
+}
+__device__ __forceinline__ uint32_t mod_i24(uint32_t x, StepDiv c, int d) { return mod_magic_i24(x, c, d); }
+#else
+typedef double StepDiv;
+__device__ __forceinline__ StepDiv step_div(const double* rtab, int d) { return rtab[d]; }
+__device__ __forceinline__ uint32_t mod_i24(uint32_t x, StepDiv c, int d) { return mod_rup_i24(x, c, d); }
+#endif
+
 // One block of 31 reverse steps i0, i0-1, ..., i0-30 of one lane's replay (ring = the 31-word
 // glibc window, advanced backwards in place).  Returns the block's selection word: bit u set
 // iff step i0-u's index ends in the sample.  bm = the lane's s-bit LDS bitmap, [word][lane],
@@ -382,8 +412,12 @@ __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uin
                                                        const double* __restrict__ rtab) {
     const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
     double rt[31];  // 1/(i+1) of the block's steps: scalar loads (uniform index)
+    StepDiv mt[31];  // (I24: the d >= 256 divisor constants)
 #pragma unroll
-    for (int u = 0; u < 31; u++) rt[u] = rtab[i0 - u + 1];
+    for (int u = 0; u < 31; u++) {
+        if (I24) mt[u] = step_div(rtab, i0 - u + 1);
+        else rt[u] = rtab[i0 - u + 1];
+    }
     const uint32_t zero = 0;
     uint32_t olds[31], pos[31];
     uint32_t nw = 0;
@@ -394,7 +428,7 @@ __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uin
             const int slot = 30 - u;
             const uint32_t rv = ring[slot];
             ring[slot] = rv - ring[(slot + 28) % 31];
-            const uint32_t j = I24 ? mod_rup_i24(rv >> 1, rt[u], ii + 1)
+            const uint32_t j = I24 ? mod_i24(rv >> 1, mt[u], ii + 1)
                                    : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
             olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), 1u << (j & 31), zero);
             pos[u] = j;
@@ -469,13 +503,17 @@ __device__ __forceinline__ uint32_t replay_block_prefix_rd(uint32_t (&ring)[31],
     // block's reciprocal loads above it, where they merge into wide scalar loads -- sunk into
     // the steps one by one, their 31 addresses spill)
     double rt[31];
+    StepDiv mt[31];
     uint32_t nw = 0, prev = 0, ppos = 0;
 #pragma unroll
     for (int u = 0; u < 31; u++) {
         const int ii = i0 - u;  // uniform, >= 1
         if (u == 0 || u == 16)  // the reciprocals in two halves (SGPR pressure)
 #pragma unroll
-            for (int k = u; k < (u == 0 ? 16 : 31); k++) rt[k] = rtab[i0 - k + 1];
+            for (int k = u; k < (u == 0 ? 16 : 31); k++) {
+                if (I24) mt[k] = step_div(rtab, i0 - k + 1);
+                else rt[k] = rtab[i0 - k + 1];
+            }
         uint32_t rd;
         const uint32_t ra = bm_lane + ((uint32_t)(ii >> 5) << RS);
         if (u == 0 || u == 16)  // the memory clobber holds the half's loads (merged) above it
@@ -485,7 +523,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix_rd(uint32_t (&ring)[31],
         const int slot = 30 - u;
         const uint32_t rv = ring[slot];
         ring[slot] = rv - ring[(slot + 28) % 31];
-        const uint32_t j = I24 ? mod_rup_i24(rv >> 1, rt[u], ii + 1)
+        const uint32_t j = I24 ? mod_i24(rv >> 1, mt[u], ii + 1)
                                : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rd), "+v"(prev));
         if (u > 0) nw |= __builtin_amdgcn_ubfe(prev, ppos, 1) << (u - 1);
@@ -4020,6 +4058,23 @@ hipError_t launch_philox_sampler(const int32_t* counts, const BatchShape& sh, do
                        sh.iters, nwaves, sh.sel_words, sample_frac, seed, offset, nwords, selw,
                        flags);
     return hipGetLastError();
+}
+
+bool build_magic_table(uint64_t* mtab, int n) {
+    bool ok = true;
+    for (int d = 0; d < n; d++) {
+        if (d < 2) {
+            mtab[d] = 0;
+            continue;
+        }
+        int l = 0;
+        while ((1 << l) < d) l++;  // ceil(log2 d), >= 1
+        const uint64_t P = 1ull << (31 + l);
+        const uint64_t m = (P + (uint64_t)d - 1) / (uint64_t)d;
+        ok = ok && m < (1ull << 32) && m * (uint64_t)d >= P && m * (uint64_t)d - P <= (1ull << l);
+        mtab[d] = m | ((uint64_t)(l - 1) << 32);
+    }
+    return ok;
 }
 
 hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st) {

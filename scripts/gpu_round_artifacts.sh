@@ -37,6 +37,11 @@ if [ "${EXTRA_BENCH:-0}" = "1" ]; then
     --hard-steps 0 --worst-steps 0 --no-cpu-baseline --profile-tag ${TAG} > gpurun_out/bench_worst_${TAG}.json \
     2> gpurun_out/bench_worst_${TAG}.err || { tail -20 gpurun_out/bench_worst_${TAG}.err; exit 1; }
   tail -c 300 gpurun_out/bench_worst_${TAG}.json
+  echo "== single-pair latency (host) + kernel trace" && timeout -k 10 300 python scripts/latency_probe.py --runs 20 \
+    > gpurun_out/latency_host_${TAG}.json 2> gpurun_out/latency_${TAG}.err || { tail -20 gpurun_out/latency_${TAG}.err; exit 1; }
+  cat gpurun_out/latency_host_${TAG}.json
+  timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/lat_${TAG} -o run --output-format csv -- \
+    python3 scripts/latency_probe.py --runs 20 > gpurun_out/lat_${TAG}.log 2>&1 || { tail -20 gpurun_out/lat_${TAG}.log; exit 1; }
 fi
 if [ "${SKIP_PROFILE:-0}" != "1" ]; then
   echo "== rocprofv3 kernel-trace stats" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG} \
