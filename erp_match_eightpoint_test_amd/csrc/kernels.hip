@@ -2879,10 +2879,12 @@ __global__ __launch_bounds__(1024) void list_prefix_kernel(const int32_t* __rest
 
 // the references of pair p that get G (stage-1 reference rows ra + c lstep of the shard): can
 // prune (LB_c (1 - 1e-5) > U (1 + 1e-5)), central (UB_c <= U gfac), window bin of rank lo >= 2
+// (slist != nullptr: the second stage's references, slist[p][0 .. scount[p]), against its U)
 __global__ __launch_bounds__(256) void consensus_grad_select_kernel(
     const int32_t* __restrict__ kcount, int stride, const double* __restrict__ lb,
     const double* __restrict__ ub, const int32_t* __restrict__ bsel, int lstep, int shard,
-    int nshards, const double* __restrict__ lU, float gfac, int32_t* __restrict__ gsel,
+    int nshards, const int32_t* __restrict__ slist, const int32_t* __restrict__ scount,
+    const double* __restrict__ lU, float gfac, int32_t* __restrict__ gsel,
     int32_t* __restrict__ gcnt, int gcap) {
     __shared__ int n;
     const int p = blockIdx.x, tid = threadIdx.x;
@@ -2891,12 +2893,13 @@ __global__ __launch_bounds__(256) void consensus_grad_select_kernel(
     if (tid == 0) n = 0;
     __syncthreads();
     if (U < __builtin_huge_val()) {
-        const int ra = (int)((int64_t)K * shard / nshards);
-        const int nr = (int)((int64_t)K * (shard + 1) / nshards) - ra;
+        const int ra = slist ? 0 : (int)((int64_t)K * shard / nshards);
+        const int nr = slist ? scount[p] : (int)((int64_t)K * (shard + 1) / nshards) - ra;
         const int nref = nr > 0 ? (nr + lstep - 1) / lstep : 0;
+        const int32_t* SL = slist ? slist + (size_t)p * stride : nullptr;
         const double Um = U * (1.0 + 1e-5), Uc = U * (double)gfac;
         for (int c = tid; c < nref; c += 256) {
-            const int row = ra + c * lstep;
+            const int row = SL ? (int)SL[c * lstep] : ra + c * lstep;
             const size_t o = (size_t)p * stride + row;
             if (lb[o] * (1.0 - 1e-5) > Um && ub[o] <= Uc && bsel[o * 2] >= 2) {
                 const int k = atomicAdd(&n, 1);
@@ -3418,7 +3421,8 @@ __global__ __launch_bounds__(256) void consensus_lipschitz2_kernel(
     const int32_t* __restrict__ n1c, const int32_t* __restrict__ zb,
     const int32_t* __restrict__ bsel, int32_t* __restrict__ l2, int32_t* __restrict__ n2c,
     int32_t* __restrict__ nfb, const float4* __restrict__ lref, const double* __restrict__ lU,
-    const int32_t* __restrict__ lcnt, int cap) {
+    const int32_t* __restrict__ lcnt, int cap, const float4* __restrict__ gref,
+    const int32_t* __restrict__ gcnt, int gcap) {
     __shared__ LipShared sh;
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
     const int n = n1c[p];
@@ -3466,6 +3470,13 @@ __global__ __launch_bounds__(256) void consensus_lipschitz2_kernel(
             UBp[i] = __builtin_huge_val();
         };
         na = lip_prune_rows(sh, na, lref + (size_t)p * cap, nref, prune);
+    }
+    if (U < __builtin_huge_val() && gref && gcnt[p] > 0) {
+        auto prune = [&](int i) {
+            LBp[i] = U * (1.0 + 5e-6);
+            UBp[i] = __builtin_huge_val();
+        };
+        na = lip_prune_grad(sh, na, gref + (size_t)p * gcap * 2, gcnt[p], U, prune);
     }
     lip_append(sh, na, l2 + (size_t)p * stride, &n2c[p]);
 }
@@ -4275,7 +4286,8 @@ hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const f
 // the pruning references' scratch: [P][cap] float4, lU [P] doubles, lcnt [P] ints, then the
 // second-stage reference list [P][stride] ints and its counts [P]
 // then the gradient references: gref [P][gcap][2] float4, gsel [P][gcap], gcnt [P], goff [P + 1]
-static int grad_cap(int stride) { return stride / kLipStep + 64; }  // >= stage-1 references
+// (>= the stage-1 references; the second stage's -- a quarter of L1 -- are capped at it)
+static int grad_cap(int stride) { return stride / 4 + 64; }
 size_t lipref_bytes(int n_pairs, int stride) {
     const size_t gcap = grad_cap(stride);
     return (size_t)n_pairs * lipref_cap(stride) * sizeof(float4) + (size_t)n_pairs * 16 +
@@ -4361,10 +4373,11 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                        trim_lo, trim_hi, (const double*)lb, (const double*)ub,
                        (const int32_t*)nullptr, (const int32_t*)nullptr, kLipStep, shard, nshards,
                        (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap);
-    if (lipg) {  // the central references' G (convexity-augmented pruning)
+    if (lipg & 1) {  // the central references' G (convexity-augmented pruning)
         hipLaunchKernelGGL(consensus_grad_select_kernel, dim3(P), dim3(256), 0, st, kcount, stride,
                            (const double*)lb, (const double*)ub, (const int32_t*)bsel, kLipStep,
-                           shard, nshards, (const double*)lr.U, gfac, lr.gsel, lr.gcnt, lr.gcap);
+                           shard, nshards, (const int32_t*)nullptr, (const int32_t*)nullptr,
+                           (const double*)lr.U, gfac, lr.gsel, lr.gcnt, lr.gcap);
         hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)lr.gcnt,
                            P, 1, 0, lr.goff);
         hipLaunchKernelGGL(consensus_grad_kernel, dim3(std::min(P * 64, 2048)), dim3(256), 0, st,
@@ -4377,7 +4390,8 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                        (const int32_t*)nullptr, rlist, stride, rcount, shard, nshards, kLipStep,
                        (const float4*)lr.ref, (const double*)lr.U, (const int32_t*)lr.cnt,
                        lr.cap, two ? lr.r2list : nullptr, two ? lr.r2cnt : nullptr,
-                       lipg ? (const float4*)lr.gref : nullptr, (const int32_t*)lr.gcnt, lr.gcap);
+                       (lipg & 1) ? (const float4*)lr.gref : nullptr, (const int32_t*)lr.gcnt,
+                       lr.gcap);
     int32_t* uoff = rcount + P;  // [n_pairs + 1] after the counts
     const int32_t* blist = rlist;
     const int32_t* bcount = rcount;
@@ -4404,11 +4418,25 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                            stride, trim_lo, trim_hi, (const double*)lb, (const double*)ub,
                            (const int32_t*)lr.r2list, (const int32_t*)lr.r2cnt, 1, shard,
                            nshards, (const int32_t*)zb, lr.ref, lr.U, lr.cnt, lr.cap);
+        if (lipg & 2) {  // G of the central second-stage references (fine bounds)
+            hipLaunchKernelGGL(consensus_grad_select_kernel, dim3(P), dim3(256), 0, st, kcount,
+                               stride, (const double*)lb, (const double*)ub, (const int32_t*)bsel,
+                               1, 0, 1, (const int32_t*)lr.r2list, (const int32_t*)lr.r2cnt,
+                               (const double*)lr.U, gfac, lr.gsel, lr.gcnt, lr.gcap);
+            hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st,
+                               (const int32_t*)lr.gcnt, P, 1, 0, lr.goff);
+            hipLaunchKernelGGL(consensus_grad_kernel, dim3(std::min(P * 64, 2048)), dim3(256), 0,
+                               st, kcount, rv, dscale, stride, trim_lo, trim_hi, (const double*)lb,
+                               (const int32_t*)bsel, (const int32_t*)lr.gsel,
+                               (const int32_t*)lr.goff, P, lr.gcap, lr.gref);
+        }
         hipLaunchKernelGGL(consensus_lipschitz2_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
                            st, kcount, rv, stride, lb, ub, (const int32_t*)rlist,
                            (const int32_t*)rcount, (const int32_t*)zb, (const int32_t*)bsel, list2,
                            n2, n2 + P, (const float4*)lr.ref, (const double*)lr.U,
-                           (const int32_t*)lr.cnt, lr.cap);
+                           (const int32_t*)lr.cnt, lr.cap,
+                           (lipg & 2) ? (const float4*)lr.gref : nullptr, (const int32_t*)lr.gcnt,
+                           lr.gcap);
         hipLaunchKernelGGL(consensus_ref2_count_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P,
                            (const int32_t*)zb, (const int32_t*)lr.r2cnt, (const int32_t*)n2,
                            (const int32_t*)(n2 + P), rcount);

@@ -867,18 +867,21 @@ def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case):
         pairs = [synth.make_pair(20200423 + i, n_kpts=2048) for i in range(6)]
         args = _batch(pairs)
         recs = {}
-        for v in ("0", "1", "1"):
+        for v in ("0", "1", "1", "3", "3"):
             out = PairBatchRunner(ctx=ctx_with(v), iters=10000).run(*args)
             torch.cuda.synchronize()
             recs.setdefault(v, []).append(results_to_numpy(out["results"]))
-        a, b = recs["0"][0], recs["1"][0]
-        assert np.array_equal(recs["1"][0].view(np.uint8), recs["1"][1].view(np.uint8))
-        for f in ("status", "M", "K", "min_idx", "R", "T", "min_dist", "near_ties"):
-            assert np.array_equal(a[f], b[f]), f
-        # (a second-stage reference the gradient prunes no longer prunes for stage 2: a few
-        # rows may move to the coarse list, so the bound is on the total, not per row)
-        assert b["binned_rows"].sum() <= a["binned_rows"].sum()
-        print(f"binned rows lipschitz {a['binned_rows'].tolist()} -> grad {b['binned_rows'].tolist()}")
+        a = recs["0"][0]
+        for v in ("1", "3"):
+            b = recs[v][0]
+            assert np.array_equal(recs[v][0].view(np.uint8), recs[v][1].view(np.uint8))
+            for f in ("status", "M", "K", "min_idx", "R", "T", "min_dist", "near_ties"):
+                assert np.array_equal(a[f], b[f]), (v, f)
+            # (a second-stage reference the gradient prunes no longer prunes for stage 2: a few
+            # rows may move to the coarse list, so the bound is on the total, not per row)
+            assert b["binned_rows"].sum() <= a["binned_rows"].sum(), v
+            print(f"binned rows lipschitz {a['binned_rows'].tolist()} -> ERP_LIPG={v} "
+                  f"{b['binned_rows'].tolist()}")
         return
     rng = np.random.default_rng({"cluster": 21, "cluster_outliers": 22, "shell": 23,
                                  "two_clusters": 25}[case])
@@ -902,8 +905,11 @@ def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case):
     r0 = D.gpu_consensus(ctx_with("0"), "cuda")(rv, tv)
     r1 = D.gpu_consensus(ctx_with("1"), "cuda")(rv, tv)
     r2 = D.gpu_consensus(ctx_with("1"), "cuda")(rv, tv)
+    r3 = D.gpu_consensus(ctx_with("3"), "cuda")(rv, tv)
     assert r1.tobytes() == r2.tobytes()
-    for r in (r0, r1):
+    assert r3.tobytes() == D.gpu_consensus(ctx_with("3"), "cuda")(rv, tv).tobytes()
+    assert r3["binned_rows"] <= r0["binned_rows"] + 64, (r3["binned_rows"], r0["binned_rows"])
+    for r in (r0, r1, r3):
         assert r["status"] == 0 and r["min_idx"] == mi
         assert abs(r["min_dist"] - dref[mi]) <= 1e-12 * abs(dref[mi])
     assert r1["binned_rows"] <= r0["binned_rows"] + 64, (r1["binned_rows"], r0["binned_rows"])
