@@ -93,7 +93,7 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_inv3", "erp_rectify_matrices", "erp_consensus_hyps_shard_dev",
             "erp_consensus_hyps_finish_dev", "erp_surf_params_default",
             "erp_surf_detect_compute_dev", "erp_epipolar_draw_dev", "erp_draw_match_dev",
-            "erp_random_shuffle_prefix"]
+            "erp_random_shuffle_prefix", "erp_ctx_set_graphs"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
@@ -162,6 +162,7 @@ def load(build_if_missing: bool = False):
     L.erp_consensus_dev.argtypes = [P, P, P, C.c_int32, C.c_double, C.c_double, P, P]
     L.erp_ctx_set_profiling.argtypes = [P, C.c_int32]
     L.erp_ctx_set_matcher.argtypes = [P, C.c_int32]
+    L.erp_ctx_set_graphs.argtypes = [P, C.c_int32]
     L.erp_crop_rotated_image_dev.argtypes = [P, P, C.c_int32, C.c_int32, C.c_float, P, P]
     L.erp_spherical_bands_dev.argtypes = [P, P, C.c_int32, C.c_int32, C.c_int32, P, P]
     L.erp_rotate_keypoints_dev.argtypes = [P, P, C.c_int32, C.c_float, C.c_int32, C.c_int32, P]
@@ -222,6 +223,10 @@ class Context:
 
     def set_profiling(self, enable: bool = True):
         check(self.L.erp_ctx_set_profiling(self.h, 1 if enable else 0), "set_profiling")
+
+    def set_graphs(self, enable: bool = True):
+        """erp_ctx_set_graphs: replay erp_pair_batch_run's launch sequence as a HIP graph"""
+        check(self.L.erp_ctx_set_graphs(self.h, 1 if enable else 0), "set_graphs")
 
     def set_matcher(self, method: int):
         """erp_ctx_set_matcher: MATCHER_MFMA_FILTER (default) or MATCHER_VALU_EXACT."""

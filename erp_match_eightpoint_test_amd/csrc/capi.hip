@@ -118,6 +118,15 @@ struct erp_ctx {
     // accumulators leave room for one sampler wave per SIMD, and one wave alone issues VALU at
     // about a third of the rate four waves reach), so the default is the standalone pair
     bool fuse_sampler = getenv("ERP_FUSE_SAMPLER") && atoi(getenv("ERP_FUSE_SAMPLER")) != 0;
+    // HIP-graph replay of erp_pair_batch_run (erp_ctx_set_graphs): key bytes -> executable graph
+    bool use_graphs = getenv("ERP_GRAPHS") && atoi(getenv("ERP_GRAPHS")) != 0;
+    struct Graph {
+        std::vector<uint8_t> key;
+        hipGraphExec_t exec = nullptr;
+        uint64_t used = 0;
+    };
+    std::vector<Graph> graphs;
+    uint64_t graph_clock = 0;
     bool rtab_valid = false;  // rtab[d] = 1/d rounded up (the sampler's exact modulo)
     bool w0_valid = false;
     uint32_t w0_seed = 0;
@@ -290,6 +299,7 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
         if (b.p) (void)hipFree(b.p);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->done) (void)hipEventDestroy(ctx->done);
+    for (auto& g : ctx->graphs) (void)hipGraphExecDestroy(g.exec);
     delete ctx;
     return ERP_OK;
 }
@@ -709,6 +719,72 @@ erp_status erp_ctx_reserve(erp_ctx* ctx, int32_t n_pairs, int32_t max_nq, int32_
     return ensure_estimator(ctx, sh, nullptr);
 }
 
+}  // extern "C"
+
+namespace {
+
+// the enqueue part of erp_pair_batch_run (every allocation and host upload done before it)
+erp_status batch_enqueue(erp_ctx* ctx, const erp_pair_batch* b, float ratio,
+                         const erp_ransac_cfg* cfg, const erp_batch_outputs* out,
+                         const erp::BatchShape& sh, erp_dmatch* matches, hipStream_t st) {
+    ERP_CK(hipMemsetAsync(ctx->flags.p, 0, (size_t)sh.n_pairs * 4, st));
+    erp_status es = run_matcher(ctx, b->desc_l, b->desc_r, b->off_l, b->off_r, sh, ratio, matches,
+                                (int32_t*)ctx->counts.p, (int32_t*)ctx->flags.p, st);
+    if (es != ERP_OK) return es;
+    {
+        StageTimer _t(ctx, ERP_STAGE_BEARINGS, st);
+        ERP_CK(erp::launch_bearings_from_matches(matches, (int32_t*)ctx->counts.p, b->kp_l, b->kp_r,
+                                                 b->off_l, b->off_r, b->width, b->height, sh,
+                                                 (double*)ctx->pts.p, out->key_left, out->key_right,
+                                                 st));
+    }
+    return run_estimator(ctx, sh, cfg, out, out->results, st);
+}
+
+template <class T>
+void key_put(std::vector<uint8_t>& k, const T& v) {
+    const uint8_t* p = reinterpret_cast<const uint8_t*>(&v);
+    k.insert(k.end(), p, p + sizeof(T));
+}
+
+// everything a captured pipeline bakes in: the call's structs and the context's scratch pointers
+// and knobs
+std::vector<uint8_t> graph_key(const erp_ctx* c, const erp_pair_batch* b, float ratio,
+                               const erp_ransac_cfg* cfg, const erp_batch_outputs* out) {
+    std::vector<uint8_t> k;
+    key_put(k, *b);
+    key_put(k, *cfg);
+    key_put(k, *out);
+    key_put(k, ratio);
+    key_put(k, c->matcher);
+    key_put(k, c->zoom);
+    key_put(k, c->bound_ratio);
+    key_put(k, c->zoom_refs);
+    key_put(k, c->lip2);
+    key_put(k, c->lipg);
+    key_put(k, c->lipg_fac);
+    key_put(k, c->fuse_sampler);
+    const DevBuf* all[] = {&c->mblk, &c->zsel, &c->part, &c->part1, &c->pu, &c->ccount, &c->cand,
+                           &c->bsel, &c->edges, &c->gfin, &c->matches, &c->counts, &c->flags,
+                           &c->pts, &c->polyR, &c->polyQ, &c->idx, &c->gram, &c->hyps, &c->rv,
+                           &c->tv, &c->kcount, &c->tmean, &c->sortbuf, &c->w0, &c->results,
+                           &c->dscale, &c->lb, &c->ub, &c->surv, &c->nsurv, &c->wins, &c->rtab,
+                           &c->limbs, &c->tsplit, &c->ovf, &c->vchunk, &c->lipref, &c->inl};
+    for (const DevBuf* d : all) key_put(k, d->p);
+    return k;
+}
+
+}  // namespace
+
+extern "C" {
+
+erp_status erp_ctx_set_graphs(erp_ctx* ctx, int32_t enable) {
+    if (!ctx) return ERP_INVALID_ARG;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    ctx->use_graphs = enable != 0;
+    return ERP_OK;
+}
+
 erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* b, float ratio,
                               const erp_ransac_cfg* cfg, const erp_batch_outputs* out,
                               void* stream) {
@@ -733,18 +809,39 @@ erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* b, float ratio
     if (es != ERP_OK) return es;
     es = upload_w0(ctx, cfg, st);
     if (es != ERP_OK) return es;
-    ERP_CK(hipMemsetAsync(ctx->flags.p, 0, (size_t)sh.n_pairs * 4, st));
-    es = run_matcher(ctx, b->desc_l, b->desc_r, b->off_l, b->off_r, sh, ratio, matches,
-                     (int32_t*)ctx->counts.p, (int32_t*)ctx->flags.p, st);
-    if (es != ERP_OK) return es;
-    {
-        StageTimer _t(ctx, ERP_STAGE_BEARINGS, st);
-        ERP_CK(erp::launch_bearings_from_matches(matches, (int32_t*)ctx->counts.p, b->kp_l, b->kp_r,
-                                                 b->off_l, b->off_r, b->width, b->height, sh,
-                                                 (double*)ctx->pts.p, out->key_left, out->key_right,
-                                                 st));
+    if (cfg->inlier_thr > 0.0f && !ensure(ctx->inl, erp::inlier_scratch_bytes(sh)))
+        return ERP_OUT_OF_MEMORY;
+    if (!ctx->use_graphs || ctx->profiling || st == nullptr)
+        return batch_enqueue(ctx, b, ratio, cfg, out, sh, matches, st);
+    // graph replay: the same call (structs, buffers, scratch) as a captured one -> one launch
+    std::vector<uint8_t> key = graph_key(ctx, b, ratio, cfg, out);
+    for (auto& g : ctx->graphs)
+        if (g.key == key) {
+            g.used = ++ctx->graph_clock;
+            ERP_CK(hipGraphLaunch(g.exec, st));
+            return ERP_OK;
+        }
+    ERP_CK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+    es = batch_enqueue(ctx, b, ratio, cfg, out, sh, matches, st);
+    hipGraph_t graph = nullptr;
+    const hipError_t ce = hipStreamEndCapture(st, &graph);
+    if (es != ERP_OK || ce != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        return es != ERP_OK ? es : ERP_HIP_ERROR;
     }
-    return run_estimator(ctx, sh, cfg, out, out->results, st);
+    hipGraphExec_t exec = nullptr;
+    const hipError_t ie = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (ie != hipSuccess) return ERP_HIP_ERROR;
+    if (ctx->graphs.size() >= 8) {  // drop the least recently used
+        auto lru = std::min_element(ctx->graphs.begin(), ctx->graphs.end(),
+                                    [](const auto& x, const auto& y) { return x.used < y.used; });
+        (void)hipGraphExecDestroy(lru->exec);
+        ctx->graphs.erase(lru);
+    }
+    ctx->graphs.push_back({std::move(key), exec, ++ctx->graph_clock});
+    ERP_CK(hipGraphLaunch(exec, st));
+    return ERP_OK;
 }
 
 erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,

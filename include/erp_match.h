@@ -223,6 +223,14 @@ typedef enum erp_matcher_method {
     ERP_MATCHER_VALU_EXACT = 1
 } erp_matcher_method;
 erp_status erp_ctx_set_matcher(erp_ctx* ctx, int32_t method);
+/* enable != 0: erp_pair_batch_run captures its launch sequence (every kernel and memset of the
+   pipeline, ~60 nodes) into a HIP graph the first time it sees a (batch, cfg, outputs, ratio,
+   scratch) combination and replays that graph on later calls with the same one -- one launch
+   instead of ~60, for the latency of small batches (configs[1]'s single pair).  Pointers are
+   baked into the graph: a call with other buffers, or one that grows the context's scratch,
+   captures anew (up to 8 graphs per context, least recently used dropped).  Not used while
+   stage timing is on or on the NULL stream.  Default off. */
+erp_status erp_ctx_set_graphs(erp_ctx* ctx, int32_t enable);
 
 /* device pointers; writes up to nq matches in ascending queryIdx order and *d_count. */
 erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,

@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def probe(runs: int, kpts: int, iters: int, seed: int) -> dict:
+def probe(runs: int, kpts: int, iters: int, seed: int, graphs: bool = False) -> dict:
     import torch
 
     from erp_match_eightpoint_test_amd import Context, PairBatchRunner, synth
@@ -36,11 +36,12 @@ def probe(runs: int, kpts: int, iters: int, seed: int) -> dict:
             t(np.array([0, kpts], np.int64)), t(np.array([0, kpts], np.int64)),
             t(np.array([p["W"]], np.int32)), t(np.array([p["H"]], np.int32)), kpts, kpts)
     ctx = Context(0)
-    run = PairBatchRunner(ctx=ctx, iters=iters)
+    ctx.set_graphs(graphs)  # erp_ctx_set_graphs: replay the captured launch sequence
+    run = PairBatchRunner(ctx=ctx, iters=iters, reuse_outputs=True)
+    st = torch.cuda.Stream(dev)  # (graphs need a capturable, non-NULL stream)
     run.reserve(1, kpts, kpts)
-    st = torch.cuda.current_stream(dev)
     for _ in range(3):
-        run.run(*args)
+        run.run(*args, stream=st.cuda_stream)
     torch.cuda.synchronize()
     host, enq = [], []
     for _ in range(runs):
@@ -54,7 +55,7 @@ def probe(runs: int, kpts: int, iters: int, seed: int) -> dict:
         host.append(t2 - t0)
     return {"single_pair_ms_median": float(np.median(host)) * 1e3,
             "enqueue_ms_median": float(np.median(enq)) * 1e3, "runs": runs, "kpts": kpts,
-            "iters": iters}
+            "iters": iters, "hip_graph": graphs}
 
 
 def _short(n: str) -> str:
@@ -97,6 +98,7 @@ def main():
     ap.add_argument("--kpts", type=int, default=4096)
     ap.add_argument("--iters", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=20200423)
+    ap.add_argument("--graph", action="store_true", help="erp_ctx_set_graphs: HIP-graph replay")
     ap.add_argument("--report", default=None, help="rocprofv3 run_kernel_trace.csv to split")
     ap.add_argument("--host-json", default=None, help="merge this probe() record into --report")
     a = ap.parse_args()
@@ -106,7 +108,7 @@ def main():
             r["host"] = json.load(open(a.host_json))
         print(json.dumps(r, indent=1))
         return
-    print(json.dumps(probe(a.runs, a.kpts, a.iters, a.seed)))
+    print(json.dumps(probe(a.runs, a.kpts, a.iters, a.seed, a.graph)))
 
 
 if __name__ == "__main__":

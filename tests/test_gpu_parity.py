@@ -335,6 +335,39 @@ def test_batch_pipeline_vs_oracle(ctx, oracle):
         assert np.allclose(d[live], dref[live], rtol=1e-12, atol=0)
 
 
+def test_batch_pipeline_hip_graph_replay(gpu_lib):
+    """erp_ctx_set_graphs: the first call captures the pipeline into a HIP graph, the next calls
+    with the same buffers replay it; other buffers or a grown scratch capture anew.  Every
+    result (and match list) equals the plain launch sequence's, byte for byte."""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner
+    pairs = [synth.make_pair(3100 + i, n_kpts=n) for i, n in enumerate([600, 900, 300])]
+    args = _batch(pairs)
+    ref = PairBatchRunner(ctx=Context(0), iters=300).run(*args, want=("matches",))
+    cg = Context(0)
+    cg.set_graphs(True)
+    run = PairBatchRunner(ctx=cg, iters=300, reuse_outputs=True)
+    st = torch.cuda.Stream()
+    outs = []
+    with torch.cuda.stream(st):
+        for _ in range(3):  # capture, replay, replay (same output buffers: reuse one dict)
+            o = run.run(*args, want=("matches",), stream=st.cuda_stream)
+            outs.append({k: v.clone() for k, v in o.items()})
+        st.synchronize()
+    for o in outs:
+        assert torch.equal(o["results"], ref["results"])
+        assert torch.equal(o["matches"], ref["matches"])
+    # a larger batch on the same context (grown scratch, new buffers): a new capture, correct
+    pairs2 = [synth.make_pair(3200 + i, n_kpts=1500) for i in range(4)]
+    args2 = _batch(pairs2)
+    ref2 = PairBatchRunner(ctx=Context(0), iters=300).run(*args2)
+    with torch.cuda.stream(st):
+        o2 = run.run(*args2, stream=st.cuda_stream)
+        st.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(o2["results"], ref2["results"])
+
+
 def test_batch_pipeline_valu_matcher_equals_mfma(gpu_lib):
     """the whole batch pipeline with the packed-FP32 exact sweep as the matcher: matches and
     results identical to the MFMA-filter pipeline (ragged pair sizes, several train chunks)"""
