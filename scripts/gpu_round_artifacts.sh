@@ -40,6 +40,9 @@ if [ "${EXTRA_BENCH:-0}" = "1" ]; then
   echo "== single-pair latency (host) + kernel trace" && timeout -k 10 300 python scripts/latency_probe.py --runs 20 \
     > gpurun_out/latency_host_${TAG}.json 2> gpurun_out/latency_${TAG}.err || { tail -20 gpurun_out/latency_${TAG}.err; exit 1; }
   cat gpurun_out/latency_host_${TAG}.json
+  timeout -k 10 300 python scripts/latency_probe.py --runs 20 --graph > gpurun_out/latency_host_graph_${TAG}.json \
+    2>> gpurun_out/latency_${TAG}.err || { tail -20 gpurun_out/latency_${TAG}.err; exit 1; }
+  cat gpurun_out/latency_host_graph_${TAG}.json
   timeout -k 10 300 rocprofv3 --kernel-trace -d gpurun_out/lat_${TAG} -o run --output-format csv -- \
     python3 scripts/latency_probe.py --runs 20 > gpurun_out/lat_${TAG}.log 2>&1 || { tail -20 gpurun_out/lat_${TAG}.log; exit 1; }
 fi
