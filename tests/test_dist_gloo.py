@@ -325,3 +325,23 @@ def test_gather_records_gloo(oracle):
                         oracle.make_cfg(iters=30))
         assert int(r["M"]) == len(mt) and int(r["K"]) == o["K"] and int(r["min_idx"]) == o["min_idx"]
         assert np.array_equal(r["R"], o["R"]) and np.array_equal(r["T"], o["T"])
+
+
+def test_min_idx_agrees_rule():
+    """the parity checks' consensus-index rule (bench.parity_check and dist.check_gathered):
+    equal indices agree; indices one apart agree only when they are the R1 / R2 rows of ONE
+    iteration (R1 then R2 pushed per iteration, src/eight_point.cpp:113-126); anything else,
+    or a +-1 without the validity flags, is a mismatch"""
+    from erp_match_eightpoint_test_amd.dist import min_idx_agrees
+    r1 = np.array([1, 0, 1, 1, 0, 1])
+    r2 = np.array([1, 1, 0, 1, 0, 1])
+    # rows: it0 -> 0, 1; it1 -> 2; it2 -> 3; it3 -> 4, 5; it4 -> none; it5 -> 6, 7
+    assert min_idx_agrees(3, 3, r1, r2) == (True, False)
+    assert min_idx_agrees(0, 1, r1, r2) == (True, True)
+    assert min_idx_agrees(5, 4, r1, r2) == (True, True)
+    assert min_idx_agrees(7, 6, r1, r2) == (True, True)
+    assert min_idx_agrees(1, 2, r1, r2) == (False, False)   # different iterations
+    assert min_idx_agrees(2, 3, r1, r2) == (False, False)
+    assert min_idx_agrees(5, 6, r1, r2) == (False, False)
+    assert min_idx_agrees(0, 2, r1, r2) == (False, False)   # two apart
+    assert min_idx_agrees(0, 1) == (False, False)           # no flags: strict
