@@ -182,7 +182,11 @@ def test_real_building2_matches_reference_output(api):
 
 # (rotation, T) gap bars in degrees against the reference's recovered estimate: the measured
 # gaps of this deterministic pipeline (profiles/r04_real_gaps.json) plus a stated margin
-GAP_BARS = {"building": (1.5, 20.0), "building2": (1.5, 20.0)}
+# (round 4 measurement, profiles/r04_real_gaps.json: building 0.72 deg / 8.71 deg, building2
+# 0.29 deg / 4.05 deg).  T is compared as an AXIS: its sign follows the sign of the winning
+# iteration's E (decomposeEssentialMat's U column), which any difference in the match set can
+# flip -- building2's T points the other way (175.95 deg) along the same axis (4.05 deg).
+GAP_BARS = {"building": (1.0, 12.0), "building2": (0.5, 7.0)}
 
 
 @pytest.mark.parametrize("pair,left,right", [
@@ -207,14 +211,15 @@ def test_real_estimate_vs_recovered_reference(api, pair, left, right):
     out = os.environ.get("ERP_REAL_GAPS_OUT")
     if out:  # the round's artifact run records the gaps (profiles/r04_real_gaps.json)
         rec = json.load(open(out)) if os.path.exists(out) else {}
-        rec[pair] = {"rotation_gap_deg": dR, "T_gap_deg": dT, "M": int(M),
+        rec[pair] = {"rotation_gap_deg": dR, "T_gap_deg": dT, "T_axis_gap_deg": min(dT, 180.0 - dT),
+                     "M": int(M),
                      "K": int(ep.last_result["K"]), "R_ours": [float(x) for x in R],
                      "T_ours": [float(x) for x in T], "R_ref": list(map(float, ref["R_vec"])),
                      "T_ref": list(map(float, ref["T_vec"])),
                      "bar_rotation_deg": GAP_BARS[pair][0], "bar_T_deg": GAP_BARS[pair][1]}
         json.dump(rec, open(out, "w"), indent=1)
     assert dR < GAP_BARS[pair][0], dR
-    assert dT < GAP_BARS[pair][1], dT
+    assert min(dT, 180.0 - dT) < GAP_BARS[pair][1], dT
 
 
 def test_real_building_matches_reference_output(api):
