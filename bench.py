@@ -862,7 +862,7 @@ def main():
                  "binned_rows_mean": float(wres["binned_rows"].mean())}
         if world == 1 and not args.no_cpu_baseline:
             threads, _ = host_cpu_share()
-            n_w = 1
+            n_w = min(3, len(wb[0]["width"]))  # (the first is a two-cluster pair, K = 2 iters)
             ora_w = [oracle_pair(p, args.iters, threads) for p in wpairs[:n_w]]
             sb = subs[0]
             b = wb[0]

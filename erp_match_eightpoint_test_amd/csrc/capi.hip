@@ -113,6 +113,14 @@ struct erp_ctx {
     // UB <= U * ERP_LIPG_FAC
     int lipg = getenv("ERP_LIPG") ? atoi(getenv("ERP_LIPG")) : 1;
     float lipg_fac = getenv("ERP_LIPG_FAC") ? (float)atof(getenv("ERP_LIPG_FAC")) : 1.1f;
+    // the refine pass's sub-bins placed on each row's Lipschitz interval around one survivor's
+    // exact rank keys (kernels.hip consensus_hint_kernel / refine_windows; ERP_REFINE_HINT=0
+    // for A/B: the boundary bins' fixed sub-bins)
+    int refine_hint = getenv("ERP_REFINE_HINT") ? atoi(getenv("ERP_REFINE_HINT")) : 1;
+    // flat pairs (the first-stage pruning kept more than this % of the rows): their first-stage
+    // references refined and the first stage re-run against them (kernels.hip
+    // consensus_flat_gate_kernel; ERP_FLAT_REFS=0 for A/B)
+    int flat_refs = getenv("ERP_FLAT_REFS") ? atoi(getenv("ERP_FLAT_REFS")) : 25;
     // the sampler and the Gram as one kernel (sampler_gram_kernel, opt-in ERP_FUSE_SAMPLER=1):
     // measured 1.6x SLOWER than the two standalone kernels (the Gram's int32
     // accumulators leave room for one sampler wave per SIMD, and one wave alone issues VALU at
@@ -591,7 +599,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (int32_t*)c->nsurv.p + sh.n_pairs,
                                             (int32_t*)c->zsel.p, c->zoom_refs, c->lip2,
                                             (int32_t*)c->sortbuf.p, c->lipref.p, c->lipg,
-                                            c->lipg_fac, st));
+                                            c->lipg_fac, c->flat_refs, c->refine_hint, st));
     }
     if (phase == 1) return ERP_OK;
     if (phase == 2)  // the bounds ran per shard (binned rows not combined): report -1
@@ -624,7 +632,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
                                             bselp, lbp,
-                                            ubp, (int32_t*)c->sortbuf.p, c->lipref.p, st));
+                                            ubp, (int32_t*)c->sortbuf.p, c->lipref.p,
+                                            c->refine_hint, st));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
@@ -763,6 +772,8 @@ std::vector<uint8_t> graph_key(const erp_ctx* c, const erp_pair_batch* b, float 
     key_put(k, c->lip2);
     key_put(k, c->lipg);
     key_put(k, c->lipg_fac);
+    key_put(k, c->refine_hint);
+    key_put(k, c->flat_refs);
     key_put(k, c->fuse_sampler);
     const DevBuf* all[] = {&c->mblk, &c->zsel, &c->part, &c->part1, &c->pu, &c->ccount, &c->cand,
                            &c->bsel, &c->edges, &c->gfin, &c->matches, &c->counts, &c->flags,

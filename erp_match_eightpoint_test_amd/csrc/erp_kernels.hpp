@@ -181,7 +181,8 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
                                    int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
-                                   void* lipref, int lipg, float gfac, hipStream_t st);
+                                   void* lipref, int lipg, float gfac, int flat_pct,
+                                   int use_hint, hipStream_t st);
 size_t lipref_bytes(int n_pairs, int stride);
 // survivors = rows with LB <= min UB (again = 1: only pairs the refine pass touched)
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,
@@ -193,7 +194,7 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
                                    const BatchShape& sh, double trim_lo, double trim_hi,
                                    const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
                                    double* lb, double* ub, int32_t* list2, void* lipref,
-                                   hipStream_t st);
+                                   int use_hint, hipStream_t st);
 hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const float* dscale,
                                  const BatchShape& sh, double trim_lo, double trim_hi,
                                  const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,

@@ -1818,16 +1818,16 @@ __device__ long block_sum_i64(long v, double* red) {
     return s;
 }
 
-// Window sum of row i (ranks [lo, hi)) by a 3-level radix select (11+11+10 bits) on the f32
-// bit patterns of the squared distances s (sqrtf is monotone, so the sorted distances are
-// sqrtf of the sorted s), then the sum of sqrtf(s) in fp64.  Four passes over the row; the
-// general fallback of consensus_rows.  Returns the sum on every thread.
-__device__ double radix_window_sum(const float* X, const float* Y, const float* Z, int K,
-                                   float xi, float yi, float zi, long lo, long hi,
-                                   uint32_t* histA, uint32_t* histB, int* ws, int* res,
-                                   double* red) {
+struct RankKeys {
+    uint32_t va, vb;  // the keys at ranks lo and hi-1
+    long lt_a, le_a;  // #keys < va, #keys <= va
+    long lt_b;        // #keys < vb
+};
+// the f32 keys of ranks ra and rb of row i by a 3-level radix select (three passes)
+__device__ RankKeys radix_rank_keys(const float* X, const float* Y, const float* Z, int K,
+                                    float xi, float yi, float zi, long ra, long rb,
+                                    uint32_t* histA, uint32_t* histB, int* ws, int* res) {
     const int tid = threadIdx.x;
-    const long ra = lo, rb = hi - 1;
     for (int k = tid; k < 2048; k += 256) histA[k] = 0;
     __syncthreads();
     for (int j = tid; j < K; j += 256) {
@@ -1870,11 +1870,28 @@ __device__ double radix_window_sum(const float* X, const float* Y, const float* 
     long ca2, cb2;
     const int ba2 = find_bin<2048>(histA, ra - ca - ca1, &ca2, ws, res);
     const int bb2 = find_bin<2048>(histB, rb - cb - cb1, &cb2, ws, res);
-    const uint32_t va = (pa << 10) | (uint32_t)ba2;  // key at rank lo
-    const uint32_t vb = (pb << 10) | (uint32_t)bb2;  // key at rank hi-1
-    const long lt_a = ca + ca1 + ca2;                // #keys < va
-    const long le_a = lt_a + histA[ba2];             // #keys <= va
-    const long lt_b = cb + cb1 + cb2;                // #keys < vb
+    RankKeys r;
+    r.va = (pa << 10) | (uint32_t)ba2;  // key at rank ra
+    r.vb = (pb << 10) | (uint32_t)bb2;  // key at rank rb
+    r.lt_a = ca + ca1 + ca2;
+    r.le_a = r.lt_a + histA[ba2];
+    r.lt_b = cb + cb1 + cb2;
+    __syncthreads();  // the histograms' readers are done before the caller reuses them
+    return r;
+}
+
+// Window sum of row i (ranks [lo, hi)) by a 3-level radix select (11+11+10 bits) on the f32
+// bit patterns of the squared distances s (sqrtf is monotone, so the sorted distances are
+// sqrtf of the sorted s), then the sum of sqrtf(s) in fp64.  Four passes over the row; the
+// general fallback of consensus_rows.  Returns the sum on every thread.
+__device__ double radix_window_sum(const float* X, const float* Y, const float* Z, int K,
+                                   float xi, float yi, float zi, long lo, long hi,
+                                   uint32_t* histA, uint32_t* histB, int* ws, int* res,
+                                   double* red) {
+    const int tid = threadIdx.x;
+    const RankKeys rk = radix_rank_keys(X, Y, Z, K, xi, yi, zi, lo, hi - 1, histA, histB, ws, res);
+    const uint32_t va = rk.va, vb = rk.vb;
+    const long le_a = rk.le_a, lt_b = rk.lt_b;
     double acc = 0.0;
     for (int j = tid; j < K; j += 256) {
         const uint32_t key = __float_as_uint(rdist2(xi, yi, zi, X[j], Y[j], Z[j]));
@@ -2294,10 +2311,12 @@ __global__ __launch_bounds__(256) void consensus_lip_refs_kernel(
     double trim_hi, const double* __restrict__ lb, const double* __restrict__ ub,
     const int32_t* __restrict__ slist, const int32_t* __restrict__ scount, int lstep, int shard,
     int nshards, const int32_t* __restrict__ zb, float4* __restrict__ lref,
-    double* __restrict__ lU, int32_t* __restrict__ lcnt, int cap) {
+    double* __restrict__ lU, int32_t* __restrict__ lcnt, int cap,
+    const int32_t* __restrict__ gate = nullptr) {
     __shared__ double red[4];
     __shared__ int nlive;
     const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
+    if (gate && gate[p] <= 0) return;  // (the flat-pair re-run: other pairs keep their refs)
     const int K = kcount[p];
     const int ra = slist ? 0 : (int)((int64_t)K * shard / nshards);
     const int n = slist ? scount[p] : (int)((int64_t)K * (shard + 1) / nshards) - ra;
@@ -2534,9 +2553,10 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     const float4* __restrict__ lref, const double* __restrict__ lU,
     const int32_t* __restrict__ lcnt, int cap, int32_t* __restrict__ r2list,
     int32_t* __restrict__ r2cnt, const float4* __restrict__ gref, const int32_t* __restrict__ gcnt,
-    int gcap) {
+    int gcap, const int32_t* __restrict__ gate = nullptr) {
     __shared__ LipShared sh;
     const int p = blockIdx.y, tid = threadIdx.x, lane = wave_lane();
+    if (gate && gate[p] <= 0) return;  // (the flat-pair re-run: other pairs keep their lists)
     const int K = kcount[p];
     const int ra = slist ? 0 : (int)((int64_t)K * shard / nshards);
     const int n = slist ? scount[p] : (int)((int64_t)K * (shard + 1) / nshards) - ra;
@@ -2631,16 +2651,73 @@ __device__ __forceinline__ void for_columns(const float* __restrict__ X, const f
     }
 }
 
+// Rank-key windows of the refine pass (round 4).  Default: the boundary bins b_a, b_b of the
+// bounds pass, 1024 sub-bins of 2^kLowBits keys each.  With a hint (consensus_hint_kernel: the
+// exact keys va, vb at ranks lo and hi-1 of one survivor h of the pair), the order statistics'
+// 1-Lipschitz property puts row i's rank-lo distance within d(i, h) of sqrtf(va) (and likewise
+// for hi-1), so the 1024 sub-bins go on that key interval instead, 2^w keys each with the
+// smallest w that covers it -- kept only when finer than the bin's own sub-bins.  A two-cluster
+// set (R1 and R2 valid in every iteration) is why: all of the far cluster's distances fall in
+// ONE bin, so the window's ~6 000 elements there were bracketed at 2^9 keys each (a relative
+// bound width ~2e-5, ~1 700 survivors per pair into the exact pass); on the interval they are
+// bracketed at 2^2-2^3 keys.  The window placement is only a heuristic: a rank that falls
+// outside its window fails the `ok` test below and the row keeps its old bounds.
+struct RefineWin {
+    uint32_t a0, a1, b0, b1;  // key windows [a0, a1) (rank lo), [b0, b1) (rank hi-1)
+    int wa, wb;               // sub-bin k of a window covers keys [x0 + (k << w), + 2^w)
+};
+__device__ __forceinline__ bool refine_interval(float dc, float delta, uint32_t* k0, int* w) {
+    const float hw = delta * 1.0001f + dc * 0x1p-17f + 0x1p-100f;
+    const float dl = fmaxf(dc - hw, 0.f), dh = dc + hw;
+    const uint32_t klo = __float_as_uint(dl * dl * (1.f - 0x1p-20f));
+    const uint32_t khi = __float_as_uint(dh * dh * (1.f + 0x1p-20f)) + 1u;
+    const uint32_t span = khi - klo;
+    const int ww = span <= (uint32_t)kNS ? 0 : 32 - __builtin_clz(span - 1u) - kSubBits;
+    *k0 = klo;
+    *w = ww;
+    return ww < kLowBits && khi < 0x7f800000u;
+}
+__device__ __forceinline__ RefineWin refine_windows(int ba, int bb, float xi, float yi, float zi,
+                                                    const float4* __restrict__ hint, int p) {
+    RefineWin W;
+    W.a0 = (uint32_t)ba << kBinShift;
+    W.a1 = (uint32_t)(ba + 1) << kBinShift;
+    W.b0 = (uint32_t)bb << kBinShift;
+    W.b1 = (uint32_t)(bb + 1) << kBinShift;
+    W.wa = W.wb = kLowBits;
+    if (!hint) return W;
+    const float4 h = hint[2 * p];
+    if (!(h.w > 0.f)) return W;
+    const float4 hk = hint[2 * p + 1];
+    const float delta = __builtin_sqrtf(rdist2(xi, yi, zi, h.x, h.y, h.z));
+    RefineWin A = W;
+    uint32_t k0;
+    int w;
+    if (refine_interval(__builtin_sqrtf(hk.x), delta, &k0, &w)) {
+        A.a0 = k0;
+        A.a1 = k0 + ((uint32_t)kNS << w);
+        A.wa = w;
+    }
+    if (refine_interval(__builtin_sqrtf(hk.y), delta, &k0, &w)) {
+        A.b0 = k0;
+        A.b1 = k0 + ((uint32_t)kNS << w);
+        A.wb = w;
+    }
+    // disjoint and in order, or identical (the default windows of one bin): else the default
+    if ((A.a0 == A.b0 && A.wa == A.wb) || A.a1 <= A.b0) return A;
+    return W;
+}
+
 // Tighter bounds for the surviving rows (4 per block, lanes rotating over the rows as in the
 // bounds kernel).  For each row: the exact s of every column (the reference's expression),
-// an fp64 sum of sqrt(s) (raw v_sqrt_f32, bracketed by its 2^-22 error bound) over the bins
-// strictly between b_a and b_b (the bins of ranks lo and
-// hi-1 from the bounds kernel), exact counts below them, and 1024-way sub-histograms (key bits
-// 18..9) of the two boundary bins.  The window's part inside a boundary bin is bracketed with
-// sub-bin resolution (2^-15 relative instead of 2^-5), so the bounds tighten by ~1000x and the
-// next selection keeps only genuine near-ties -- this is what makes a two-cluster row set
-// (R1 and R2 valid in every iteration: every row's mean within 1 % of the minimum) cheap.
-// A row whose ranks do not fall into b_a / b_b under the exact binning keeps its old bounds.
+// an fp64 sum of sqrt(s) (raw v_sqrt_f32, bracketed by its 2^-22 error bound) over the keys
+// strictly between the two rank windows (refine_windows: by default the bins b_a, b_b of ranks
+// lo and hi-1 from the bounds kernel), exact counts below them, and 1024-way sub-histograms of
+// the two windows.  The window's part inside them is bracketed with sub-bin resolution (2^-15
+// relative instead of 2^-5 with the default windows; 2^-20..2^-21 on hinted intervals), so the
+// bounds tighten by ~1000x and the next selection keeps only genuine near-ties -- this is what
+// makes a two-cluster row set (every row's mean within 1 % of the minimum) cheap.
+// A row whose ranks do not fall into its windows under the exact binning keeps its old bounds.
 __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
                                        const float* __restrict__ rv,
                                        const float* __restrict__ dscale, int stride,
@@ -2650,7 +2727,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
                                        const int32_t* __restrict__ bsel, double* __restrict__ lb,
                                        double* __restrict__ ub, const int32_t* __restrict__ list,
                                        int lstride, const int32_t* __restrict__ lcount, int step,
-                                       int p, int vb) {
+                                       const float4* __restrict__ hint, int p, int vb) {
     __shared__ uint32_t sub[kRefineRows][2][kNS];
     __shared__ double inner[kRefineRows];
     __shared__ int below[kRefineRows][2];
@@ -2669,10 +2746,13 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     const float* Y = X + stride;
     const float* Z = Y + stride;
     const int base = bounds_elo(dscale[p]) << kMantBits;
-    const int32_t* S = list + (size_t)p * lstride;
-    auto srow = [&](int k) { return (int)S[(size_t)k * step]; };
+    // (list == nullptr: the rows 0, step, 2 step, ... themselves -- the first-stage references
+    // of a flat pair, launch_consensus_bounds)
+    const int32_t* S = list ? list + (size_t)p * lstride : nullptr;
+    auto srow = [&](int k) { return S ? (int)S[(size_t)k * step] : k * step; };
     float xi[kRefineRows], yi[kRefineRows], zi[kRefineRows];
-    int ba[kRefineRows], bb[kRefineRows];
+    uint32_t a0[kRefineRows], b0[kRefineRows];  // the windows (a1 = a0 + (kNS << wa), ...)
+    int wa[kRefineRows], wb[kRefineRows];
     float acc[kRefineRows];  // per-thread partial sums (<= ceil(K/256) terms; bracketed below)
     int bel_a[kRefineRows], bel_b[kRefineRows];
 #pragma unroll
@@ -2682,8 +2762,13 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
         xi[t] = X[row];
         yi[t] = Y[row];
         zi[t] = Z[row];
-        ba[t] = bsel[((size_t)p * stride + row) * 2] + base;   // as key >> kBinShift
-        bb[t] = bsel[((size_t)p * stride + row) * 2 + 1] + base;
+        const RefineWin W = refine_windows(bsel[((size_t)p * stride + row) * 2] + base,
+                                           bsel[((size_t)p * stride + row) * 2 + 1] + base,
+                                           xi[t], yi[t], zi[t], hint, p);
+        a0[t] = W.a0;
+        b0[t] = W.b0;
+        wa[t] = W.wa;
+        wb[t] = W.wb;
         acc[t] = 0.f;
         bel_a[t] = 0;
         bel_b[t] = 0;
@@ -2700,15 +2785,18 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
         for (int t = 0; t < kRefineRows; t++) {
             const float s = rdist2(xi[t], yi[t], zi[t], xj, yj, zj);
             const uint32_t key = __float_as_uint(s);
-            const int e = (int)(key >> kBinShift);
-            bel_a[t] += e < ba[t];
-            bel_b[t] += e < bb[t];
-            // branch-free inner sum (raw v_sqrt_f32, <= 1 ulp; f32 accumulation) -- only the
-            // boundary-bin counts take a (short, divergent) branch
-            acc[t] += (e > ba[t] && e < bb[t]) ? __builtin_amdgcn_sqrtf(s) : 0.f;
-            if (e == ba[t] || e == bb[t]) {
+            const bool ba_ = key < a0[t], bb_ = key < b0[t];
+            bel_a[t] += ba_;
+            bel_b[t] += bb_;
+            // sub-bin indices (a key below a window wraps to a huge index)
+            const uint32_t ia = (key - a0[t]) >> wa[t], ib = (key - b0[t]) >> wb[t];
+            const bool ina = ia < (uint32_t)kNS;
+            // branch-free inner sum (raw v_sqrt_f32, <= 1 ulp; f32 accumulation) over the keys
+            // in [a1, b0) -- only the window counts take a (short, divergent) branch
+            acc[t] += (!ba_ && !ina && bb_) ? __builtin_amdgcn_sqrtf(s) : 0.f;
+            if (ina || ib < (uint32_t)kNS) {
                 const int r = (lane + t) & (kRefineRows - 1);
-                atomicAdd(&sub[r][e == ba[t] ? 0 : 1][(key >> kLowBits) & (kNS - 1u)], 1u);
+                atomicAdd(&sub[r][ina ? 0 : 1][ina ? ia : ib], 1u);
             }
         }
     });
@@ -2720,22 +2808,21 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
         atomicAdd(&below[r][1], bel_b[t]);
     }
     __syncthreads();
-    // per row (one wave): bracket the window's part inside the two boundary bins
+    // per row (one wave): bracket the window's part inside the two key windows
     const int r = tid >> 6, sl = tid & 63;
     if (s0 + r >= nl) return;
     const int row = srow(s0 + r);
-    const int bA = bsel[((size_t)p * stride + row) * 2] + base;
-    const int bB = bsel[((size_t)p * stride + row) * 2 + 1] + base;
+    const RefineWin W = refine_windows(bsel[((size_t)p * stride + row) * 2] + base,
+                                       bsel[((size_t)p * stride + row) * 2 + 1] + base, X[row],
+                                       Y[row], Z[row], hint, p);
     const int cA = below[r][0], cB = below[r][1];
-    // sub-bin k of bin b (as key >> kBinShift) covers keys [((b << kSubBits) | k) << kLowBits,
-    // + 2^kLowBits)
-    // (k = 1024 is sub-bin 0 of bin b + 1: every d in sub-bin k is <= sub_lo(b, k + 1), as
-    // sqrtf is monotone)
-    auto sub_lo = [&](int b, int k) {
-        return (double)__builtin_sqrtf(__uint_as_float((uint32_t)((b << kSubBits) + k) << kLowBits));
+    // sub-bin k of a window [x0, ...) covers keys [x0 + (k << w), x0 + ((k + 1) << w)); every d
+    // in it is <= the lower edge of sub-bin k + 1 (sqrtf is monotone)
+    auto sub_lo = [&](uint32_t x0, int w, int k) {
+        return (double)__builtin_sqrtf(__uint_as_float(x0 + ((uint32_t)k << w)));
     };
-    // the window's ranks inside bin A: [max(lo, cA), min(hi, cA + nA)); inside bin B (when
-    // distinct): [cB, hi).  Count per sub-bin, clipped to those rank ranges, times the
+    // the window's ranks inside window A: [max(lo, cA), min(hi, cA + nA)); inside window B
+    // (when distinct): [cB, hi).  Count per sub-bin, clipped to those rank ranges, times the
     // sub-bin's d-range gives the bounds.
     double L = 0.0, U = 0.0;
     int nA = 0, nB = 0;
@@ -2748,13 +2835,14 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
         nA += __shfl_xor(nA, o, 64);
         nB += __shfl_xor(nB, o, 64);
     }
-    const bool same = bA == bB;
+    const bool same = W.a0 == W.b0;
     bool ok = cA <= lo && lo < cA + nA && (same ? (hi - 1 < cA + nA) : (cB <= hi - 1 && hi - 1 < cB + nB));
     if (ok) {
         // sub-bins in ascending order: thread sl owns k = 16 sl .. 16 sl + 15
         for (int part = 0; part < (same ? 1 : 2); part++) {
             const uint32_t* hh = sub[r][part];
-            const int b = part ? bB : bA;
+            const uint32_t x0 = part ? W.b0 : W.a0;
+            const int w = part ? W.wb : W.wa;
             const int c0 = part ? cB : cA;
             int cnt = 0;
             for (int q = 0; q < 16; q++) cnt += (int)hh[16 * sl + q];
@@ -2768,10 +2856,10 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
             for (int q = 0; q < 16; q++) {
                 const int k = 16 * sl + q;
                 const int n = (int)hh[k];
-                const int a0 = max(cum, lo), a1 = min(cum + n, hi);
-                if (a1 > a0) {  // (only the sub-bins the rank window overlaps)
-                    L += (double)(a1 - a0) * sub_lo(b, k);
-                    U += (double)(a1 - a0) * sub_lo(b, k + 1);
+                const int a0_ = max(cum, lo), a1_ = min(cum + n, hi);
+                if (a1_ > a0_) {  // (only the sub-bins the rank window overlaps)
+                    L += (double)(a1_ - a0_) * sub_lo(x0, w, k);
+                    U += (double)(a1_ - a0_) * sub_lo(x0, w, k + 1);
                 }
                 cum += n;
             }
@@ -2796,6 +2884,76 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
         double* up = ub + (size_t)p * stride + row;
         *lp = fmax(*lp, nl);
         *up = fmin(*up, nu);
+    }
+}
+
+// The refine pass's rank-key hint (refine_windows): per pair with > kRefineMin survivors, the
+// survivor h with the smallest UB (lowest row on ties) and the exact keys va, vb at its ranks
+// lo and hi-1 (radix_rank_keys: three passes over the pair's K columns, one block per pair).
+// hint[2p] = (x_h, y_h, z_h, 1), hint[2p + 1] = (va, vb) as floats; (.., 0) = no hint.
+// surv == nullptr: the candidates are the rows 0, step, 2 step, ... < nsurv[p] (a flat pair's
+// first-stage references) instead of the survivor list.
+__global__ __launch_bounds__(256) void consensus_hint_kernel(
+    const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride, double trim_lo,
+    double trim_hi, const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv, int step,
+    const double* __restrict__ ub, float4* __restrict__ hint) {
+    __shared__ uint32_t histA[2048], histB[2048];
+    __shared__ int ws[8];
+    __shared__ int res[2];
+    __shared__ double rb_u[4];
+    __shared__ int rb_r[4];
+    const int p = blockIdx.x, tid = threadIdx.x;
+    const int K = kcount[p], ns = nsurv[p];
+    const long lo = (long)(K * trim_lo), hi = (long)(K * trim_hi);
+    if (ns <= kRefineMin || hi <= lo) {
+        if (tid == 0) hint[2 * p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+    const int32_t* S = surv ? surv + (size_t)p * stride : nullptr;
+    const int nc = S ? ns : (ns + step - 1) / step;
+    double bu = __builtin_inf();
+    int br = 0x7fffffff;
+    for (int k = tid; k < nc; k += 256) {
+        const int row = S ? (int)S[k] : k * step;
+        const double u = ub[(size_t)p * stride + row];
+        if (u < bu || (u == bu && row < br)) {
+            bu = u;
+            br = row;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double u = __shfl_xor(bu, o, 64);
+        const int r = __shfl_xor(br, o, 64);
+        if (u < bu || (u == bu && r < br)) {
+            bu = u;
+            br = r;
+        }
+    }
+    if ((tid & 63) == 0) {
+        rb_u[tid >> 6] = bu;
+        rb_r[tid >> 6] = br;
+    }
+    __syncthreads();
+    bu = rb_u[0];
+    br = rb_r[0];
+    for (int q = 1; q < 4; q++)
+        if (rb_u[q] < bu || (rb_u[q] == bu && rb_r[q] < br)) {
+            bu = rb_u[q];
+            br = rb_r[q];
+        }
+    if (br == 0x7fffffff) {  // (no finite UB: no hint)
+        if (tid == 0) hint[2 * p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        return;
+    }
+    const float* X = rv + (size_t)p * 3 * stride;
+    const float* Y = X + stride;
+    const float* Z = Y + stride;
+    const float xh = X[br], yh = Y[br], zh = Z[br];
+    const RankKeys rk = radix_rank_keys(X, Y, Z, K, xh, yh, zh, lo, hi - 1, histA, histB, ws, res);
+    if (tid == 0) {
+        hint[2 * p] = make_float4(xh, yh, zh, 1.f);
+        hint[2 * p + 1] = make_float4(__uint_as_float(rk.va), __uint_as_float(rk.vb), 0.f, 0.f);
     }
 }
 
@@ -3332,6 +3490,35 @@ __global__ __launch_bounds__(256) void consensus_pick_central_kernel(
     if (tid == 0) count[p] = min(n_s, cap);
 }
 
+// ---- flat pairs (round 4, ERP_FLAT_REFS) -------------------------------------------------
+// A pair whose first-stage pruning kept more than flat_pct % of its rows is flat: every
+// trimmed mean lies within the coarse bounds' 2^-5 of the minimum (the two-cluster sets of R1
+// and R2 both valid in every iteration: K = 2 iters, every T within ~1e-3 of min T), so the
+// references prune nothing and the list pass bins almost every row.  For such a pair the
+// first-stage references themselves are refined (consensus_hint_kernel on the best of them +
+// consensus_refine_kernel with the hinted key windows: bounds ~1e-7 wide instead of 2^-5) and
+// the first stage re-runs against them: with U and the references' LB exact to ~1e-7 the
+// pruning radius LB(c) - U is the true T(c) - min T, and a numpy model of a worst-case pair
+// (K = 20 000) keeps ~700 rows instead of ~19 000.  Every pruning stays rigorous (the same
+// Lipschitz test, tighter bounds).  Sets the per-pair gate nflat[p] = K (flat) or 0 and resets
+// the flat pairs' list counts for the re-run.
+__global__ void consensus_flat_gate_kernel(const int32_t* __restrict__ kcount,
+                                           int32_t* __restrict__ rcount,
+                                           int32_t* __restrict__ r2cnt, int n_pairs, int flat_pct,
+                                           double trim_lo, double trim_hi,
+                                           int32_t* __restrict__ nflat) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n_pairs) return;
+    const int K = kcount[p];
+    const int lo = (int)(K * trim_lo), hi = (int)(K * trim_hi);
+    const bool flat = K >= kLipMinK && hi > lo && (int64_t)rcount[p] * 100 > (int64_t)flat_pct * K;
+    nflat[p] = flat ? K : 0;
+    if (flat) {
+        rcount[p] = 0;
+        if (r2cnt) r2cnt[p] = 0;
+    }
+}
+
 // ---- second pre-pruning stage (ERP_LIP2, default on) ------------------------------------
 // After the first stage a configs[1] pair still lists ~16 % of its rows (L1): the rows near
 // the minimum, where T is flat and the references every 16th row, with bounds 2^-5 wide, stop
@@ -3505,14 +3692,14 @@ __global__ __launch_bounds__(256, ERP_REFINE_MINB) void consensus_refine_kernel(
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
     const int32_t* __restrict__ bsel, double* __restrict__ lb, double* __restrict__ ub,
     const int32_t* __restrict__ list, int lstride, const int32_t* __restrict__ lcount, int step,
-    const int32_t* __restrict__ uoff, int n_pairs) {
+    const float4* __restrict__ hint, const int32_t* __restrict__ uoff, int n_pairs) {
     const int total = uoff[n_pairs];  // units of kRefineRows listed rows, pairs with > kRefineMin
     for (int g = blockIdx.x; g < total; g += gridDim.x) {
         int p, u;
         pair_of_item(uoff, n_pairs, g, &p, &u);
         __syncthreads();  // the previous item's LDS readers are done
         consensus_refine_block(kcount, rv, dscale, stride, trim_lo, trim_hi, surv, nsurv, bsel,
-                               lb, ub, list, lstride, lcount, step, p, u);
+                               lb, ub, list, lstride, lcount, step, hint, p, u);
     }
 }
 
@@ -4287,12 +4474,15 @@ hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const f
 // second-stage reference list [P][stride] ints and its counts [P]
 // then the gradient references: gref [P][gcap][2] float4, gsel [P][gcap], gcnt [P], goff [P + 1]
 // (>= the stage-1 references; the second stage's -- a quarter of L1 -- are capped at it)
+// then the refine pass's rank-key hints [P][2] float4 (consensus_hint_kernel), then the flat
+// gate [P] ints (consensus_flat_gate_kernel)
 static int grad_cap(int stride) { return stride / 4 + 64; }
 size_t lipref_bytes(int n_pairs, int stride) {
     const size_t gcap = grad_cap(stride);
     return (size_t)n_pairs * lipref_cap(stride) * sizeof(float4) + (size_t)n_pairs * 16 +
            (size_t)n_pairs * stride * 4 + 64 + (size_t)n_pairs * gcap * 2 * sizeof(float4) +
-           (size_t)n_pairs * gcap * 4 + (size_t)n_pairs * 8 + 128;
+           (size_t)n_pairs * gcap * 4 + (size_t)n_pairs * 8 + 128 +
+           (size_t)n_pairs * 2 * sizeof(float4) + 16 + (size_t)n_pairs * 4;
 }
 struct LipRefViews {
     float4* ref;
@@ -4306,6 +4496,8 @@ struct LipRefViews {
     int32_t* gcnt;
     int32_t* goff;
     int gcap;
+    float4* hint;
+    int32_t* nflat;
 };
 static LipRefViews lipref_views(void* base, int n_pairs, int stride) {
     LipRefViews v;
@@ -4322,6 +4514,9 @@ static LipRefViews lipref_views(void* base, int n_pairs, int stride) {
     v.gsel = reinterpret_cast<int32_t*>(v.gref + (size_t)n_pairs * v.gcap * 2);
     v.gcnt = v.gsel + (size_t)n_pairs * v.gcap;
     v.goff = v.gcnt + n_pairs;
+    uintptr_t hb = reinterpret_cast<uintptr_t>(v.goff + n_pairs + 1);
+    v.hint = reinterpret_cast<float4*>((hb + 15) & ~(uintptr_t)15);
+    v.nflat = reinterpret_cast<int32_t*>(v.hint + (size_t)n_pairs * 2);
     return v;
 }
 
@@ -4330,7 +4525,8 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
                                    int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
-                                   void* lipref, int lipg, float gfac, hipStream_t st) {
+                                   void* lipref, int lipg, float gfac, int flat_pct,
+                                   int use_hint, hipStream_t st) {
     hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     const int stride = 2 * sh.iters;
     if (!rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
@@ -4393,6 +4589,38 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                        (lipg & 1) ? (const float4*)lr.gref : nullptr, (const int32_t*)lr.gcnt,
                        lr.gcap);
     int32_t* uoff = rcount + P;  // [n_pairs + 1] after the counts
+    if (flat_pct > 0 && nshards == 1) {
+        // flat pairs: refine the first-stage references, then re-run the first stage
+        hipLaunchKernelGGL(consensus_flat_gate_kernel, dim3((P + 255) / 256), dim3(256), 0, st,
+                           kcount, rcount, two ? lr.r2cnt : nullptr, P, flat_pct, trim_lo,
+                           trim_hi, lr.nflat);
+        const float4* hint = nullptr;
+        if (use_hint) {
+            hipLaunchKernelGGL(consensus_hint_kernel, dim3(P), dim3(256), 0, st, kcount, rv,
+                               stride, trim_lo, trim_hi, (const int32_t*)nullptr,
+                               (const int32_t*)lr.nflat, kLipStep, (const double*)ub, lr.hint);
+            hint = lr.hint;
+        }
+        hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)lr.nflat,
+                           P, kRefineRows * kLipStep, kRefineMin, uoff);
+        hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv,
+                           dscale, stride, trim_lo, trim_hi, (const int32_t*)nullptr,
+                           (const int32_t*)lr.nflat, (const int32_t*)bsel, lb, ub,
+                           (const int32_t*)nullptr, stride, (const int32_t*)nullptr, kLipStep,
+                           hint, (const int32_t*)uoff, P);
+        hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
+                           trim_lo, trim_hi, (const double*)lb, (const double*)ub,
+                           (const int32_t*)nullptr, (const int32_t*)nullptr, kLipStep, 0, 1,
+                           (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap,
+                           (const int32_t*)lr.nflat);
+        hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
+                           st, kcount, rv, stride, lb, ub, (const int32_t*)nullptr,
+                           (const int32_t*)nullptr, rlist, stride, rcount, 0, 1, kLipStep,
+                           (const float4*)lr.ref, (const double*)lr.U, (const int32_t*)lr.cnt,
+                           lr.cap, two ? lr.r2list : nullptr, two ? lr.r2cnt : nullptr,
+                           (const float4*)nullptr, (const int32_t*)lr.gcnt, lr.gcap,
+                           (const int32_t*)lr.nflat);
+    }
     const int32_t* blist = rlist;
     const int32_t* bcount = rcount;
     if (two) {
@@ -4467,22 +4695,29 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
                                    const BatchShape& sh, double trim_lo, double trim_hi,
                                    const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
                                    double* lb, double* ub, int32_t* list2, void* lipref,
-                                   hipStream_t st) {
+                                   int use_hint, hipStream_t st) {
     // scratch after nsurv[n_pairs] and the bounds-list counts[n_pairs]: the unit prefix
     // [n_pairs + 1], then the counts of list2 [n_pairs]
     const int P = sh.n_pairs, stride = 2 * sh.iters, l2stride = sortbuf_len(sh.iters);
     int32_t* uoff = const_cast<int32_t*>(nsurv) + 2 * P;
     int32_t* n2 = uoff + P + 1;
+    const LipRefViews lr = lipref_views(lipref, P, stride);
+    // (0) the rank-key hint of pairs with > kRefineMin survivors (use_hint = 0: none)
+    const float4* hint = nullptr;
+    if (use_hint) {
+        hipLaunchKernelGGL(consensus_hint_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
+                           trim_lo, trim_hi, surv, nsurv, 1, (const double*)ub, lr.hint);
+        hint = lr.hint;
+    }
     // (A) the reference survivors (every kRefStep-th) of pairs with > kRefineMin survivors
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, P,
                        kRefineRows * kRefStep, kRefineMin, uoff);
     hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
                        stride, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, surv, stride,
-                       (const int32_t*)nullptr, kRefStep, (const int32_t*)uoff, P);
+                       (const int32_t*)nullptr, kRefStep, hint, (const int32_t*)uoff, P);
     // (B) Lipschitz pruning of the other survivors against the refined references
     const hipError_t me = hipMemsetAsync(n2, 0, sizeof(int32_t) * P, st);
     if (me != hipSuccess) return me;
-    const LipRefViews lr = lipref_views(lipref, P, stride);
     hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
                        trim_lo, trim_hi, (const double*)lb, (const double*)ub, surv, nsurv,
                        kRefStep, 0, 1, (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap);
@@ -4496,7 +4731,7 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
                        kRefineRows, 0, uoff);
     hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
                        stride, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, (const int32_t*)list2,
-                       l2stride, (const int32_t*)n2, 1, (const int32_t*)uoff, P);
+                       l2stride, (const int32_t*)n2, 1, hint, (const int32_t*)uoff, P);
     return hipGetLastError();
 }
 

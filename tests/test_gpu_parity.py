@@ -948,6 +948,77 @@ def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case):
     assert r1["binned_rows"] <= r0["binned_rows"] + 64, (r1["binned_rows"], r0["binned_rows"])
 
 
+@pytest.mark.parametrize("case", ["two_clusters", "twin_pairs", "bench_pairs"])
+def test_consensus_refine_hint_and_flat_exact(gpu_lib, oracle, monkeypatch, case):
+    """the refine pass's hinted sub-bin windows (ERP_REFINE_HINT; kernels.hip
+    consensus_hint_kernel / refine_windows) and the flat-pair route (ERP_FLAT_REFS: the
+    first-stage references refined, the first stage re-run against them) keep every result
+    field of the run without them, are deterministic run to run, and leave no more survivors
+    for the exact pass -- on a synthetic two-cluster set against the oracle, on two-cluster
+    configs[1]-shaped pairs (the bench's worst-case seeds, R1 and R2 valid in every iteration;
+    the first against the oracle's consensus on its own rotation vectors) and on the default
+    bench pairs through the batch pipeline"""
+    import json
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
+    from erp_match_eightpoint_test_amd import dist as D
+
+    def ctx_with(hint, flat):
+        monkeypatch.setenv("ERP_REFINE_HINT", hint)
+        monkeypatch.setenv("ERP_FLAT_REFS", flat)
+        return Context(0)
+
+    variants = (("0", "0"), ("1", "0"), ("1", "25"), ("1", "25"))
+    fields = ("status", "M", "K", "min_idx", "R", "T", "min_dist", "near_ties")
+    if case in ("twin_pairs", "bench_pairs"):
+        if case == "twin_pairs":
+            seeds = json.load(open(os.path.join(os.path.dirname(__file__), "..", "scripts",
+                                                "twin_seeds.json")))["seeds"]
+            pairs = [synth.make_pair(seeds[i], n_kpts=4096, inlier_frac=0.98)
+                     for i in (0, 3, 4, 5)]
+        else:
+            pairs = [synth.make_pair(20200423 + i, n_kpts=4096) for i in range(8)]
+        args = _batch(pairs)
+        recs = []
+        for v in variants:
+            out = PairBatchRunner(ctx=ctx_with(*v), iters=10000).run(*args, want=("rvec",))
+            torch.cuda.synchronize()
+            recs.append((results_to_numpy(out["results"]), out["rvec"][0].cpu().numpy()))
+        a, rv0 = recs[0]
+        assert np.array_equal(recs[2][0].view(np.uint8), recs[3][0].view(np.uint8))
+        for b, _ in recs[1:]:
+            for f in fields:
+                assert np.array_equal(a[f], b[f]), f
+        # hinted windows: never more survivors; the flat route: never more binned rows
+        assert np.all(recs[1][0]["survivors"] <= a["survivors"])
+        assert np.all(recs[2][0]["binned_rows"] <= recs[1][0]["binned_rows"])
+        for name, (r, _) in zip(("none", "hint", "hint+flat"), recs[:3]):
+            print(f"{case} {name}: survivors {r['survivors'].tolist()} "
+                  f"binned_rows {r['binned_rows'].tolist()}")
+        if case == "twin_pairs":
+            assert a["K"][0] == 20000  # the two-cluster regime
+            assert recs[2][0]["binned_rows"][0] < a["binned_rows"][0] // 4
+            _, mi, _ = oracle.consensus(rv0[:int(a["K"][0])])
+            assert int(recs[2][0]["min_idx"][0]) == mi
+        return
+    rng = np.random.default_rng(26)
+    K = 8000
+    a_ = rng.standard_normal((K // 2, 3)) * 6e-5 + np.array([0.1, 0.2, 0.3])
+    b_ = rng.standard_normal((K - K // 2, 3)) * 6e-5 + np.array([-1.2, 0.9, 0.4])
+    rv = np.concatenate([a_, b_])[rng.permutation(K)].astype(np.float32)
+    tv = rng.standard_normal((K, 3)).astype(np.float32)
+    _, mi, dref = oracle.consensus(rv)
+    res = [D.gpu_consensus(ctx_with(*v), "cuda")(rv, tv) for v in variants]
+    assert res[2].tobytes() == res[3].tobytes()
+    for r in res:
+        assert r["status"] == 0 and r["min_idx"] == mi
+        assert abs(r["min_dist"] - dref[mi]) <= 1e-12 * abs(dref[mi])
+    assert res[1]["survivors"] <= res[0]["survivors"]
+    assert res[2]["binned_rows"] <= res[1]["binned_rows"]
+    print(f"survivors {[int(r['survivors']) for r in res[:3]]} "
+          f"binned_rows {[int(r['binned_rows']) for r in res[:3]]}")
+
+
 def test_consensus_small_set_bins_every_row(ctx, oracle):
     """below 1024 rows there is no pre-pruning: every row is binned."""
     from erp_match_eightpoint_test_amd import dist as D
