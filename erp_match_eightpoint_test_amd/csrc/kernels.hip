@@ -1887,9 +1887,10 @@ __device__ RankKeys radix_rank_keys(const float* X, const float* Y, const float*
 __device__ double radix_window_sum(const float* X, const float* Y, const float* Z, int K,
                                    float xi, float yi, float zi, long lo, long hi,
                                    uint32_t* histA, uint32_t* histB, int* ws, int* res,
-                                   double* red) {
+                                   double* red, RankKeys* keys_out = nullptr) {
     const int tid = threadIdx.x;
     const RankKeys rk = radix_rank_keys(X, Y, Z, K, xi, yi, zi, lo, hi - 1, histA, histB, ws, res);
+    if (keys_out) *keys_out = rk;
     const uint32_t va = rk.va, vb = rk.vb;
     const long le_a = rk.le_a, lt_b = rk.lt_b;
     double acc = 0.0;
@@ -2225,7 +2226,10 @@ __device__ __forceinline__ void consensus_bounds_unit(const int32_t* __restrict_
             const int c1 = min(max(nc, lo), hi);
             const float w = (float)(c1 - c0);
             L = __builtin_fmaf(w, el[q], L);
-            U = __builtin_fmaf(w, eu[q], U);
+            // (0 * inf: the last bin's upper edge is +inf, and until r04 every row whose rank
+            // window reached the top slice -- a two-cluster set's rank hi-1 in bin ~571 --
+            // got UB = NaN, so its pair's U was NaN and the pre-pruning never ran)
+            U = w > 0.f ? __builtin_fmaf(w, eu[q], U) : U;
             sel_a = (cum <= lo && lo < nc) ? sl * per + q : sel_a;
             sel_b = (cum <= hi - 1 && hi - 1 < nc) ? sl * per + q : sel_b;
             cum = nc;
@@ -2268,10 +2272,10 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(
 // c = 0, kLipStep, 2 kLipStep, ... (1/16 of the rows); with U = their smallest UB, a row i with
 // d(i, c) < LB(c) - U for some reference c has T(i) > U >= the final min UB, so it cannot be the
 // argmin and skips the K-column histogram pass.  The test runs in squared f32 distances against
-// per-reference thresholds thr_c = (LB_c (1 - 1e-5) - U (1 + 1e-5))^2 (1 - 1e-5): the 1e-5
-// margins cover the f32 rounding of s (<= 5u), the reference's own f32 distances and fp64 sum
-// (<= 4u relative) and the rounding of thr, so a pruned row's LB = U (1 + 5e-6) is rigorous and
-// strictly above every UB that select compares against.  Pruned rows get [LB, +inf) and no
+// per-reference thresholds thr_c = (LB_c (1 - M) - U (1 + M))^2 (1 - M): the margins M (kLipM,
+// 1e-6) cover the f32 rounding of s (<= 5u), the reference's own f32 distances and fp64 sum
+// and the rounding of thr, so a pruned row's LB = U (1 + M / 2) is rigorous and strictly above
+// every UB that select compares against.  Pruned rows get [LB, +inf) and no
 // boundary bins (select drops them); the others are appended (any order) to the per-pair list
 // that the second bounds pass reads.  Synthetic configs[1] pairs (one cluster of ~1e4 valid
 // rotations): ~80 % of the rows are pruned for ~1/16 + ~1/20 of the full pass's distances.
@@ -2297,15 +2301,28 @@ static_assert((kLip2Step & (kLip2Step - 1)) == 0, "power of two (is_ref2)");
 // gathers, ~20 per block of 512 rows) the kernels spent ~80 % of their wave cycles waiting
 // (SQ_WAIT_ANY, profiles/r03_sq_lipschitz.txt).
 constexpr int kLipChunk2 = 512;  // references per LDS chunk
+// The Lipschitz tests' relative margin M (round 4: 1e-6; 1e-5 until r04, ERP_LIP_MARGIN for A/B).
+// The reference's T is computed from f32 distances: d_ref = d (1 +- 2.5u) per element (dx, the
+// square, two adds), so its order statistics and T_ref = T (1 +- 2.5u) (+ the fp64 sum's
+// w 2^-53), and T_ref(i) >= LB_c (1 - 5u) - d(i, c).  The test s_f32(i, c) < thr_c with
+// thr_c = (LB_c (1 - M) - U (1 + M))^2 (1 - M) (s_f32 = d^2 (1 +- 4u), thr rounded to f32: u)
+// gives d(i, c) < LB_c (1 - M) - U (1 + M), so T_ref(i) > LB_c (M - 5u) + U (1 + M) >= U (1 + M)
+// for M >= 6u = 3.6e-7: a pruned row's LB = U (1 + M / 2) is rigorous and strictly above every
+// UB that select compares against.  The margin matters where T is flat: on a two-cluster set
+// (every T within ~6e-5 of min T ~ 1.3) M = 1e-5 alone removes ~2.6e-5 of every pruning radius.
+#ifndef ERP_LIP_MARGIN
+#define ERP_LIP_MARGIN 1e-6
+#endif
+constexpr double kLipM = ERP_LIP_MARGIN;
+constexpr double kLipPrunedLB = 1.0 + 0.5 * kLipM;
 int lipref_cap(int stride) { return stride / kLip2Step + 64; }  // >= refs of any mode
 
 // one block per pair.  Modes: stage 1 (slist == nullptr, zb == nullptr): rows ra + c lstep of
 // the shard (pairs with K >= kLipMinK); list mode (slist, zb == nullptr): survivor-list
 // positions c lstep (pairs with > kRefineMin survivors, before the refine pass); stage 2 (slist =
 // L1, zb): L1 positions c lstep of the pairs with a second stage, U also <= the stage-1 U
-// already in lU[p].  Only references with LB_c > U (1 + 1e-5) can prune; their radius is
-// thr_c = (LB_c (1 - 1e-5) - U (1 + 1e-5))^2 (1 - 1e-5) in squared f32 distance (the header
-// of consensus_lipschitz_kernel has the margins).
+// already in lU[p].  Only references with LB_c > U (1 + M) can prune; their radius is
+// thr_c = (LB_c (1 - M) - U (1 + M))^2 (1 - M) in squared f32 distance (kLipM has the margins).
 __global__ __launch_bounds__(256) void consensus_lip_refs_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride, double trim_lo,
     double trim_hi, const double* __restrict__ lb, const double* __restrict__ ub,
@@ -2344,14 +2361,14 @@ __global__ __launch_bounds__(256) void consensus_lip_refs_kernel(
         }
         return;
     }
-    const double Um = U * (1.0 + 1e-5);
+    const double Um = U * (1.0 + kLipM);
     const float* X = rv + (size_t)p * 3 * stride;
     float4* R = lref + (size_t)p * cap;
     for (int c = tid; c < nref; c += 256) {
         const int row = rowpos(c * lstep);
-        const double a = lb[(size_t)p * stride + row] * (1.0 - 1e-5) - Um;
+        const double a = lb[(size_t)p * stride + row] * (1.0 - kLipM) - Um;
         if (a > 0.0) {
-            const float thr = (float)(a * a * (1.0 - 1e-5));
+            const float thr = (float)(a * a * (1.0 - kLipM));
             R[atomicAdd(&nlive, 1)] = make_float4(X[row], X[stride + row], X[2 * stride + row], thr);
         }
     }
@@ -2532,10 +2549,10 @@ __device__ void lip_append(const LipShared& sh, int na, int32_t* __restrict__ li
 // c = 0, kLipStep, 2 kLipStep, ... (1/16 of the rows); with U = their smallest UB, a row i with
 // d(i, c) < LB(c) - U for some reference c has T(i) > U >= the final min UB, so it cannot be the
 // argmin and skips the K-column histogram pass.  The test runs in squared f32 distances against
-// per-reference thresholds thr_c = (LB_c (1 - 1e-5) - U (1 + 1e-5))^2 (1 - 1e-5): the 1e-5
-// margins cover the f32 rounding of s (<= 5u), the reference's own f32 distances and fp64 sum
-// (<= 4u relative) and the rounding of thr, so a pruned row's LB = U (1 + 5e-6) is rigorous and
-// strictly above every UB that select compares against.  Pruned rows get [LB, +inf) and no
+// per-reference thresholds thr_c = (LB_c (1 - M) - U (1 + M))^2 (1 - M): the margins M (kLipM,
+// 1e-6) cover the f32 rounding of s (<= 5u), the reference's own f32 distances and fp64 sum
+// and the rounding of thr, so a pruned row's LB = U (1 + M / 2) is rigorous and strictly above
+// every UB that select compares against.  Pruned rows get [LB, +inf) and no
 // boundary bins (select drops them); the others are appended (any order) to the per-pair list
 // that the second bounds pass reads.  Synthetic configs[1] pairs (one cluster of ~1e4 valid
 // rotations): ~84 % of the rows are pruned.
@@ -2580,8 +2597,8 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
         const int k = i0 + 256 * h + tid;
         bool act = k < n && (k % lstep) != 0;
         const int i = act ? (SL ? (int)SL[k] : ra + k) : 0;
-        if (act && SL && prune_on && LBp[i] > U * (1.0 + 1e-5)) {
-            LBp[i] = fmax(LBp[i], U * (1.0 + 5e-6));
+        if (act && SL && prune_on && LBp[i] > U * (1.0 + kLipM)) {
+            LBp[i] = fmax(LBp[i], U * kLipPrunedLB);
             UBp[i] = __builtin_huge_val();
             act = false;
         }
@@ -2599,7 +2616,7 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     if (tid == 3) sh.cnt[3] = 0;  // (batch counters 0 .. 3 start at zero)
     if (prune_on && m > 0) {
         auto prune = [&](int i) {
-            LBp[i] = SL ? fmax(LBp[i], U * (1.0 + 5e-6)) : U * (1.0 + 5e-6);
+            LBp[i] = SL ? fmax(LBp[i], U * kLipPrunedLB) : U * kLipPrunedLB;
             UBp[i] = __builtin_huge_val();
         };
         na = lip_prune_rows(sh, na, lref + (size_t)p * cap, m, prune);
@@ -2662,6 +2679,13 @@ __device__ __forceinline__ void for_columns(const float* __restrict__ X, const f
 // bound width ~2e-5, ~1 700 survivors per pair into the exact pass); on the interval they are
 // bracketed at 2^2-2^3 keys.  The window placement is only a heuristic: a rank that falls
 // outside its window fails the `ok` test below and the row keeps its old bounds.
+constexpr int kHintCands = 4;
+constexpr int kHintManyRows = 256;
+struct HintCand {
+    double T;
+    int32_t row;  // -1: none
+    uint32_t va, vb, pad;
+};
 struct RefineWin {
     uint32_t a0, a1, b0, b1;  // key windows [a0, a1) (rank lo), [b0, b1) (rank hi-1)
     int wa, wb;               // sub-bin k of a window covers keys [x0 + (k << w), + 2^w)
@@ -2677,8 +2701,29 @@ __device__ __forceinline__ bool refine_interval(float dc, float delta, uint32_t*
     *w = ww;
     return ww < kLowBits && khi < 0x7f800000u;
 }
+// the hint of pair p (the candidate with the smallest exact mean; consensus_hint_kernel):
+// h.w = 0 when there is none, else (x_h, y_h, z_h, 1) and the rank keys in *va, *vb
+__device__ __forceinline__ float4 pick_hint(const HintCand* __restrict__ cand, const float* __restrict__ X,
+                                            int stride, int p, uint32_t* va, uint32_t* vb) {
+    int best = -1;
+    double bT = 0.0;
+#pragma unroll
+    for (int q = 0; q < kHintCands; q++) {
+        const HintCand c = cand[(size_t)p * kHintCands + q];
+        if (c.row >= 0 && (best < 0 || c.T < bT || (c.T == bT && c.row < best))) {
+            best = c.row;
+            bT = c.T;
+            *va = c.va;
+            *vb = c.vb;
+        }
+    }
+    if (best < 0) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return make_float4(X[best], X[stride + best], X[2 * stride + best], 1.f);
+}
 __device__ __forceinline__ RefineWin refine_windows(int ba, int bb, float xi, float yi, float zi,
-                                                    const float4* __restrict__ hint, int p) {
+                                                    const HintCand* __restrict__ hint,
+                                                    const float* __restrict__ X, int stride,
+                                                    int p) {
     RefineWin W;
     W.a0 = (uint32_t)ba << kBinShift;
     W.a1 = (uint32_t)(ba + 1) << kBinShift;
@@ -2686,19 +2731,19 @@ __device__ __forceinline__ RefineWin refine_windows(int ba, int bb, float xi, fl
     W.b1 = (uint32_t)(bb + 1) << kBinShift;
     W.wa = W.wb = kLowBits;
     if (!hint) return W;
-    const float4 h = hint[2 * p];
+    uint32_t va = 0, vb = 0;
+    const float4 h = pick_hint(hint, X, stride, p, &va, &vb);
     if (!(h.w > 0.f)) return W;
-    const float4 hk = hint[2 * p + 1];
     const float delta = __builtin_sqrtf(rdist2(xi, yi, zi, h.x, h.y, h.z));
     RefineWin A = W;
     uint32_t k0;
     int w;
-    if (refine_interval(__builtin_sqrtf(hk.x), delta, &k0, &w)) {
+    if (refine_interval(__builtin_sqrtf(__uint_as_float(va)), delta, &k0, &w)) {
         A.a0 = k0;
         A.a1 = k0 + ((uint32_t)kNS << w);
         A.wa = w;
     }
-    if (refine_interval(__builtin_sqrtf(hk.y), delta, &k0, &w)) {
+    if (refine_interval(__builtin_sqrtf(__uint_as_float(vb)), delta, &k0, &w)) {
         A.b0 = k0;
         A.b1 = k0 + ((uint32_t)kNS << w);
         A.wb = w;
@@ -2727,9 +2772,9 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
                                        const int32_t* __restrict__ bsel, double* __restrict__ lb,
                                        double* __restrict__ ub, const int32_t* __restrict__ list,
                                        int lstride, const int32_t* __restrict__ lcount, int step,
-                                       const float4* __restrict__ hint, int p, int vb) {
+                                       const HintCand* __restrict__ hint, int p, int vb) {
     __shared__ uint32_t sub[kRefineRows][2][kNS];
-    __shared__ double inner[kRefineRows];
+    __shared__ double inner_w[4][kRefineRows];  // [wave][row]
     __shared__ int below[kRefineRows][2];
     const int tid = threadIdx.x, lane = wave_lane();
     const int K = kcount[p];
@@ -2764,7 +2809,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
         zi[t] = Z[row];
         const RefineWin W = refine_windows(bsel[((size_t)p * stride + row) * 2] + base,
                                            bsel[((size_t)p * stride + row) * 2 + 1] + base,
-                                           xi[t], yi[t], zi[t], hint, p);
+                                           xi[t], yi[t], zi[t], hint, X, stride, p);
         a0[t] = W.a0;
         b0[t] = W.b0;
         wa[t] = W.wa;
@@ -2775,7 +2820,6 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     }
     for (int q = tid; q < kRefineRows * 2 * kNS; q += 256) (&sub[0][0][0])[q] = 0u;
     if (tid < kRefineRows) {
-        inner[tid] = 0.0;
         below[tid][0] = 0;
         below[tid][1] = 0;
     }
@@ -2800,10 +2844,23 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
             }
         }
     });
+    // the inner sums in a fixed order (a wave tree, then the waves in order): fp64 LDS atomics
+    // made the last bits -- and with them a borderline pruning decision of the flat-pair route,
+    // whose references' refined bounds set U -- depend on the arrival order
+#pragma unroll
+    for (int r = 0; r < kRefineRows; r++) {
+        float v = 0.f;
+#pragma unroll
+        for (int t = 0; t < kRefineRows; t++)
+            if (((lane + t) & (kRefineRows - 1)) == r) v = acc[t];
+        double d = (double)v;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+        if (lane == 0) inner_w[tid >> 6][r] = d;
+    }
 #pragma unroll
     for (int t = 0; t < kRefineRows; t++) {
         const int r = (lane + t) & (kRefineRows - 1);
-        atomicAdd(&inner[r], (double)acc[t]);
         atomicAdd(&below[r][0], bel_a[t]);
         atomicAdd(&below[r][1], bel_b[t]);
     }
@@ -2814,7 +2871,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     const int row = srow(s0 + r);
     const RefineWin W = refine_windows(bsel[((size_t)p * stride + row) * 2] + base,
                                        bsel[((size_t)p * stride + row) * 2 + 1] + base, X[row],
-                                       Y[row], Z[row], hint, p);
+                                       Y[row], Z[row], hint, X, stride, p);
     const int cA = below[r][0], cB = below[r][1];
     // sub-bin k of a window [x0, ...) covers keys [x0 + (k << w), x0 + ((k + 1) << w)); every d
     // in it is <= the lower edge of sub-bin k + 1 (sqrtf is monotone)
@@ -2872,7 +2929,7 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     }
     if (sl == 0 && ok) {
         const double w = (double)(hi - lo);
-        const double in = inner[r];
+        const double in = ((inner_w[0][r] + inner_w[1][r]) + inner_w[2][r]) + inner_w[3][r];
         // the inner sum used the raw v_sqrt_f32 (<= 2^-23 relative, flushes below 2^-126) and
         // per-thread f32 sums of n <= ceil(K/256) non-negative terms (relative error <= n 2^-24,
         // then exact enough in fp64): bracket it by 2^-22 + (n + 1) 2^-24 relative plus 2^-63
@@ -2887,73 +2944,90 @@ __device__ void consensus_refine_block(const int32_t* __restrict__ kcount,
     }
 }
 
-// The refine pass's rank-key hint (refine_windows): per pair with > kRefineMin survivors, the
-// survivor h with the smallest UB (lowest row on ties) and the exact keys va, vb at its ranks
-// lo and hi-1 (radix_rank_keys: three passes over the pair's K columns, one block per pair).
-// hint[2p] = (x_h, y_h, z_h, 1), hint[2p + 1] = (va, vb) as floats; (.., 0) = no hint.
-// surv == nullptr: the candidates are the rows 0, step, 2 step, ... < nsurv[p] (a flat pair's
-// first-stage references) instead of the survivor list.
+// The refine pass's rank-key hint (refine_windows): per pair with > kRefineMin survivors, a
+// survivor h near the minimum and the exact keys va, vb at its ranks lo and hi-1; pairs with
+// <= min_nc candidates get none.  h = the candidate with the smallest exact trimmed mean among
+// the kHintCands survivors with the smallest UB (lowest row on ties): on a two-cluster set the
+// UBs of both clusters' rows lie within the coarse bounds' 2^-5 of each other, and a hint from
+// the far cluster leaves every near-cluster row its default windows.  Block (p, q) takes
+// candidate q (radix_window_sum: four passes over the pair's K columns) into cand[p][q], and
+// the refine pass picks the best per pair (pick_hint).  surv == nullptr: the candidates are the rows 0, step,
+// 2 step, ... < nsurv[p] (a flat pair's first-stage references) instead of the survivor list.
 __global__ __launch_bounds__(256) void consensus_hint_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride, double trim_lo,
     double trim_hi, const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv, int step,
-    const double* __restrict__ ub, float4* __restrict__ hint) {
+    int min_nc, const double* __restrict__ ub, HintCand* __restrict__ cand) {
     __shared__ uint32_t histA[2048], histB[2048];
     __shared__ int ws[8];
     __shared__ int res[2];
+    __shared__ double red[8];
     __shared__ double rb_u[4];
     __shared__ int rb_r[4];
-    const int p = blockIdx.x, tid = threadIdx.x;
+    const int p = blockIdx.x, q = blockIdx.y, tid = threadIdx.x;
     const int K = kcount[p], ns = nsurv[p];
     const long lo = (long)(K * trim_lo), hi = (long)(K * trim_hi);
-    if (ns <= kRefineMin || hi <= lo) {
-        if (tid == 0) hint[2 * p] = make_float4(0.f, 0.f, 0.f, 0.f);
-        return;
-    }
     const int32_t* S = surv ? surv + (size_t)p * stride : nullptr;
     const int nc = S ? ns : (ns + step - 1) / step;
-    double bu = __builtin_inf();
+    HintCand* out = cand + (size_t)p * kHintCands + q;
+    if (ns <= kRefineMin || hi <= lo || nc <= min_nc || q >= nc) {
+        if (tid == 0) out->row = -1;
+        return;
+    }
+    // the (q+1)-th smallest (UB, row): q + 1 rounds of a block argmin excluding the rows taken
+    int taken[kHintCands];
     int br = 0x7fffffff;
-    for (int k = tid; k < nc; k += 256) {
-        const int row = S ? (int)S[k] : k * step;
-        const double u = ub[(size_t)p * stride + row];
-        if (u < bu || (u == bu && row < br)) {
-            bu = u;
-            br = row;
+    for (int e = 0; e <= q; e++) {
+        double bu = __builtin_inf();
+        br = 0x7fffffff;
+        for (int k = tid; k < nc; k += 256) {
+            const int row = S ? (int)S[k] : k * step;
+            bool t = false;
+            for (int f = 0; f < e; f++) t |= taken[f] == row;
+            const double u = ub[(size_t)p * stride + row];
+            if (!t && (u < bu || (u == bu && row < br))) {
+                bu = u;
+                br = row;
+            }
         }
-    }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double u = __shfl_xor(bu, o, 64);
-        const int r = __shfl_xor(br, o, 64);
-        if (u < bu || (u == bu && r < br)) {
-            bu = u;
-            br = r;
+        for (int o = 32; o > 0; o >>= 1) {
+            const double u = __shfl_xor(bu, o, 64);
+            const int r = __shfl_xor(br, o, 64);
+            if (u < bu || (u == bu && r < br)) {
+                bu = u;
+                br = r;
+            }
         }
-    }
-    if ((tid & 63) == 0) {
-        rb_u[tid >> 6] = bu;
-        rb_r[tid >> 6] = br;
-    }
-    __syncthreads();
-    bu = rb_u[0];
-    br = rb_r[0];
-    for (int q = 1; q < 4; q++)
-        if (rb_u[q] < bu || (rb_u[q] == bu && rb_r[q] < br)) {
-            bu = rb_u[q];
-            br = rb_r[q];
+        __syncthreads();  // (the previous round's readers of rb_u / rb_r are done)
+        if ((tid & 63) == 0) {
+            rb_u[tid >> 6] = bu;
+            rb_r[tid >> 6] = br;
         }
-    if (br == 0x7fffffff) {  // (no finite UB: no hint)
-        if (tid == 0) hint[2 * p] = make_float4(0.f, 0.f, 0.f, 0.f);
+        __syncthreads();
+        bu = rb_u[0];
+        br = rb_r[0];
+        for (int w = 1; w < 4; w++)
+            if (rb_u[w] < bu || (rb_u[w] == bu && rb_r[w] < br)) {
+                bu = rb_u[w];
+                br = rb_r[w];
+            }
+        taken[e] = br;
+    }
+    if (br == 0x7fffffff) {  // (no finite UB left)
+        if (tid == 0) out->row = -1;
         return;
     }
     const float* X = rv + (size_t)p * 3 * stride;
     const float* Y = X + stride;
     const float* Z = Y + stride;
-    const float xh = X[br], yh = Y[br], zh = Z[br];
-    const RankKeys rk = radix_rank_keys(X, Y, Z, K, xh, yh, zh, lo, hi - 1, histA, histB, ws, res);
+    RankKeys rk;
+    const double T = radix_window_sum(X, Y, Z, K, X[br], Y[br], Z[br], lo, hi, histA, histB, ws,
+                                      res, red, &rk);
     if (tid == 0) {
-        hint[2 * p] = make_float4(xh, yh, zh, 1.f);
-        hint[2 * p + 1] = make_float4(__uint_as_float(rk.va), __uint_as_float(rk.vb), 0.f, 0.f);
+        out->T = T;
+        out->row = br;
+        out->va = rk.va;
+        out->vb = rk.vb;
     }
 }
 
@@ -3526,7 +3600,7 @@ __global__ void consensus_flat_gate_kernel(const int32_t* __restrict__ kcount,
 // (64 bins per binade of s, ~2^-7 wide, consensus_zoom_unit with a list step), and the other
 // L1 rows are tested against them exactly as against the first-stage references (T is
 // 1-Lipschitz): with U2 = min(U1, min UB over the second-stage references), any UB >= min T, a
-// row with d(i, c) < LB(c) - U2 has T(i) > U2, so its LB = U2 (1 + 5e-6) is rigorous.  Only
+// row with d(i, c) < LB(c) - U2 has T(i) > U2, so its LB = U2 (1 + M / 2) is rigorous.  Only
 // the rows that survive (L2) get the coarse K-column histogram.  On the fixture pair of
 // configs[1] (tests/golden/find_4096_it10k.npz) this bins 408 fine + ~620 coarse rows instead
 // of ~1630 coarse rows after the 625 first-stage references (a numpy model of the two tests).
@@ -3651,9 +3725,9 @@ __global__ __launch_bounds__(256) void consensus_lipschitz2_kernel(
     __syncthreads();
     if (tid == 3) sh.cnt[3] = 0;
     if (U < __builtin_huge_val() && nref > 0) {
-        // (a pruned row's LB = U (1 + 5e-6) is rigorous for a reference row too)
+        // (a pruned row's LB = U (1 + M / 2) is rigorous for a reference row too)
         auto prune = [&](int i) {
-            LBp[i] = U * (1.0 + 5e-6);
+            LBp[i] = U * kLipPrunedLB;
             UBp[i] = __builtin_huge_val();
         };
         na = lip_prune_rows(sh, na, lref + (size_t)p * cap, nref, prune);
@@ -3692,7 +3766,7 @@ __global__ __launch_bounds__(256, ERP_REFINE_MINB) void consensus_refine_kernel(
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
     const int32_t* __restrict__ bsel, double* __restrict__ lb, double* __restrict__ ub,
     const int32_t* __restrict__ list, int lstride, const int32_t* __restrict__ lcount, int step,
-    const float4* __restrict__ hint, const int32_t* __restrict__ uoff, int n_pairs) {
+    const HintCand* __restrict__ hint, const int32_t* __restrict__ uoff, int n_pairs) {
     const int total = uoff[n_pairs];  // units of kRefineRows listed rows, pairs with > kRefineMin
     for (int g = blockIdx.x; g < total; g += gridDim.x) {
         int p, u;
@@ -3896,34 +3970,53 @@ __global__ __launch_bounds__(1024) void consensus_select_kernel(const int32_t* _
     __syncthreads();
     double minub = sm[0];
     for (int w = 1; w < 16; w++) minub = fmin(minub, sm[w]);
-    // compaction in any order (the survivors' means are written per row and the final pass
-    // scans rows in index order): coalesced strided reads, one LDS atomic per wave
-    if (tid == 0) ws[0] = 0;
-    __syncthreads();
-    const int lane = tid & 63;
-    for (int k0 = 0; k0 < K; k0 += 4096) {
+    // compaction in row order: the refine pass takes every 16th survivor by list position as
+    // its references, so an arrival-order list (one LDS atomic per wave, until r04) made the
+    // reference set -- and, once the refined references prune well, the survivor count --
+    // differ run to run.  Wave w owns the rows [w C, (w + 1) C): pass 1 counts its survivors
+    // (ballots), one prefix over the 16 wave counts, pass 2 writes them in order (the L re-read
+    // hits L2); two barriers instead of a block scan per 1024 rows
+    const int lane = tid & 63, wv = tid >> 6;
+    const int C = ((K + 15) / 16 + 63) & ~63;
+    const int r0 = wv * C, r1 = min(K, r0 + C);
+    int cnt = 0;
+    for (int k0 = r0; k0 < r1; k0 += 256) {
         double l[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const int k = k0 + j * 1024 + tid;
-            l[j] = k < K ? L[k] : __builtin_huge_val();
+            const int k = k0 + j * 64 + lane;
+            l[j] = k < r1 ? L[k] : __builtin_huge_val();
         }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
-            const int k = k0 + j * 1024 + tid;
-            const bool keep = k < K && l[j] <= minub;
-            if (k < K && !keep) Tm[k] = __builtin_huge_val();
-            const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
-            if (bal) {
-                int base = 0;
-                if (lane == 0) base = atomicAdd(&ws[0], __builtin_popcountll(bal));
-                base = __shfl(base, 0, 64);
-                if (keep) S[base + __builtin_popcountll(bal & ((1ull << lane) - 1ull))] = k;
-            }
+            const int k = k0 + j * 64 + lane;
+            const bool keep = k < r1 && l[j] <= minub;
+            if (k < r1 && !keep) Tm[k] = __builtin_huge_val();
+            cnt += __builtin_popcountll(__builtin_amdgcn_ballot_w64(keep));
         }
     }
+    if (lane == 0) ws[wv] = cnt;
     __syncthreads();
-    if (tid == 0) nsurv[p] = ws[0];
+    int base = 0;
+    for (int w = 0; w < wv; w++) base += ws[w];
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (int k0 = r0; k0 < r1; k0 += 256) {
+        double l[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = k0 + j * 64 + lane;
+            l[j] = k < r1 ? L[k] : __builtin_huge_val();
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int k = k0 + j * 64 + lane;
+            const bool keep = k < r1 && l[j] <= minub;
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(keep);
+            if (keep) S[base + __builtin_popcountll(bal & below)] = k;
+            base += __builtin_popcountll(bal);
+        }
+    }
+    if (tid == 1023) nsurv[p] = base;  // (the last wave's end = the total)
 }
 
 // exact sorted-sequential trimmed mean of one row (std::sort + std::accumulate semantics)
@@ -4474,15 +4567,15 @@ hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const f
 // second-stage reference list [P][stride] ints and its counts [P]
 // then the gradient references: gref [P][gcap][2] float4, gsel [P][gcap], gcnt [P], goff [P + 1]
 // (>= the stage-1 references; the second stage's -- a quarter of L1 -- are capped at it)
-// then the refine pass's rank-key hints [P][2] float4 (consensus_hint_kernel), then the flat
-// gate [P] ints (consensus_flat_gate_kernel)
+// then the flat gate [P] ints (consensus_flat_gate_kernel) and the refine pass's rank-key hint
+// candidates [P][kHintCands] (consensus_hint_kernel)
 static int grad_cap(int stride) { return stride / 4 + 64; }
 size_t lipref_bytes(int n_pairs, int stride) {
     const size_t gcap = grad_cap(stride);
     return (size_t)n_pairs * lipref_cap(stride) * sizeof(float4) + (size_t)n_pairs * 16 +
            (size_t)n_pairs * stride * 4 + 64 + (size_t)n_pairs * gcap * 2 * sizeof(float4) +
            (size_t)n_pairs * gcap * 4 + (size_t)n_pairs * 8 + 128 +
-           (size_t)n_pairs * 2 * sizeof(float4) + 16 + (size_t)n_pairs * 4;
+           (size_t)n_pairs * 4 + 16 + (size_t)n_pairs * kHintCands * sizeof(HintCand);
 }
 struct LipRefViews {
     float4* ref;
@@ -4496,8 +4589,8 @@ struct LipRefViews {
     int32_t* gcnt;
     int32_t* goff;
     int gcap;
-    float4* hint;
     int32_t* nflat;
+    HintCand* hcand;
 };
 static LipRefViews lipref_views(void* base, int n_pairs, int stride) {
     LipRefViews v;
@@ -4514,9 +4607,9 @@ static LipRefViews lipref_views(void* base, int n_pairs, int stride) {
     v.gsel = reinterpret_cast<int32_t*>(v.gref + (size_t)n_pairs * v.gcap * 2);
     v.gcnt = v.gsel + (size_t)n_pairs * v.gcap;
     v.goff = v.gcnt + n_pairs;
-    uintptr_t hb = reinterpret_cast<uintptr_t>(v.goff + n_pairs + 1);
-    v.hint = reinterpret_cast<float4*>((hb + 15) & ~(uintptr_t)15);
-    v.nflat = reinterpret_cast<int32_t*>(v.hint + (size_t)n_pairs * 2);
+    v.nflat = v.goff + n_pairs + 1;
+    uintptr_t cb = reinterpret_cast<uintptr_t>(v.nflat + n_pairs);
+    v.hcand = reinterpret_cast<HintCand*>((cb + 15) & ~(uintptr_t)15);
     return v;
 }
 
@@ -4594,12 +4687,12 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
         hipLaunchKernelGGL(consensus_flat_gate_kernel, dim3((P + 255) / 256), dim3(256), 0, st,
                            kcount, rcount, two ? lr.r2cnt : nullptr, P, flat_pct, trim_lo,
                            trim_hi, lr.nflat);
-        const float4* hint = nullptr;
+        const HintCand* hint = nullptr;
         if (use_hint) {
-            hipLaunchKernelGGL(consensus_hint_kernel, dim3(P), dim3(256), 0, st, kcount, rv,
-                               stride, trim_lo, trim_hi, (const int32_t*)nullptr,
-                               (const int32_t*)lr.nflat, kLipStep, (const double*)ub, lr.hint);
-            hint = lr.hint;
+            hipLaunchKernelGGL(consensus_hint_kernel, dim3(P, kHintCands), dim3(256), 0, st,
+                               kcount, rv, stride, trim_lo, trim_hi, (const int32_t*)nullptr,
+                               (const int32_t*)lr.nflat, kLipStep, 0, (const double*)ub, lr.hcand);
+            hint = lr.hcand;
         }
         hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)lr.nflat,
                            P, kRefineRows * kLipStep, kRefineMin, uoff);
@@ -4703,11 +4796,14 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
     int32_t* n2 = uoff + P + 1;
     const LipRefViews lr = lipref_views(lipref, P, stride);
     // (0) the rank-key hint of pairs with > kRefineMin survivors (use_hint = 0: none)
-    const float4* hint = nullptr;
+    const HintCand* hint = nullptr;
     if (use_hint) {
-        hipLaunchKernelGGL(consensus_hint_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
-                           trim_lo, trim_hi, surv, nsurv, 1, (const double*)ub, lr.hint);
-        hint = lr.hint;
+        // (pairs with <= kHintManyRows survivors -- a one-cluster pair after the zoom has ~20 --
+        // keep the default windows: the hint's K-column passes would cost more than they save)
+        hipLaunchKernelGGL(consensus_hint_kernel, dim3(P, kHintCands), dim3(256), 0, st, kcount,
+                           rv, stride, trim_lo, trim_hi, surv, nsurv, 1, kHintManyRows,
+                           (const double*)ub, lr.hcand);
+        hint = lr.hcand;
     }
     // (A) the reference survivors (every kRefStep-th) of pairs with > kRefineMin survivors
     hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, P,

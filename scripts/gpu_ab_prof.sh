@@ -7,6 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 bash scripts/gpu_ab.sh || exit 1
 for V in ${VALUES:-0 1}; do
-  echo "== rocprofv3 $KNOB=$V" && env $KNOB=$V timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$V -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 0 --warmup 2 ${BENCH_ARGS:-} > gpurun_out/prof_${TAG}_$V.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_$V.log; exit 1; }
+  W=$(echo "$V" | tr '/' '_')  # (path-valued knobs: ERP_LIB_PATH variant libraries)
+  echo "== rocprofv3 $KNOB=$V" && env $KNOB=$V timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${TAG}_$W -o run --output-format csv -- python3 bench.py --no-cpu-baseline --steps 0 --warmup 2 ${BENCH_ARGS:-} > gpurun_out/prof_${TAG}_$W.log 2>&1 || { tail -20 gpurun_out/prof_${TAG}_$W.log; exit 1; }
 done
 find gpurun_out -path "*prof_${TAG}_*" -name "*kernel_stats.csv" | head
