@@ -362,15 +362,13 @@ __device__ __forceinline__ uint32_t mod_i24(uint32_t x, StepDiv c, int d) { retu
 //   steps i >= s (replay_block_draws):   sel = bm[j];  bm[j] := 0
 //   steps 1 <= i < s (replay_block_prefix): sel = bm[j];  bm[j] := bm[i]
 //   the block straddling s / running below step 1 (replay_block_mixed): per step
-// A position j >= s is clamped to s (one v_min_u32 per draw): bit s is 0 (positions s .. the
-// allocation's end are cleared by the kernel's prologue) and its word is allocated.  Until r04
-// the clamp was left out, relying on gfx950 returning 0 and dropping writes for words beyond the
-// workgroup's LDS allocation (scripts/dev/lds_oob.hip, one kernel alone on the GPU); with other
-// streams' kernels on the same CUs those masked ORs corrupted the co-resident workgroups' LDS
-// (consensus histograms: binned_rows off by 1-2 on ~10 % of the pairs whenever the bench's
-// sub-batches overlapped, none with the Philox sampler; scripts/dev/determinism_streams.py).
-// The LDS ops' results are consumed kReplayLag steps after issue, so the traffic streams
-// without waits.
+// A position j >= s needs no clamp: its bit is 0 (positions s .. the allocation's end are
+// cleared by the kernel's prologue) or its word lies beyond the workgroup's LDS allocation,
+// where gfx950 returns 0 and drops the write (scripts/dev/lds_oob.hip: measured up to 512 KB,
+// i.e. j < 65536 = the keypoint cap).  (r04: a variant clamping j to s, +1 VALU per draw, was
+// 5 % slower and left the overlapped-streams binned_rows differences of DESIGN.md 5c exactly as
+// they were, so those writes are not what perturbs co-resident kernels.)  The LDS ops' results
+// are consumed kReplayLag steps after issue, so the traffic streams without waits.
 // (bm_lane = LDS byte address of the lane's word 0; words are 2^RS B apart -- 256 B for the
 // standalone sampler's [word][lane], 1 KB for the fused kernel's [word][wave][lane]: the address
 // is one v_lshl_add_u32 of j >> 5)
@@ -432,9 +430,8 @@ __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uin
             const int slot = 30 - u;
             const uint32_t rv = ring[slot];
             ring[slot] = rv - ring[(slot + 28) % 31];
-            // (j >= s clamped to s: bit s is clear and inside the allocation)
-            const uint32_t j = min(I24 ? mod_i24(rv >> 1, mt[u], ii + 1)
-                                       : mod_rup(rv >> 1, rt[u], (double)(ii + 1)), (uint32_t)s);
+            const uint32_t j = I24 ? mod_i24(rv >> 1, mt[u], ii + 1)
+                                   : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
             olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), 1u << (j & 31), zero);
             pos[u] = j;
         }
@@ -557,11 +554,10 @@ __device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uin
         ring[slot] = rv - ring[(slot + 28) % 31];
         if (ii < 1) continue;
         const double r = rtab[ii + 1];
-        // (j >= s clamped to s: bit s is clear and inside the allocation)
-        const uint32_t j = min(mod_rup(rv >> 1, r, (double)(ii + 1)), (uint32_t)s);
+        const uint32_t j = mod_rup(rv >> 1, r, (double)(ii + 1));
         // bm[i] (read before the clear: j = i keeps the bit)
         const uint32_t bi = ii < s ? (bm[bm_index<RS>(ii >> 5, lane)] >> (ii & 31)) & 1u : 0u;
-        uint32_t* wp = &bm[bm_index<RS>((int)(j >> 5), lane)];
+        uint32_t* wp = &bm[bm_index<RS>((int)(j >> 5), lane)];  // j >= s: a cleared or out-of-allocation word
         const uint32_t old = atomicAnd(wp, ~(1u << (j & 31)));
         if (ii < s) atomicOr(wp, bi << (j & 31));
         word |= __builtin_amdgcn_ubfe(old, j, 1) << u;
@@ -619,8 +615,6 @@ __device__ __forceinline__ uint32_t replay_block_draws_ilp(uint32_t (&ring)[31],
     const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
     uint32_t jj[31];
     block_positions<I24>(ring, i0, rtab, jj);
-#pragma unroll
-    for (int u = 0; u < 31; u++) jj[u] = min(jj[u], (uint32_t)s);  // (bit s: clear, allocated)
     const uint32_t zero = 0;
     uint32_t olds[31];
     uint32_t nw[4] = {0, 0, 0, 0};
@@ -713,9 +707,7 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     // in front of every fp64 instruction; nothing else in this kernel depends on fp64 rounding)
     asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\ts_nop 3" ::: "memory");
     // positions < s available, every other bitmap word of the allocation (nalloc words: the
-    // batch's largest s, rounded up to the allocation granule) clear -- no write past it (see
-    // the clamp above: out-of-allocation writes are not safely dropped when other kernels share
-    // the CU)
+    // batch's largest s, rounded up to the allocation granule) clear
     for (int k = 0; k < nalloc; k++)
         bm[k * 64 + lane] = k < (s >> 5) ? ~0u : k == (s >> 5) ? (1u << (s & 31)) - 1u : 0u;
     uint32_t ring[31];
@@ -1145,9 +1137,9 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
 // MFMA-only and a VALU-only wave on one CU run concurrently).  12 waves per workgroup, one
 // workgroup per CU: each SIMD holds one sampler wave and two MFMA waves (<= 168 VGPRs).
 // LDS: [limb ring: 2 x 14 KB][selection ring: 2 x 2 KB] ... [bitmaps: rows x kFSw x 64 words]
-// with the bitmaps at the TOP of the allocation; draw positions j >= s are clamped to s (bit s
-// is clear and allocated: the replay blocks' rule since r04, see replay_block_draws) and the
-// rows between s and the allocated count are cleared by the prologue.  The
+// with the bitmaps at the TOP of the allocation, so a draw position j >= s whose word lies past
+// the allocated rows reads 0 and its write is dropped (sampler_kernel's rule, same measured
+// gfx950 behaviour); rows between s and the allocated count are cleared by the prologue.  The
 // Gram epilogue (fused eigen) reuses the whole allocation as the [36][257] double stage.
 constexpr int kFSw = 4;
 constexpr int kFMw = 8;
