@@ -121,6 +121,13 @@ constexpr int kFStageB = kFHiB + kFST * kFT * 4;  // + 512
 #ifndef ERP_FILTER_CHAINS
 #define ERP_FILTER_CHAINS 2
 #endif
+// bounds-only stages at the start of a chunk (recomputed for candidates after its last stage):
+// the running bound G the candidate test compares with only falls as rows are seen, so tiles
+// tested early against a loose G are stored and re-scored for nothing (r04 A/B knob)
+#ifndef ERP_FILTER_WARM
+#define ERP_FILTER_WARM 1
+#endif
+constexpr int kFWarm = ERP_FILTER_WARM;
 
 __device__ __forceinline__ bf16x8 round8(const float4 a, const float4 b, float s) {
     const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -403,14 +410,21 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     // one stage: wait for its DMAs (issued during the previous stage), barrier, the next
     // stage's DMAs into the other buffer (whose reads finished before this barrier), 4 tiles,
     // then (except in the final recompute) the query's running bound and candidate threshold
+    // (the first `warm` stages run bounds-only -- kFWarm, or every stage of a short chunk --
+    // and are recomputed for candidates after the last)
+    const int warm = min(kFWarm, nstages);
+    const int last = nstages + warm - 1;  // iterations 0 .. last
     auto stage = [&](auto bufc, int it) {
         constexpr int BUF = decltype(bufc)::value;
         char* sb = sm + BUF * kFStageB;
-        const int st = it == nstages ? 0 : it;
+        const int st = it < nstages ? it : it - nstages;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (it < nstages) dma(sm + (1 - BUF) * kFStageB, it + 1 == nstages ? 0 : it + 1);
-        tiles(sb, t0 + st * kFST * kFT, it > 0);
+        if (it < last) {
+            const int nx = it + 1 < nstages ? it + 1 : it + 1 - nstages;
+            dma(sm + (1 - BUF) * kFStageB, nx);
+        }
+        tiles(sb, t0 + st * kFST * kFT, it >= warm);
         if (it < nstages) {
 #pragma unroll
             for (int j = 0; j < 2; j++) {
@@ -420,12 +434,12 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
             }
         }
     };
-    // stage sequence: 0 (bounds only), 1 .. nstages - 1, then 0 again (candidates only, against
-    // the chunk's final bound); LDS buffers alternate
+    // stage sequence: 0 .. warm - 1 (bounds only), warm .. nstages - 1, then 0 .. warm - 1 again
+    // (candidates only, against the chunk's final bound); LDS buffers alternate
     dma(sm, 0);
-    for (int it = 0; it <= nstages; it += 2) {
+    for (int it = 0; it <= last; it += 2) {
         stage(std::integral_constant<int, 0>{}, it);
-        if (it + 1 <= nstages) stage(std::integral_constant<int, 1>{}, it + 1);
+        if (it + 1 <= last) stage(std::integral_constant<int, 1>{}, it + 1);
     }
 #pragma unroll
     for (int j = 0; j < 2; j++) {
