@@ -144,3 +144,27 @@ def test_rotate_pixel_bit_exact(oracle, harness):
         for r, c in zip(rows, cols[: len(rows)]):
             harness.erph_rotate_pixel(int(r), int(c), _p(m), W, H, _p(o))
             assert (int(o[0]), int(o[1])) == oracle.rotate_pixel(r, c, m, W, H), (r, c)
+
+
+def test_lipschitz_margin_error_model():
+    """the error model behind the consensus pruning margin (kernels.hip kLipM = 1e-6): the
+    reference's distance sqrt((double) s) with s = (dx*dx + dy*dy) + dz*dz in f32 (dx = f32(xi
+    - xj)) is within 2.5u (u = 2^-24) of the exact distance between the f32 rotation vectors, so
+    the trimmed means T_ref = T (1 +- 2.5u) and M >= 6u = 3.6e-7 keeps a pruned row's LB rigorous.
+    Checked on rotation vectors of the two regimes the pruning meets: a tight cluster (distances
+    ~1e-4) and two far clusters (~2.6), plus uniform ones."""
+    rng = np.random.default_rng(7)
+    u = 2.0 ** -24
+    for scale, centre in ((6e-5, (0.1, 0.2, 0.3)), (1.0, (0.0, 0.0, 0.0)), (6e-5, (-1.2, 0.9, 0.4))):
+        a = (rng.standard_normal((4000, 3)) * scale + np.array(centre)).astype(np.float32)
+        b = np.concatenate([a[2000:], (rng.standard_normal((2000, 3)) * 6e-5 + 0.2).astype(np.float32)])
+        d = (a - b).astype(np.float32)  # f32 differences (one rounding each)
+        s = ((d[:, 0] * d[:, 0]) + (d[:, 1] * d[:, 1])) + (d[:, 2] * d[:, 2])  # f32, reference order
+        assert s.dtype == np.float32
+        d_ref = np.sqrt(s.astype(np.float64))
+        ex = a.astype(np.longdouble) - b.astype(np.longdouble)
+        d_ex = np.sqrt((ex * ex).sum(axis=1))
+        live = d_ex > 0
+        rel = np.abs(d_ref[live] - d_ex[live]) / d_ex[live]
+        assert rel.max() <= 2.5 * u * (1 + 1e-6), rel.max() / u
+        assert 6 * u <= 1e-6  # the margin kernels.hip uses covers 6u
