@@ -123,9 +123,12 @@ constexpr int kFStageB = kFHiB + kFST * kFT * 4;  // + 512
 #endif
 // bounds-only stages at the start of a chunk (recomputed for candidates after its last stage):
 // the running bound G the candidate test compares with only falls as rows are seen, so tiles
-// tested early against a loose G are stored and re-scored for nothing (r04 A/B knob)
+// tested early against a loose G are stored and re-scored for nothing.  Same-box A/Bs per
+// 768-pair step (profiles/r04c_ab_filter_warm.txt): 1 (until r04) filter + rescore 2.78 + 1.57
+// ms; 4: 2.78 + 1.35; 8: 2.87-2.92 + 1.23 (kept, +1.5-2 % pairs/s); 12: 3.03 + 1.17; 16: 3.16 +
+// 1.13 (the recomputed quarter of the chunk's MFMAs starts to cost more than it saves)
 #ifndef ERP_FILTER_WARM
-#define ERP_FILTER_WARM 1
+#define ERP_FILTER_WARM 8
 #endif
 constexpr int kFWarm = ERP_FILTER_WARM;
 
@@ -410,9 +413,9 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     // one stage: wait for its DMAs (issued during the previous stage), barrier, the next
     // stage's DMAs into the other buffer (whose reads finished before this barrier), 4 tiles,
     // then (except in the final recompute) the query's running bound and candidate threshold
-    // (the first `warm` stages run bounds-only -- kFWarm, or every stage of a short chunk --
-    // and are recomputed for candidates after the last)
-    const int warm = min(kFWarm, nstages);
+    // (the first `warm` stages run bounds-only -- kFWarm, at most a quarter of the chunk's, at
+    // least one -- and are recomputed for candidates after the last)
+    const int warm = max(1, min(kFWarm, nstages / 4));
     const int last = nstages + warm - 1;  // iterations 0 .. last
     auto stage = [&](auto bufc, int it) {
         constexpr int BUF = decltype(bufc)::value;

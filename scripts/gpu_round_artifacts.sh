@@ -4,8 +4,9 @@
 #   1. the GPU parity tests (SKIP_TESTS=1 skips them: the bench / profile passes alone), with the
 #      real-pair gaps against the reference's recovered (R, T) written to real_gaps_<TAG>.json;
 #   2. the default bench (with the CPU baseline and the oracle parity check);
-#   3. EXTRA_BENCH=1: the counter-based sampler line (--sampler philox) and the worst-case batch
-#      as the timed batch (--main-batch worst, for its stage times);
+#   3. EXTRA_BENCH=1: the counter-based sampler line (--sampler philox), the worst-case batch
+#      as the timed batch (--main-batch worst, for its stage times), configs[2]'s shape
+#      (--kpts 2048 --pairs 1024) and the single-pair latency probe;
 #   4. a rocprofv3 kernel-trace --stats run and two PMC passes (FETCH_SIZE, WRITE_SIZE; separate
 #      passes, kernel trace only) of the bench workload with --steps 0 --warmup 2: bench.py then
 #      runs only its serial profile pass (the default step's sub-batches one after the other), so
@@ -37,6 +38,11 @@ if [ "${EXTRA_BENCH:-0}" = "1" ]; then
     --hard-steps 0 --worst-steps 0 --no-cpu-baseline --profile-tag ${TAG} > gpurun_out/bench_worst_${TAG}.json \
     2> gpurun_out/bench_worst_${TAG}.err || { tail -20 gpurun_out/bench_worst_${TAG}.err; exit 1; }
   tail -c 300 gpurun_out/bench_worst_${TAG}.json
+  echo "== bench configs[2] shape (2048 x 2048 keypoints, 1024 pairs per step)" && timeout -k 10 600 \
+    python bench.py --kpts 2048 --pairs 1024 --hard-steps 0 --worst-steps 0 --profile-tag ${TAG} \
+    > gpurun_out/bench_configs2_${TAG}.json 2> gpurun_out/bench_configs2_${TAG}.err \
+    || { tail -20 gpurun_out/bench_configs2_${TAG}.err; exit 1; }
+  tail -c 300 gpurun_out/bench_configs2_${TAG}.json
   echo "== single-pair latency (host) + kernel trace" && timeout -k 10 300 python scripts/latency_probe.py --runs 20 \
     > gpurun_out/latency_host_${TAG}.json 2> gpurun_out/latency_${TAG}.err || { tail -20 gpurun_out/latency_${TAG}.err; exit 1; }
   cat gpurun_out/latency_host_${TAG}.json
