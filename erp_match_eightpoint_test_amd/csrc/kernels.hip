@@ -333,8 +333,10 @@ __device__ __forceinline__ uint32_t mod_rup_i24(uint32_t x, double r, int d) {
 // one shift by a scalar (2 VALU, 6 cycles) replaces v_cvt_f64_u32 + v_fma_f64 (8 cycles); the
 // remainder stays one v_mad_i32_i24.  The table mtab[d] = m_d | (l_d - 1) << 32 sits right after
 // the reciprocal table (rtab + kRecipTable), read by scalar loads like it.
+// (default since r04: sampler 6.66 / 6.63 -> 6.43 / 6.42 ms per 768-pair step in a same-box A/B,
+// profiles/r04c_ab_sampler_magic.txt; every sampler / full-size fixture test green on it)
 #ifndef ERP_SAMPLER_MAGIC
-#define ERP_SAMPLER_MAGIC 0
+#define ERP_SAMPLER_MAGIC 1
 #endif
 __device__ __forceinline__ uint32_t mod_magic_i24(uint32_t x, uint64_t mt, int d) {
     const uint32_t q = __umulhi(x, (uint32_t)mt) >> (uint32_t)(mt >> 32);
