@@ -21,8 +21,10 @@ for i in range(S):
     j = 0 if same else i
     b = bench.to_device(pairs[j * B // S:(j + 1) * B // S], "cuda")
     ctx = Context(0)
-    subs.append(dict(b=b, run=PairBatchRunner(ctx=ctx, iters=10000,
-                                              sampler=int(os.environ.get("SAMPLER", "0"))),
+    # SAMPLERS: one sampler per sub-batch (comma list), else SAMPLER for all
+    smp = os.environ.get("SAMPLERS")
+    sv = int(smp.split(",")[i]) if smp else int(os.environ.get("SAMPLER", "0"))
+    subs.append(dict(b=b, run=PairBatchRunner(ctx=ctx, iters=10000, sampler=sv),
                      st=torch.cuda.Stream()))
 
 
@@ -59,6 +61,10 @@ for k in ("ovl0", "ovl1", "ser1"):
             bad.append(f)
             print(f"{k}: field {f} differs on pairs {ne[:10].tolist()}: {a[ne[:3]].tolist()} vs {c[ne[:3]].tolist()}")
     print(k, "identical to ser0:", not bad)
+for k in ("ovl0", "ovl1"):
+    br0, br1 = r["ser0"]["binned_rows"].reshape(S, -1), r[k]["binned_rows"].reshape(S, -1)
+    print(k, "sub-batches whose records differ from their serial run:",
+          [i for i in range(S) if not np.array_equal(br0[i], br1[i])])
 if same:
     for k in ("ser0", "ovl0", "ovl1"):
         br = r[k]["binned_rows"].reshape(S, -1)
