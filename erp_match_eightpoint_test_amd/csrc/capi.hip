@@ -2,6 +2,7 @@
 // orchestration of the hot-path kernels on one HIP stream.  No host round trip inside a
 // pipeline run (match counts, sample sizes and hypothesis counts stay on the device).
 #include <hip/hip_runtime.h>
+#include <cstdio>
 #include <cstdlib>
 
 #include <stdint.h>
@@ -34,14 +35,36 @@ struct DevBuf {
     size_t n = 0;
 };
 
+// Debug: ERP_ALLOC_PAD = N gives every buffer N canary bytes (0xA5) past its end;
+// erp_debug_check_pads() reports buffers whose canary a kernel overwrote.
+size_t alloc_pad() {
+    static const size_t pad = getenv("ERP_ALLOC_PAD") ? (size_t)atoll(getenv("ERP_ALLOC_PAD")) : 0;
+    return pad;
+}
+std::mutex g_pad_mu;
+std::vector<std::pair<void*, size_t>> g_padded;
+
 // grow-only device buffer; returns false on allocation failure
 bool ensure(DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.n >= bytes) return true;
-    if (b.p) (void)hipFree(b.p);
+    const size_t pad = alloc_pad();
+    if (b.p) {
+        if (pad) {
+            std::lock_guard<std::mutex> g(g_pad_mu);
+            for (auto& e : g_padded)
+                if (e.first == b.p) e = g_padded.back(), g_padded.pop_back();
+        }
+        (void)hipFree(b.p);
+    }
     b.p = nullptr;
     b.n = 0;
-    if (hipMalloc(&b.p, bytes) != hipSuccess) return false;
+    if (hipMalloc(&b.p, bytes + pad) != hipSuccess) return false;
+    if (pad) {
+        if (hipMemset((char*)b.p + bytes, 0xA5, pad) != hipSuccess) return false;
+        std::lock_guard<std::mutex> g(g_pad_mu);
+        g_padded.emplace_back(b.p, bytes);
+    }
     b.n = bytes;
     return true;
 }
@@ -96,6 +119,11 @@ struct erp_ctx {
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
         rtab, limbs, tsplit, ovf, remap_scr, vchunk, lipref, inl;
     DevBuf extra[13];         // erp_ctx_scratch_internal slots (1-11 SURF, 12 viz)
+    // debug (ERP_DEBUG_SNAP=1): lb, ub and the first-stage list counts right after the bounds
+    // pass, fetched with erp_debug_snapshot
+    bool snap_on = getenv("ERP_DEBUG_SNAP") && atoi(getenv("ERP_DEBUG_SNAP")) != 0;
+    DevBuf snap;
+    size_t snap_bytes = 0;
     uint64_t surf_key = 0;    // (W, H, params) of the SURF layer table in extra[1]
     uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
     // consensus zoom levels (0-2; ERP_ZOOM_LEVELS, an A/B knob)
@@ -600,6 +628,20 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (int32_t*)c->zsel.p, c->zoom_refs, c->lip2,
                                             (int32_t*)c->sortbuf.p, c->lipref.p, c->lipg,
                                             c->lipg_fac, c->flat_refs, c->refine_hint, st));
+    }
+    if (c->snap_on && phase == 0) {
+        const size_t nrow = (size_t)sh.n_pairs * 2 * sh.iters;
+        // (kernels.hip lipref_cap at the default second-stage step 4)
+        const size_t lrb = (size_t)sh.n_pairs * (2 * sh.iters / 4 + 64) * 16 + (size_t)sh.n_pairs * 12;
+        c->snap_bytes = nrow * 16 + (size_t)sh.n_pairs * 4 + lrb;
+        if (!ensure(c->snap, c->snap_bytes)) return ERP_OUT_OF_MEMORY;
+        ERP_CK(hipMemcpyAsync(c->snap.p, lbp, nrow * 8, hipMemcpyDeviceToDevice, st));
+        ERP_CK(hipMemcpyAsync((char*)c->snap.p + nrow * 8, ubp, nrow * 8, hipMemcpyDeviceToDevice, st));
+        ERP_CK(hipMemcpyAsync((char*)c->snap.p + nrow * 16, (int32_t*)c->nsurv.p + sh.n_pairs,
+                              (size_t)sh.n_pairs * 4, hipMemcpyDeviceToDevice, st));
+        // + the first-stage references (float4 [P][cap]), their U [P] f64 and counts [P] i32
+        ERP_CK(hipMemcpyAsync((char*)c->snap.p + nrow * 16 + (size_t)sh.n_pairs * 4, c->lipref.p, lrb,
+                              hipMemcpyDeviceToDevice, st));
     }
     if (phase == 1) return ERP_OK;
     if (phase == 2)  // the bounds ran per shard (binned rows not combined): report -1
@@ -1143,3 +1185,38 @@ erp_status erp_eight_point_estimation(erp_ctx* ctx, const double* h_bl, const do
 }
 
 }  // extern "C"
+
+// debug (ERP_ALLOC_PAD): buffers whose canary bytes were overwritten, reported on stderr;
+// returns their number (0 without ERP_ALLOC_PAD)
+extern "C" int erp_debug_check_pads(void) {
+    const size_t pad = alloc_pad();
+    if (!pad) return 0;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    std::lock_guard<std::mutex> g(g_pad_mu);
+    std::vector<unsigned char> h(pad);
+    int bad = 0;
+    for (auto& e : g_padded) {
+        if (hipMemcpy(h.data(), (char*)e.first + e.second, pad, hipMemcpyDeviceToHost) != hipSuccess)
+            return -1;
+        size_t first = pad, last = 0;
+        for (size_t i = 0; i < pad; i++)
+            if (h[i] != 0xA5) first = std::min(first, i), last = i;
+        if (first < pad) {
+            bad++;
+            fprintf(stderr, "erp_debug_check_pads: buffer of %zu bytes at %p: canary bytes %zu .. %zu overwritten\n",
+                    e.second, e.first, first, last);
+        }
+    }
+    return bad;
+}
+
+// debug (ERP_DEBUG_SNAP=1): the last run's snapshot (lb [P][2 iters] f64, ub, first-stage
+// counts [P] i32) into host memory; returns the snapshot's size in bytes (0: none)
+extern "C" long long erp_debug_snapshot(erp_ctx* ctx, void* host, size_t bytes) {
+    if (!ctx || !ctx->snap_bytes) return 0;
+    if (host && bytes >= ctx->snap_bytes) {
+        if (hipDeviceSynchronize() != hipSuccess) return -1;
+        if (hipMemcpy(host, ctx->snap.p, ctx->snap_bytes, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    }
+    return (long long)ctx->snap_bytes;
+}

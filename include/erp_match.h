@@ -231,6 +231,16 @@ erp_status erp_ctx_set_matcher(erp_ctx* ctx, int32_t method);
    captures anew (up to 8 graphs per context, least recently used dropped).  Not used while
    stage timing is on or on the NULL stream.  Default off. */
 erp_status erp_ctx_set_graphs(erp_ctx* ctx, int32_t enable);
+/* debugging hooks (no reference counterpart), inert unless their environment variable is set
+   when the buffers / context are created:
+   ERP_ALLOC_PAD = N: every device buffer gets N canary bytes past its end;
+   erp_debug_check_pads() returns how many canaries a kernel overwrote (reported on stderr).
+   ERP_DEBUG_SNAP = 1: erp_pair_batch_run keeps a device copy of lb, ub ([P][2 iters] f64 each),
+   the first-stage list counts ([P] i32) and the first-stage Lipschitz references right after
+   the bounds pass; erp_debug_snapshot copies it to host (returns its size; host NULL: size
+   only). */
+int erp_debug_check_pads(void);
+long long erp_debug_snapshot(erp_ctx* ctx, void* host, size_t bytes);
 
 /* device pointers; writes up to nq matches in ascending queryIdx order and *d_count. */
 erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,
