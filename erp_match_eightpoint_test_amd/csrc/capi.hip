@@ -698,6 +698,21 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                            (int32_t*)c->nsurv.p + sh.n_pairs, sh, cfg->sample_frac, cfg->trim_lo, cfg->trim_hi,
                                            (float*)c->sortbuf.p, results, st));
     }
+    if (c->snap_on && phase == 0 && c->snap_bytes) {
+        // + the consensus's rotation vectors (SoA [P][3][2 iters] f32) as they are at its end
+        const size_t rvb = (size_t)sh.n_pairs * 6 * sh.iters * 4;
+        const size_t head = c->snap_bytes;
+        DevBuf keep = c->snap;
+        if (c->snap.n < head + rvb) {
+            c->snap = DevBuf();
+            if (!ensure(c->snap, head + rvb)) return ERP_OUT_OF_MEMORY;
+            ERP_CK(hipMemcpyAsync(c->snap.p, keep.p, head, hipMemcpyDeviceToDevice, st));
+            ERP_CK(hipStreamSynchronize(st));
+            (void)hipFree(keep.p);
+        }
+        ERP_CK(hipMemcpyAsync((char*)c->snap.p + head, c->rv.p, rvb, hipMemcpyDeviceToDevice, st));
+        c->snap_bytes = head + rvb;
+    }
     return ERP_OK;
 }
 

@@ -55,6 +55,24 @@ L = subs[0]["run"].ctx.L
 if os.environ.get("ERP_ALLOC_PAD"):
     print("canaries overwritten after the serial run:", L.erp_debug_check_pads())
 r.update(ovl0=overlapped(), ovl1=overlapped(), ser1=serial())
+# REPEAT = n: n more overlapped runs, counting the records whose result fields (everything but
+# the work diagnostics binned_rows / survivors) differ from the serial run's
+rep = int(os.environ.get("REPEAT", "0"))
+if rep:
+    a0 = r["ser0"]["results"].view(RESULT_DTYPE).reshape(-1)
+    res_fields = [f for f in RESULT_DTYPE.names if f not in ("binned_rows", "survivors")]
+    nbad = nbr = 0
+    for _ in range(rep):
+        c = overlapped()["results"].view(RESULT_DTYPE).reshape(-1)
+        bad = np.zeros(len(a0), bool)
+        for f in res_fields:
+            bad |= np.any((a0[f] != c[f]).reshape(len(a0), -1), axis=1)
+        nbad += int(bad.sum())
+        nbr += int((a0["binned_rows"] != c["binned_rows"]).sum())
+        if bad.any():
+            print("result fields differ on pairs", np.nonzero(bad)[0].tolist())
+    print(f"REPEAT {rep}: {rep * len(a0)} overlapped records, {nbad} with a result field unlike the "
+          f"serial run's, {nbr} with other binned_rows")
 if os.environ.get("ERP_ALLOC_PAD"):
     print("canaries overwritten after all runs:", L.erp_debug_check_pads())
 for k in ("ser1", "ovl0", "ovl1"):
@@ -97,7 +115,8 @@ if os.environ.get("ERP_DEBUG_SNAP") == "1":
             o += P * cap * 16
             lU = buf[o:o + 8 * P].view(np.float64)
             lcnt = buf[o + 8 * P:o + 12 * P].view(np.int32)
-            out.append((lb, ub, cnt, lref, lU, lcnt))
+            rvend = buf[o + 12 * P:].view(np.float32).reshape(P, 3, -1) if n > o + 12 * P else None
+            out.append((lb, ub, cnt, lref, lU, lcnt, rvend))
         return out
 
     def run_and_snap(f):
@@ -128,13 +147,32 @@ if os.environ.get("ERP_DEBUG_SNAP") == "1":
                     msg.append(f"   row {j}: lb {lb0[p, j]!r} vs {lb1[p, j]!r}, ub {ub0[p, j]!r} vs {ub1[p, j]!r}")
             print(f"snap {name} sub-batch {i}: counts differ on {len(dc)} pairs", *msg, sep="\n  ")
 
+    # the consensus's SoA rotation vectors at the end of the run: equal to the AOS rvec output
+    # (written by the same compaction) in every run?
+    for name, sx, rk in (("ser", s0, "ser0"), ("ovl", s1, None)):
+        for i in range(len(subs)):
+            rvend = sx[i][6]
+            if rvend is None:
+                continue
+            K = r["ser0"]["results"].view(RESULT_DTYPE).reshape(-1)["K"][i * 128:(i + 1) * 128]
+            nb = 0
+            for p in range(128):
+                k = int(K[p])
+                aos = r["ser0"]["rvec"][i * 128 + p, :k] if "rvec" in WANT else None
+                if aos is not None and not np.array_equal(rvend[p, :, :k].T, aos):
+                    nb += 1
+                    if nb <= 2:
+                        d = np.nonzero(np.any(rvend[p, :, :k].T != aos, axis=1))[0]
+                        print(f"  {name} sub {i} pair {p}: {len(d)} rows of rv changed, first {d[:4].tolist()}")
+            print(f"rv at the end, {name} sub-batch {i}: {nb} pairs with rv unlike the rvec output")
+
     # the first-stage Lipschitz test of the rows whose pruning differs, redone on the host from
     # the serial snapshot (kernels.hip consensus_lip_refs_kernel / lip_prune_rows, M = 1e-6)
     if "rvec" in WANT:
         M = 1e-6
         for i in range(len(subs)):
-            lb0, ub0, c0, lr0, lU0, lc0 = s0[i]
-            lb1, ub1, c1, lr1, lU1, lc1 = s1[i]
+            lb0, ub0, c0, lr0, lU0, lc0 = s0[i][:6]
+            lb1, ub1, c1, lr1, lU1, lc1 = s1[i][:6]
             K = r["ser0"]["results"].view(RESULT_DTYPE).reshape(-1)["K"][i * 128:(i + 1) * 128]
             for p in np.nonzero(c0 != c1)[0][:2]:
                 k = int(K[p])
