@@ -28,8 +28,27 @@ PUBLIC_HEADERS = ["erp_match.h", os.path.join("erp", "feature_matcher.hpp"),
 # distances must round exactly like the reference's x86-64 code (no FMA contraction).
 # Never add -ffast-math / -fno-hip-fp32-correctly-rounded-divide-sqrt: sqrtf must be
 # correctly rounded for bit-exact DMatch.distance.
+# No packed-FP32 instructions in any kernel (v_pk_add/mul/fma_f32, v_pk_mov_b32): on MI355X a
+# packed-FP32 result read one or two instructions later by another VALU op can come back with
+# a stale LO half while other waves on the CU issue int8 / bf16 MFMAs (the Gram and matcher
+# kernels of the other streams) -- measured by scripts/dev/pk_synth.py: ~3e7 wrong lo halves
+# per 10 ms beside v_mfma_i32_32x32x32_i8, none alone.  That was the
+# round-4 overlap nondeterminism.  The device cc1 drops the feature; the host cc1 ignores it
+# (its "not a recognized feature" warning is filtered below).
+NO_PACKED_FP32 = ["-Xclang", "-target-feature", "-Xclang", "-packed-fp32-ops"]
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-Wall",
-            "-Wno-unused-function", f"--offload-arch={ARCH}"]
+            "-Wno-unused-function", f"--offload-arch={ARCH}", *NO_PACKED_FP32]
+_HOST_FEATURE_WARNING = "'-packed-fp32-ops' is not a recognized feature for this target"
+
+
+def _run_filtered(cmd):
+    """run a hipcc command, dropping the host cc1's warning about the device-only feature"""
+    r = subprocess.run(cmd, stderr=subprocess.PIPE, text=True)
+    err = "".join(line for line in r.stderr.splitlines(True) if _HOST_FEATURE_WARNING not in line)
+    if err:
+        sys.stderr.write(err)
+    if r.returncode != 0:
+        raise subprocess.CalledProcessError(r.returncode, cmd)
 # per-source extras: the matcher's MFMA accumulators in VGPRs (the filter's bounds read them
 # directly; the default AGPR form costs one v_accvgpr_read per element) and no NaN quieting in
 # its min trees (finite descriptors; matcher.hip header)
@@ -74,12 +93,12 @@ def build(force: bool = False, verbose: bool = False, lib_path: str = LIB_PATH,
     def run(cmd):
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+        _run_filtered(cmd)
     with ThreadPoolExecutor(jobs) as ex:
         for f in [ex.submit(run, c) for c in cmds]:
             f.result()
     tmp = lib_path + ".tmp"
-    subprocess.run([HIPCC, *CXXFLAGS, "-shared", "-o", tmp, *objs], check=True)
+    _run_filtered([HIPCC, *CXXFLAGS, "-shared", "-o", tmp, *objs])
     os.replace(tmp, lib_path)
     for o in objs:
         os.remove(o)

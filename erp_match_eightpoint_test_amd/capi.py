@@ -93,7 +93,7 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_inv3", "erp_rectify_matrices", "erp_consensus_hyps_shard_dev",
             "erp_consensus_hyps_finish_dev", "erp_surf_params_default",
             "erp_surf_detect_compute_dev", "erp_epipolar_draw_dev", "erp_draw_match_dev",
-            "erp_random_shuffle_prefix", "erp_ctx_set_graphs", "erp_debug_check_pads",
+            "erp_random_shuffle_prefix", "erp_ctx_set_graphs", "erp_debug_check_pads", "erp_debug_lip_counters",
             "erp_debug_snapshot"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
@@ -166,6 +166,8 @@ def load(build_if_missing: bool = False):
     L.erp_ctx_set_graphs.argtypes = [P, C.c_int32]
     L.erp_debug_check_pads.restype = C.c_int
     L.erp_debug_check_pads.argtypes = []
+    L.erp_debug_lip_counters.restype = C.c_int
+    L.erp_debug_lip_counters.argtypes = [C.c_void_p]
     L.erp_debug_snapshot.restype = C.c_longlong
     L.erp_debug_snapshot.argtypes = [P, C.c_void_p, C.c_size_t]
     L.erp_crop_rotated_image_dev.argtypes = [P, P, C.c_int32, C.c_int32, C.c_float, P, P]

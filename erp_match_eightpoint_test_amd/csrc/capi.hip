@@ -156,6 +156,13 @@ struct erp_ctx {
     bool fuse_sampler = getenv("ERP_FUSE_SAMPLER") && atoi(getenv("ERP_FUSE_SAMPLER")) != 0;
     // HIP-graph replay of erp_pair_batch_run (erp_ctx_set_graphs): key bytes -> executable graph
     bool use_graphs = getenv("ERP_GRAPHS") && atoi(getenv("ERP_GRAPHS")) != 0;
+    // debug (ERP_DEBUG_STAGES, a bit mask; default every stage): which stage groups
+    // erp_pair_batch_run enqueues -- 1 matcher + gather, 2 jump polynomials + windows, 4 sampler,
+    // 8 Gram (with the fused eigen), 32 eigen fallback + estimate, 16 consensus.  A skipped stage leaves the previous call's
+    // scratch in place, so after one full call the later stages still read valid inputs (the
+    // LDS-interference probe, scripts/dev/lds_guard_probe.py, runs one stage group at a time)
+    // (read at every erp_pair_batch_run)
+    int dbg_stages = -1;
     struct Graph {
         std::vector<uint8_t> key;
         hipGraphExec_t exec = nullptr;
@@ -527,12 +534,12 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
     auto* flags = (int32_t*)c->flags.p;
     auto* hyps = (out && out->hyps) ? out->hyps : (erp_hypothesis*)c->hyps.p;
     if (cfg->sampler == ERP_SAMPLER_PHILOX) {  // counter-based: no jump polynomials / windows
-        {
+        if (c->dbg_stages & 4) {
             StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
             ERP_CK(erp::launch_philox_sampler(counts, sh, cfg->sample_frac, cfg->seed, cfg->offset,
                                               sh.max_nq, (uint32_t*)c->idx.p, flags, st));
         }
-        {
+        if (c->dbg_stages & 8) {
             StageTimer _t(ctx, ERP_STAGE_GRAM, st);
             ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
                                          cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
@@ -540,7 +547,7 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
                                          ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr,
                                          ERP_FUSE_EIGEN == 2 ? hyps : nullptr, cfg->valid_abs, st));
         }
-        {
+        if (c->dbg_stages & 32) {
             StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
             ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
                                      cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
@@ -548,11 +555,11 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
         }
         return run_inliers(c, sh, cfg, hyps, st);
     }
-    {
+    if (c->dbg_stages & 2) {
         StageTimer _t(ctx, ERP_STAGE_JUMP_PREP, st);
         ERP_CK(erp::launch_jump_prep(counts, sh, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p, st));
     }
-    {
+    if (c->dbg_stages & 2) {
         StageTimer _t(ctx, ERP_STAGE_WINDOWS, st);
         ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
                                    (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
@@ -571,20 +578,22 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
                 (double*)c->gram.p, ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr, st));
         }
     } else {
-        {
+        if (c->dbg_stages & 4) {
             StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
             ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
                                        (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
                                        (uint32_t*)c->wins.p, (uint32_t*)c->idx.p, flags, st, 1));
         }
-        StageTimer _t(ctx, ERP_STAGE_GRAM, st);
-        ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
-                                     cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
-                                     out ? out->samples : nullptr,
-                                     ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr,
-                                     ERP_FUSE_EIGEN == 2 ? hyps : nullptr, cfg->valid_abs, st));
+        if (c->dbg_stages & 8) {
+            StageTimer _t(ctx, ERP_STAGE_GRAM, st);
+            ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
+                                         cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
+                                         out ? out->samples : nullptr,
+                                         ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr,
+                                         ERP_FUSE_EIGEN == 2 ? hyps : nullptr, cfg->valid_abs, st));
+        }
     }
-    {
+    if (c->dbg_stages & 32) {
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
         ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
                                  cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
@@ -721,6 +730,7 @@ erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                          const erp_batch_outputs* out, erp_pair_result* results, hipStream_t st) {
     erp_status es = run_hypotheses(c, sh, cfg, out, st);
     if (es != ERP_OK) return es;
+    if (!(c->dbg_stages & 16)) return ERP_OK;
     return run_consensus(c, sh, cfg, out, results, st, true);
 }
 
@@ -793,6 +803,11 @@ namespace {
 erp_status batch_enqueue(erp_ctx* ctx, const erp_pair_batch* b, float ratio,
                          const erp_ransac_cfg* cfg, const erp_batch_outputs* out,
                          const erp::BatchShape& sh, erp_dmatch* matches, hipStream_t st) {
+    {
+        const char* m = getenv("ERP_DEBUG_STAGES");
+        ctx->dbg_stages = m ? (int)strtol(m, nullptr, 0) : -1;
+    }
+    if (!(ctx->dbg_stages & 1)) return run_estimator(ctx, sh, cfg, out, out->results, st);
     ERP_CK(hipMemsetAsync(ctx->flags.p, 0, (size_t)sh.n_pairs * 4, st));
     erp_status es = run_matcher(ctx, b->desc_l, b->desc_r, b->off_l, b->off_r, sh, ratio, matches,
                                 (int32_t*)ctx->counts.p, (int32_t*)ctx->flags.p, st);
@@ -1203,6 +1218,8 @@ erp_status erp_eight_point_estimation(erp_ctx* ctx, const double* h_bl, const do
 
 // debug (ERP_ALLOC_PAD): buffers whose canary bytes were overwritten, reported on stderr;
 // returns their number (0 without ERP_ALLOC_PAD)
+extern "C" int erp_debug_lip_counters(uint32_t* out64) { return erp::debug_lip_counters(out64); }
+
 extern "C" int erp_debug_check_pads(void) {
     const size_t pad = alloc_pad();
     if (!pad) return 0;

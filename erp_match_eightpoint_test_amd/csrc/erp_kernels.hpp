@@ -119,6 +119,7 @@ hipError_t launch_philox_sampler(const int32_t* counts, const BatchShape& sh, do
                                  uint32_t seed, uint64_t offset, int max_m, uint32_t* selw,
                                  int32_t* flags, hipStream_t st);
 hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st);
+int debug_lip_counters(uint32_t* out64);
 // Gram of every iteration's sample on int8 MFMA (exact fixed-point sums) -> gram[p][36][iters];
 // limbs = scratch of gram_limbs_bytes(sh); samples (debug, may be NULL) = the sampled indices.
 // evec != NULL fuses the eigen stage's inverse iteration (pairs with s >= 9) into the Gram

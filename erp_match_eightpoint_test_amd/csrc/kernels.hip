@@ -409,6 +409,11 @@ __device__ __forceinline__ void lds_wait_step(uint32_t& o, int v) {
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(o) : : "memory");
 }
 
+// ERP_SAMPLER_CLAMP=1: draw positions j >= s clamped to s (every LDS access inside the
+// allocation; a development variant for the LDS-interference probe)
+#ifndef ERP_SAMPLER_CLAMP
+#define ERP_SAMPLER_CLAMP 0
+#endif
 // steps i >= s: one LDS op per draw, no clamp, no validity select (~10 VALU per draw)
 template <bool I24, int RS = 8>
 __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uint32_t* bm,
@@ -432,8 +437,9 @@ __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uin
             const int slot = 30 - u;
             const uint32_t rv = ring[slot];
             ring[slot] = rv - ring[(slot + 28) % 31];
-            const uint32_t j = I24 ? mod_i24(rv >> 1, mt[u], ii + 1)
-                                   : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
+            uint32_t j = I24 ? mod_i24(rv >> 1, mt[u], ii + 1)
+                             : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
+            if (ERP_SAMPLER_CLAMP) j = min(j, (uint32_t)s);  // (bit s: clear and allocated)
             olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), 1u << (j & 31), zero);
             pos[u] = j;
         }
@@ -556,7 +562,8 @@ __device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uin
         ring[slot] = rv - ring[(slot + 28) % 31];
         if (ii < 1) continue;
         const double r = rtab[ii + 1];
-        const uint32_t j = mod_rup(rv >> 1, r, (double)(ii + 1));
+        uint32_t j = mod_rup(rv >> 1, r, (double)(ii + 1));
+        if (ERP_SAMPLER_CLAMP) j = min(j, (uint32_t)s);
         // bm[i] (read before the clear: j = i keeps the bit)
         const uint32_t bi = ii < s ? (bm[bm_index<RS>(ii >> 5, lane)] >> (ii & 31)) & 1u : 0u;
         uint32_t* wp = &bm[bm_index<RS>((int)(j >> 5), lane)];  // j >= s: a cleared or out-of-allocation word
@@ -2407,9 +2414,28 @@ struct LipShared {
     double red[4];
     int cnt[4];
 };
+#ifndef ERP_LIP_VERIFY
+#define ERP_LIP_VERIFY 0
+#endif
+#if ERP_LIP_VERIFY
+// debug (ERP_LIP_VERIFY=1 builds): lip_prune_rows re-checks its LDS operands against their
+// global sources after every batch's tests -- [0] staged references that differ, [1] candidate
+// rows whose coordinates differ from the rotation vectors, [8..] the first mismatches
+__device__ uint32_t g_lip_dbg[64];
+__device__ void lip_dbg_note(int kind, uint32_t a, uint32_t b, uint32_t c) {
+    atomicAdd(&g_lip_dbg[kind], 1u);
+    const uint32_t k = atomicAdd(&g_lip_dbg[2], 1u);
+    if (k < 14) {
+        g_lip_dbg[8 + 4 * k] = (uint32_t)kind;
+        g_lip_dbg[9 + 4 * k] = a;
+        g_lip_dbg[10 + 4 * k] = b;
+        g_lip_dbg[11 + 4 * k] = c;
+    }
+}
+#endif
 template <class Prune>
 __device__ int lip_prune_rows(LipShared& sh, int na, const float4* __restrict__ R, int m,
-                              Prune prune) {
+                              Prune prune, const float* __restrict__ Xv = nullptr, int xstride = 0) {
     const int tid = threadIdx.x, lane = wave_lane();
     int t = 0;
     for (int c0 = 0; c0 < m && na > 0; c0 += kLipChunk2) {
@@ -2446,6 +2472,28 @@ __device__ int lip_prune_rows(LipShared& sh, int na, const float4* __restrict__ 
                 }
             }
             const bool p0 = v0 && (neg0 >> 31), p1 = v1 && (neg1 >> 31);
+#if ERP_LIP_VERIFY
+            if (tid < kLipBatch) {
+                const int c = q0 + tid;
+                const float4 g = c < nc ? R[c0 + c] : make_float4(0.f, 0.f, 0.f, -1.f);
+                const float4 l = sh.refs[c];
+                if (__float_as_uint(g.x) != __float_as_uint(l.x) || __float_as_uint(g.y) != __float_as_uint(l.y) ||
+                    __float_as_uint(g.z) != __float_as_uint(l.z) || __float_as_uint(g.w) != __float_as_uint(l.w))
+                    lip_dbg_note(0, (uint32_t)c, __float_as_uint(l.w), __float_as_uint(g.w));
+            }
+            if (Xv) {
+                const float4 aa[2] = {a0, a1};
+                const bool vv[2] = {v0, v1};
+                for (int u = 0; u < 2; u++) {
+                    if (!vv[u]) continue;
+                    const int row = __float_as_int(aa[u].w);
+                    if (row < 0 || row >= xstride || __float_as_uint(Xv[row]) != __float_as_uint(aa[u].x) ||
+                        __float_as_uint(Xv[xstride + row]) != __float_as_uint(aa[u].y) ||
+                        __float_as_uint(Xv[2 * xstride + row]) != __float_as_uint(aa[u].z))
+                        lip_dbg_note(1, (uint32_t)row, __float_as_uint(aa[u].x), (uint32_t)(2 * tid + u));
+                }
+            }
+#endif
             if (p0) prune(__float_as_int(a0.w));
             if (p1) prune(__float_as_int(a1.w));
             const bool k0 = v0 && !p0, k1 = v1 && !p1;
@@ -2631,7 +2679,7 @@ __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
             LBp[i] = SL ? fmax(LBp[i], U * kLipPrunedLB) : U * kLipPrunedLB;
             UBp[i] = __builtin_huge_val();
         };
-        na = lip_prune_rows(sh, na, lref + (size_t)p * cap, m, prune);
+        na = lip_prune_rows(sh, na, lref + (size_t)p * cap, m, prune, X, stride);
     }
     if (prune_on && gref && gcnt[p] > 0) {  // the rows left against the central references' G
         auto prune = [&](int i) {
@@ -4378,6 +4426,19 @@ bool build_magic_table(uint64_t* mtab, int n) {
         mtab[d] = m | ((uint64_t)(l - 1) << 32);
     }
     return ok;
+}
+
+// debug counters of ERP_LIP_VERIFY builds (0 = copied and reset; -1 = not a verify build)
+int debug_lip_counters(uint32_t* out64) {
+#if ERP_LIP_VERIFY
+    if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_lip_dbg), 64 * 4) != hipSuccess) return 1;
+    static const uint32_t zero[64] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lip_dbg), zero, 64 * 4) != hipSuccess) return 1;
+    return 0;
+#else
+    (void)out64;
+    return -1;
+#endif
 }
 
 hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st) {

@@ -241,6 +241,10 @@ erp_status erp_ctx_set_graphs(erp_ctx* ctx, int32_t enable);
    only). */
 int erp_debug_check_pads(void);
 long long erp_debug_snapshot(erp_ctx* ctx, void* host, size_t bytes);
+/* debug counters of a library built with -DERP_LIP_VERIFY=1 (the Lipschitz pruning pass
+   re-checks its LDS operands against their global sources): copies 64 words into out64 and
+   resets them; returns 0, or -1 for a library built without the check. */
+int erp_debug_lip_counters(uint32_t* out64);
 
 /* device pointers; writes up to nq matches in ascending queryIdx order and *d_count. */
 erp_status erp_match_knn2_ratio(erp_ctx* ctx, const float* d_query, int32_t nq,

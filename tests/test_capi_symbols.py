@@ -63,6 +63,38 @@ def test_gfx950_code_object():
     assert b"gfx950" in data
 
 
+def _device_isa(lib_path, tmp_path):
+    """disassembly of the library's gfx950 code object (llvm-objdump --offloading extracts the
+    bundles next to its input, so a copy goes to tmp_path first)"""
+    import shutil
+    import subprocess
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    if not os.path.exists(objdump):
+        pytest.skip("llvm-objdump not available")
+    src = tmp_path / "lib.so"
+    shutil.copy(lib_path, src)
+    subprocess.run([objdump, "--offloading", str(src)], check=True, cwd=tmp_path,
+                   capture_output=True)
+    cos = [p for p in tmp_path.iterdir() if "gfx950" in p.name]
+    assert cos, "no gfx950 code object in the library"
+    return "".join(subprocess.run([objdump, "-d", "--mcpu=gfx950", str(p)], check=True,
+                                  capture_output=True, text=True).stdout for p in cos)
+
+
+def test_no_packed_fp32_instructions(tmp_path):
+    """No kernel of the product uses packed-FP32 VALU instructions: on MI355X their LO half can
+    read back stale while other waves of the CU issue int8 / bf16 MFMAs (the
+    round-4 overlapped-streams nondeterminism; scripts/dev/pk_synth.py measures it).  The build
+    drops the target feature (_build.NO_PACKED_FP32); this guards against a source or flag
+    change bringing them back."""
+    from erp_match_eightpoint_test_amd import _build
+    _build.build()
+    isa = _device_isa(_build.LIB_PATH, tmp_path)
+    assert "v_mfma_i32_32x32x32_i8" in isa and "v_mfma_f32_32x32x16_bf16" in isa
+    packed = sorted(set(re.findall(r"\bv_pk_(?:add|mul|fma|mov)_(?:f32|b32)\b", isa)))
+    assert packed == [], packed
+
+
 @pytest.mark.parametrize("seed,offset,m,n", [(1, 0, 300, 7), (1, 80, 4000, 7), (7, 3, 9, 5),
                                              (1, 0, 1, 1), (1, 0, 20, 0), (3, 12345, 2, 2)])
 def test_random_shuffle_prefix_matches_glibc(lib, oracle, seed, offset, m, n):
