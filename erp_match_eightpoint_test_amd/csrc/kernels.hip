@@ -364,13 +364,14 @@ __device__ __forceinline__ uint32_t mod_i24(uint32_t x, StepDiv c, int d) { retu
 //   steps i >= s (replay_block_draws):   sel = bm[j];  bm[j] := 0
 //   steps 1 <= i < s (replay_block_prefix): sel = bm[j];  bm[j] := bm[i]
 //   the block straddling s / running below step 1 (replay_block_mixed): per step
-// A position j >= s needs no clamp: its bit is 0 (positions s .. the allocation's end are
-// cleared by the kernel's prologue) or its word lies beyond the workgroup's LDS allocation,
-// where gfx950 returns 0 and drops the write (scripts/dev/lds_oob.hip: measured up to 512 KB,
-// i.e. j < 65536 = the keypoint cap).  (r04: a variant clamping j to s, +1 VALU per draw, was
-// 5 % slower and left the overlapped-streams binned_rows differences of DESIGN.md 5c exactly as
-// they were, so those writes are not what perturbs co-resident kernels.)  The LDS ops' results
-// are consumed kReplayLag steps after issue, so the traffic streams without waits.
+// A position j >= s is clamped to s (ERP_SAMPLER_CLAMP, default since r05): bit s is 0 (the
+// prologue clears every word of the allocation past the positions < s) and its word is
+// allocated, so no LDS access leaves the workgroup's allocation.  Until r05 the clamp was left
+// out (one v_min_u32 per draw, sampler ~5 % slower), relying on gfx950 dropping writes and
+// returning 0 beyond the allocation (scripts/dev/lds_oob.hip; and an LDS guard kernel beside
+// the sampler saw no foreign write, profiles/r05a_lds_guard_stage_bisect.txt) -- undocumented
+// behaviour a drop-in exact path should not rest on.  The LDS ops' results are consumed
+// kReplayLag steps after issue, so the traffic streams without waits.
 // (bm_lane = LDS byte address of the lane's word 0; words are 2^RS B apart -- 256 B for the
 // standalone sampler's [word][lane], 1 KB for the fused kernel's [word][wave][lane]: the address
 // is one v_lshl_add_u32 of j >> 5)
@@ -409,12 +410,12 @@ __device__ __forceinline__ void lds_wait_step(uint32_t& o, int v) {
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(o) : : "memory");
 }
 
-// ERP_SAMPLER_CLAMP=1: draw positions j >= s clamped to s (every LDS access inside the
-// allocation; a development variant for the LDS-interference probe)
+// ERP_SAMPLER_CLAMP=0 (A/B only): the r04 clamp-free draws (positions j >= s address words
+// past the allocation)
 #ifndef ERP_SAMPLER_CLAMP
-#define ERP_SAMPLER_CLAMP 0
+#define ERP_SAMPLER_CLAMP 1
 #endif
-// steps i >= s: one LDS op per draw, no clamp, no validity select (~10 VALU per draw)
+// steps i >= s: one LDS op per draw, positions clamped to s, no validity select
 template <bool I24, int RS = 8>
 __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uint32_t* bm,
                                                        int lane, int i0, int s,
@@ -624,6 +625,9 @@ __device__ __forceinline__ uint32_t replay_block_draws_ilp(uint32_t (&ring)[31],
     const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
     uint32_t jj[31];
     block_positions<I24>(ring, i0, rtab, jj);
+    if (ERP_SAMPLER_CLAMP)
+#pragma unroll
+        for (int u = 0; u < 31; u++) jj[u] = min(jj[u], (uint32_t)s);  // (bit s: clear, allocated)
     const uint32_t zero = 0;
     uint32_t olds[31];
     uint32_t nw[4] = {0, 0, 0, 0};
@@ -1146,9 +1150,9 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
 // MFMA-only and a VALU-only wave on one CU run concurrently).  12 waves per workgroup, one
 // workgroup per CU: each SIMD holds one sampler wave and two MFMA waves (<= 168 VGPRs).
 // LDS: [limb ring: 2 x 14 KB][selection ring: 2 x 2 KB] ... [bitmaps: rows x kFSw x 64 words]
-// with the bitmaps at the TOP of the allocation, so a draw position j >= s whose word lies past
-// the allocated rows reads 0 and its write is dropped (sampler_kernel's rule, same measured
-// gfx950 behaviour); rows between s and the allocated count are cleared by the prologue.  The
+// with the bitmaps at the TOP of the allocation; draw positions j >= s are clamped to s (row
+// s / 32 is allocated, bit s clear: sampler_kernel's rule); rows between s and the allocated
+// count are cleared by the prologue.  The
 // Gram epilogue (fused eigen) reuses the whole allocation as the [36][257] double stage.
 constexpr int kFSw = 4;
 constexpr int kFMw = 8;

@@ -1,0 +1,88 @@
+"""The bench's shipped execution shape on the GPU: the sub-batches of one step, each on its own
+context and HIP stream, enqueued at once (bench.py call()).  Compared byte for byte with the
+same sub-batches run one after the other, and against the oracle on one pair of every
+sub-batch (src/eight_point.cpp:129-149 is a deterministic sort + accumulate + min_element, so
+the answer must not depend on which kernels share the CUs).
+
+Round 4 shipped a library whose overlapped records differed from the serial ones: binned_rows
+on ~10 % of the pairs and, at ~2e-4 per pair, min_idx / R / T.  The cause was packed-FP32
+results corrupted while other streams' int8 MFMA Gram kernels ran on the same CUs (DESIGN.md
+5d).  These tests pin the fix."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import bench
+
+pytestmark = pytest.mark.gpu
+
+S, PER, ITERS, KPTS = 6, 48, 10000, 4096
+
+
+@pytest.fixture(scope="module")
+def overlap_setup():
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner
+    pairs = bench.make_batch(0, S * PER, KPTS, 20200423)
+    subs = []
+    for i in range(S):
+        b = bench.to_device(pairs[i * PER:(i + 1) * PER], "cuda")
+        subs.append(dict(b=b, run=PairBatchRunner(ctx=Context(0), iters=ITERS),
+                         st=torch.cuda.Stream()))
+    return pairs, subs
+
+
+def _run(sb, want=()):
+    import torch
+    b = sb["b"]
+    with torch.cuda.stream(sb["st"]):
+        o = sb["run"].run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"], b["off_r"],
+                          b["width"], b["height"], b["max_nq"], b["max_nt"], want=want,
+                          stream=sb["st"].cuda_stream)
+    return o
+
+
+def _overlapped(subs):
+    import torch
+    outs = [_run(sb)["results"] for sb in subs]  # every sub-batch enqueued before any finishes
+    torch.cuda.synchronize()
+    return np.concatenate([o.cpu().numpy() for o in outs])
+
+
+def _serial(subs, want=()):
+    import torch
+    outs = []
+    for sb in subs:
+        outs.append(_run(sb, want))
+        torch.cuda.synchronize()
+    return outs
+
+
+def test_overlapped_streams_equal_serial(overlap_setup):
+    """three overlapped runs of the 6-stream step, each byte-identical to the serial run"""
+    _, subs = overlap_setup
+    ser = np.concatenate([o["results"].cpu().numpy() for o in _serial(subs)])
+    for rep in range(3):
+        ovl = _overlapped(subs)
+        diff = np.nonzero(np.any(ovl != ser, axis=1))[0]
+        assert diff.size == 0, f"run {rep}: {diff.size} of {len(ser)} records differ: {diff[:10]}"
+    assert np.array_equal(np.concatenate([o["results"].cpu().numpy() for o in _serial(subs)]), ser)
+
+
+def test_overlapped_streams_against_oracle(overlap_setup, oracle):
+    """one pair of every sub-batch (a different position in each) of an overlapped run against
+    the oracle: status, M, K, min_idx, R and T, and the match list bit-exact"""
+    from erp_match_eightpoint_test_amd import results_to_numpy
+    pairs, subs = overlap_setup
+    res = results_to_numpy(_overlapped(subs))
+    matches = [o["matches"].cpu().numpy() for o in _serial(subs, want=("matches",))]
+    nthreads = max(1, min(16, len(os.sched_getaffinity(0))))
+    picks = [i * PER + (7 * i) % PER for i in range(S)]
+    ora = [bench.oracle_pair(pairs[k], ITERS, nthreads) for k in picks]
+    got = np.stack([res[k] for k in picks])
+    mt = np.stack([matches[k // PER][k % PER] for k in picks])
+    par = bench.parity_check(got, mt, ora)
+    assert par["all_equal"], par
