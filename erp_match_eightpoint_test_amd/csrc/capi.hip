@@ -117,7 +117,7 @@ struct erp_ctx {
     DevBuf zsel;              // consensus zoom: the survivors' rank-window bins (level 1 grid)
     DevBuf part, part1, pu, ccount, cand, bsel, edges, gfin, matches, counts, flags, pts, polyR, polyQ, idx, gram, hyps, rv, tv, kcount, tmean,
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
-        rtab, limbs, tsplit, ovf, remap_scr, vchunk, lipref, inl;
+        rtab, limbs, tsplit, ovf, remap_scr, vchunk, lipref, inl, hlite;
     DevBuf extra[13];         // erp_ctx_scratch_internal slots (1-11 SURF, 12 viz)
     // debug (ERP_DEBUG_SNAP=1): lb, ub and the first-stage list counts right after the bounds
     // pass, fetched with erp_debug_snapshot
@@ -335,7 +335,7 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->results, &ctx->in_a, &ctx->in_b, &ctx->in_c, &ctx->in_d,
                      &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins,
                      &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf, &ctx->remap_scr, &ctx->vchunk,
-                     &ctx->lipref, &ctx->inl};
+                     &ctx->lipref, &ctx->inl, &ctx->hlite};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     for (DevBuf& b : ctx->extra)
@@ -458,6 +458,7 @@ erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_bat
               ensure(c->lipref, erp::lipref_bytes((int)P, 2 * sh.iters)) && ensure(c->edges, erp::consensus_edges_bytes((int)P)) &&
               ensure(c->nsurv, P * 20 + 8) && ensure(c->vchunk, erp::valid_chunk_bytes(sh));
     if (ok && !(out && out->hyps)) ok = ensure(c->hyps, P * sh.iters * sizeof(erp_hypothesis));
+    if (ok) ok = ensure(c->hlite, erp::hyp_lite_bytes(sh));
     if (ok && !(out && out->tvec)) ok = ensure(c->tv, P * 6 * sh.iters * 4);
     if (ok && !(out && out->dist)) ok = ensure(c->tmean, P * 2 * sh.iters * 8);
     if (!ok) return ERP_OUT_OF_MEMORY;
@@ -526,9 +527,20 @@ erp_status run_inliers(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_c
     return ERP_OK;
 }
 
-// estimator stages after counts/pts are in place
+// the lite estimates (launch_eigen's hl: R1, R2, T as f32 SoA + per-wave counts, no records)
+// when nothing reads the records: the caller did not ask for them, the opt-in inlier count is
+// off (it adds into the records) and the estimate is not fused into the Gram kernel
+bool use_lite(const erp_ransac_cfg* cfg, const erp_batch_outputs* out) {
+    return !(out && out->hyps) && !(cfg->inlier_thr > 0.0f) && ERP_FUSE_EIGEN != 2;
+}
+float* lite_hl(erp_ctx* c) { return (float*)c->hlite.p; }
+int32_t* lite_wsum(erp_ctx* c, const erp::BatchShape& sh) {
+    return (int32_t*)(lite_hl(c) + (size_t)sh.n_pairs * 9 * sh.iters);
+}
+
+// estimator stages after counts/pts are in place (lite: the estimates in the lite layout)
 erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
-                          const erp_batch_outputs* out, hipStream_t st) {
+                          const erp_batch_outputs* out, hipStream_t st, bool lite = false) {
     erp_ctx* ctx = c;
     auto* counts = (int32_t*)c->counts.p;
     auto* flags = (int32_t*)c->flags.p;
@@ -551,7 +563,8 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
             StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
             ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
                                      cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
-                                     want_e(cfg, out)));
+                                     want_e(cfg, out), lite ? lite_hl(c) : nullptr,
+                                     lite ? lite_wsum(c, sh) : nullptr));
         }
         return run_inliers(c, sh, cfg, hyps, st);
     }
@@ -597,7 +610,8 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
         ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
                                  cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
-                                 want_e(cfg, out)));
+                                 want_e(cfg, out), lite ? lite_hl(c) : nullptr,
+                                 lite ? lite_wsum(c, sh) : nullptr));
     }
     return run_inliers(c, sh, cfg, hyps, st);
 }
@@ -610,7 +624,8 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
 erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
                          const erp_batch_outputs* out, erp_pair_result* results, hipStream_t st,
                          bool from_hyps, int phase = 0, int shard = 0, int nshards = 1,
-                         double* lb_ = nullptr, double* ub_ = nullptr, int32_t* bsel_ = nullptr) {
+                         double* lb_ = nullptr, double* ub_ = nullptr, int32_t* bsel_ = nullptr,
+                         bool lite = false) {
     erp_ctx* ctx = c;
     double* lbp = lb_ ? lb_ : (double*)c->lb.p;
     double* ubp = ub_ ? ub_ : (double*)c->ub.p;
@@ -620,7 +635,12 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     auto* hyps = (out && out->hyps) ? out->hyps : (erp_hypothesis*)c->hyps.p;
     auto* tv = (out && out->tvec) ? out->tvec : (float*)c->tv.p;
     auto* tmean = (out && out->dist) ? out->dist : (double*)c->tmean.p;
-    if (from_hyps && phase != 2) {
+    if (from_hyps && phase != 2 && lite) {
+        StageTimer _t(ctx, ERP_STAGE_VALID_COMPACT, st);
+        ERP_CK(erp::launch_valid_place(counts, lite_hl(c), lite_wsum(c, sh), sh, cfg->sample_frac,
+                                       (float*)c->rv.p, tv, (int32_t*)c->kcount.p,
+                                       out ? out->rvec : nullptr, (float*)c->dscale.p, st));
+    } else if (from_hyps && phase != 2) {
         StageTimer _t(ctx, ERP_STAGE_VALID_COMPACT, st);
         ERP_CK(erp::launch_valid_compact(counts, hyps, sh, cfg->sample_frac,
                                          (int32_t*)c->vchunk.p, (float*)c->rv.p, tv,
@@ -728,10 +748,12 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
 
 erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
                          const erp_batch_outputs* out, erp_pair_result* results, hipStream_t st) {
-    erp_status es = run_hypotheses(c, sh, cfg, out, st);
+    const bool lite = use_lite(cfg, out);
+    erp_status es = run_hypotheses(c, sh, cfg, out, st, lite);
     if (es != ERP_OK) return es;
     if (!(c->dbg_stages & 16)) return ERP_OK;
-    return run_consensus(c, sh, cfg, out, results, st, true);
+    return run_consensus(c, sh, cfg, out, results, st, true, 0, 0, 1, nullptr, nullptr, nullptr,
+                         lite);
 }
 
 }  // namespace
@@ -852,7 +874,8 @@ std::vector<uint8_t> graph_key(const erp_ctx* c, const erp_pair_batch* b, float 
                            &c->pts, &c->polyR, &c->polyQ, &c->idx, &c->gram, &c->hyps, &c->rv,
                            &c->tv, &c->kcount, &c->tmean, &c->sortbuf, &c->w0, &c->results,
                            &c->dscale, &c->lb, &c->ub, &c->surv, &c->nsurv, &c->wins, &c->rtab,
-                           &c->limbs, &c->tsplit, &c->ovf, &c->vchunk, &c->lipref, &c->inl};
+                           &c->limbs, &c->tsplit, &c->ovf, &c->vchunk, &c->lipref, &c->inl,
+                           &c->hlite};
     for (const DevBuf* d : all) key_put(k, d->p);
     return k;
 }

@@ -149,7 +149,15 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
 // then the estimate (rank-2 fix, decomposition, Euler angles, validity) -> hyps
 hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
                         double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
-                        hipStream_t st, int fused = 0, bool want_e = true);
+                        hipStream_t st, int fused = 0, bool want_e = true,
+                        float* hl = nullptr, int32_t* wsum = nullptr);
+// (hl != NULL, round 5: the estimates go to the lite layout -- hl[p][9][iters] f32 R1, R2, T,
+// an invalid rotation's x NaN, plus per-64-iteration-wave counts / bounding boxes wsum -- in
+// hyp_lite_bytes(sh) (hl, then wsum), for launch_valid_place instead of records)
+size_t hyp_lite_bytes(const BatchShape& sh);
+hipError_t launch_valid_place(const int32_t* counts, const float* hl, const int32_t* wsum,
+                              const BatchShape& sh, double sample_frac, float* rv, float* tv,
+                              int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st);
 // (want_e = false: estimate_kernel leaves the records' E unwritten -- the batch pipeline when the
 // caller did not ask for the hypothesis records; nothing downstream reads E)
 // the opt-in inlier count (cfg.inlier_thr > 0): every iteration's matches with

@@ -1506,6 +1506,69 @@ __global__ __launch_bounds__(64) ERP_EST_ATTR void estimate_kernel(const int32_t
     estimate_store(e, valid_abs, hyps + (size_t)p * iters + h, with_e != 0);
 }
 
+// The batch pipeline's estimate when nothing asks for the hypothesis records (round 5): instead
+// of 120-B records that valid_count / valid_scatter read back twice (~3.1 GB per 768-pair
+// step), each iteration's R1, R2, T go to hl[p][9][iters] as f32 SoA (36 B, coalesced; an
+// invalid rotation's x is NaN: valid implies max |euler| < 1.57, so a valid x is finite), and
+// each 64-iteration wave writes its valid-rotation count and their bounding box to
+// wsum[p][wave][8] -- what valid_place_kernel needs to place R1-then-R2 in iteration order
+// (src/eight_point.cpp:117-126) without re-reading the iterations twice.
+__global__ __launch_bounds__(64) ERP_EST_ATTR void estimate_lite_kernel(
+    const int32_t* __restrict__ counts, const double* __restrict__ evec, int iters,
+    double sample_frac, double valid_abs, float* __restrict__ hl, int32_t* __restrict__ wsum) {
+    const int p = blockIdx.y, w = blockIdx.x, lane = threadIdx.x;
+    const int h = w * 64 + lane;
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1) return;  // (uniform: valid_place_kernel reports K = 0 for the pair)
+    Hyp hy;
+    hy.R1_valid = hy.R2_valid = 0;
+    if (h < iters) {
+        const double* ei = evec + (size_t)p * 9 * iters + h;
+        double e[9];
+#pragma unroll
+        for (int k = 0; k < 9; k++) e[k] = ei[(size_t)k * iters];
+        estimate_from_e(e, valid_abs, hy);
+        float* o = hl + (size_t)p * 9 * iters + h;
+        const float qnan = __builtin_nanf("");
+        o[0] = hy.R1_valid ? hy.R1[0] : qnan;
+        o[(size_t)1 * iters] = hy.R1[1];
+        o[(size_t)2 * iters] = hy.R1[2];
+        o[(size_t)3 * iters] = hy.R2_valid ? hy.R2[0] : qnan;
+        o[(size_t)4 * iters] = hy.R2[1];
+        o[(size_t)5 * iters] = hy.R2[2];
+#pragma unroll
+        for (int k = 0; k < 3; k++) o[(size_t)(6 + k) * iters] = hy.T[k];
+    }
+    int cnt = (hy.R1_valid != 0) + (hy.R2_valid != 0);
+    float mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        if (hy.R1_valid) {
+            mn[k] = fminf(mn[k], hy.R1[k]);
+            mx[k] = fmaxf(mx[k], hy.R1[k]);
+        }
+        if (hy.R2_valid) {
+            mn[k] = fminf(mn[k], hy.R2[k]);
+            mx[k] = fmaxf(mx[k], hy.R2[k]);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        cnt += __shfl_xor(cnt, o, 64);
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            mn[k] = fminf(mn[k], __shfl_xor(mn[k], o, 64));
+            mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], o, 64));
+        }
+    }
+    if (lane < 8) {
+        const int32_t v = lane == 0 ? cnt : lane < 4 ? __float_as_int(mn[lane - 1])
+                          : lane < 7 ? __float_as_int(mx[lane - 4]) : 0;
+        wsum[((size_t)p * gridDim.x + w) * 8 + lane] = v;
+    }
+}
+
 // push R1 (if valid) then R2 (if valid) per iteration, in iteration order
 // Two launches over (chunk of 1024 iterations, pair): valid_count_kernel writes each chunk's
 // number of valid rotations and its bounding box; valid_scatter_kernel adds the totals of the
@@ -1633,6 +1696,80 @@ __global__ __launch_bounds__(1024) void valid_scatter_kernel(const int32_t* __re
             X[k * stride + pos] = R[k];
             T[3 * pos + k] = hy.T[k];
             if (A) A[3 * pos + k] = R[k];
+        }
+        pos++;
+    }
+}
+
+// valid_count + valid_scatter for the lite estimates: a block per (chunk of 1024 iterations,
+// pair) adds the valid counts of the 64-iteration waves before its chunk (wsum, <= ~160 values),
+// block-scans its chunk and writes the valid rotations in push order (iteration, R1, R2);
+// chunk 0 also writes K and the bounding-box scale (the same min / max values valid_count
+// reduces, so dscale is bit-identical to the record path's)
+__global__ __launch_bounds__(1024) void valid_place_kernel(
+    const int32_t* __restrict__ counts, const float* __restrict__ hl, int iters,
+    double sample_frac, const int32_t* __restrict__ wsum, int nwaves, float* __restrict__ rv,
+    float* __restrict__ tv, int32_t* __restrict__ kcount, float* __restrict__ rv_aos,
+    float* __restrict__ dscale) {
+    __shared__ int ws[16];
+    __shared__ int sbase[16];
+    const int p = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int M = counts[p];
+    if ((int)(M * sample_frac) < 1) {
+        if (c == 0 && tid == 0) kcount[p] = 0;
+        return;
+    }
+    const int32_t* vw = wsum + (size_t)p * nwaves * 8;
+    const int upto = c == 0 ? nwaves : min(16 * c, nwaves);  // waves before this chunk (all for 0)
+    int part = 0;
+    for (int q = tid; q < upto; q += 1024) part += vw[q * 8];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (lane == 0) sbase[tid >> 6] = part;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < 16; w++) base += sbase[w];
+    if (c == 0) {
+        if (tid == 0) {
+            kcount[p] = base;
+            double d2 = 0;
+            for (int k = 0; k < 3; k++) {
+                float a = kInf, b = -kInf;
+                for (int q = 0; q < nwaves; q++) {
+                    a = fminf(a, __int_as_float(vw[q * 8 + 1 + k]));
+                    b = fmaxf(b, __int_as_float(vw[q * 8 + 4 + k]));
+                }
+                const double e = base > 0 ? (double)b - (double)a : 0.0;
+                d2 += e * e;
+            }
+            dscale[p] = (float)(sqrt(d2) * (1.0 + 1e-6));
+        }
+        base = 0;
+    }
+    const int h = c * 1024 + tid;
+    float r[9];
+    bool v1 = false, v2 = false;
+    if (h < iters) {
+        const float* x = hl + (size_t)p * 9 * iters + h;
+#pragma unroll
+        for (int k = 0; k < 9; k++) r[k] = x[(size_t)k * iters];
+        v1 = !__builtin_isnan(r[0]);
+        v2 = !__builtin_isnan(r[3]);
+    }
+    int total;
+    int pos = base + block_exclusive_scan<1024>((int)v1 + (int)v2, ws, &total);
+    const int stride = 2 * iters;
+    float* X = rv + (size_t)p * 3 * stride;
+    float* T = tv + (size_t)p * 3 * stride;
+    float* A = rv_aos ? rv_aos + (size_t)p * 3 * stride : nullptr;
+#pragma unroll
+    for (int which = 0; which < 2; which++) {
+        if (!(which ? v2 : v1)) continue;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            X[k * stride + pos] = r[3 * which + k];
+            T[3 * pos + k] = r[6 + k];
+            if (A) A[3 * pos + k] = r[3 * which + k];
         }
         pos++;
     }
@@ -4531,7 +4668,7 @@ hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream
 
 hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchShape& sh,
                         double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
-                        hipStream_t st, int fused, bool want_e) {
+                        hipStream_t st, int fused, bool want_e, float* hl, int32_t* wsum) {
     dim3 grid((sh.iters + 63) / 64, sh.n_pairs);
     // fused >= 1: gram_mfma_kernel ran the inverse iteration (s >= 9) already; fused == 2: and
     // the estimate of its settled lanes, the fallback / thin kernels estimate their own lanes
@@ -4544,9 +4681,26 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
     // (M is only known on the device: the thin instantiation returns at once for s >= 9)
     hipLaunchKernelGGL(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters,
                        sample_frac, evec, own, valid_abs);
-    if (fused != 2)
+    if (fused != 2 && hl)
+        hipLaunchKernelGGL(estimate_lite_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
+                           sample_frac, valid_abs, hl, wsum);
+    else if (fused != 2)
         hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
                            sample_frac, valid_abs, hyps, (int)want_e);
+    return hipGetLastError();
+}
+
+size_t hyp_lite_bytes(const BatchShape& sh) {
+    const size_t P = sh.n_pairs, nw = (sh.iters + 63) / 64;
+    return P * 9 * sh.iters * sizeof(float) + P * nw * 8 * sizeof(int32_t);
+}
+
+hipError_t launch_valid_place(const int32_t* counts, const float* hl, const int32_t* wsum,
+                              const BatchShape& sh, double sample_frac, float* rv, float* tv,
+                              int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st) {
+    dim3 grid((sh.iters + 1023) / 1024, sh.n_pairs);
+    hipLaunchKernelGGL(valid_place_kernel, grid, dim3(1024), 0, st, counts, hl, sh.iters,
+                       sample_frac, wsum, (sh.iters + 63) / 64, rv, tv, kcount, rv_aos, dscale);
     return hipGetLastError();
 }
 

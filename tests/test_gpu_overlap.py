@@ -75,9 +75,9 @@ def test_overlapped_streams_equal_serial(overlap_setup):
 def test_overlapped_streams_against_oracle(overlap_setup, oracle):
     """one pair of every sub-batch (a different position in each) of an overlapped run against
     the oracle: status, M, K, min_idx, R and T, and the match list bit-exact"""
-    from erp_match_eightpoint_test_amd import results_to_numpy
+    from erp_match_eightpoint_test_amd.capi import RESULT_DTYPE
     pairs, subs = overlap_setup
-    res = results_to_numpy(_overlapped(subs))
+    res = np.ascontiguousarray(_overlapped(subs)).view(RESULT_DTYPE).reshape(-1)
     matches = [o["matches"].cpu().numpy() for o in _serial(subs, want=("matches",))]
     nthreads = max(1, min(16, len(os.sched_getaffinity(0))))
     picks = [i * PER + (7 * i) % PER for i in range(S)]
@@ -86,3 +86,21 @@ def test_overlapped_streams_against_oracle(overlap_setup, oracle):
     mt = np.stack([matches[k // PER][k % PER] for k in picks])
     par = bench.parity_check(got, mt, ora)
     assert par["all_equal"], par
+
+
+def test_lite_estimates_equal_records(overlap_setup):
+    """the batch pipeline's lite estimates (R1, R2, T as f32 SoA + per-wave counts, placed by
+    valid_place_kernel; no 120-B records) against the record path (taken whenever the caller
+    asks for the records): the consensus inputs (rvec, tvec in push order) and every result
+    record byte-identical"""
+    import torch
+    _, subs = overlap_setup
+    sb = subs[1]
+    lite = _run(sb, want=("rvec", "tvec"))
+    torch.cuda.synchronize()
+    lite = {k: v.cpu().numpy() for k, v in lite.items()}
+    rec = _run(sb, want=("rvec", "tvec", "hyps"))
+    torch.cuda.synchronize()
+    rec = {k: v.cpu().numpy() for k, v in rec.items()}
+    for k in ("results", "rvec", "tvec"):
+        assert np.array_equal(lite[k].view(np.uint8), rec[k].view(np.uint8)), k
