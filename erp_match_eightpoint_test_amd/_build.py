@@ -20,7 +20,7 @@ ARCH = os.environ.get("ERP_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["kernels.hip", "matcher.hip", "capi.hip", "remap.hip", "remap_api.hip", "surf.hip", "surf_api.hip", "viz.hip",
            "host_api.cpp"]
-HEADERS = ["erp_device.hpp", "erp_kernels.hpp", "erp_remap.hpp", "erp_surf.hpp"]
+HEADERS = ["erp_device.hpp", "erp_kernels.hpp", "erp_remap.hpp", "erp_surf.hpp", "erp_launch.hpp"]
 PUBLIC_HEADERS = ["erp_match.h", os.path.join("erp", "feature_matcher.hpp"),
                   os.path.join("erp", "eight_point.hpp")]
 

@@ -44,19 +44,26 @@ size_t alloc_pad() {
 std::mutex g_pad_mu;
 std::vector<std::pair<void*, size_t>> g_padded;
 
+// frees b (and forgets its canary record)
+void free_buf(DevBuf& b) {
+    if (!b.p) return;
+    if (alloc_pad()) {
+        std::lock_guard<std::mutex> g(g_pad_mu);
+        const auto it = std::find_if(g_padded.begin(), g_padded.end(),
+                                     [&](const std::pair<void*, size_t>& e) { return e.first == b.p; });
+        if (it != g_padded.end()) g_padded.erase(it);
+    }
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.n = 0;
+}
+
 // grow-only device buffer; returns false on allocation failure
 bool ensure(DevBuf& b, size_t bytes) {
     if (bytes == 0) bytes = 16;
     if (b.n >= bytes) return true;
     const size_t pad = alloc_pad();
-    if (b.p) {
-        if (pad) {
-            std::lock_guard<std::mutex> g(g_pad_mu);
-            for (auto& e : g_padded)
-                if (e.first == b.p) e = g_padded.back(), g_padded.pop_back();
-        }
-        (void)hipFree(b.p);
-    }
+    if (b.p) free_buf(b);
     b.p = nullptr;
     b.n = 0;
     if (hipMalloc(&b.p, bytes + pad) != hipSuccess) return false;
@@ -336,10 +343,9 @@ erp_status erp_ctx_destroy(erp_ctx* ctx) {
                      &ctx->dscale, &ctx->lb, &ctx->ub, &ctx->surv, &ctx->nsurv, &ctx->wins,
                      &ctx->rtab, &ctx->limbs, &ctx->tsplit, &ctx->ovf, &ctx->remap_scr, &ctx->vchunk,
                      &ctx->lipref, &ctx->inl, &ctx->hlite};
-    for (DevBuf* b : all)
-        if (b->p) (void)hipFree(b->p);
-    for (DevBuf& b : ctx->extra)
-        if (b.p) (void)hipFree(b.p);
+    for (DevBuf* b : all) free_buf(*b);
+    for (DevBuf& b : ctx->extra) free_buf(b);
+    free_buf(ctx->snap);
     for (hipEvent_t e : ctx->ev_pool) (void)hipEventDestroy(e);
     if (ctx->done) (void)hipEventDestroy(ctx->done);
     for (auto& g : ctx->graphs) (void)hipGraphExecDestroy(g.exec);
@@ -737,7 +743,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
             if (!ensure(c->snap, head + rvb)) return ERP_OUT_OF_MEMORY;
             ERP_CK(hipMemcpyAsync(c->snap.p, keep.p, head, hipMemcpyDeviceToDevice, st));
             ERP_CK(hipStreamSynchronize(st));
-            (void)hipFree(keep.p);
+            free_buf(keep);
         }
         ERP_CK(hipMemcpyAsync((char*)c->snap.p + head, c->rv.p, rvb, hipMemcpyDeviceToDevice, st));
         c->snap_bytes = head + rvb;
@@ -830,6 +836,19 @@ erp_status batch_enqueue(erp_ctx* ctx, const erp_pair_batch* b, float ratio,
         ctx->dbg_stages = m ? (int)strtol(m, nullptr, 0) : -1;
     }
     if (!(ctx->dbg_stages & 1)) return run_estimator(ctx, sh, cfg, out, out->results, st);
+    // the optional outputs read zero past each pair's M / K / s, call after call (a HIP-graph
+    // replay or a reused buffer would otherwise keep an earlier call's entries there)
+    const size_t P = (size_t)sh.n_pairs, I = (size_t)sh.iters, Q = (size_t)b->max_nq;
+    const size_t smax = (size_t)std::max((int)(Q * cfg->sample_frac), 1);
+    const struct {
+        void* p;
+        size_t bytes;
+    } opt[] = {{out->matches, P * Q * sizeof(erp_dmatch)}, {out->key_left, P * Q * 8},
+               {out->key_right, P * Q * 8}, {out->hyps, P * I * sizeof(erp_hypothesis)},
+               {out->samples, P * I * smax * 4}, {out->rvec, P * 2 * I * 12},
+               {out->tvec, P * 2 * I * 12}, {out->dist, P * 2 * I * 8}};
+    for (const auto& o : opt)
+        if (o.p) ERP_CK(hipMemsetAsync(o.p, 0, o.bytes, st));
     ERP_CK(hipMemsetAsync(ctx->flags.p, 0, (size_t)sh.n_pairs * 4, st));
     erp_status es = run_matcher(ctx, b->desc_l, b->desc_r, b->off_l, b->off_r, sh, ratio, matches,
                                 (int32_t*)ctx->counts.p, (int32_t*)ctx->flags.p, st);
@@ -917,7 +936,13 @@ erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* b, float ratio
     if (es != ERP_OK) return es;
     if (cfg->inlier_thr > 0.0f && !ensure(ctx->inl, erp::inlier_scratch_bytes(sh)))
         return ERP_OUT_OF_MEMORY;
-    if (!ctx->use_graphs || ctx->profiling || st == nullptr)
+    // plain enqueue: graphs off, stage timing on, the NULL stream, the debug snapshot (its
+    // buffer growth synchronises), or a stream the caller is capturing already (the enqueue
+    // then becomes part of the caller's graph)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (st != nullptr) ERP_CK(hipStreamIsCapturing(st, &cap));
+    if (!ctx->use_graphs || ctx->profiling || st == nullptr || ctx->snap_on ||
+        cap != hipStreamCaptureStatusNone)
         return batch_enqueue(ctx, b, ratio, cfg, out, sh, matches, st);
     // graph replay: the same call (structs, buffers, scratch) as a captured one -> one launch
     std::vector<uint8_t> key = graph_key(ctx, b, ratio, cfg, out);

@@ -17,6 +17,7 @@
 // trimmed-mean consensus   src/eight_point.cpp:129-149                 consensus_bounds / _select /
 //                                                                      _refine / _rows / _final
 #include <hip/hip_runtime.h>
+#include <atomic>
 
 #include <math.h>
 
@@ -27,6 +28,7 @@
 
 #include "erp_device.hpp"
 #include "erp_kernels.hpp"
+#include "erp_launch.hpp"
 
 namespace erp {
 
@@ -4442,13 +4444,13 @@ __global__ void set_i64x4_kernel(int64_t* p, int64_t a, int64_t b, int64_t c, in
 
 // ====================================================================== launchers =======
 hipError_t launch_set_i32(int32_t* p, int32_t v, hipStream_t st) {
-    hipLaunchKernelGGL(set_i32_kernel, dim3(1), dim3(1), 0, st, p, v);
+    ERP_LAUNCH(set_i32_kernel, dim3(1), dim3(1), 0, st, p, v);
     return hipGetLastError();
 }
 
 hipError_t launch_set_i64x4(int64_t* p, int64_t a, int64_t b, int64_t c, int64_t d,
                             hipStream_t st) {
-    hipLaunchKernelGGL(set_i64x4_kernel, dim3(1), dim3(1), 0, st, p, a, b, c, d);
+    ERP_LAUNCH(set_i64x4_kernel, dim3(1), dim3(1), 0, st, p, a, b, c, d);
     return hipGetLastError();
 }
 void init_constants() {
@@ -4477,14 +4479,14 @@ hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t
                                         const BatchShape& sh, double* pts, erp_point2f* key_l,
                                         erp_point2f* key_r, hipStream_t st) {
     dim3 grid((sh.max_nq + 255) / 256, sh.n_pairs);
-    hipLaunchKernelGGL(bearings_from_matches_kernel, grid, dim3(256), 0, st, matches, counts, kp_l,
+    ERP_LAUNCH(bearings_from_matches_kernel, grid, dim3(256), 0, st, matches, counts, kp_l,
                        kp_r, off_l, off_r, width, height, sh.max_nq, pts, key_l, key_r);
     return hipGetLastError();
 }
 
 hipError_t launch_bearings_direct(const erp_point2f* kl, const erp_point2f* kr, int32_t m,
                                   int32_t W, int32_t H, double* pts, hipStream_t st) {
-    hipLaunchKernelGGL(bearings_direct_kernel, dim3((m + 255) / 256 + (m == 0)), dim3(256), 0, st, kl,
+    ERP_LAUNCH(bearings_direct_kernel, dim3((m + 255) / 256 + (m == 0)), dim3(256), 0, st, kl,
                        kr, m, W, H, pts);
     return hipGetLastError();
 }
@@ -4496,11 +4498,26 @@ static int q_needed(int iters) {
     return kq;
 }
 
+// dynamic LDS above 64 KB is requested from the runtime first (hipFuncAttribute-
+// MaxDynamicSharedMemorySize); the largest size set per kernel is remembered, so the call is
+// made only when a launch needs more than any earlier one
+static hipError_t ensure_dyn_lds(const void* fn, size_t bytes, std::atomic<size_t>& done) {
+    if (bytes <= 64 * 1024 || bytes <= done.load(std::memory_order_relaxed)) return hipSuccess;
+    const hipError_t e =
+        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    if (e == hipSuccess) {
+        size_t cur = done.load();
+        while (cur < bytes && !done.compare_exchange_weak(cur, bytes)) {
+        }
+    }
+    return e;
+}
+
 hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_t* polyR,
                             uint32_t* polyQ, hipStream_t st) {
     // sample_frac is only used to skip pairs with sample_n < 1; pass a tiny positive value so
     // every pair with M >= 2 gets polynomials (the sampler decides on its own)
-    hipLaunchKernelGGL(jump_prep_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, 1.0,
+    ERP_LAUNCH(jump_prep_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, 1.0,
                        q_needed(sh.iters), polyR, polyQ);
     return hipGetLastError();
 }
@@ -4511,7 +4528,7 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
                           hipStream_t st, int part) {
     const int nwaves = (sh.iters + 63) / 64;
     if (part == 0) {
-        hipLaunchKernelGGL(sampler_window_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts,
+        ERP_LAUNCH(sampler_window_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts,
                            polyR, polyQ, w0, nwaves, sample_frac, wins);
     } else {
         // positions 0 .. max_s, rounded up to the LDS allocation granule (1280 B = 5 words on
@@ -4520,12 +4537,17 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
         // ERP_SAMPLER_ILP=1: the blocks with their 31 positions computed first (A/B knob)
         static const bool ilp = getenv("ERP_SAMPLER_ILP") && atoi(getenv("ERP_SAMPLER_ILP")) != 0;
+        // (s up to 16 383 at the 65 535-keypoint cap: 515 words x 256 B = 129 KB)
+        static std::atomic<size_t> lds_set[2];
+        const hipError_t le = ilp ? ensure_dyn_lds((const void*)sampler_kernel<true>, shmem, lds_set[1])
+                                  : ensure_dyn_lds((const void*)sampler_kernel<false>, shmem, lds_set[0]);
+        if (le != hipSuccess) return le;
         if (ilp)
-            hipLaunchKernelGGL(sampler_kernel<true>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st,
+            ERP_LAUNCH(sampler_kernel<true>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st,
                                counts, wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags,
                                nwords);
         else
-            hipLaunchKernelGGL(sampler_kernel<false>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st,
+            ERP_LAUNCH(sampler_kernel<false>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st,
                                counts, wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags,
                                nwords);
     }
@@ -4540,13 +4562,10 @@ hipError_t launch_philox_sampler(const int32_t* counts, const BatchShape& sh, do
     // one CU's LDS: 640 words = M <= 20 480; a pair with more matches gets ERP_INVALID_ARG
     const int nwords = std::min((max_m + 31) / 32, 640);
     const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
-    if (shmem > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute((const void*)philox_sampler_kernel,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)shmem);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(philox_sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
+    static std::atomic<size_t> lds_set{0};
+    const hipError_t le = ensure_dyn_lds((const void*)philox_sampler_kernel, shmem, lds_set);
+    if (le != hipSuccess) return le;
+    ERP_LAUNCH(philox_sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
                        sh.iters, nwaves, sh.sel_words, sample_frac, seed, offset, nwords, selw,
                        flags);
     return hipGetLastError();
@@ -4583,7 +4602,7 @@ int debug_lip_counters(uint32_t* out64) {
 }
 
 hipError_t launch_recip_table(int n, double* rtab, int32_t* bad, hipStream_t st) {
-    hipLaunchKernelGGL(recip_table_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, rtab, bad);
+    ERP_LAUNCH(recip_table_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, rtab, bad);
     return hipGetLastError();
 }
 
@@ -4596,21 +4615,21 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
                             double* gram, int32_t* samples, double* evec,
                             erp_hypothesis* hyps, double valid_abs, hipStream_t st) {
     const int nwaves = (sh.iters + 63) / 64;
-    hipLaunchKernelGGL(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
+    ERP_LAUNCH(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
                        pts, sh.max_nq, sh.sel_words, limbs);
     const int nhb = (sh.iters + kGramIters - 1) / kGramIters;
-    hipLaunchKernelGGL(gram_mfma_kernel, dim3(nhb * sh.n_pairs), dim3(64 * kGramWaves), 0, st, counts, limbs,
+    ERP_LAUNCH(gram_mfma_kernel, dim3(nhb * sh.n_pairs), dim3(64 * kGramWaves), 0, st, counts, limbs,
                        selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb, evec, hyps,
                        valid_abs);
     if (samples)
-        hipLaunchKernelGGL(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
+        ERP_LAUNCH(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
                            sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);
     return hipGetLastError();
 }
 
 hipError_t launch_gram_limbs(const int32_t* counts, const double* pts, const BatchShape& sh,
                              int8_t* limbs, hipStream_t st) {
-    hipLaunchKernelGGL(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
+    ERP_LAUNCH(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
                        pts, sh.max_nq, sh.sel_words, limbs);
     return hipGetLastError();
 }
@@ -4649,20 +4668,23 @@ hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* wins, cons
     size_t bytes;
     sampler_gram_lds(sh, &rows, &bm_base, &bytes);
     if (bytes > (size_t)kFMaxLds) return hipErrorInvalidValue;
+    static std::atomic<size_t> lds_set{0};
+    const hipError_t le = ensure_dyn_lds((const void*)sampler_gram_kernel, bytes, lds_set);
+    if (le != hipSuccess) return le;
     const int nwaves = (sh.iters + 63) / 64;
     const int nhb = (sh.iters + kFIters - 1) / kFIters;
     uint32_t* sw = samples ? selw : nullptr;
-    hipLaunchKernelGGL(sampler_gram_kernel, dim3(nhb * sh.n_pairs), dim3(kFThreads), bytes, st,
+    ERP_LAUNCH(sampler_gram_kernel, dim3(nhb * sh.n_pairs), dim3(kFThreads), bytes, st,
                        counts, wins, limbs, rtab, sh.iters, nwaves, sh.sel_words, sample_frac,
                        rows, bm_base, flags, sw, gram, nhb, evec, fused_diag());
     if (samples)
-        hipLaunchKernelGGL(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
+        ERP_LAUNCH(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
                            sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);
     return hipGetLastError();
 }
 
 hipError_t launch_gram_all(const double* pts, int32_t m, double* gram, hipStream_t st) {
-    hipLaunchKernelGGL(gram_all_kernel, dim3(1), dim3(256), 0, st, pts, m, gram);
+    ERP_LAUNCH(gram_all_kernel, dim3(1), dim3(256), 0, st, pts, m, gram);
     return hipGetLastError();
 }
 
@@ -4674,18 +4696,18 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
     // the estimate of its settled lanes, the fallback / thin kernels estimate their own lanes
     erp_hypothesis* own = fused == 2 ? hyps : nullptr;
     if (!fused)
-        hipLaunchKernelGGL(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters,
+        ERP_LAUNCH(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters,
                            sample_frac, evec, nullptr, valid_abs);
-    hipLaunchKernelGGL(eigen_fallback_kernel, grid, dim3(64), 0, st, counts, gram, sh.iters,
+    ERP_LAUNCH(eigen_fallback_kernel, grid, dim3(64), 0, st, counts, gram, sh.iters,
                        sample_frac, evec, own, valid_abs);
     // (M is only known on the device: the thin instantiation returns at once for s >= 9)
-    hipLaunchKernelGGL(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters,
+    ERP_LAUNCH(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters,
                        sample_frac, evec, own, valid_abs);
     if (fused != 2 && hl)
-        hipLaunchKernelGGL(estimate_lite_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
+        ERP_LAUNCH(estimate_lite_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
                            sample_frac, valid_abs, hl, wsum);
     else if (fused != 2)
-        hipLaunchKernelGGL(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
+        ERP_LAUNCH(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
                            sample_frac, valid_abs, hyps, (int)want_e);
     return hipGetLastError();
 }
@@ -4699,7 +4721,7 @@ hipError_t launch_valid_place(const int32_t* counts, const float* hl, const int3
                               const BatchShape& sh, double sample_frac, float* rv, float* tv,
                               int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st) {
     dim3 grid((sh.iters + 1023) / 1024, sh.n_pairs);
-    hipLaunchKernelGGL(valid_place_kernel, grid, dim3(1024), 0, st, counts, hl, sh.iters,
+    ERP_LAUNCH(valid_place_kernel, grid, dim3(1024), 0, st, counts, hl, sh.iters,
                        sample_frac, wsum, (sh.iters + 63) / 64, rv, tv, kcount, rv_aos, dscale);
     return hipGetLastError();
 }
@@ -4722,11 +4744,11 @@ hipError_t launch_inliers(const int32_t* counts, const double* pts, const BatchS
     const float lo = t > d ? (float)(t - d) : 0.0f;  // (|res32| < 0 never holds)
     const float hi = (float)(t + d);
     const dim3 g((sh.iters + 63) / 64, sh.n_pairs);
-    hipLaunchKernelGGL(inlier_prep_kernel, g, dim3(64), 0, st, counts, (const erp_hypothesis*)hyps,
+    ERP_LAUNCH(inlier_prep_kernel, g, dim3(64), 0, st, counts, (const erp_hypothesis*)hyps,
                        sh.iters, sample_frac, ec64, ec32);
-    hipLaunchKernelGGL(inlier_points_kernel, dim3(mpad / 256, sh.n_pairs), dim3(256), 0, st, counts,
+    ERP_LAUNCH(inlier_points_kernel, dim3(mpad / 256, sh.n_pairs), dim3(256), 0, st, counts,
                        pts, sh.max_nq, mpad, u32);
-    hipLaunchKernelGGL(inlier_count_kernel, g, dim3(64), 0, st, counts, (const float*)u32,
+    ERP_LAUNCH(inlier_count_kernel, g, dim3(64), 0, st, counts, (const float*)u32,
                        (const float*)ec32, (const double*)ec64, pts, sh.max_nq, mpad, sh.iters,
                        sample_frac, lo, hi, t, hyps);
     return hipGetLastError();
@@ -4741,9 +4763,9 @@ hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyp
                                 float* rv, float* tv, int32_t* kcount, float* rv_aos,
                                 float* dscale, hipStream_t st) {
     dim3 grid((sh.iters + 1023) / 1024, sh.n_pairs);
-    hipLaunchKernelGGL(valid_count_kernel, grid, dim3(1024), 0, st, counts, hyps, sh.iters,
+    ERP_LAUNCH(valid_count_kernel, grid, dim3(1024), 0, st, counts, hyps, sh.iters,
                        sample_frac, vchunk);
-    hipLaunchKernelGGL(valid_scatter_kernel, grid, dim3(1024), 0, st, counts, hyps, sh.iters,
+    ERP_LAUNCH(valid_scatter_kernel, grid, dim3(1024), 0, st, counts, hyps, sh.iters,
                        sample_frac, vchunk, rv, tv, kcount, rv_aos, dscale);
     return hipGetLastError();
 }
@@ -4751,7 +4773,7 @@ hipError_t launch_valid_compact(const int32_t* counts, const erp_hypothesis* hyp
 hipError_t launch_consensus_input(const float* rvec, const float* tvec, int K, int stride, float* rv,
                                   float* tv, int32_t* kcount, float* dscale, int32_t* flags,
                                   hipStream_t st) {
-    hipLaunchKernelGGL(consensus_input_kernel, dim3(1), dim3(1024), 0, st, rvec, tvec, K, stride, rv,
+    ERP_LAUNCH(consensus_input_kernel, dim3(1), dim3(1024), 0, st, rvec, tvec, K, stride, rv,
                        tv, kcount, dscale, flags);
     return hipGetLastError();
 }
@@ -4771,23 +4793,23 @@ hipError_t launch_consensus_zoom(const int32_t* kcount, const float* rv, const f
     int32_t* zb = reinterpret_cast<int32_t*>(edges + (size_t)P * 4 * kNB);
     int32_t* uoff = nsurv + 2 * P;  // free until the refine pass (launch_consensus_refine)
     if (level == 1)
-        hipLaunchKernelGGL((consensus_zoom_prep_kernel<6, kMantBits>), dim3(P), dim3(256), 0, st,
+        ERP_LAUNCH((consensus_zoom_prep_kernel<6, kMantBits>), dim3(P), dim3(256), 0, st,
                            kcount, dscale, surv, (const int32_t*)nsurv, bsel, 1, stride, trim_lo,
                            trim_hi, zb, edz);
     else  // the level-1 windows (zsel) -> the 256-per-binade grid
-        hipLaunchKernelGGL((consensus_zoom_prep_kernel<8, 6>), dim3(P), dim3(256), 0, st, kcount,
+        ERP_LAUNCH((consensus_zoom_prep_kernel<8, 6>), dim3(P), dim3(256), 0, st, kcount,
                            dscale, surv, (const int32_t*)nsurv, (const int32_t*)zsel, 0, stride,
                            trim_lo, trim_hi, zb, edz);
-    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)nsurv, P,
+    ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)nsurv, P,
                        kBoundRows, kZoomMin, uoff);
     const int max_units = P * ((stride + kBoundRows - 1) / kBoundRows);
     if (level == 1)
-        hipLaunchKernelGGL(consensus_zoom_kernel<6>, dim3(max_units), dim3(256), 0, st, kcount, rv,
+        ERP_LAUNCH(consensus_zoom_kernel<6>, dim3(max_units), dim3(256), 0, st, kcount, rv,
                            (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb,
                            ub, surv, (const int32_t*)nsurv, (const int32_t*)uoff, P, zsel, 1,
                            dscale, (int32_t*)nullptr);
     else
-        hipLaunchKernelGGL(consensus_zoom_kernel<8>, dim3(max_units), dim3(256), 0, st, kcount, rv,
+        ERP_LAUNCH(consensus_zoom_kernel<8>, dim3(max_units), dim3(256), 0, st, kcount, rv,
                            (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb,
                            ub, surv, (const int32_t*)nsurv, (const int32_t*)uoff, P, zsel, 1,
                            dscale, (int32_t*)nullptr);
@@ -4851,7 +4873,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
                                    void* lipref, int lipg, float gfac, int flat_pct,
                                    int use_hint, hipStream_t st) {
-    hipLaunchKernelGGL(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
+    ERP_LAUNCH(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     const int stride = 2 * sh.iters;
     if (!rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
         if (rcount) {
@@ -4860,7 +4882,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
         }
         const int rows = (stride + nshards - 1) / nshards + 1;  // >= any shard's rows
         dim3 grid((rows + kBoundRows - 1) / kBoundRows, sh.n_pairs);
-        hipLaunchKernelGGL(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
+        ERP_LAUNCH(consensus_bounds_kernel, grid, dim3(256), 0, st, kcount, rv, dscale,
                            edges, stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, 1);
         return hipGetLastError();
     }
@@ -4869,11 +4891,11 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
     const int srows = (stride + nshards - 1) / nshards + 1;  // >= any shard's rows
     const int nref = (srows + kLipStep - 1) / kLipStep;
     dim3 g1((nref + kBoundRows - 1) / kBoundRows, sh.n_pairs);
-    hipLaunchKernelGGL(consensus_bounds_kernel, g1, dim3(256), 0, st, kcount, rv, dscale, edges,
+    ERP_LAUNCH(consensus_bounds_kernel, g1, dim3(256), 0, st, kcount, rv, dscale, edges,
                        stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, kLipStep);
     if (zoom_refs) {  // the central references on the zoom grid: a tighter U for the pruning
         int32_t* cnt = rcount - sh.n_pairs;  // (nsurv[0 .. P): free until the first select)
-        hipLaunchKernelGGL(consensus_pick_central_kernel, dim3(sh.n_pairs), dim3(256), 0, st,
+        ERP_LAUNCH(consensus_pick_central_kernel, dim3(sh.n_pairs), dim3(256), 0, st,
                            kcount, (const double*)ub, stride, shard, nshards, rlist, cnt,
                            zoom_refs > 1 ? 1 : 0);
         const hipError_t ze = launch_consensus_zoom(kcount, rv, dscale, edges, sh, trim_lo,
@@ -4889,23 +4911,23 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
         const hipError_t m1 = hipMemsetAsync(lr.r2cnt, 0, sizeof(int32_t) * P, st);
         if (m1 != hipSuccess) return m1;
     }
-    hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
+    ERP_LAUNCH(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
                        trim_lo, trim_hi, (const double*)lb, (const double*)ub,
                        (const int32_t*)nullptr, (const int32_t*)nullptr, kLipStep, shard, nshards,
                        (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap);
     if (lipg & 1) {  // the central references' G (convexity-augmented pruning)
-        hipLaunchKernelGGL(consensus_grad_select_kernel, dim3(P), dim3(256), 0, st, kcount, stride,
+        ERP_LAUNCH(consensus_grad_select_kernel, dim3(P), dim3(256), 0, st, kcount, stride,
                            (const double*)lb, (const double*)ub, (const int32_t*)bsel, kLipStep,
                            shard, nshards, (const int32_t*)nullptr, (const int32_t*)nullptr,
                            (const double*)lr.U, gfac, lr.gsel, lr.gcnt, lr.gcap);
-        hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)lr.gcnt,
+        ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)lr.gcnt,
                            P, 1, 0, lr.goff);
-        hipLaunchKernelGGL(consensus_grad_kernel, dim3(std::min(P * 64, 2048)), dim3(256), 0, st,
+        ERP_LAUNCH(consensus_grad_kernel, dim3(std::min(P * 64, 2048)), dim3(256), 0, st,
                            kcount, rv, dscale, stride, trim_lo, trim_hi, (const double*)lb,
                            (const int32_t*)bsel, (const int32_t*)lr.gsel, (const int32_t*)lr.goff,
                            P, lr.gcap, lr.gref);
     }
-    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
+    ERP_LAUNCH(consensus_lipschitz_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
                        st, kcount, rv, stride, lb, ub, (const int32_t*)nullptr,
                        (const int32_t*)nullptr, rlist, stride, rcount, shard, nshards, kLipStep,
                        (const float4*)lr.ref, (const double*)lr.U, (const int32_t*)lr.cnt,
@@ -4915,29 +4937,29 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
     int32_t* uoff = rcount + P;  // [n_pairs + 1] after the counts
     if (flat_pct > 0 && nshards == 1) {
         // flat pairs: refine the first-stage references, then re-run the first stage
-        hipLaunchKernelGGL(consensus_flat_gate_kernel, dim3((P + 255) / 256), dim3(256), 0, st,
+        ERP_LAUNCH(consensus_flat_gate_kernel, dim3((P + 255) / 256), dim3(256), 0, st,
                            kcount, rcount, two ? lr.r2cnt : nullptr, P, flat_pct, trim_lo,
                            trim_hi, lr.nflat);
         const HintCand* hint = nullptr;
         if (use_hint) {
-            hipLaunchKernelGGL(consensus_hint_kernel, dim3(P, kHintCands), dim3(256), 0, st,
+            ERP_LAUNCH(consensus_hint_kernel, dim3(P, kHintCands), dim3(256), 0, st,
                                kcount, rv, stride, trim_lo, trim_hi, (const int32_t*)nullptr,
                                (const int32_t*)lr.nflat, kLipStep, 0, (const double*)ub, lr.hcand);
             hint = lr.hcand;
         }
-        hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)lr.nflat,
+        ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)lr.nflat,
                            P, kRefineRows * kLipStep, kRefineMin, uoff);
-        hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv,
+        ERP_LAUNCH(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv,
                            dscale, stride, trim_lo, trim_hi, (const int32_t*)nullptr,
                            (const int32_t*)lr.nflat, (const int32_t*)bsel, lb, ub,
                            (const int32_t*)nullptr, stride, (const int32_t*)nullptr, kLipStep,
                            hint, (const int32_t*)uoff, P);
-        hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
+        ERP_LAUNCH(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
                            trim_lo, trim_hi, (const double*)lb, (const double*)ub,
                            (const int32_t*)nullptr, (const int32_t*)nullptr, kLipStep, 0, 1,
                            (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap,
                            (const int32_t*)lr.nflat);
-        hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
+        ERP_LAUNCH(consensus_lipschitz_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
                            st, kcount, rv, stride, lb, ub, (const int32_t*)nullptr,
                            (const int32_t*)nullptr, rlist, stride, rcount, 0, 1, kLipStep,
                            (const float4*)lr.ref, (const double*)lr.U, (const int32_t*)lr.cnt,
@@ -4954,53 +4976,53 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
         float* edz = edges + (size_t)P * 2 * kNB;
         int32_t* zb = reinterpret_cast<int32_t*>(edges + (size_t)P * 4 * kNB);
         int32_t* n2 = uoff + P + 1;
-        hipLaunchKernelGGL(consensus_ref2_prep_kernel, dim3(P), dim3(256), 0, st, kcount, dscale,
+        ERP_LAUNCH(consensus_ref2_prep_kernel, dim3(P), dim3(256), 0, st, kcount, dscale,
                            (const double*)ub, (const int32_t*)bsel, (const int32_t*)rcount, stride,
                            trim_lo, trim_hi, shard, nshards, zb, edz);
-        hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st,
+        ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st,
                            (const int32_t*)lr.r2cnt, P, kBoundRows, 0, uoff);
         const int units2 = P * ((stride / kLip2Step + 1 + kBoundRows - 1) / kBoundRows);
-        hipLaunchKernelGGL(consensus_zoom_kernel<6>, dim3(units2), dim3(256), 0, st, kcount, rv,
+        ERP_LAUNCH(consensus_zoom_kernel<6>, dim3(units2), dim3(256), 0, st, kcount, rv,
                            (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb, ub,
                            (const int32_t*)lr.r2list, (const int32_t*)lr.r2cnt,
                            (const int32_t*)uoff, P, zsel, 1, dscale, bsel);
         const hipError_t m2 = hipMemsetAsync(n2, 0, sizeof(int32_t) * 2 * P, st);  // + nfb
         if (m2 != hipSuccess) return m2;
-        hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv,
+        ERP_LAUNCH(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv,
                            stride, trim_lo, trim_hi, (const double*)lb, (const double*)ub,
                            (const int32_t*)lr.r2list, (const int32_t*)lr.r2cnt, 1, shard,
                            nshards, (const int32_t*)zb, lr.ref, lr.U, lr.cnt, lr.cap);
         if (lipg & 2) {  // G of the central second-stage references (fine bounds)
-            hipLaunchKernelGGL(consensus_grad_select_kernel, dim3(P), dim3(256), 0, st, kcount,
+            ERP_LAUNCH(consensus_grad_select_kernel, dim3(P), dim3(256), 0, st, kcount,
                                stride, (const double*)lb, (const double*)ub, (const int32_t*)bsel,
                                1, 0, 1, (const int32_t*)lr.r2list, (const int32_t*)lr.r2cnt,
                                (const double*)lr.U, gfac, lr.gsel, lr.gcnt, lr.gcap);
-            hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st,
+            ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st,
                                (const int32_t*)lr.gcnt, P, 1, 0, lr.goff);
-            hipLaunchKernelGGL(consensus_grad_kernel, dim3(std::min(P * 64, 2048)), dim3(256), 0,
+            ERP_LAUNCH(consensus_grad_kernel, dim3(std::min(P * 64, 2048)), dim3(256), 0,
                                st, kcount, rv, dscale, stride, trim_lo, trim_hi, (const double*)lb,
                                (const int32_t*)bsel, (const int32_t*)lr.gsel,
                                (const int32_t*)lr.goff, P, lr.gcap, lr.gref);
         }
-        hipLaunchKernelGGL(consensus_lipschitz2_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
+        ERP_LAUNCH(consensus_lipschitz2_kernel, dim3((srows + 511) / 512, P), dim3(256), 0,
                            st, kcount, rv, stride, lb, ub, (const int32_t*)rlist,
                            (const int32_t*)rcount, (const int32_t*)zb, (const int32_t*)bsel, list2,
                            n2, n2 + P, (const float4*)lr.ref, (const double*)lr.U,
                            (const int32_t*)lr.cnt, lr.cap,
                            (lipg & 2) ? (const float4*)lr.gref : nullptr, (const int32_t*)lr.gcnt,
                            lr.gcap);
-        hipLaunchKernelGGL(consensus_ref2_count_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P,
+        ERP_LAUNCH(consensus_ref2_count_kernel, dim3((P + 255) / 256), dim3(256), 0, st, P,
                            (const int32_t*)zb, (const int32_t*)lr.r2cnt, (const int32_t*)n2,
                            (const int32_t*)(n2 + P), rcount);
         blist = list2;
         bcount = n2;
     }
-    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, bcount, P, kBoundRows, 0,
+    ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, bcount, P, kBoundRows, 0,
                        uoff);
     // one block per unit of the longest possible lists: the live units come first in dispatch
     // order, the trailing blocks exit after one load
     const int max_units = P * ((stride + kBoundRows - 1) / kBoundRows);
-    hipLaunchKernelGGL(consensus_bounds_list_kernel, dim3(max_units), dim3(256), 0, st,
+    ERP_LAUNCH(consensus_bounds_list_kernel, dim3(max_units), dim3(256), 0, st,
                        kcount, rv, dscale, edges, stride, trim_lo, trim_hi, lb, ub, bsel, blist,
                        bcount, (const int32_t*)uoff, P);
     return hipGetLastError();
@@ -5010,7 +5032,7 @@ hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, cons
                                    const BatchShape& sh, double trim_lo, double trim_hi,
                                    int32_t* surv, int32_t* nsurv, double* tmean, int again,
                                    hipStream_t st) {
-    hipLaunchKernelGGL(consensus_select_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, kcount, lb, ub,
+    ERP_LAUNCH(consensus_select_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, kcount, lb, ub,
                        2 * sh.iters, trim_lo, trim_hi, surv, nsurv, tmean, again);
     return hipGetLastError();
 }
@@ -5031,32 +5053,32 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
     if (use_hint) {
         // (pairs with <= kHintManyRows survivors -- a one-cluster pair after the zoom has ~20 --
         // keep the default windows: the hint's K-column passes would cost more than they save)
-        hipLaunchKernelGGL(consensus_hint_kernel, dim3(P, kHintCands), dim3(256), 0, st, kcount,
+        ERP_LAUNCH(consensus_hint_kernel, dim3(P, kHintCands), dim3(256), 0, st, kcount,
                            rv, stride, trim_lo, trim_hi, surv, nsurv, 1, kHintManyRows,
                            (const double*)ub, lr.hcand);
         hint = lr.hcand;
     }
     // (A) the reference survivors (every kRefStep-th) of pairs with > kRefineMin survivors
-    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, P,
+    ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, P,
                        kRefineRows * kRefStep, kRefineMin, uoff);
-    hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
+    ERP_LAUNCH(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
                        stride, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, surv, stride,
                        (const int32_t*)nullptr, kRefStep, hint, (const int32_t*)uoff, P);
     // (B) Lipschitz pruning of the other survivors against the refined references
     const hipError_t me = hipMemsetAsync(n2, 0, sizeof(int32_t) * P, st);
     if (me != hipSuccess) return me;
-    hipLaunchKernelGGL(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
+    ERP_LAUNCH(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
                        trim_lo, trim_hi, (const double*)lb, (const double*)ub, surv, nsurv,
                        kRefStep, 0, 1, (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap);
-    hipLaunchKernelGGL(consensus_lipschitz_kernel, dim3((stride + 511) / 512, P), dim3(256), 0, st,
+    ERP_LAUNCH(consensus_lipschitz_kernel, dim3((stride + 511) / 512, P), dim3(256), 0, st,
                        kcount, rv, stride, lb, ub, surv, nsurv, list2, l2stride, n2, 0, 1,
                        kRefStep, (const float4*)lr.ref, (const double*)lr.U,
                        (const int32_t*)lr.cnt, lr.cap, (int32_t*)nullptr, (int32_t*)nullptr,
                        (const float4*)nullptr, (const int32_t*)nullptr, 0);
     // (C) the survivors the references did not prune
-    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)n2, P,
+    ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)n2, P,
                        kRefineRows, 0, uoff);
-    hipLaunchKernelGGL(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
+    ERP_LAUNCH(consensus_refine_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
                        stride, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, (const int32_t*)list2,
                        l2stride, (const int32_t*)n2, 1, hint, (const int32_t*)uoff, P);
     return hipGetLastError();
@@ -5067,9 +5089,9 @@ hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const f
                                  const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
                                  double* tmean, hipStream_t st) {
     int32_t* uoff = const_cast<int32_t*>(nsurv) + 2 * sh.n_pairs;  // as in launch_consensus_refine
-    hipLaunchKernelGGL(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, sh.n_pairs, 1, 0,
+    ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, sh.n_pairs, 1, 0,
                        uoff);
-    hipLaunchKernelGGL(consensus_rows_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
+    ERP_LAUNCH(consensus_rows_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
                        2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, tmean,
                        (const int32_t*)uoff, sh.n_pairs);
     return hipGetLastError();
@@ -5086,7 +5108,7 @@ hipError_t launch_consensus_final(const int32_t* counts, const int32_t* kcount, 
                                   const int32_t* nsurv, const int32_t* nbin, const BatchShape& sh,
                                   double sample_frac, double trim_lo, double trim_hi,
                                   float* sortbuf, erp_pair_result* results, hipStream_t st) {
-    hipLaunchKernelGGL(consensus_final_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, kcount,
+    ERP_LAUNCH(consensus_final_kernel, dim3(sh.n_pairs), dim3(1024), 0, st, counts, kcount,
                        rv, tv, tmean, flags, nsurv, nbin, 2 * sh.iters, sortbuf_len(sh.iters), sample_frac,
                        trim_lo, trim_hi, sortbuf, results);
     return hipGetLastError();

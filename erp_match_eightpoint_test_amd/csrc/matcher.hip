@@ -21,6 +21,7 @@
 #include <type_traits>
 
 #include "erp_kernels.hpp"
+#include "erp_launch.hpp"
 
 namespace erp {
 
@@ -1045,14 +1046,14 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
     if (e == hipSuccess) e = hipMemsetAsync(sent, 0, 128, st);
     if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(sent + 128), 0x7f800000u, 1, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(knn2_split_kernel, dim3((sh.max_nt + 63) / 64, sh.n_pairs), dim3(256), 0,
+    ERP_LAUNCH(knn2_split_kernel, dim3((sh.max_nt + 63) / 64, sh.n_pairs), dim3(256), 0,
                        st, desc_t, off_t, sh.max_nt, thi, tn, tmax);
     int32_t* ctile;
     bf16x8* cval;
     cand_split(sh, cand, &ctile, &cval);
     const int qblocks = (sh.max_nq + kFQ - 1) / kFQ;
     if ((size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 >= (1ull << 31)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(knn2_filter_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
+    ERP_LAUNCH(knn2_filter_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
                        st, desc_q, thi, tn, tmax, off_q, off_t, sh.fchunk_len, sh.fchunks,
                        sh.max_nq, sh.max_nt, qblocks, pu, ccount, ctile, cval,
                        (const bf16x8*)sent, (const float*)(sent + 128), (int)cand_tile_array());
@@ -1066,14 +1067,14 @@ hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const i
     int32_t* ctile;
     bf16x8* cval;
     cand_split(sh, cand, &ctile, &cval);
-    hipLaunchKernelGGL(set_i32_kernel, dim3(1), dim3(1), 0, st, ovf, 0);
+    ERP_LAUNCH(set_i32_kernel, dim3(1), dim3(1), 0, st, ovf, 0);
     const int qblocks = (sh.max_nq + 255) / 256;
-    hipLaunchKernelGGL(knn2_rescore_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
+    ERP_LAUNCH(knn2_rescore_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
                        st, desc_q, desc_t, off_q, off_t, sh.max_nq, sh.fchunk_len, sh.fchunks,
                        split_tmax(sh, split), pu, ccount, ctile, cval, part, ovf, qblocks,
                        sh.fchunks == 1 ? ratio : -1.f,  // (bound decisions need one chunk)
                        (int)cand_tile_array());
-    hipLaunchKernelGGL(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
+    ERP_LAUNCH(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
                        sh.max_nq, sh.fchunk_len, sh.fchunks, ovf, part);
     return hipGetLastError();
 }
@@ -1082,7 +1083,7 @@ hipError_t launch_knn2_exact(const float* desc_q, const float* desc_t, const int
                              const int64_t* off_t, const BatchShape& sh, Top2* xpart,
                              hipStream_t st) {
     dim3 grid((sh.max_nq + kXQ - 1) / kXQ, sh.xchunks, sh.n_pairs);
-    hipLaunchKernelGGL(knn2_exact_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
+    ERP_LAUNCH(knn2_exact_kernel, grid, dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
                        sh.xchunk_len, sh.xchunks, sh.max_nq, xpart);
     return hipGetLastError();
 }
@@ -1090,7 +1091,7 @@ hipError_t launch_knn2_exact(const float* desc_q, const float* desc_t, const int
 hipError_t launch_knn2_fold(const Top2* part, const int64_t* off_q, const int64_t* off_t,
                             const BatchShape& sh, int chunk_len, int chunks, Top2* out,
                             hipStream_t st) {
-    hipLaunchKernelGGL(knn2_fold_kernel, dim3((sh.max_nq + 255) / 256, sh.n_pairs), dim3(256), 0,
+    ERP_LAUNCH(knn2_fold_kernel, dim3((sh.max_nq + 255) / 256, sh.n_pairs), dim3(256), 0,
                        st, part, off_q, off_t, chunk_len, chunks, sh.max_nq, out);
     return hipGetLastError();
 }
@@ -1104,9 +1105,9 @@ hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64
                              erp_dmatch* matches, int32_t* counts, int32_t* flags,
                              int32_t* bcount, hipStream_t st) {
     const dim3 grid(std::max(1, (sh.max_nq + kMergeBlock - 1) / kMergeBlock), sh.n_pairs);
-    hipLaunchKernelGGL(knn2_merge_count_kernel, grid, dim3(kMergeBlock), 0, st, part, off_q, off_t,
+    ERP_LAUNCH(knn2_merge_count_kernel, grid, dim3(kMergeBlock), 0, st, part, off_q, off_t,
                        chunk_len, chunks, sh.max_nq, ratio, bcount);
-    hipLaunchKernelGGL(knn2_merge_kernel, grid, dim3(kMergeBlock), 0, st, part, off_q, off_t,
+    ERP_LAUNCH(knn2_merge_kernel, grid, dim3(kMergeBlock), 0, st, part, off_q, off_t,
                        chunk_len, chunks, sh.max_nq, ratio, (const int32_t*)bcount, matches, counts,
                        flags);
     return hipGetLastError();

@@ -22,6 +22,7 @@
 
 #include "erp_device.hpp"
 #include "erp_remap.hpp"
+#include "erp_launch.hpp"
 
 namespace erp {
 
@@ -164,14 +165,14 @@ hipError_t launch_remap(const RemapJobs& jobs, int n_jobs, int max_out_rows, int
     if (e != hipSuccess) return e;
     dim3 grid((max_out_cols + kRmCols - 1) / kRmCols, (max_out_rows + kRmRows - 1) / kRmRows,
               n_jobs);
-    hipLaunchKernelGGL(remap_kernel, grid, dim3(256), 0, st, jobs, W, H, scr);
-    hipLaunchKernelGGL(remap_fixup_kernel, dim3(256), dim3(256), 0, st, jobs, W, H, scr);
+    ERP_LAUNCH(remap_kernel, grid, dim3(256), 0, st, jobs, W, H, scr);
+    ERP_LAUNCH(remap_fixup_kernel, dim3(256), dim3(256), 0, st, jobs, W, H, scr);
     return hipGetLastError();
 }
 
 hipError_t launch_band_keypoints(erp_point2f* d_kp, const BandKeypointArgs& a, hipStream_t st) {
     if (a.end[3] <= 0) return hipSuccess;
-    hipLaunchKernelGGL(band_keypoints_kernel, dim3((a.end[3] + 255) / 256), dim3(256), 0, st, d_kp,
+    ERP_LAUNCH(band_keypoints_kernel, dim3((a.end[3] + 255) / 256), dim3(256), 0, st, d_kp,
                        a);
     return hipGetLastError();
 }

@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #include "erp_surf.hpp"
+#include "erp_launch.hpp"
 
 namespace erp {
 
@@ -743,11 +744,11 @@ hipError_t launch_surf_detect(const uint8_t* images, int n_images, int W, int H,
     const size_t npix = (size_t)n_images * W * H;
     const uint8_t* gray = images;
     if (channels == 3) {
-        hipLaunchKernelGGL(surf_gray_kernel, dim3(2048), dim3(256), 0, st, images, 3, npix, scr.gray);
+        ERP_LAUNCH(surf_gray_kernel, dim3(2048), dim3(256), 0, st, images, 3, npix, scr.gray);
         gray = scr.gray;
     }
-    hipLaunchKernelGGL(surf_integral_rows_kernel, dim3(H, n_images), dim3(256), 0, st, gray, W, H, scr.sum);
-    hipLaunchKernelGGL(surf_integral_cols_kernel, dim3((W + 1 + 255) / 256, n_images), dim3(256), 0, st,
+    ERP_LAUNCH(surf_integral_rows_kernel, dim3(H, n_images), dim3(256), 0, st, gray, W, H, scr.sum);
+    ERP_LAUNCH(surf_integral_cols_kernel, dim3((W + 1 + 255) / 256, n_images), dim3(256), 0, st,
                        W, H, scr.sum);
     hipError_t e = hipMemsetAsync(scr.det, 0, plan.det_per_img * n_images * sizeof(float), st);
     if (e != hipSuccess) return e;
@@ -756,26 +757,26 @@ hipError_t launch_surf_detect(const uint8_t* images, int n_images, int W, int H,
         const int ms = plan.max_size0 << o;
         if (o == 0) {
             const size_t lds = sizeof(int32_t) * (kHTJ + ms) * (16 + ms);
-            hipLaunchKernelGGL(surf_hessian_tile_kernel<1>,
+            ERP_LAUNCH(surf_hessian_tile_kernel<1>,
                                dim3(((W + kHTJ - 1) / kHTJ) * ((H + 15) / 16) * n_images), dim3(256), lds, st, scr.sum, W, H, plan.d_layers, lb, le, ms, plan.det_per_img,
                                scr.det);
         } else if (W >= 2 && H >= 2) {
             const size_t lds = sizeof(int32_t) * 4 * ((2 * kHTJ + ms + 1) / 2) * ((16 + ms + 1) / 2);
-            hipLaunchKernelGGL(surf_hessian_tile_kernel<2>,
+            ERP_LAUNCH(surf_hessian_tile_kernel<2>,
                                dim3(((W / 2 + kHTJ - 1) / kHTJ) * ((H / 2 + 7) / 8) * n_images), dim3(512), lds, st,
                                scr.sum, W, H, plan.d_layers, lb, le, ms, plan.det_per_img, scr.det);
         }
     }
     if (plan.samples_hi > 0)
-        hipLaunchKernelGGL(surf_hessian_hi_kernel, dim3(plan.samples_hi, n_images), dim3(256), 0, st,
+        ERP_LAUNCH(surf_hessian_hi_kernel, dim3(plan.samples_hi, n_images), dim3(256), 0, st,
                            scr.sum, W, H, plan.d_layers, plan.n_tiled * plan.n_layers0, plan.n_layers,
                            plan.det_per_img, scr.det);
     e = hipMemsetAsync(counts, 0, sizeof(int32_t) * n_images, st);
     if (e != hipSuccess) return e;
     if (plan.mid_cells > 0)
-        hipLaunchKernelGGL(surf_extrema_kernel, dim3(plan.mid_cells, n_images), dim3(256), 0, st,
+        ERP_LAUNCH(surf_extrema_kernel, dim3(plan.mid_cells, n_images), dim3(256), 0, st,
                            scr.sum, W, H, plan.d_layers, plan.d_mid, plan.n_mid, plan.det_per_img, scr.det, plan.threshold, max_kp, scr.raw, counts);
-    hipLaunchKernelGGL(surf_sort_kernel, dim3((max_kp + 255) / 256, n_images), dim3(256), 0, st, scr.raw,
+    ERP_LAUNCH(surf_sort_kernel, dim3((max_kp + 255) / 256, n_images), dim3(256), 0, st, scr.raw,
                        counts, max_kp, scr.sorted);
     return hipGetLastError();
 }
@@ -787,13 +788,13 @@ hipError_t launch_surf_describe(const uint8_t* images, int n_images, int W, int 
     const uint8_t* gray = channels == 3 ? (const uint8_t*)scr.gray : images;
     hipError_t e = hipMemsetAsync(scr.nitems, 0, sizeof(int32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(surf_orient_kernel, dim3(min(ng, 8192)), dim3(64), 0, st, scr.sum, W, H,
+    ERP_LAUNCH(surf_orient_kernel, dim3(min(ng, 8192)), dim3(64), 0, st, scr.sum, W, H,
                        n_images, max_kp, d_kpre, g0, ng, scr.sorted, plan.consts, scr.pool, scr.slot,
                        scr.max_win, scr.jobs, scr.items, scr.nitems);
-    hipLaunchKernelGGL(surf_window_kernel, dim3(8192), dim3(256), 0, st, gray, W, H, n_images, d_kpre,
+    ERP_LAUNCH(surf_window_kernel, dim3(8192), dim3(256), 0, st, gray, W, H, n_images, d_kpre,
                        g0, (const float*)scr.pool, scr.pool, scr.slot, (const SurfJob*)scr.jobs,
                        (const int2*)scr.items, (const int32_t*)scr.nitems);
-    hipLaunchKernelGGL(surf_descriptor_kernel, dim3(min(ng, 4096)), dim3(256), 0, st, n_images, max_kp,
+    ERP_LAUNCH(surf_descriptor_kernel, dim3(min(ng, 4096)), dim3(256), 0, st, n_images, max_kp,
                        d_kpre, g0, ng, (const float*)scr.pool, scr.slot, (const SurfJob*)scr.jobs,
                        scr.desc, plan.consts);
     return hipGetLastError();
@@ -801,7 +802,7 @@ hipError_t launch_surf_describe(const uint8_t* images, int n_images, int W, int 
 
 hipError_t launch_surf_compact(int n_images, const SurfScratch& scr, int max_kp, erp_keypoint* kp_out,
                                float* desc_out, int32_t* counts, hipStream_t st) {
-    hipLaunchKernelGGL(surf_compact_kernel, dim3(n_images), dim3(1024), 0, st, scr.sorted, scr.desc,
+    ERP_LAUNCH(surf_compact_kernel, dim3(n_images), dim3(1024), 0, st, scr.sorted, scr.desc,
                        max_kp, counts, kp_out, desc_out);
     return hipGetLastError();
 }

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "../../include/erp_match.h"
+#include "erp_launch.hpp"
 
 int32_t erp_ctx_device_internal(erp_ctx* ctx);                          // capi.hip
 void* erp_ctx_stamp_buffer_internal(erp_ctx* ctx, size_t bytes, uint32_t* epoch, bool* fresh);
@@ -345,7 +346,7 @@ erp_status erp_epipolar_draw_dev(erp_ctx* ctx, const erp_point2f* h_key_left,
         if (h_random_idx) h_random_idx[t] = idx[t];
     }
     memcpy(k.e, E, sizeof(k.e));
-    hipLaunchKernelGGL(epipolar_kernel,
+    ERP_LAUNCH_S(epipolar_kernel,
                        dim3((out_width + 255) / 256, (out_height + kEpiRows - 1) / kEpiRows),
                        dim3(256), 0, st, k, out_width, out_height, d_out);
     return hipGetLastError() == hipSuccess ? ERP_OK : ERP_HIP_ERROR;
@@ -372,10 +373,10 @@ erp_status erp_draw_match_dev(erp_ctx* ctx, const uint8_t* d_left, const uint8_t
     if (fresh && hipMemsetAsync(win, 0, (size_t)(npix + 4) * 4, st) != hipSuccess)
         return ERP_HIP_ERROR;
     if (m > 0)
-        hipLaunchKernelGGL(match_lines_kernel, dim3(m), dim3(256), 0, st, d_key_left, d_key_right,
+        ERP_LAUNCH_S(match_lines_kernel, dim3(m), dim3(256), 0, st, d_key_left, d_key_right,
                            m, W, H, epoch, win);
     const int64_t groups = (npix + 3) / 4;
-    hipLaunchKernelGGL(draw_match_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st,
+    ERP_LAUNCH_S(draw_match_kernel, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, st,
                        d_left, d_right, win, epoch, m, npix, d_out);
     return hipGetLastError() == hipSuccess ? ERP_OK : ERP_HIP_ERROR;
 }

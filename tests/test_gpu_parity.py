@@ -368,6 +368,36 @@ def test_batch_pipeline_hip_graph_replay(gpu_lib):
     assert torch.equal(o2["results"], ref2["results"])
 
 
+def test_graph_replay_with_new_contents_equals_fresh_run(gpu_lib):
+    """reuse_outputs + graphs: the SAME input buffers refilled with other pairs of the same shape
+    replay the captured graph; every output (results, match lists, R_vec_arr) equals a fresh
+    plain run of those pairs byte for byte, including the entries past each pair's M / K (the
+    pipeline zeroes the optional outputs inside the graph: ADVICE r04)"""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner
+    sizes = [600, 900, 300]
+    args = _batch([synth.make_pair(3300 + i, n_kpts=n) for i, n in enumerate(sizes)])
+    args_b = _batch([synth.make_pair(3400 + i, n_kpts=n, inlier_frac=0.5) for i, n in enumerate(sizes)])
+    want = ("matches", "rvec", "tvec")
+    cg = Context(0)
+    cg.set_graphs(True)
+    run = PairBatchRunner(ctx=cg, iters=300, reuse_outputs=True)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        run.run(*args, want=want, stream=st.cuda_stream)  # capture (pairs A)
+        st.synchronize()
+        for a, b in zip(args, args_b):  # refill the same buffers with pairs B
+            if isinstance(a, torch.Tensor):
+                a.copy_(b)
+        o = run.run(*args, want=want, stream=st.cuda_stream)  # replay
+        st.synchronize()
+        got = {k: v.clone() for k, v in o.items()}
+    ref = PairBatchRunner(ctx=Context(0), iters=300).run(*args_b, want=want)
+    torch.cuda.synchronize()
+    for k in ("results",) + want:
+        assert torch.equal(got[k], ref[k]), k
+
+
 def test_batch_pipeline_valu_matcher_equals_mfma(gpu_lib):
     """the whole batch pipeline with the packed-FP32 exact sweep as the matcher: matches and
     results identical to the MFMA-filter pipeline (ragged pair sizes, several train chunks)"""
