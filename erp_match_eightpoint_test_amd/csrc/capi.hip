@@ -400,9 +400,12 @@ bool ensure_matcher(erp_ctx* c, const erp::BatchShape& sh) {
 }
 
 // per-chunk partials -> (fold when there are several chunks) -> ratio test + compaction
+// bo != nullptr: the merge also gathers the matched keypoints and writes their bearings
+// (bearings_from_matches_kernel's work, one launch fewer)
 erp_status fold_and_merge(erp_ctx* ctx, const int64_t* oq, const int64_t* ot,
                           const erp::BatchShape& sh, int chunk_len, int chunks, float ratio,
-                          erp_dmatch* matches, int32_t* counts, int32_t* flags, hipStream_t st) {
+                          erp_dmatch* matches, int32_t* counts, int32_t* flags, hipStream_t st,
+                          const erp::BearingOut* bo = nullptr) {
     StageTimer _t(ctx, ERP_STAGE_KNN2_MERGE, st);
     const erp::Top2* part = (const erp::Top2*)ctx->part.p;
     if (chunks > 1) {
@@ -412,7 +415,7 @@ erp_status fold_and_merge(erp_ctx* ctx, const int64_t* oq, const int64_t* ot,
     }
     // a single chunk spanning the whole train set
     ERP_CK(erp::launch_knn2_merge(part, oq, ot, sh, sh.max_nt, 1, ratio, matches, counts, flags,
-                                  (int32_t*)ctx->mblk.p, st));
+                                  (int32_t*)ctx->mblk.p, st, bo));
     return ERP_OK;
 }
 
@@ -420,21 +423,23 @@ erp_status fold_and_merge(erp_ctx* ctx, const int64_t* oq, const int64_t* ot,
 // the exact packed-FP32 sweep, merge
 erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int64_t* oq,
                        const int64_t* ot, const erp::BatchShape& sh, float ratio,
-                       erp_dmatch* matches, int32_t* counts, int32_t* flags, hipStream_t st) {
+                       erp_dmatch* matches, int32_t* counts, int32_t* flags, hipStream_t st,
+                       const erp::BearingOut* bo = nullptr) {
     if (ctx->matcher == ERP_MATCHER_VALU_EXACT) {
         {
             StageTimer _t(ctx, ERP_STAGE_KNN2_EXACT, st);
             ERP_CK(erp::launch_knn2_exact(dq, dt, oq, ot, sh, (erp::Top2*)ctx->part.p, st));
         }
         return fold_and_merge(ctx, oq, ot, sh, sh.xchunk_len, sh.xchunks, ratio, matches, counts,
-                              flags, st);
+                              flags, st, bo);
     }
     auto* pu = (float2*)ctx->pu.p;
     auto* cc = (int32_t*)ctx->ccount.p;
     void* cand = ctx->cand.p;
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_FILTER, st);
-        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand, st));
+        ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand, st,
+                                       (int32_t*)ctx->ovf.p));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_RESCORE, st);
@@ -443,7 +448,7 @@ erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int
                                         ctx->bound_ratio ? ratio : -1.f, st));
     }
     return fold_and_merge(ctx, oq, ot, sh, sh.fchunk_len, sh.fchunks, ratio, matches, counts,
-                          flags, st);
+                          flags, st, bo);
 }
 
 erp_status ensure_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_batch_outputs* out) {
@@ -645,7 +650,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         StageTimer _t(ctx, ERP_STAGE_VALID_COMPACT, st);
         ERP_CK(erp::launch_valid_place(counts, lite_hl(c), lite_wsum(c, sh), sh, cfg->sample_frac,
                                        (float*)c->rv.p, tv, (int32_t*)c->kcount.p,
-                                       out ? out->rvec : nullptr, (float*)c->dscale.p, st));
+                                       out ? out->rvec : nullptr, (float*)c->dscale.p,
+                                       (float*)c->edges.p, st));
     } else if (from_hyps && phase != 2) {
         StageTimer _t(ctx, ERP_STAGE_VALID_COMPACT, st);
         ERP_CK(erp::launch_valid_compact(counts, hyps, sh, cfg->sample_frac,
@@ -653,16 +659,30 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                          (int32_t*)c->kcount.p, out ? out->rvec : nullptr,
                                          (float*)c->dscale.p, st));
     }
+    // small batches (the single-pair call of src/automatic.cpp:117-126): every row gets its
+    // K-column histogram, no Lipschitz pre-pruning, no zoom or refine stage.  For one pair at
+    // 10k iterations that pass is ~25-35 us of the whole GPU, against ~20 dependent small
+    // launches (~0.2 ms) of the pruning stages, which only pay when many pairs share the chip
+    // or K is large: the route is taken when n_pairs (2 iters)^2 <= 2e9 (one pair up to ~22k
+    // iterations, five at 10k; configs[4]'s 100k-iteration find keeps the pruning), and never
+    // for the row-sharded phases.  ERP_SMALL_BATCH = n overrides: batches of <= n pairs take it
+    // (0 = never; read at every call)
+    const char* sb_env = getenv("ERP_SMALL_BATCH");
+    const double kk = 2.0 * sh.iters;
+    const bool small = phase == 0 && nshards == 1 &&
+                       (sb_env ? sh.n_pairs <= atoi(sb_env) : sh.n_pairs * kk * kk <= 2e9);
+    const bool prune = !small;
     if (phase != 2) {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
         ERP_CK(erp::launch_consensus_bounds((int32_t*)c->kcount.p, (float*)c->rv.p,
                                             (float*)c->dscale.p, (float*)c->edges.p, sh,
                                             cfg->trim_lo, cfg->trim_hi, lbp, ubp, bselp, shard,
-                                            nshards, (int32_t*)c->surv.p,
-                                            (int32_t*)c->nsurv.p + sh.n_pairs,
+                                            nshards, prune ? (int32_t*)c->surv.p : nullptr,
+                                            prune ? (int32_t*)c->nsurv.p + sh.n_pairs : nullptr,
                                             (int32_t*)c->zsel.p, c->zoom_refs, c->lip2,
                                             (int32_t*)c->sortbuf.p, c->lipref.p, c->lipg,
-                                            c->lipg_fac, c->flat_refs, c->refine_hint, st));
+                                            c->lipg_fac, c->flat_refs, c->refine_hint, st,
+                                            from_hyps && lite));  // (valid_place wrote the edges)
     }
     if (c->snap_on && phase == 0) {
         const size_t nrow = (size_t)sh.n_pairs * 2 * sh.iters;
@@ -688,7 +708,12 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, 0,
                                             st));
     }
-    for (int level = 1; level <= c->zoom; level++) {
+    // small batches skip the zoom too: the exact pass takes the first selection's survivors
+    // (~150 for a typical pair, one grid-wide launch); single pair 0.487 -> 0.437 ms
+    // (profiles/r05g_latency_ab.txt; ERP_SMALL_ZOOM=1 keeps it)
+    const char* sz_env = getenv("ERP_SMALL_ZOOM");
+    const int zoom_levels = prune || (sz_env && atoi(sz_env) != 0) ? c->zoom : 0;
+    for (int level = 1; level <= zoom_levels; level++) {
         {
             StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
             ERP_CK(erp::launch_consensus_zoom((int32_t*)c->kcount.p, (float*)c->rv.p,
@@ -703,7 +728,9 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p, tmean, 0,
                                             st));
     }
-    {
+    // (small batches: no refine stage either -- the exact pass takes the survivors in one
+    // grid-wide launch; the refine stage's ~8 dependent launches cost a single pair more)
+    if (prune) {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_REFINE, st);
         ERP_CK(erp::launch_consensus_refine((int32_t*)c->kcount.p, (float*)c->rv.p,
                                             (float*)c->dscale.p, sh, cfg->trim_lo, cfg->trim_hi,
@@ -712,7 +739,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             ubp, (int32_t*)c->sortbuf.p, c->lipref.p,
                                             c->refine_hint, st));
     }
-    {
+    if (prune) {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
         ERP_CK(erp::launch_consensus_select((int32_t*)c->kcount.p, lbp,
                                             ubp, sh, cfg->trim_lo, cfg->trim_hi,
@@ -730,7 +757,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_FINAL, st);
         ERP_CK(erp::launch_consensus_final(counts, (int32_t*)c->kcount.p, (float*)c->rv.p, tv, tmean,
                                            flags, (int32_t*)c->nsurv.p,
-                                           (int32_t*)c->nsurv.p + sh.n_pairs, sh, cfg->sample_frac, cfg->trim_lo, cfg->trim_hi,
+                                           prune ? (int32_t*)c->nsurv.p + sh.n_pairs : nullptr, sh,
+                                           cfg->sample_frac, cfg->trim_lo, cfg->trim_hi,
                                            (float*)c->sortbuf.p, results, st));
     }
     if (c->snap_on && phase == 0 && c->snap_bytes) {
@@ -850,16 +878,13 @@ erp_status batch_enqueue(erp_ctx* ctx, const erp_pair_batch* b, float ratio,
     for (const auto& o : opt)
         if (o.p) ERP_CK(hipMemsetAsync(o.p, 0, o.bytes, st));
     ERP_CK(hipMemsetAsync(ctx->flags.p, 0, (size_t)sh.n_pairs * 4, st));
+    // the merge writes the gather + bearings as it places each match (src/spherical_surf.cpp:
+    // 155-162, src/eight_point.cpp:163-186; bearings_from_matches_kernel's work)
+    const erp::BearingOut bo{b->kp_l, b->kp_r, b->width, b->height, (double*)ctx->pts.p,
+                             out->key_left, out->key_right};
     erp_status es = run_matcher(ctx, b->desc_l, b->desc_r, b->off_l, b->off_r, sh, ratio, matches,
-                                (int32_t*)ctx->counts.p, (int32_t*)ctx->flags.p, st);
+                                (int32_t*)ctx->counts.p, (int32_t*)ctx->flags.p, st, &bo);
     if (es != ERP_OK) return es;
-    {
-        StageTimer _t(ctx, ERP_STAGE_BEARINGS, st);
-        ERP_CK(erp::launch_bearings_from_matches(matches, (int32_t*)ctx->counts.p, b->kp_l, b->kp_r,
-                                                 b->off_l, b->off_r, b->width, b->height, sh,
-                                                 (double*)ctx->pts.p, out->key_left, out->key_right,
-                                                 st));
-    }
     return run_estimator(ctx, sh, cfg, out, out->results, st);
 }
 
@@ -888,6 +913,8 @@ std::vector<uint8_t> graph_key(const erp_ctx* c, const erp_pair_batch* b, float 
     key_put(k, c->refine_hint);
     key_put(k, c->flat_refs);
     key_put(k, c->fuse_sampler);
+    const char* sb_env = getenv("ERP_SMALL_BATCH");  // (run_consensus's route)
+    key_put(k, sb_env ? atoi(sb_env) : -1);
     const DevBuf* all[] = {&c->mblk, &c->zsel, &c->part, &c->part1, &c->pu, &c->ccount, &c->cand,
                            &c->bsel, &c->edges, &c->gfin, &c->matches, &c->counts, &c->flags,
                            &c->pts, &c->polyR, &c->polyQ, &c->idx, &c->gram, &c->hyps, &c->rv,

@@ -15,6 +15,19 @@ constexpr int kPolyWords = 31;    // glibc TYPE_3 degree
 constexpr int kCandSlots = 28;    // matcher: tiles with candidate rows kept per (query, train
                                   // chunk, lane half) (more: exact sweep of the chunk)
 
+// the batch pipeline's gather + bearings (bearings_from_matches_kernel's work), done by
+// knn2_merge_kernel as it places each match (src/spherical_surf.cpp:155-162 +
+// src/eight_point.cpp:163-186): pts[p][max_nq + 1][6] (the last row the zero pad of the Gram
+// batches), optional valid_key_left / right
+struct BearingOut {
+    const erp_point2f* kp_l;
+    const erp_point2f* kp_r;
+    const int32_t* width;
+    const int32_t* height;
+    double* pts;
+    erp_point2f* key_l;
+    erp_point2f* key_r;
+};
 struct Top2 {                     // partial k=2 result of one train chunk for one query
     float d0;                     // best squared distance
     int32_t j0;                   // its train index (lowest index among ties)
@@ -64,11 +77,13 @@ void init_constants();            // reduction table for the jump polynomials (o
 // knn2_split_bytes(sh) (bf16 rows, norms, per-pair max norm); cand = knn2_cand_bytes(sh).
 size_t knn2_split_bytes(const BatchShape& sh);
 size_t knn2_cand_bytes(const BatchShape& sh);
+// (ovf: the rescore's overflow scratch below; its counter ovf[0] is zeroed here)
 hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
                               const int64_t* off_t, const BatchShape& sh, void* split,
-                              float2* pu, int32_t* ccount, void* cand, hipStream_t st);
+                              float2* pu, int32_t* ccount, void* cand, hipStream_t st,
+                              int32_t* ovf);
 // ovf = scratch of 4 + 12 * n_pairs * max_nq * fchunks bytes: overflowed (pair, query, chunk)
-// for the exact sweep
+// for the exact sweep (counter zeroed by the launch_knn2_filter before it)
 hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,
                                const int64_t* off_t, const BatchShape& sh, void* split,
                                const float2* pu, const int32_t* ccount, void* cand, Top2* part,
@@ -88,7 +103,8 @@ size_t knn2_merge_scratch_bytes(const BatchShape& sh);
 hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
                              const BatchShape& sh, int chunk_len, int chunks, float ratio,
                              erp_dmatch* matches, int32_t* counts, int32_t* flags,
-                             int32_t* bcount, hipStream_t st);
+                             int32_t* bcount, hipStream_t st,
+                             const BearingOut* bo = nullptr);
 hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t* counts,
                                         const erp_point2f* kp_l, const erp_point2f* kp_r,
                                         const int64_t* off_l, const int64_t* off_r,
@@ -157,7 +173,8 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
 size_t hyp_lite_bytes(const BatchShape& sh);
 hipError_t launch_valid_place(const int32_t* counts, const float* hl, const int32_t* wsum,
                               const BatchShape& sh, double sample_frac, float* rv, float* tv,
-                              int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st);
+                              int32_t* kcount, float* rv_aos, float* dscale, float* edges,
+                              hipStream_t st);
 // (want_e = false: estimate_kernel leaves the records' E unwritten -- the batch pipeline when the
 // caller did not ask for the hypothesis records; nothing downstream reads E)
 // the opt-in inlier count (cfg.inlier_thr > 0): every iteration's matches with
@@ -191,7 +208,8 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
                                    int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
                                    void* lipref, int lipg, float gfac, int flat_pct,
-                                   int use_hint, hipStream_t st);
+                                   int use_hint, hipStream_t st,
+                                   bool edges_ready = false);
 size_t lipref_bytes(int n_pairs, int stride);
 // survivors = rows with LB <= min UB (again = 1: only pairs the refine pass touched)
 hipError_t launch_consensus_select(const int32_t* kcount, const double* lb, const double* ub,

@@ -135,43 +135,53 @@ __device__ __forceinline__ void pmul_wave(const uint32_t* a, const uint32_t* b, 
     if (lane < 31) out[lane] = r;
 }
 
+// x^(2^j) mod P, j < kPow2: the host builds it once (init_constants)
+constexpr int kPow2 = 48;  // bits of M - 1 (< 2^16) + 6 + kMaxQ (24) fit
+__constant__ uint32_t c_pow2[kPow2][31];
+
 // glibc jump-ahead polynomials of one pair (one block of 16 waves):
 //   R_l = x^(l(M-1)) mod P (l = 0..64) and Q_k = x^(64(M-1) 2^k) (k < nq_needed).
-// R_1 by left-to-right square-and-shift (multiplying by x is a shift plus one fold), R_2..R_64
-// in six doubling levels (R_{h+j} = R_h R_j, the level's products spread over the waves),
-// the Q_k by repeated squaring: ~26 dependent products instead of ~95.
+// R_1 and every Q_k are products of table powers: x^((M-1) 2^sh) = prod over the set bits b of
+// M-1 of x^(2^(b + sh)) (sh = 0 for R_1, 6 + k for Q_k), each on a wave of its own, all at once;
+// then R_2..R_64 in six doubling levels (R_{h+j} = R_h R_j, the level's products spread over
+// the waves).  popcount(M-1) - 1 + 6 dependent products (11 at M = 2700) instead of the ~26
+// of square-and-shift plus repeated squaring (single-pair latency: 28 -> ~12 us).
 __global__ __launch_bounds__(1024) void jump_prep_kernel(const int32_t* __restrict__ counts,
                                                          double sample_frac, int nq_needed,
                                                          uint32_t* __restrict__ polyR,
                                                          uint32_t* __restrict__ polyQ) {
     __shared__ uint32_t Rl[65][32];
-    __shared__ uint32_t tq[2][32];
+    __shared__ uint32_t tq[16][2][32];
+    __shared__ uint32_t fac[16][16][32];  // each wave's table factors, staged once
     const int p = blockIdx.x, lane = wave_lane(), wid = threadIdx.x >> 6;
     const int M = counts[p];
     if ((int)(M * sample_frac) < 1 || M < 2) return;
     uint32_t cred[30];
 #pragma unroll
     for (int d = 0; d < 30; d++) cred[d] = lane < 31 ? c_red[d][lane] : 0u;
-    // R_1 (wave 0)
-    if (wid == 0) {
-        const uint32_t e = (uint32_t)(M - 1);
-        const int top = 31 - __builtin_clz(e);
-        int cur = 0;  // result lives in tq[cur]
-        if (lane < 31) tq[0][lane] = lane == 1 ? 1u : 0u;  // x^1 (top bit)
-        for (int bit = top - 1; bit >= 0; bit--) {
-            pmul_wave(tq[cur], tq[cur], tq[cur ^ 1], cred);
+    const uint32_t e = (uint32_t)(M - 1);  // >= 1
+    uint32_t* Q = polyQ + (size_t)p * kMaxQ * 31;
+    // products: item 0 = R_1 (shift 0), item 1 + k = Q_k (shift 6 + k)
+    for (int item = wid; item <= nq_needed; item += 16) {
+        const int sh = item == 0 ? 0 : 6 + (item - 1);
+        // the factors x^(2^(b + sh)) into LDS, all loads in flight at once (pmul_wave reads its
+        // second operand per lane: from constant memory that is a dependent load per term)
+        int nf = 0;
+        for (uint32_t rest = e; rest; rest &= rest - 1u, nf++)  // (uniform)
+            if (lane < 31) fac[wid][nf][lane] = c_pow2[__builtin_ctz(rest) + sh][lane];
+        int cur = 0;
+        if (lane < 31) tq[wid][0][lane] = fac[wid][0][lane];
+        for (int f = 1; f < nf; f++) {
+            pmul_wave(tq[wid][cur], fac[wid][f], tq[wid][cur ^ 1], cred);
             cur ^= 1;
-            if ((e >> bit) & 1u) {
-                const uint32_t hi = tq[cur][30];
-                const uint32_t v = lane == 0 ? 0u : tq[cur][lane - 1 < 0 ? 0 : lane - 1];
-                const uint32_t add = (lane == 0 || lane == 28) ? hi : 0u;
-                if (lane < 31) tq[cur ^ 1][lane] = v + add;
-                cur ^= 1;
-            }
         }
         if (lane < 31) {
-            Rl[0][lane] = lane == 0 ? 1u : 0u;
-            Rl[1][lane] = tq[cur][lane];
+            if (item == 0) {
+                Rl[0][lane] = lane == 0 ? 1u : 0u;
+                Rl[1][lane] = tq[wid][cur][lane];
+            } else {
+                Q[(item - 1) * 31 + lane] = tq[wid][cur][lane];
+            }
         }
     }
     __syncthreads();
@@ -181,18 +191,6 @@ __global__ __launch_bounds__(1024) void jump_prep_kernel(const int32_t* __restri
     }
     uint32_t* R = polyR + (size_t)p * 65 * 31;
     for (int t = threadIdx.x; t < 65 * 31; t += 1024) R[t] = Rl[t / 31][t % 31];
-    if (wid == 0) {
-        uint32_t* Q = polyQ + (size_t)p * kMaxQ * 31;
-        if (lane < 31) tq[0][lane] = Rl[64][lane];
-        int cur = 0;
-        for (int k = 0; k < nq_needed; k++) {
-            if (k > 0) {
-                pmul_wave(tq[cur], tq[cur], tq[cur ^ 1], cred);
-                cur ^= 1;
-            }
-            if (lane < 31) Q[k * 31 + lane] = tq[cur][lane];
-        }
-    }
 }
 
 // window (31 words in win[]) -> apply polynomial c: win <- x^d window.  ext: 61 words scratch.
@@ -1486,6 +1484,41 @@ __global__ __launch_bounds__(64) void eigen_fallback_kernel(const int32_t* __res
     for (int k = 0; k < 9; k++) eo[(size_t)k * iters] = e[k];
 }
 
+// the fused pipeline's leftovers in ONE launch (single-pair latency: one dispatch fewer): pairs
+// with s < 9 take eigen_kernel<true>'s thin path, the others eigen_fallback_kernel's (only the
+// lanes the Gram kernel's inverse iteration left NaN)
+__global__ __launch_bounds__(64) void eigen_rest_kernel(const int32_t* __restrict__ counts,
+                                                        const double* __restrict__ gram, int iters,
+                                                        double sample_frac,
+                                                        double* __restrict__ evec,
+                                                        erp_hypothesis* __restrict__ hyps,
+                                                        double valid_abs) {
+    const int p = blockIdx.y;
+    const int h = blockIdx.x * 64 + threadIdx.x;
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || h >= iters) return;
+    double* eo = evec + (size_t)p * 9 * iters + h;
+    const double* gi = gram + (size_t)p * 36 * iters + h;
+    double e[9];
+    if (s < 9) {
+        double g36[36], G[81];
+#pragma unroll
+        for (int k = 0; k < 36; k++) g36[k] = gi[(size_t)k * iters];
+        gram36_to_full(g36, G);
+        gram_jacobi9(G, s, e);
+    } else {
+        if (!__builtin_isnan(eo[0])) return;
+        gram_min_eigvec9_jacobi(gi, iters, 0, e);
+    }
+    if (hyps) {
+        estimate_store(e, valid_abs, hyps + (size_t)p * iters + h);
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 9; k++) eo[(size_t)k * iters] = e[k];
+}
+
 #ifdef ERP_EST_WAVES
 #define ERP_EST_ATTR __attribute__((amdgpu_waves_per_eu(ERP_EST_WAVES)))
 #else
@@ -1515,9 +1548,15 @@ __global__ __launch_bounds__(64) ERP_EST_ATTR void estimate_kernel(const int32_t
 // each 64-iteration wave writes its valid-rotation count and their bounding box to
 // wsum[p][wave][8] -- what valid_place_kernel needs to place R1-then-R2 in iteration order
 // (src/eight_point.cpp:117-126) without re-reading the iterations twice.
+// REST (batches with fewer waves than the chip has SIMDs, e.g. one pair): eigen_rest_kernel's
+// work -- the thin path of s < 9 pairs, the Jacobi fallback of lanes the Gram kernel left NaN --
+// in this launch too (one dependent launch fewer; the wider register budget costs nothing when
+// the chip is mostly idle)
+template <bool REST>
 __global__ __launch_bounds__(64) ERP_EST_ATTR void estimate_lite_kernel(
     const int32_t* __restrict__ counts, const double* __restrict__ evec, int iters,
-    double sample_frac, double valid_abs, float* __restrict__ hl, int32_t* __restrict__ wsum) {
+    double sample_frac, double valid_abs, float* __restrict__ hl, int32_t* __restrict__ wsum,
+    const double* __restrict__ gram) {
     const int p = blockIdx.y, w = blockIdx.x, lane = threadIdx.x;
     const int h = w * 64 + lane;
     const int M = counts[p];
@@ -1530,6 +1569,18 @@ __global__ __launch_bounds__(64) ERP_EST_ATTR void estimate_lite_kernel(
         double e[9];
 #pragma unroll
         for (int k = 0; k < 9; k++) e[k] = ei[(size_t)k * iters];
+        if (REST) {
+            const double* gi = gram + (size_t)p * 36 * iters + h;
+            if (s < 9) {
+                double g36[36], G[81];
+#pragma unroll
+                for (int k = 0; k < 36; k++) g36[k] = gi[(size_t)k * iters];
+                gram36_to_full(g36, G);
+                gram_jacobi9(G, s, e);
+            } else if (__builtin_isnan(e[0])) {
+                gram_min_eigvec9_jacobi(gi, iters, 0, e);
+            }
+        }
         estimate_from_e(e, valid_abs, hy);
         float* o = hl + (size_t)p * 9 * iters + h;
         const float qnan = __builtin_nanf("");
@@ -1698,80 +1749,6 @@ __global__ __launch_bounds__(1024) void valid_scatter_kernel(const int32_t* __re
             X[k * stride + pos] = R[k];
             T[3 * pos + k] = hy.T[k];
             if (A) A[3 * pos + k] = R[k];
-        }
-        pos++;
-    }
-}
-
-// valid_count + valid_scatter for the lite estimates: a block per (chunk of 1024 iterations,
-// pair) adds the valid counts of the 64-iteration waves before its chunk (wsum, <= ~160 values),
-// block-scans its chunk and writes the valid rotations in push order (iteration, R1, R2);
-// chunk 0 also writes K and the bounding-box scale (the same min / max values valid_count
-// reduces, so dscale is bit-identical to the record path's)
-__global__ __launch_bounds__(1024) void valid_place_kernel(
-    const int32_t* __restrict__ counts, const float* __restrict__ hl, int iters,
-    double sample_frac, const int32_t* __restrict__ wsum, int nwaves, float* __restrict__ rv,
-    float* __restrict__ tv, int32_t* __restrict__ kcount, float* __restrict__ rv_aos,
-    float* __restrict__ dscale) {
-    __shared__ int ws[16];
-    __shared__ int sbase[16];
-    const int p = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
-    const int M = counts[p];
-    if ((int)(M * sample_frac) < 1) {
-        if (c == 0 && tid == 0) kcount[p] = 0;
-        return;
-    }
-    const int32_t* vw = wsum + (size_t)p * nwaves * 8;
-    const int upto = c == 0 ? nwaves : min(16 * c, nwaves);  // waves before this chunk (all for 0)
-    int part = 0;
-    for (int q = tid; q < upto; q += 1024) part += vw[q * 8];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-    if (lane == 0) sbase[tid >> 6] = part;
-    __syncthreads();
-    int base = 0;
-    for (int w = 0; w < 16; w++) base += sbase[w];
-    if (c == 0) {
-        if (tid == 0) {
-            kcount[p] = base;
-            double d2 = 0;
-            for (int k = 0; k < 3; k++) {
-                float a = kInf, b = -kInf;
-                for (int q = 0; q < nwaves; q++) {
-                    a = fminf(a, __int_as_float(vw[q * 8 + 1 + k]));
-                    b = fmaxf(b, __int_as_float(vw[q * 8 + 4 + k]));
-                }
-                const double e = base > 0 ? (double)b - (double)a : 0.0;
-                d2 += e * e;
-            }
-            dscale[p] = (float)(sqrt(d2) * (1.0 + 1e-6));
-        }
-        base = 0;
-    }
-    const int h = c * 1024 + tid;
-    float r[9];
-    bool v1 = false, v2 = false;
-    if (h < iters) {
-        const float* x = hl + (size_t)p * 9 * iters + h;
-#pragma unroll
-        for (int k = 0; k < 9; k++) r[k] = x[(size_t)k * iters];
-        v1 = !__builtin_isnan(r[0]);
-        v2 = !__builtin_isnan(r[3]);
-    }
-    int total;
-    int pos = base + block_exclusive_scan<1024>((int)v1 + (int)v2, ws, &total);
-    const int stride = 2 * iters;
-    float* X = rv + (size_t)p * 3 * stride;
-    float* T = tv + (size_t)p * 3 * stride;
-    float* A = rv_aos ? rv_aos + (size_t)p * 3 * stride : nullptr;
-#pragma unroll
-    for (int which = 0; which < 2; which++) {
-        if (!(which ? v2 : v1)) continue;
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            X[k * stride + pos] = r[3 * which + k];
-            T[3 * pos + k] = r[6 + k];
-            if (A) A[3 * pos + k] = r[3 * which + k];
         }
         pos++;
     }
@@ -2236,6 +2213,116 @@ __global__ __launch_bounds__(256) void consensus_edges_kernel(const float* __res
     for (int b = threadIdx.x; b < kNB; b += 256) {
         ed[b] = bin_lower_d(elo, b);
         ed[kNB + b] = bin_upper_d(elo, b);
+    }
+}
+
+// valid_count + valid_scatter for the lite estimates: a block per (chunk of 1024 iterations,
+// pair) adds the valid counts of the 64-iteration waves before its chunk (wsum, <= ~160 values),
+// block-scans its chunk and writes the valid rotations in push order (iteration, R1, R2);
+// chunk 0 also writes K and the bounding-box scale (the same min / max values valid_count
+// reduces, so dscale is bit-identical to the record path's)
+__global__ __launch_bounds__(1024) void valid_place_kernel(
+    const int32_t* __restrict__ counts, const float* __restrict__ hl, int iters,
+    double sample_frac, const int32_t* __restrict__ wsum, int nwaves, float* __restrict__ rv,
+    float* __restrict__ tv, int32_t* __restrict__ kcount, float* __restrict__ rv_aos,
+    float* __restrict__ dscale, float* __restrict__ edges) {
+    __shared__ int ws[16];
+    __shared__ int sbase[16];
+    __shared__ float ds_s;
+    const int p = blockIdx.y, c = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    const int M = counts[p];
+    if ((int)(M * sample_frac) < 1) {
+        if (c == 0 && tid == 0) kcount[p] = 0;
+        return;
+    }
+    const int32_t* vw = wsum + (size_t)p * nwaves * 8;
+    const int upto = c == 0 ? nwaves : min(16 * c, nwaves);  // waves before this chunk (all for 0)
+    int part = 0;
+    for (int q = tid; q < upto; q += 1024) part += vw[q * 8];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (lane == 0) sbase[tid >> 6] = part;
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < 16; w++) base += sbase[w];
+    if (c == 0) {
+        // the bounding box over every wave's: six block-wide min / max reductions (one serial
+        // thread walking ~160 waves' boxes cost ~25 us of a single pair's latency)
+        __shared__ float box[6][16];
+        float mn[3] = {kInf, kInf, kInf}, mx[3] = {-kInf, -kInf, -kInf};
+        for (int q = tid; q < nwaves; q += 1024) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                mn[k] = fminf(mn[k], __int_as_float(vw[q * 8 + 1 + k]));
+                mx[k] = fmaxf(mx[k], __int_as_float(vw[q * 8 + 4 + k]));
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                mn[k] = fminf(mn[k], __shfl_xor(mn[k], o, 64));
+                mx[k] = fmaxf(mx[k], __shfl_xor(mx[k], o, 64));
+            }
+        if (lane == 0)
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                box[k][tid >> 6] = mn[k];
+                box[3 + k][tid >> 6] = mx[k];
+            }
+        __syncthreads();
+        if (tid == 0) {
+            kcount[p] = base;
+            double d2 = 0;
+            for (int k = 0; k < 3; k++) {
+                float a = kInf, b = -kInf;
+                for (int w = 0; w < 16; w++) {
+                    a = fminf(a, box[k][w]);
+                    b = fmaxf(b, box[3 + k][w]);
+                }
+                const double e = base > 0 ? (double)b - (double)a : 0.0;
+                d2 += e * e;
+            }
+            dscale[p] = (float)(sqrt(d2) * (1.0 + 1e-6));
+            ds_s = dscale[p];
+        }
+        if (edges) {  // consensus_edges_kernel's table (one launch fewer)
+            __syncthreads();
+            const int elo = bounds_elo(ds_s);
+            float* ed = edges + (size_t)p * 2 * kNB;
+            for (int b = tid; b < kNB; b += 1024) {
+                ed[b] = bin_lower_d(elo, b);
+                ed[kNB + b] = bin_upper_d(elo, b);
+            }
+        }
+        base = 0;
+    }
+    const int h = c * 1024 + tid;
+    float r[9];
+    bool v1 = false, v2 = false;
+    if (h < iters) {
+        const float* x = hl + (size_t)p * 9 * iters + h;
+#pragma unroll
+        for (int k = 0; k < 9; k++) r[k] = x[(size_t)k * iters];
+        v1 = !__builtin_isnan(r[0]);
+        v2 = !__builtin_isnan(r[3]);
+    }
+    int total;
+    int pos = base + block_exclusive_scan<1024>((int)v1 + (int)v2, ws, &total);
+    const int stride = 2 * iters;
+    float* X = rv + (size_t)p * 3 * stride;
+    float* T = tv + (size_t)p * 3 * stride;
+    float* A = rv_aos ? rv_aos + (size_t)p * 3 * stride : nullptr;
+#pragma unroll
+    for (int which = 0; which < 2; which++) {
+        if (!(which ? v2 : v1)) continue;
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            X[k * stride + pos] = r[3 * which + k];
+            T[3 * pos + k] = r[6 + k];
+            if (A) A[3 * pos + k] = r[3 * which + k];
+        }
+        pos++;
     }
 }
 
@@ -4116,10 +4203,17 @@ __global__ __launch_bounds__(256) void consensus_rows_kernel(
     const int32_t* __restrict__ surv, const int32_t* __restrict__ nsurv,
     const int32_t* __restrict__ bsel, double* __restrict__ tmean, const int32_t* __restrict__ uoff,
     int n_pairs) {
-    const int total = uoff[n_pairs];  // one unit per survivor
+    // one unit per survivor; uoff == nullptr (batches of <= 16 pairs): the pairs' survivor
+    // counts are walked here instead of a list_prefix_kernel launch
+    int total = 0;
+    if (uoff) total = uoff[n_pairs];
+    else
+        for (int q = 0; q < n_pairs; q++) total += nsurv[q];
     for (int g = blockIdx.x; g < total; g += gridDim.x) {
-        int p, u;
-        pair_of_item(uoff, n_pairs, g, &p, &u);
+        int p = 0, u = g;
+        if (uoff) pair_of_item(uoff, n_pairs, g, &p, &u);
+        else
+            while (u >= nsurv[p]) u -= nsurv[p++];
         __syncthreads();  // the previous row's LDS readers are done
         consensus_rows_block(kcount, rv, dscale, stride, trim_lo, trim_hi, surv, nsurv, bsel,
                              tmean, p, u);
@@ -4284,7 +4378,7 @@ __global__ __launch_bounds__(1024) void consensus_final_kernel(
     r.min_idx = -1;
     r.near_ties = 0;
     r.survivors = nsurv[p];
-    r.binned_rows = nbin[p] < 0 ? K : (K + kLipStep - 1) / kLipStep + nbin[p];
+    r.binned_rows = !nbin || nbin[p] < 0 ? K : (K + kLipStep - 1) / kLipStep + nbin[p];
     r.min_dist = 0.0;
     const int fl = flags ? flags[p] : 0;
     if (fl & 1) r.status = ERP_TOO_FEW_POINTS;
@@ -4469,6 +4563,20 @@ void init_constants() {
         for (int k = 0; k < 31; k++) v[k] = nv[k];
     }
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_red), red, sizeof(red));
+    // x^(2^j) mod P by repeated squaring (x^d = x^(d-3) + x^(d-31) folds the product's top)
+    uint32_t pw[kPow2][31] = {};
+    pw[0][1] = 1;
+    for (int j = 1; j < kPow2; j++) {
+        uint32_t c[61] = {};
+        for (int a = 0; a < 31; a++)
+            for (int b = 0; b < 31; b++) c[a + b] += pw[j - 1][a] * pw[j - 1][b];
+        for (int d = 60; d >= 31; d--) {
+            c[d - 3] += c[d];
+            c[d - 31] += c[d];
+        }
+        for (int k = 0; k < 31; k++) pw[j][k] = c[k];
+    }
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pow2), pw, sizeof(pw));
 }
 
 
@@ -4692,20 +4800,30 @@ hipError_t launch_eigen(const int32_t* counts, const double* gram, const BatchSh
                         double sample_frac, double valid_abs, double* evec, erp_hypothesis* hyps,
                         hipStream_t st, int fused, bool want_e, float* hl, int32_t* wsum) {
     dim3 grid((sh.iters + 63) / 64, sh.n_pairs);
+    // small batches with lite estimates: the leftovers inside the estimate launch
+    const bool rest_inline = fused == 1 && hl && (size_t)grid.x * grid.y <= 1024;
     // fused >= 1: gram_mfma_kernel ran the inverse iteration (s >= 9) already; fused == 2: and
     // the estimate of its settled lanes, the fallback / thin kernels estimate their own lanes
     erp_hypothesis* own = fused == 2 ? hyps : nullptr;
-    if (!fused)
+    if (!fused) {
         ERP_LAUNCH(eigen_kernel<false>, grid, dim3(64), 0, st, counts, gram, sh.iters,
                            sample_frac, evec, nullptr, valid_abs);
-    ERP_LAUNCH(eigen_fallback_kernel, grid, dim3(64), 0, st, counts, gram, sh.iters,
-                       sample_frac, evec, own, valid_abs);
-    // (M is only known on the device: the thin instantiation returns at once for s >= 9)
-    ERP_LAUNCH(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters,
-                       sample_frac, evec, own, valid_abs);
-    if (fused != 2 && hl)
-        ERP_LAUNCH(estimate_lite_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
-                           sample_frac, valid_abs, hl, wsum);
+        ERP_LAUNCH(eigen_fallback_kernel, grid, dim3(64), 0, st, counts, gram, sh.iters,
+                           sample_frac, evec, own, valid_abs);
+        // (M is only known on the device: the thin instantiation returns at once for s >= 9)
+        ERP_LAUNCH(eigen_kernel<true>, grid, dim3(64), 0, st, counts, gram, sh.iters,
+                           sample_frac, evec, own, valid_abs);
+    } else if (!rest_inline) {  // the Gram kernel ran the common inverse iteration: fallback
+        // + thin in one launch
+        ERP_LAUNCH(eigen_rest_kernel, grid, dim3(64), 0, st, counts, gram, sh.iters,
+                           sample_frac, evec, own, valid_abs);
+    }
+    if (fused != 2 && hl && rest_inline)
+        ERP_LAUNCH(estimate_lite_kernel<true>, grid, dim3(64), 0, st, counts, evec, sh.iters,
+                           sample_frac, valid_abs, hl, wsum, gram);
+    else if (fused != 2 && hl)
+        ERP_LAUNCH(estimate_lite_kernel<false>, grid, dim3(64), 0, st, counts, evec, sh.iters,
+                           sample_frac, valid_abs, hl, wsum, gram);
     else if (fused != 2)
         ERP_LAUNCH(estimate_kernel, grid, dim3(64), 0, st, counts, evec, sh.iters,
                            sample_frac, valid_abs, hyps, (int)want_e);
@@ -4719,10 +4837,12 @@ size_t hyp_lite_bytes(const BatchShape& sh) {
 
 hipError_t launch_valid_place(const int32_t* counts, const float* hl, const int32_t* wsum,
                               const BatchShape& sh, double sample_frac, float* rv, float* tv,
-                              int32_t* kcount, float* rv_aos, float* dscale, hipStream_t st) {
+                              int32_t* kcount, float* rv_aos, float* dscale, float* edges,
+                              hipStream_t st) {
     dim3 grid((sh.iters + 1023) / 1024, sh.n_pairs);
     ERP_LAUNCH(valid_place_kernel, grid, dim3(1024), 0, st, counts, hl, sh.iters,
-                       sample_frac, wsum, (sh.iters + 63) / 64, rv, tv, kcount, rv_aos, dscale);
+                       sample_frac, wsum, (sh.iters + 63) / 64, rv, tv, kcount, rv_aos, dscale,
+                       edges);
     return hipGetLastError();
 }
 
@@ -4872,8 +4992,9 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
                                    int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
                                    void* lipref, int lipg, float gfac, int flat_pct,
-                                   int use_hint, hipStream_t st) {
-    ERP_LAUNCH(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
+                                   int use_hint, hipStream_t st, bool edges_ready) {
+    if (!edges_ready)
+        ERP_LAUNCH(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     const int stride = 2 * sh.iters;
     if (!rlist) {  // every row of the shard (rcount = -1: no pre-pruning)
         if (rcount) {
@@ -5089,8 +5210,11 @@ hipError_t launch_consensus_rows(const int32_t* kcount, const float* rv, const f
                                  const int32_t* surv, const int32_t* nsurv, const int32_t* bsel,
                                  double* tmean, hipStream_t st) {
     int32_t* uoff = const_cast<int32_t*>(nsurv) + 2 * sh.n_pairs;  // as in launch_consensus_refine
-    ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, sh.n_pairs, 1, 0,
-                       uoff);
+    if (sh.n_pairs <= 16)
+        uoff = nullptr;  // (consensus_rows_kernel walks the counts itself: one launch fewer)
+    else
+        ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, nsurv, sh.n_pairs, 1, 0,
+                           uoff);
     ERP_LAUNCH(consensus_rows_kernel, dim3(2048), dim3(256), 0, st, kcount, rv, dscale,
                        2 * sh.iters, trim_lo, trim_hi, surv, nsurv, bsel, tmean,
                        (const int32_t*)uoff, sh.n_pairs);

@@ -20,6 +20,7 @@
 
 #include <type_traits>
 
+#include "erp_device.hpp"
 #include "erp_kernels.hpp"
 #include "erp_launch.hpp"
 
@@ -153,8 +154,12 @@ __global__ __launch_bounds__(256) void knn2_split_kernel(const float* __restrict
                                                          const int64_t* __restrict__ off_t,
                                                          int max_nt, bf16x8* __restrict__ thi,
                                                          float* __restrict__ tn,
-                                                         uint32_t* __restrict__ tmax) {
+                                                         uint32_t* __restrict__ tmax,
+                                                         int32_t* __restrict__ ovf) {
     const int p = blockIdx.y, tid = threadIdx.x;
+    // the rescore's overflow-list counter starts at zero (knn2_rescore runs after this kernel;
+    // one launch fewer than a separate reset: single-pair latency)
+    if (ovf && blockIdx.x == 0 && p == 0 && tid == 0) ovf[0] = 0;
     const int j = blockIdx.x * 64 + (tid >> 2), part = tid & 3;
     const int64_t tbase = off_t[p];
     const int nt = (int)(off_t[p + 1] - tbase);
@@ -956,10 +961,14 @@ __global__ __launch_bounds__(kMergeBlock) void knn2_merge_kernel(
     const Top2* __restrict__ part, const int64_t* __restrict__ off_q,
     const int64_t* __restrict__ off_t, int chunk_len, int chunks, int max_nq, float ratio,
     const int32_t* __restrict__ bcount, erp_dmatch* __restrict__ out,
-    int32_t* __restrict__ counts, int32_t* __restrict__ flags) {
+    int32_t* __restrict__ counts, int32_t* __restrict__ flags, BearingOut bo) {
     __shared__ int ws[16];
     __shared__ int base_s;
     const int p = blockIdx.y, b = blockIdx.x, nb = gridDim.x;
+    if (bo.pts && b == 0 && threadIdx.x == 0) {  // zero sentinel row (pads the Gram batches)
+        double* z = bo.pts + ((size_t)p * (max_nq + 1) + max_nq) * 6;
+        for (int k = 0; k < 6; k++) z[k] = 0.0;
+    }
     const int nq = (int)(off_q[p + 1] - off_q[p]);
     const int nt = (int)(off_t[p + 1] - off_t[p]);
     if (nt < 2 || nq <= 0) {
@@ -996,10 +1005,20 @@ __global__ __launch_bounds__(kMergeBlock) void knn2_merge_kernel(
     const bool keep = merge_one(part + (size_t)p * chunks * max_nq, max_nq, nch, q, nq, ratio, J, d0);
     int total;
     const int pos = block_exclusive_scan<kMergeBlock>(keep ? 1 : 0, ws, &total);  // syncs base_s
-    if (keep) out[(size_t)p * max_nq + base_s + pos] = erp_dmatch{q, J, 0, d0};
+    if (!keep) return;
+    const int m = base_s + pos;
+    out[(size_t)p * max_nq + m] = erp_dmatch{q, J, 0, d0};
+    if (bo.pts) {
+        const erp_point2f kl = bo.kp_l[off_q[p] + q];
+        const erp_point2f kr = bo.kp_r[off_t[p] + J];
+        double* o = bo.pts + ((size_t)p * (max_nq + 1) + m) * 6;
+        pixel_to_bearing(bo.width[p], bo.height[p], kl.x, kl.y, o);
+        pixel_to_bearing(bo.width[p], bo.height[p], kr.x, kr.y, o + 3);
+        if (bo.key_l) bo.key_l[(size_t)p * max_nq + m] = kl;
+        if (bo.key_r) bo.key_r[(size_t)p * max_nq + m] = kr;
+    }
 }
 
-__global__ void set_i32_kernel(int32_t* p, int32_t v) { *p = v; }
 
 }  // namespace
 
@@ -1037,7 +1056,8 @@ static char* split_sentinel(const BatchShape& sh, void* split) {
 
 hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
                               const int64_t* off_t, const BatchShape& sh, void* split,
-                              float2* pu, int32_t* ccount, void* cand, hipStream_t st) {
+                              float2* pu, int32_t* ccount, void* cand, hipStream_t st,
+                              int32_t* ovf) {
     bf16x8* thi = (bf16x8*)split;
     float* tn = (float*)(thi + (size_t)sh.n_pairs * sh.max_nt * 8);
     uint32_t* tmax = split_tmax(sh, split);
@@ -1047,7 +1067,7 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
     if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(sent + 128), 0x7f800000u, 1, st);
     if (e != hipSuccess) return e;
     ERP_LAUNCH(knn2_split_kernel, dim3((sh.max_nt + 63) / 64, sh.n_pairs), dim3(256), 0,
-                       st, desc_t, off_t, sh.max_nt, thi, tn, tmax);
+                       st, desc_t, off_t, sh.max_nt, thi, tn, tmax, ovf);
     int32_t* ctile;
     bf16x8* cval;
     cand_split(sh, cand, &ctile, &cval);
@@ -1067,7 +1087,7 @@ hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const i
     int32_t* ctile;
     bf16x8* cval;
     cand_split(sh, cand, &ctile, &cval);
-    ERP_LAUNCH(set_i32_kernel, dim3(1), dim3(1), 0, st, ovf, 0);
+    // (ovf[0] was zeroed by knn2_split_kernel, launch_knn2_filter)
     const int qblocks = (sh.max_nq + 255) / 256;
     ERP_LAUNCH(knn2_rescore_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
                        st, desc_q, desc_t, off_q, off_t, sh.max_nq, sh.fchunk_len, sh.fchunks,
@@ -1103,13 +1123,14 @@ size_t knn2_merge_scratch_bytes(const BatchShape& sh) {
 hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64_t* off_t,
                              const BatchShape& sh, int chunk_len, int chunks, float ratio,
                              erp_dmatch* matches, int32_t* counts, int32_t* flags,
-                             int32_t* bcount, hipStream_t st) {
+                             int32_t* bcount, hipStream_t st, const BearingOut* bo) {
     const dim3 grid(std::max(1, (sh.max_nq + kMergeBlock - 1) / kMergeBlock), sh.n_pairs);
+    const BearingOut none{};
     ERP_LAUNCH(knn2_merge_count_kernel, grid, dim3(kMergeBlock), 0, st, part, off_q, off_t,
                        chunk_len, chunks, sh.max_nq, ratio, bcount);
     ERP_LAUNCH(knn2_merge_kernel, grid, dim3(kMergeBlock), 0, st, part, off_q, off_t,
                        chunk_len, chunks, sh.max_nq, ratio, (const int32_t*)bcount, matches, counts,
-                       flags);
+                       flags, bo ? *bo : none);
     return hipGetLastError();
 }
 

@@ -104,3 +104,26 @@ def test_lite_estimates_equal_records(overlap_setup):
     rec = {k: v.cpu().numpy() for k, v in rec.items()}
     for k in ("results", "rvec", "tvec"):
         assert np.array_equal(lite[k].view(np.uint8), rec[k].view(np.uint8)), k
+
+
+def test_small_batch_route_equals_pruning_route(overlap_setup, monkeypatch):
+    """a batch of <= ERP_SMALL_BATCH pairs bins every row (no pre-pruning: the single-pair
+    latency route); the same pairs through the pruning route give every result field equal
+    (only the work counts binned_rows / survivors may differ)"""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
+    pairs, _ = overlap_setup
+    b = bench.to_device(pairs[:6], "cuda")
+    args = (b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"], b["off_r"], b["width"],
+            b["height"], b["max_nq"], b["max_nt"])
+    res = {}
+    for route, limit in (("all_rows", "8"), ("prune", "0")):
+        monkeypatch.setenv("ERP_SMALL_BATCH", limit)
+        out = PairBatchRunner(ctx=Context(0), iters=ITERS).run(*args)
+        torch.cuda.synchronize()
+        res[route] = results_to_numpy(out["results"])
+    a, c = res["all_rows"], res["prune"]
+    for f in a.dtype.names:
+        if f not in ("binned_rows", "survivors"):
+            assert np.array_equal(a[f], c[f]), f
+    assert np.all(a["binned_rows"] == a["K"]) and np.all(c["binned_rows"] < c["K"])

@@ -283,6 +283,15 @@ def test_eight_point_estimation_api(ctx, oracle):
 
 
 # ---------------------------------------------------------------------- batch pipeline
+@pytest.fixture(params=["prune", "all_rows"])
+def consensus_path(request, monkeypatch):
+    """both consensus routes: the Lipschitz / gradient / second-stage pre-pruning that batches
+    of more than ERP_SMALL_BATCH pairs take, and the every-row bounds pass of small batches (the
+    single-pair call, capi.hip run_consensus)"""
+    monkeypatch.setenv("ERP_SMALL_BATCH", "0" if request.param == "prune" else "1000000")
+    return request.param
+
+
 def _batch(pairs, device="cuda"):
     import torch
     dl = np.concatenate([p["desc_l"] for p in pairs])
@@ -730,7 +739,7 @@ def test_hypothesis_sharded_dev_padded_blocks(ctx, world):
 
 @pytest.mark.parametrize("world,iters", [(2, 500), (3, 500), (8, 500), (5, 4000), (2, 100000),
                                          (8, 100000)])
-def test_consensus_row_shards_equal_unsharded(ctx, world, iters):
+def test_consensus_row_shards_equal_unsharded(ctx, world, iters, consensus_path):
     """configs[4]'s sharded consensus: the K^2 bounds pass split into `world` row shards
     (erp_consensus_hyps_shard_dev per shard: reference rows, Lipschitz pre-pruning against the
     shard's own references, the kept rows; summed as the RCCL all_reduce would) then
@@ -763,7 +772,7 @@ def test_consensus_row_shards_equal_unsharded(ctx, world, iters):
 
 
 @pytest.mark.parametrize("K", [1, 2, 3, 5, 40, 1000])
-def test_consensus_dev_vs_oracle(ctx, oracle, K):
+def test_consensus_dev_vs_oracle(ctx, oracle, K, consensus_path):
     from erp_match_eightpoint_test_amd import dist as D
     rng = np.random.default_rng(K)
     rv = (rng.standard_normal((K, 3)) * 0.01).astype(np.float32)
@@ -777,7 +786,7 @@ def test_consensus_dev_vs_oracle(ctx, oracle, K):
     assert np.array_equal(res["R"], rv[mi]) and np.array_equal(res["T"], tv[mi])
 
 
-def test_consensus_bimodal_many_survivors(ctx, oracle):
+def test_consensus_bimodal_many_survivors(ctx, oracle, consensus_path):
     """two far clusters (R1 and R2 both valid): the bounds prune little; still exact."""
     from erp_match_eightpoint_test_amd import dist as D
     rng = np.random.default_rng(9)
@@ -790,7 +799,7 @@ def test_consensus_bimodal_many_survivors(ctx, oracle):
     assert res["min_idx"] == mi
 
 
-def test_consensus_heavy_duplicates(ctx, oracle):
+def test_consensus_heavy_duplicates(ctx, oracle, consensus_path):
     """few distinct R vectors repeated many times: zero distances put the window ranks in the
     underflow bin, which takes the radix fallback of consensus_rows."""
     from erp_match_eightpoint_test_amd import dist as D
@@ -804,7 +813,7 @@ def test_consensus_heavy_duplicates(ctx, oracle):
     assert res["min_idx"] == mi
 
 
-def test_consensus_survivor_means_bimodal_pair(ctx, oracle):
+def test_consensus_survivor_means_bimodal_pair(ctx, oracle, consensus_path):
     """a full-size synthetic pair whose R1 and R2 are both valid in every iteration (K = 2I):
     thousands of consensus survivors; their trimmed means must match the oracle's."""
     from erp_match_eightpoint_test_amd import PairBatchRunner, results_to_numpy
@@ -842,7 +851,7 @@ def test_consensus_nonfinite_input_is_invalid_arg(ctx):
 
 
 @pytest.mark.parametrize("case", ["wide_range", "dup_block", "tiny_cluster"])
-def test_consensus_bounds_wide_dynamic_range(ctx, oracle, case):
+def test_consensus_bounds_wide_dynamic_range(ctx, oracle, case, consensus_path):
     """binned-distance bounds when the window's ranks sit in the lowest binades of the
     40-binade range (tight cluster + rotations near the validity limit, many exact duplicates):
     the winner and every survivor's mean stay exact."""
@@ -872,7 +881,7 @@ def test_consensus_bounds_wide_dynamic_range(ctx, oracle, case):
 
 @pytest.mark.parametrize("case", ["cluster", "cluster_outliers", "shell", "uniform_cube",
                                   "two_clusters"])
-def test_consensus_lipschitz_prepruning(ctx, oracle, case):
+def test_consensus_lipschitz_prepruning(ctx, oracle, case, consensus_path):
     """K >= 1024: the bounds pass first bins every 32nd row, rows provably beaten through the
     1-Lipschitz bound T(i) >= T(c) - d(i, c) skip the histogram pass.  The winner and its mean
     stay exact; on a single cluster most rows are pruned (binned_rows well below K); on a shell
@@ -906,13 +915,13 @@ def test_consensus_lipschitz_prepruning(ctx, oracle, case):
     assert np.array_equal(res["R"], rv[mi]) and np.array_equal(res["T"], tv[mi])
     assert abs(res["min_dist"] - dref[mi]) <= 1e-12 * abs(dref[mi])
     assert (K + 31) // 32 <= res["binned_rows"] <= K  # (the reference rows: every 32nd)
-    if case in ("cluster", "cluster_outliers", "uniform_cube"):
+    if case in ("cluster", "cluster_outliers", "uniform_cube") and consensus_path == "prune":
         assert res["binned_rows"] < K // 2, res["binned_rows"]
 
 
 @pytest.mark.parametrize("case", ["cluster", "cluster_outliers", "shell", "two_clusters",
                                   "bench_pairs"])
-def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case):
+def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case, consensus_path):
     """the convexity-augmented pruning (central references' distance gradient G, ERP_LIPG) keeps
     every result field the Lipschitz-only run gives (status, K, min_idx, R, T, min_dist,
     near_ties), is deterministic run to run (every byte, binned_rows included), and bins no more
@@ -979,7 +988,7 @@ def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case):
 
 
 @pytest.mark.parametrize("case", ["two_clusters", "twin_pairs", "bench_pairs"])
-def test_consensus_refine_hint_and_flat_exact(gpu_lib, oracle, monkeypatch, case):
+def test_consensus_refine_hint_and_flat_exact(gpu_lib, oracle, monkeypatch, case, consensus_path):
     """the refine pass's hinted sub-bin windows (ERP_REFINE_HINT; kernels.hip
     consensus_hint_kernel / refine_windows) and the flat-pair route (ERP_FLAT_REFS: the
     first-stage references refined, the first stage re-run against them) keep every result
@@ -1027,7 +1036,8 @@ def test_consensus_refine_hint_and_flat_exact(gpu_lib, oracle, monkeypatch, case
                   f"binned_rows {r['binned_rows'].tolist()}")
         if case == "twin_pairs":
             assert a["K"][0] == 20000  # the two-cluster regime
-            assert recs[2][0]["binned_rows"][0] < a["binned_rows"][0] // 4
+            if consensus_path == "prune":
+                assert recs[2][0]["binned_rows"][0] < a["binned_rows"][0] // 4
             _, mi, _ = oracle.consensus(rv0[:int(a["K"][0])])
             assert int(recs[2][0]["min_idx"][0]) == mi
         return
@@ -1049,7 +1059,7 @@ def test_consensus_refine_hint_and_flat_exact(gpu_lib, oracle, monkeypatch, case
           f"binned_rows {[int(r['binned_rows']) for r in res[:3]]}")
 
 
-def test_consensus_small_set_bins_every_row(ctx, oracle):
+def test_consensus_small_set_bins_every_row(ctx, oracle, consensus_path):
     """below 1024 rows there is no pre-pruning: every row is binned."""
     from erp_match_eightpoint_test_amd import dist as D
     rng = np.random.default_rng(31)
