@@ -786,22 +786,37 @@ def main():
     lat = None
     if args.steps > 0:
         b1 = to_device(pairs[:1], dev)
-        ctx1 = Context(local)
-        ctx1.set_matcher(0 if args.matcher == "mfma" else 1)
-        run1 = PairBatchRunner(ctx=ctx1, iters=args.iters, sampler=SAMPLER)
-        run1.reserve(1, b1["max_nq"], b1["max_nt"])
-        ts = []
-        for k in range(23):
-            torch.cuda.synchronize()
-            ta = time.perf_counter()
-            run1.run(b1["desc_l"], b1["desc_r"], b1["kp_l"], b1["kp_r"], b1["off_l"], b1["off_r"],
-                     b1["width"], b1["height"], b1["max_nq"], b1["max_nt"])
-            torch.cuda.synchronize()
-            if k >= 3:
-                ts.append(time.perf_counter() - ta)
-        lat = {"single_pair_ms": float(np.median(ts)) * 1e3,
+
+        def lat_run(graphs: bool) -> tuple:
+            ctx1 = Context(local)
+            ctx1.set_matcher(0 if args.matcher == "mfma" else 1)
+            ctx1.set_graphs(graphs)  # erp_ctx_set_graphs: replay the captured launch sequence
+            run1 = PairBatchRunner(ctx=ctx1, iters=args.iters, sampler=SAMPLER,
+                                   reuse_outputs=graphs)
+            run1.reserve(1, b1["max_nq"], b1["max_nt"])
+            st1 = torch.cuda.Stream(dev) if graphs else None  # (capture needs a non-NULL stream)
+            ts, rec = [], None
+            for k in range(23):
+                torch.cuda.synchronize()
+                ta = time.perf_counter()
+                o = run1.run(b1["desc_l"], b1["desc_r"], b1["kp_l"], b1["kp_r"], b1["off_l"],
+                             b1["off_r"], b1["width"], b1["height"], b1["max_nq"], b1["max_nt"],
+                             stream=st1.cuda_stream if st1 is not None else None)
+                torch.cuda.synchronize()
+                if k >= 3:
+                    ts.append(time.perf_counter() - ta)
+                rec = o["results"].cpu().numpy().tobytes()
+            return float(np.median(ts)) * 1e3, rec
+
+        eager_ms, eager_rec = lat_run(False)
+        graph_ms, graph_rec = lat_run(True)
+        lat = {"single_pair_ms": min(eager_ms, graph_ms),
+               "single_pair_ms_eager": eager_ms, "single_pair_ms_graph": graph_ms,
+               "graph_record_equals_eager": graph_rec == eager_rec,
                "note": f"one {args.kpts}x{args.kpts} pair, {args.iters} iterations, batch of 1, "
-                       "host-timed, median of 20"}
+                       "host-timed (sync before and after each call), median of 20; eager = "
+                       "launches enqueued per call, graph = the context's captured HIP graph "
+                       "replayed (erp_ctx_set_graphs); single_pair_ms = the faster of the two"}
     # a harder batch through the same contexts and streams (beside the headline, not `value`):
     # half the left keypoints without a true partner, more descriptor noise (0.035: much more
     # and the 0.3 ratio test rejects the true partners too), 30 % of the true matches at wrong

@@ -593,6 +593,8 @@ __device__ __forceinline__ void lds_wait_n(uint32_t& o, int n) {
 // a wave alone on its SIMD has nothing else to cover the masked-OR latency: the ILP variants keep
 // up to 15 in flight (the lgkmcnt limit) instead of kReplayLag
 constexpr int kIlpLag = 15;
+// the latency blocks' default (1: step by step, 2: positions first; ERP_SAMPLER_LAT overrides)
+constexpr int kSamplerLatMode = 2;
 
 // ---- the same blocks with the 31 draw positions computed FIRST (ILP variants) ---------------
 // A block's 31 positions depend only on the ring words the previous block left (the backwards
@@ -687,6 +689,149 @@ __device__ __forceinline__ uint32_t replay_block_ilp(uint32_t (&ring)[31], uint3
     return replay_block_mixed<RS>(ring, bm, lane, i, s, rtab);
 }
 
+// ---- latency variant (sampler_kernel<2>: waves alone on their SIMDs) -----------------------
+// SQ counters of the single-pair path (profiles/r05n_sq_latency.txt): the standalone sampler's
+// lone waves sat at s_waitcnt ~40 % of their cycles.  Each block's 31 divisor constants come
+// by scalar loads issued at the block's start, and SMEM returns out of order, so their first use
+// waits lgkmcnt(0): an L2 round trip per block that also drains the block's in-flight masked
+// ORs.  Four waves per SIMD hide that; one does not.  Here the constants of the NEXT block are
+// fetched by vector loads (counted by vmcnt, apart from the LDS ops) one block ahead, and the
+// prefix blocks keep bm[i] in a register window (no per-step LDS round trip).  Raw 64-bit
+// words: the magic pair for d >= 256 blocks (ERP_SAMPLER_MAGIC), else the fp64 reciprocal.
+template <bool I24>
+__device__ __forceinline__ uint32_t lat_mod(uint32_t x, uint64_t c, int d) {
+    if (I24) return mod_i24(x, __builtin_bit_cast(StepDiv, c), d);
+    return mod_rup(x, __builtin_bit_cast(double, c), (double)d);
+}
+
+// block kinds: 0 draws (d >= 256), 1 draws, 2 prefix (d >= 256), 3 prefix, 4 mixed / ending
+__device__ __forceinline__ int lat_kind(int i, int s) {
+    if (i - 30 >= s) return i - 30 >= 255 ? 0 : 1;
+    if (i < s && i - 30 >= 1) return i - 30 >= 255 ? 2 : 3;
+    return 4;
+}
+
+// the constants of block i0 (kinds 0-3: every d = i0 - u + 1 >= 2) by vector loads
+__device__ __forceinline__ void lat_fetch(const double* __restrict__ rtab, int i0, int kind,
+                                          uint64_t (&c)[31]) {
+    const uint64_t* t = reinterpret_cast<const uint64_t*>(rtab) +
+                        ((kind == 0 || kind == 2) && ERP_SAMPLER_MAGIC ? kRecipTable : 0);
+    int d0 = i0 + 1;
+    asm volatile("" : "+v"(d0));  // a VGPR index: global (vmcnt) loads, not scalar ones
+#pragma unroll
+    for (int u = 0; u < 31; u++) c[u] = t[d0 - u];
+}
+// a use of every constant of a set before the next set's loads are issued: the compiler's wait
+// for this set (vmcnt) then cannot count the next set's loads in (at a loop head it would wait
+// vmcnt(0), i.e. for the loads just issued)
+__device__ __forceinline__ void lat_ready(uint64_t (&c)[31]) {
+#pragma unroll
+    for (int u = 0; u < 28; u += 4)
+        asm volatile("" : "+v"(c[u]), "+v"(c[u + 1]), "+v"(c[u + 2]), "+v"(c[u + 3]));
+    asm volatile("" : "+v"(c[28]), "+v"(c[29]), "+v"(c[30]));
+}
+
+// PF: the block's 31 positions first (31 independent modulo chains for the scheduler to
+// interleave: a lone wave has no other wave to cover a chain's dependent-issue latency), then the
+// masked ORs with up to kIlpLag in flight; else each step's chain in turn (lag kReplayLag)
+template <bool I24, bool PF>
+__device__ __forceinline__ void lat_positions(uint32_t (&ring)[31], int i0, const uint64_t (&c)[31],
+                                              uint32_t (&jj)[31]) {
+#pragma unroll
+    for (int u = 0; u < 31; u++) {
+        const int slot = 30 - u;
+        const uint32_t rv = ring[slot];
+        ring[slot] = rv - ring[(slot + 28) % 31];
+        jj[u] = lat_mod<I24>(rv >> 1, c[u], i0 - u + 1);
+    }
+}
+
+template <bool I24, bool PF, int RS = 8>
+__device__ __forceinline__ uint32_t replay_block_draws_lat(uint32_t (&ring)[31], uint32_t* bm,
+                                                           int lane, int i0, int s,
+                                                           const uint64_t (&c)[31]) {
+    constexpr int LAG = PF ? kIlpLag : kReplayLag;
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
+    const uint32_t zero = 0;
+    uint32_t olds[31], jj[31];
+    if (PF) lat_positions<I24, PF>(ring, i0, c, jj);
+    uint32_t nw[2] = {0, 0};
+#pragma unroll
+    for (int u = 0; u < 31 + LAG; u++) {
+        if (u < 31) {
+            if (!PF) {
+                const int slot = 30 - u;
+                const uint32_t rv = ring[slot];
+                ring[slot] = rv - ring[(slot + 28) % 31];
+                jj[u] = lat_mod<I24>(rv >> 1, c[u], i0 - u + 1);
+            }
+            if (ERP_SAMPLER_CLAMP) jj[u] = min(jj[u], (uint32_t)s);
+            olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, jj[u]), 1u << (jj[u] & 31), zero);
+        }
+        const int v = u - LAG;
+        if (v >= 0) {
+            lds_wait_n(olds[v], min(30 - v, LAG));
+            nw[v & 1] |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
+        }
+    }
+    return nw[0] | nw[1];
+}
+
+template <bool I24, bool PF, int RS = 8>
+__device__ __forceinline__ uint32_t replay_block_prefix_lat(uint32_t (&ring)[31], uint32_t* bm,
+                                                            int lane, int i0,
+                                                            const uint64_t (&c)[31]) {
+    constexpr int LAG = PF ? kIlpLag : kReplayLag;
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
+    const int base = i0 - 30;  // >= 1
+    const int wA = i0 >> 5, wB = base >> 5;
+    // (compiler-tracked reads: its wait for them is at least as strict as needed, since the
+    // masked ORs issued after them only add to the count)
+    const uint32_t hi = bm[bm_index<RS>(wA, lane)], lo = bm[bm_index<RS>(wB, lane)];
+    uint32_t win = wA == wB ? (lo >> (base & 31)) : __builtin_amdgcn_alignbit(hi, lo, base & 31);
+    uint32_t olds[31], jj[31];
+    if (PF) lat_positions<I24, PF>(ring, i0, c, jj);
+    uint32_t nw[2] = {0, 0};
+#pragma unroll
+    for (int u = 0; u < 31 + LAG; u++) {
+        if (u < 31) {
+            if (!PF) {
+                const int slot = 30 - u;
+                const uint32_t rv = ring[slot];
+                ring[slot] = rv - ring[(slot + 28) % 31];
+                jj[u] = lat_mod<I24>(rv >> 1, c[u], i0 - u + 1);
+            }
+            const uint32_t j = jj[u];
+            const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)win, 30 - u, 1);  // bm[i]
+            const uint32_t bit = 1u << (j & 31);
+            olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), bit, bsp & bit);
+            const uint32_t t = min(j - (uint32_t)base, 31u);
+            const uint32_t m = 1u << t;
+            win = (win & ~m) | (bsp & m);
+        }
+        const int v = u - LAG;
+        if (v >= 0) {
+            lds_wait_n(olds[v], min(30 - v, LAG));
+            nw[v & 1] |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
+        }
+    }
+    return nw[0] | nw[1];
+}
+
+template <bool PF, int RS>
+__device__ __forceinline__ uint32_t replay_block_lat(uint32_t (&ring)[31], uint32_t* bm, int lane,
+                                                     int i, int s, int kind,
+                                                     const double* __restrict__ rtab,
+                                                     const uint64_t (&c)[31]) {
+    switch (kind) {
+        case 0: return replay_block_draws_lat<true, PF, RS>(ring, bm, lane, i, s, c);
+        case 1: return replay_block_draws_lat<false, PF, RS>(ring, bm, lane, i, s, c);
+        case 2: return replay_block_prefix_lat<true, PF, RS>(ring, bm, lane, i, c);
+        case 3: return replay_block_prefix_lat<false, PF, RS>(ring, bm, lane, i, c);
+        default: return replay_block_mixed<RS>(ring, bm, lane, i, s, rtab);
+    }
+}
+
 // the 31 reverse steps i .. i-30 of one lane's replay, by block kind (uniform: i and s are)
 template <int RS>
 __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t* bm, int lane,
@@ -704,7 +849,10 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
 
 // One lane = one iteration; writes the iteration's selection bitmap in block space:
 // sel[p][w][b][lane] bit u <-> index i = M-1-31b-u (b = 0 .. (M-1)/31), exactly s bits set.
-template <bool ILP>
+// MODE 0: the throughput blocks; 1: the ILP blocks (A/B knob); 2: the latency blocks (constants
+// prefetched one block ahead by vector loads, two blocks per loop trip so that the two constant
+// sets alternate without register copies)
+template <int MODE>
 __global__ __launch_bounds__(64) void sampler_kernel(
     const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins, int nwaves, int nbw,
     double sample_frac, const double* __restrict__ rtab, uint32_t* __restrict__ selw,
@@ -733,14 +881,32 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     const int b0 = (M - 1) / 31, u0 = (M - 1) % 31;  // slot of position 0
     int i = M - 1, b = 0, emitted = 0;
     uint32_t lastw = 0;
-    while (i >= 1) {
-        const uint32_t word = ILP ? replay_block_ilp<8>(ring, bm, lane, i, s, rtab)
-                                  : replay_block<8>(ring, bm, lane, i, s, rtab);
+    auto emit = [&](uint32_t word) {
         emitted += __builtin_popcount(word);
         if (b == b0) lastw = word;
         else out[(size_t)b * 64] = word;
         i -= 31;
         b++;
+    };
+    if (MODE >= 2) {
+        uint64_t ca[31] = {}, cb[31] = {};
+        int ka = lat_kind(i, s);
+        if (ka < 4) lat_fetch(rtab, i, ka, ca);
+        while (i >= 1) {
+            const int kb = i - 31 >= 1 ? lat_kind(i - 31, s) : 4;
+            lat_ready(ca);
+            if (kb < 4) lat_fetch(rtab, i - 31, kb, cb);
+            emit(replay_block_lat<MODE == 3, 8>(ring, bm, lane, i, s, ka, rtab, ca));
+            if (i < 1) break;
+            ka = i - 31 >= 1 ? lat_kind(i - 31, s) : 4;
+            lat_ready(cb);
+            if (ka < 4) lat_fetch(rtab, i - 31, ka, ca);
+            emit(replay_block_lat<MODE == 3, 8>(ring, bm, lane, i, s, kb, rtab, cb));
+        }
+    } else {
+        while (i >= 1)
+            emit(MODE == 1 ? replay_block_ilp<8>(ring, bm, lane, i, s, rtab)
+                           : replay_block<8>(ring, bm, lane, i, s, rtab));
     }
     if (bm[lane] & 1u) {  // position 0 still unresolved: its value 0 stays in the prefix
         lastw |= 1u << u0;
@@ -4643,21 +4809,29 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         // gfx950, scripts/dev/lds_oob.hip) so that no word of the allocation goes uncleared
         const int nwords = (sh.max_s / 32 + 1 + 4) / 5 * 5;
         const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
-        // ERP_SAMPLER_ILP=1: the blocks with their 31 positions computed first (A/B knob)
+        // ERP_SAMPLER_ILP=1: the blocks with their 31 positions computed first (A/B knob).
+        // The latency blocks (modes 2 / 3) where the launch leaves most SIMDs with at most one
+        // wave (<= 1024 waves); ERP_SAMPLER_LAT = 0 / 1 / 2 forces mode 0 / 2 / 3
         static const bool ilp = getenv("ERP_SAMPLER_ILP") && atoi(getenv("ERP_SAMPLER_ILP")) != 0;
+        static const int lat_env = getenv("ERP_SAMPLER_LAT") ? atoi(getenv("ERP_SAMPLER_LAT")) : -1;
+        const int lat = lat_env >= 0 ? lat_env : (long)nwaves * sh.n_pairs <= 1024 ? kSamplerLatMode : 0;
+        const int mode = ilp ? 1 : lat == 1 ? 2 : lat == 2 ? 3 : 0;
         // (s up to 16 383 at the 65 535-keypoint cap: 515 words x 256 B = 129 KB)
-        static std::atomic<size_t> lds_set[2];
-        const hipError_t le = ilp ? ensure_dyn_lds((const void*)sampler_kernel<true>, shmem, lds_set[1])
-                                  : ensure_dyn_lds((const void*)sampler_kernel<false>, shmem, lds_set[0]);
+        static std::atomic<size_t> lds_set[4];
+        const void* fns[4] = {(const void*)sampler_kernel<0>, (const void*)sampler_kernel<1>,
+                              (const void*)sampler_kernel<2>, (const void*)sampler_kernel<3>};
+        const hipError_t le = ensure_dyn_lds(fns[mode], shmem, lds_set[mode]);
         if (le != hipSuccess) return le;
-        if (ilp)
-            ERP_LAUNCH(sampler_kernel<true>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st,
-                               counts, wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags,
-                               nwords);
-        else
-            ERP_LAUNCH(sampler_kernel<false>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st,
-                               counts, wins, nwaves, sh.sel_words, sample_frac, rtab, selw, flags,
-                               nwords);
+#define ERP_SAMPLER_LAUNCH(M)                                                                  \
+    ERP_LAUNCH(sampler_kernel<M>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts, wins, \
+               nwaves, sh.sel_words, sample_frac, rtab, selw, flags, nwords)
+        switch (mode) {
+            case 1: ERP_SAMPLER_LAUNCH(1); break;
+            case 2: ERP_SAMPLER_LAUNCH(2); break;
+            case 3: ERP_SAMPLER_LAUNCH(3); break;
+            default: ERP_SAMPLER_LAUNCH(0); break;
+        }
+#undef ERP_SAMPLER_LAUNCH
     }
     return hipGetLastError();
 }
