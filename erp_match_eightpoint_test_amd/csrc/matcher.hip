@@ -133,6 +133,15 @@ constexpr int kFStageB = kFHiB + kFST * kFT * 4;  // + 512
 #define ERP_FILTER_WARM 8
 #endif
 constexpr int kFWarm = ERP_FILTER_WARM;
+// running bound from the two smallest (tile, group) minima per lane (round 5) instead of the
+// minima of two fixed row groups (ERP_FILTER_TOP2=0)
+#ifndef ERP_FILTER_TOP2
+#define ERP_FILTER_TOP2 1
+#endif
+// timing ablations only (wrong results): 1 = no candidate slot stores
+#ifndef ERP_FILTER_ABLATE
+#define ERP_FILTER_ABLATE 0
+#endif
 
 __device__ __forceinline__ bf16x8 round8(const float4 a, const float4 b, float s) {
     const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
@@ -200,14 +209,14 @@ __device__ __forceinline__ float second4(float a0, float a1, float b0, float b1)
     return fminf(fmaxf(m1, o1), fminf(m2, o2));
 }
 
-// A candidate slot is one 32-B record: the tile's 16 bounds as bf16, with the tile's index
-// (tile0 / 32 < 2048: rows < 65536, chunk lengths are multiples of 32) in the 16 mantissa LSBs
-// (bit 2 d of the index in dword d's low half, bit 2 d + 1 in its high half).  The knn2_rescore
-// side widens each value by 2^-6 |v| instead of 2^-8 |v| (round to nearest: 1/2 ulp, the
-// replaced LSB: 1 ulp, so |v - u'| <= 3 2^-8 |v|).  Before round 3 the tile index went to a
-// separate int32 array: a scattered 4-B store per slot that HBM wrote as a whole sector (the
-// filter's slot writes 0.72 GB per 192-pair launch against 0.35 GB of bounds; ERP_CAND_TILE_ARRAY=1
-// keeps that layout for A/B).
+// A candidate slot is one 32-B record: the tile's 16 bounds as bf16, and the tile's index
+// (tile0) in a parallel int32 array at the same slot index (since r05; with the interleaved slot
+// layout of cand_slot() a wave's 64 indices are one coalesced 256-B store).  knn2_rescore widens
+// each value by 2^-8 |v| (round to nearest: 1/2 ulp).  r03e-r05 embedded the index in the 16
+// mantissa LSBs instead (bit 2 d in dword d's low half, bit 2 d + 1 in its high half; widening
+// 2^-6 |v|): with the [list][slot] layout of those rounds a separate index was a scattered 4-B
+// store per slot that HBM wrote as a whole sector.  ERP_CAND_TILE_ARRAY=0 keeps the embedded
+// form for A/B.
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ bf16x8 cand_embed_tile(bf16x8 b, int g, int tile0) {
     const uint32_t ti = (uint32_t)tile0 >> 5;
@@ -231,7 +240,22 @@ __device__ __forceinline__ int cand_tile(bf16x8 v0, bf16x8 v1) {
     return (int)(ti << 5);
 }
 
-__global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restrict__ dq,
+#if ERP_FILTER_CHAINS == 3
+#define ERP_FILTER_WAVES __attribute__((amdgpu_waves_per_eu(3)))  // <= 168 VGPRs: 3 waves per SIMD
+#else
+#define ERP_FILTER_WAVES
+#endif
+// Slot record index of list (pair p, chunk ch, query q, lane half h), slot sl: the lists of 32
+// consecutive queries (a 32-query block) x 2 halves are interleaved slot by slot,
+//   [pair][chunk][query / 32][slot][half][query % 32],
+// so that the 64 lanes of a filter chain (32 queries x 2 halves) store slot sl to one contiguous
+// 2-KB run and the 32 lanes of a rescore half-wave read it as one 1-KB run.  (Until r05 the
+// layout was [list][slot]: every lane's record on its own line, one 16-B piece at a time.)
+__device__ __forceinline__ size_t cand_slot(int p, int ch, int chunks, int nqb, int q, int h, int sl) {
+    return ((((size_t)p * chunks + ch) * nqb + (q >> 5)) * kCandSlots + sl) * 64 + h * 32 + (q & 31);
+}
+
+__global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const float* __restrict__ dq,
                                                           const bf16x8* __restrict__ thi,
                                                           const float* __restrict__ tn,
                                                           const uint32_t* __restrict__ tmax,
@@ -334,7 +358,42 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     struct Acc2 {
         f32x16 a0, a1;
     };
+    struct Frag {
+        bf16x8 ah[4];
+        f32x16 ci;
+    };
+    auto tile_frags = [&](const char* sb, int u) __attribute__((always_inline)) -> Frag {
+        Frag f;
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            f.ah[c] = *reinterpret_cast<const bf16x8*>(sb + rd_hi[c] + u * kFT * kFRowB);
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+            const float4 t4 = *reinterpret_cast<const float4*>(sb + rd_tu + 4 * (u * kFT + 8 * g));
+            f.ci[4 * g] = t4.x;
+            f.ci[4 * g + 1] = t4.y;
+            f.ci[4 * g + 2] = t4.z;
+            f.ci[4 * g + 3] = t4.w;
+        }
+        return f;
+    };
+    auto tile_mma_f = [&](const Frag& f) __attribute__((always_inline)) -> Acc2 {
+        const bf16x8(&ah)[4] = f.ah;
+        const f32x16& ci = f.ci;
+        Acc2 r;
+        r.a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[0], qh[0][0], ci, 0, 0, 0);
+#pragma unroll
+        for (int c = 1; c < 4; c++)
+            r.a0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[c], qh[0][c], r.a0, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        r.a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[0], qh[1][0], ci, 0, 0, 0);
+#pragma unroll
+        for (int c = 1; c < 4; c++)
+            r.a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[c], qh[1][c], r.a1, 0, 0, 0);
+        return r;
+    };
     auto tile_mma = [&](const char* sb, int u) __attribute__((always_inline)) -> Acc2 {
+        (void)tile_mma_f;
         bf16x8 ah[4];
 #pragma unroll
         for (int c = 0; c < 4; c++)
@@ -364,7 +423,8 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
             r.a1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[c], qh[1][c], r.a1, 0, 0, 0);
         return r;
     };
-    auto tile_epi = [&](int j, f32x16 e, int tile0, bool extract) __attribute__((always_inline)) {
+    // updc: std::integral_constant<bool, false> in the final recompute of the warm stages
+    auto tile_epi = [&](int j, f32x16 e, int tile0, bool extract, auto updc) __attribute__((always_inline)) {
         float ta = min3f(e[0], e[1], e[2]);
         ta = min3f(ta, e[3], e[4]);
         ta = min3f(ta, e[5], e[6]);
@@ -373,15 +433,28 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
         tb = min3f(tb, e[11], e[12]);
         tb = min3f(tb, e[13], e[14]);
         tb = min2f(tb, e[15]);
+#if ERP_FILTER_TOP2
+        // the lane's two smallest minima over all (tile, 8-row group)s seen: gm[j][0] <= gm[j][1],
+        // minima of two disjoint row sets, so 2 rows have u' <= gm[j][1]; tighter than a fixed
+        // split of the rows into two groups whenever both smallest rows fall in one group.  Not
+        // in the final recompute of the warm stages: a (tile, group) seen twice could fill both
+        // places with one row set (the fixed-group minima were idempotent)
+        if (decltype(updc)::value) {
+            const float lo = min2f(ta, tb), hi = fmaxf(ta, tb);
+            gm[j][1] = min2f(fmaxf(gm[j][0], lo), min2f(gm[j][1], hi));
+            gm[j][0] = min2f(gm[j][0], lo);
+        }
+#else
         gm[j][0] = min2f(gm[j][0], ta);
         gm[j][1] = min2f(gm[j][1], tb);
+#endif
         // a lane whose 16 rows of the tile may hold a candidate stores them whole (16 bounds
         // as bf16 carrying the tile index: two 16-B stores); knn2_rescore picks the rows under
         // the final bound (widening each stored value by its bf16 rounding and the replaced LSB)
         if (extract && min2f(ta, tb) <= thr[j]) {
             const int sl = ncand[j]++;
-            if (sl < kCandSlots) {
-                const size_t slot = (size_t)cl[j] * kCandSlots + sl;
+            if (sl < kCandSlots && !ERP_FILTER_ABLATE) {
+                const size_t slot = cand_slot(p, ch, chunks, (max_nq + 31) >> 5, qi[j], h, sl);
                 if (tile_array) ctile[slot] = tile0;
 #pragma unroll
                 for (int g = 0; g < 2; g++) {
@@ -396,23 +469,40 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     // the stage's 4 tiles.  ERP_FILTER_CHAINS == 2: software-pipelined by one chain -- tile u's
     // second chain is reduced after tile u + 1's MFMAs are issued, so neither chain's drain is
     // waited on (+16 live VGPRs)
-    auto tiles = [&](const char* sb, int tb0, bool extract) __attribute__((always_inline)) {
-#if ERP_FILTER_CHAINS == 2
+    auto tiles = [&](const char* sb, int tb0, bool extract, auto updc) __attribute__((always_inline)) {
+#if ERP_FILTER_CHAINS == 3
+        // as 2, and tile u + 1's fragment reads issued right after tile u's MFMAs (in flight
+        // during them and the epilogues) instead of in front of tile u + 1's MFMAs, where each
+        // tile waited lgkmcnt(0) on its own reads
+        f32x16 prev;
+        (void)tile_mma;
+        Frag f = tile_frags(sb, 0);
+#pragma unroll
+        for (int u = 0; u < kFST; u++) {
+            const Acc2 acc = tile_mma_f(f);
+            __builtin_amdgcn_sched_barrier(0);
+            if (u + 1 < kFST) f = tile_frags(sb, u + 1);
+            tile_epi(0, acc.a0, tb0 + u * kFT, extract, updc);
+            if (u > 0) tile_epi(1, prev, tb0 + (u - 1) * kFT, extract, updc);
+            prev = acc.a1;
+        }
+        tile_epi(1, prev, tb0 + (kFST - 1) * kFT, extract, updc);
+#elif ERP_FILTER_CHAINS == 2
         f32x16 prev;
 #pragma unroll
         for (int u = 0; u < kFST; u++) {
             const Acc2 acc = tile_mma(sb, u);
-            tile_epi(0, acc.a0, tb0 + u * kFT, extract);
-            if (u > 0) tile_epi(1, prev, tb0 + (u - 1) * kFT, extract);
+            tile_epi(0, acc.a0, tb0 + u * kFT, extract, updc);
+            if (u > 0) tile_epi(1, prev, tb0 + (u - 1) * kFT, extract, updc);
             prev = acc.a1;
         }
-        tile_epi(1, prev, tb0 + (kFST - 1) * kFT, extract);
+        tile_epi(1, prev, tb0 + (kFST - 1) * kFT, extract, updc);
 #else
 #pragma unroll
         for (int u = 0; u < kFST; u++) {
             const Acc2 acc = tile_mma(sb, u);
-            tile_epi(0, acc.a0, tb0 + u * kFT, extract);
-            tile_epi(1, acc.a1, tb0 + u * kFT, extract);
+            tile_epi(0, acc.a0, tb0 + u * kFT, extract, updc);
+            tile_epi(1, acc.a1, tb0 + u * kFT, extract, updc);
         }
 #endif
     };
@@ -423,7 +513,7 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     // least one -- and are recomputed for candidates after the last)
     const int warm = max(1, min(kFWarm, nstages / 4));
     const int last = nstages + warm - 1;  // iterations 0 .. last
-    auto stage = [&](auto bufc, int it) {
+    auto stage = [&](auto bufc, auto updc, int it) {
         constexpr int BUF = decltype(bufc)::value;
         char* sb = sm + BUF * kFStageB;
         const int st = it < nstages ? it : it - nstages;
@@ -433,7 +523,7 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
             const int nx = it + 1 < nstages ? it + 1 : it + 1 - nstages;
             dma(sm + (1 - BUF) * kFStageB, nx);
         }
-        tiles(sb, t0 + st * kFST * kFT, it >= warm);
+        tiles(sb, t0 + st * kFST * kFT, it >= warm, updc);
         if (it < nstages) {
 #pragma unroll
             for (int j = 0; j < 2; j++) {
@@ -446,9 +536,21 @@ __global__ __launch_bounds__(256) void knn2_filter_kernel(const float* __restric
     // stage sequence: 0 .. warm - 1 (bounds only), warm .. nstages - 1, then 0 .. warm - 1 again
     // (candidates only, against the chunk's final bound); LDS buffers alternate
     dma(sm, 0);
-    for (int it = 0; it <= last; it += 2) {
-        stage(std::integral_constant<int, 0>{}, it);
-        if (it + 1 <= last) stage(std::integral_constant<int, 1>{}, it + 1);
+    {
+        const std::integral_constant<int, 0> b0{};
+        const std::integral_constant<int, 1> b1{};
+        const std::integral_constant<bool, true> u1{};
+        const std::integral_constant<bool, false> u0{};
+        int it = 0;
+        for (; it + 1 < nstages; it += 2) {
+            stage(b0, u1, it);
+            stage(b1, u1, it + 1);
+        }
+        if (it < nstages) stage(b0, u1, it++);
+        for (; it <= last; it++) {  // the recompute (buffer = iteration parity)
+            if (it & 1) stage(b1, u0, it);
+            else stage(b0, u0, it);
+        }
     }
 #pragma unroll
     for (int j = 0; j < 2; j++) {
@@ -584,7 +686,7 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
         for (int h = 0; h < 2; h++) {
             const int n = h ? n1 : n0;
             for (int k = 0; k < n; k++) {
-                const size_t slot = (l0 + h) * kCandSlots + k;
+                const size_t slot = cand_slot(p, c, chunks, (max_nq + 31) >> 5, q, h, k);
                 const bf16x8 v0 = cval[slot * 2], v1 = cval[slot * 2 + 1];
                 const int tile0 = tile_array ? ctile[slot] : cand_tile(v0, v1);
 #pragma unroll
@@ -1023,15 +1125,16 @@ __global__ __launch_bounds__(kMergeBlock) void knn2_merge_kernel(
 }  // namespace
 
 // ====================================================================== launchers =======
-// ERP_CAND_TILE_ARRAY=1: the tile index of a candidate slot in its own int32 array (the
-// layout before round 3, an A/B knob); default: inside the slot's bf16 bounds
+// ERP_CAND_TILE_ARRAY=0: the tile index embedded in the slot's bf16 mantissa LSBs (the r03e-r05
+// form, an A/B knob); default: its own int32 array (profiles/r05q_ab_slots.txt)
 static bool cand_tile_array() {
-    static const bool v = getenv("ERP_CAND_TILE_ARRAY") && atoi(getenv("ERP_CAND_TILE_ARRAY")) != 0;
+    static const bool v = !getenv("ERP_CAND_TILE_ARRAY") || atoi(getenv("ERP_CAND_TILE_ARRAY")) != 0;
     return v;
 }
 
 size_t knn2_cand_bytes(const BatchShape& sh) {
-    return (size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 * kCandSlots * (2 * sizeof(bf16x8) + 4);
+    return (size_t)sh.n_pairs * ((sh.max_nq + 31) / 32 * 32) * sh.fchunks * 2 * kCandSlots *
+           (2 * sizeof(bf16x8) + 4);
 }
 
 size_t knn2_split_bytes(const BatchShape& sh) {  // rows, tu, tmax, sentinel row (+ align)
@@ -1040,7 +1143,7 @@ size_t knn2_split_bytes(const BatchShape& sh) {  // rows, tu, tmax, sentinel row
 }
 
 static void cand_split(const BatchShape& sh, void* cand, int32_t** ctile, bf16x8** cval) {
-    const size_t lists = (size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 * kCandSlots;
+    const size_t lists = (size_t)sh.n_pairs * ((sh.max_nq + 31) / 32 * 32) * sh.fchunks * 2 * kCandSlots;
     *cval = (bf16x8*)cand;
     *ctile = (int32_t*)(*cval + lists * 2);
 }
