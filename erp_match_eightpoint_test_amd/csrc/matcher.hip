@@ -75,8 +75,11 @@ __device__ int block_exclusive_scan(int v, int* ws, int* total) {
 //     (each <= 2^-24 3 S) add < 2e-5 S, so |a - e| <= 0.0078444 S for the reference's exact
 //     f32 value e, against eps = 0x1.08p-7 = 0.0080566: u = a + eps S >= e + 2.1e-4 S and
 //     l = a - eps S <= e - 2.1e-4 S.  QB = |q|^2 (1 + eps) + tiny turns u' into u = u' + QB.
-//     Running bound: every lane keeps two group minima of u' (its elements 0-7 and 8-15 are
-//     disjoint train rows), so the second smallest of a query's four group minima (both lane
+//     Running bound: every lane keeps the two smallest of its (tile, 8-row group) minima of u'
+//     (a tile's elements 0-7 and 8-15 are disjoint train rows; since r05, before which the
+//     groups were fixed -- all tiles' elements 0-7, all 8-15 -- and looser whenever both
+//     smallest rows fell in one of them: rescore 1.21 -> 0.89 ms per step), two minima of
+//     disjoint row sets, so the second smallest of a query's four kept minima (both lane
 //     halves) G bounds the chunk's second smallest u' from above, and G + QB >= e_(2) (the
 //     true second-neighbour distance).  A row t with e_t <= e_(2) (both neighbours and all
 //     their ties) has l_t <= e_(2) - 2.1e-4 S_t <= G + QB, i.e.
@@ -209,14 +212,15 @@ __device__ __forceinline__ float second4(float a0, float a1, float b0, float b1)
     return fminf(fmaxf(m1, o1), fminf(m2, o2));
 }
 
-// A candidate slot is one 32-B record: the tile's 16 bounds as bf16, and the tile's index
-// (tile0) in a parallel int32 array at the same slot index (since r05; with the interleaved slot
-// layout of cand_slot() a wave's 64 indices are one coalesced 256-B store).  knn2_rescore widens
-// each value by 2^-8 |v| (round to nearest: 1/2 ulp).  r03e-r05 embedded the index in the 16
-// mantissa LSBs instead (bit 2 d in dword d's low half, bit 2 d + 1 in its high half; widening
-// 2^-6 |v|): with the [list][slot] layout of those rounds a separate index was a scattered 4-B
-// store per slot that HBM wrote as a whole sector.  ERP_CAND_TILE_ARRAY=0 keeps the embedded
-// form for A/B.
+// A candidate slot is one 32-B record: the tile's 16 bounds as bf16, with the tile's index
+// (tile0 / 32 < 2048: rows < 65536, chunk lengths are multiples of 32) in the 16 mantissa LSBs
+// (bit 2 d of the index in dword d's low half, bit 2 d + 1 in its high half).  The knn2_rescore
+// side widens each value by 2^-6 |v| instead of 2^-8 |v| (round to nearest: 1/2 ulp, the
+// replaced LSB: 1 ulp, so |v - u'| <= 3 2^-8 |v|).  Before round 3 the tile index went to a
+// separate int32 array: a scattered 4-B store per slot that HBM wrote as a whole sector (the
+// filter's slot writes 0.72 GB per 192-pair launch against 0.35 GB of bounds;
+// ERP_CAND_TILE_ARRAY=1 keeps that layout for A/B; with the interleaved slots of
+// ERP_CAND_INTERLEAVE=1 its stores coalesce, profiles/r05q_ab_slots.txt).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ bf16x8 cand_embed_tile(bf16x8 b, int g, int tile0) {
     const uint32_t ti = (uint32_t)tile0 >> 5;
@@ -245,14 +249,23 @@ __device__ __forceinline__ int cand_tile(bf16x8 v0, bf16x8 v1) {
 #else
 #define ERP_FILTER_WAVES
 #endif
-// Slot record index of list (pair p, chunk ch, query q, lane half h), slot sl: the lists of 32
-// consecutive queries (a 32-query block) x 2 halves are interleaved slot by slot,
-//   [pair][chunk][query / 32][slot][half][query % 32],
-// so that the 64 lanes of a filter chain (32 queries x 2 halves) store slot sl to one contiguous
-// 2-KB run and the 32 lanes of a rescore half-wave read it as one 1-KB run.  (Until r05 the
-// layout was [list][slot]: every lane's record on its own line, one 16-B piece at a time.)
+// Slot record index of list (pair p, chunk ch, query q, lane half h), slot sl.  Default: the
+// list's slots contiguous, [pair][query][chunk][half][slot] (query space padded to 32): a lane's
+// successive records fill whole lines.  ERP_CAND_INTERLEAVE=1 (an A/B knob, round 5) interleaves
+// the lists of 32 consecutive queries x 2 halves slot by slot, [pair][chunk][query / 32][slot]
+// [half][query % 32], so that a filter chain's 64 lanes store one slot index to one 2-KB run:
+// filter 2.96 -> 2.89 ms per step, but lanes that stop extracting leave holes in their lines --
+// filter writes 124 -> 194 MB and rescore reads 200 -> 217 MB per 128-pair launch
+// (profiles/r05q_ab_slots.txt), so the contiguous lists stay.
+#ifndef ERP_CAND_INTERLEAVE
+#define ERP_CAND_INTERLEAVE 0
+#endif
 __device__ __forceinline__ size_t cand_slot(int p, int ch, int chunks, int nqb, int q, int h, int sl) {
+#if ERP_CAND_INTERLEAVE
     return ((((size_t)p * chunks + ch) * nqb + (q >> 5)) * kCandSlots + sl) * 64 + h * 32 + (q & 31);
+#else  // [list][slot], list = ((pair, query, chunk), half) in the padded query space
+    return ((((size_t)p * (nqb * 32) + q) * chunks + ch) * 2 + h) * kCandSlots + sl;
+#endif
 }
 
 __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const float* __restrict__ dq,
@@ -1125,10 +1138,10 @@ __global__ __launch_bounds__(kMergeBlock) void knn2_merge_kernel(
 }  // namespace
 
 // ====================================================================== launchers =======
-// ERP_CAND_TILE_ARRAY=0: the tile index embedded in the slot's bf16 mantissa LSBs (the r03e-r05
-// form, an A/B knob); default: its own int32 array (profiles/r05q_ab_slots.txt)
+// ERP_CAND_TILE_ARRAY=1: the tile index of a candidate slot in its own int32 array (the
+// layout before round 3, an A/B knob); default: inside the slot's bf16 bounds
 static bool cand_tile_array() {
-    static const bool v = !getenv("ERP_CAND_TILE_ARRAY") || atoi(getenv("ERP_CAND_TILE_ARRAY")) != 0;
+    static const bool v = getenv("ERP_CAND_TILE_ARRAY") && atoi(getenv("ERP_CAND_TILE_ARRAY")) != 0;
     return v;
 }
 
