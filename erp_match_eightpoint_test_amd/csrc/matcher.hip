@@ -244,8 +244,12 @@ __device__ __forceinline__ int cand_tile(bf16x8 v0, bf16x8 v1) {
     return (int)(ti << 5);
 }
 
-#if ERP_FILTER_CHAINS == 3
-#define ERP_FILTER_WAVES __attribute__((amdgpu_waves_per_eu(3)))  // <= 168 VGPRs: 3 waves per SIMD
+// ERP_FILTER_MIN_WAVES = n > 0: amdgpu_waves_per_eu(n) (A/B knob; 3 for the CHAINS == 3 form)
+#ifndef ERP_FILTER_MIN_WAVES
+#define ERP_FILTER_MIN_WAVES (ERP_FILTER_CHAINS == 3 ? 3 : 0)
+#endif
+#if ERP_FILTER_MIN_WAVES > 0
+#define ERP_FILTER_WAVES __attribute__((amdgpu_waves_per_eu(ERP_FILTER_MIN_WAVES)))
 #else
 #define ERP_FILTER_WAVES
 #endif
