@@ -32,8 +32,8 @@ STAGE_KERNEL = {
     "knn2_filter": "knn2_filter_kernel",
     "knn2_rescore": "knn2_rescore_kernel", "knn2_merge": "knn2_merge_kernel",
     "bearings": "bearings_from_matches_kernel", "jump_prep": "jump_prep_kernel",
-    "windows": "sampler_window_kernel", "sampler": "sampler_kernel<false>", "gram": "gram_mfma_kernel",
-    "eigen": "eigen_kernel<false>", "valid_compact": "valid_compact_kernel",
+    "windows": "sampler_window_kernel", "sampler": "sampler_kernel<0>", "gram": "gram_mfma_kernel",
+    "eigen": "estimate_lite_kernel<false>", "valid_compact": "valid_place_kernel",
     "consensus_bounds": "consensus_bounds_kernel", "consensus_select": "consensus_select_kernel",
     "consensus_refine": "consensus_refine_kernel", "consensus_rows": "consensus_rows_kernel",
     "consensus_final": "consensus_final_kernel",
@@ -130,9 +130,9 @@ def main():
             n = len(disp[k])
             lines.append(f"{k:36s} dispatches={n:3d} " +
                          " ".join(f"{c}={x / n:.4g}" for c, x in sorted(v.items())))
-        smp = acc.get("sampler_kernel<false>")
+        smp = acc.get("sampler_kernel<0>")
         if smp and a.draws > 0:
-            n = len(disp["sampler_kernel<false>"])
+            n = len(disp["sampler_kernel<0>"])
             wd = a.draws / 64.0  # wave-level draws per launch
             lines.append(f"# sampler: {a.draws:.4g} draws per launch -> "
                          f"{smp['SQ_INSTS_VALU'] / n / wd:.2f} VALU and "
