@@ -105,12 +105,6 @@ hipError_t launch_knn2_merge(const Top2* part, const int64_t* off_q, const int64
                              erp_dmatch* matches, int32_t* counts, int32_t* flags,
                              int32_t* bcount, hipStream_t st,
                              const BearingOut* bo = nullptr);
-hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t* counts,
-                                        const erp_point2f* kp_l, const erp_point2f* kp_r,
-                                        const int64_t* off_l, const int64_t* off_r,
-                                        const int32_t* width, const int32_t* height,
-                                        const BatchShape& sh, double* pts, erp_point2f* key_l,
-                                        erp_point2f* key_r, hipStream_t st);
 hipError_t launch_bearings_direct(const erp_point2f* kl, const erp_point2f* kr, int32_t m,
                                   int32_t W, int32_t H, double* pts, hipStream_t st);
 hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_t* polyR,

@@ -72,33 +72,7 @@ __device__ int block_exclusive_scan(int v, int* ws, int* total) {
     return base + x - v;
 }
 
-// ============================================================== gather + bearings =======
-__global__ void bearings_from_matches_kernel(const erp_dmatch* __restrict__ matches,
-                                             const int32_t* __restrict__ counts,
-                                             const erp_point2f* __restrict__ kp_l,
-                                             const erp_point2f* __restrict__ kp_r,
-                                             const int64_t* __restrict__ off_l,
-                                             const int64_t* __restrict__ off_r,
-                                             const int32_t* __restrict__ width,
-                                             const int32_t* __restrict__ height, int max_nq,
-                                             double* __restrict__ pts, erp_point2f* key_l,
-                                             erp_point2f* key_r) {
-    const int p = blockIdx.y;
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m == 0) {  // zero sentinel row used to pad Gram batches
-        double* z = pts + ((size_t)p * (max_nq + 1) + max_nq) * 6;
-        for (int k = 0; k < 6; k++) z[k] = 0.0;
-    }
-    if (m >= counts[p]) return;
-    const erp_dmatch dm = matches[(size_t)p * max_nq + m];
-    const erp_point2f kl = kp_l[off_l[p] + dm.queryIdx];
-    const erp_point2f kr = kp_r[off_r[p] + dm.trainIdx];
-    double* o = pts + ((size_t)p * (max_nq + 1) + m) * 6;
-    pixel_to_bearing(width[p], height[p], kl.x, kl.y, o);
-    pixel_to_bearing(width[p], height[p], kr.x, kr.y, o + 3);
-    if (key_l) key_l[(size_t)p * max_nq + m] = kl;
-    if (key_r) key_r[(size_t)p * max_nq + m] = kr;
-}
+// (the batch pipeline's gather + bearings: knn2_merge_kernel since r05, matcher.hip)
 
 __global__ void bearings_direct_kernel(const erp_point2f* __restrict__ kl,
                                        const erp_point2f* __restrict__ kr, int m, int W, int H,
@@ -4745,18 +4719,6 @@ void init_constants() {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(c_pow2), pw, sizeof(pw));
 }
 
-
-hipError_t launch_bearings_from_matches(const erp_dmatch* matches, const int32_t* counts,
-                                        const erp_point2f* kp_l, const erp_point2f* kp_r,
-                                        const int64_t* off_l, const int64_t* off_r,
-                                        const int32_t* width, const int32_t* height,
-                                        const BatchShape& sh, double* pts, erp_point2f* key_l,
-                                        erp_point2f* key_r, hipStream_t st) {
-    dim3 grid((sh.max_nq + 255) / 256, sh.n_pairs);
-    ERP_LAUNCH(bearings_from_matches_kernel, grid, dim3(256), 0, st, matches, counts, kp_l,
-                       kp_r, off_l, off_r, width, height, sh.max_nq, pts, key_l, key_r);
-    return hipGetLastError();
-}
 
 hipError_t launch_bearings_direct(const erp_point2f* kl, const erp_point2f* kr, int32_t m,
                                   int32_t W, int32_t H, double* pts, hipStream_t st) {

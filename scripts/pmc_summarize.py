@@ -31,7 +31,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STAGE_KERNEL = {
     "knn2_filter": "knn2_filter_kernel",
     "knn2_rescore": "knn2_rescore_kernel", "knn2_merge": "knn2_merge_kernel",
-    "bearings": "bearings_from_matches_kernel", "jump_prep": "jump_prep_kernel",
+    "jump_prep": "jump_prep_kernel",
     "windows": "sampler_window_kernel", "sampler": "sampler_kernel<0>", "gram": "gram_mfma_kernel",
     "eigen": "estimate_lite_kernel<false>", "valid_compact": "valid_place_kernel",
     "consensus_bounds": "consensus_bounds_kernel", "consensus_select": "consensus_select_kernel",
