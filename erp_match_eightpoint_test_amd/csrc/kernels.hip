@@ -890,6 +890,149 @@ __global__ __launch_bounds__(64) void sampler_kernel(
     if (emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
 }
 
+// ---- split replay (round 5; launches of <= 256 workgroups, e.g. one pair) -------------------
+// A lone wave replays an iteration's M - 1 steps one after the other (~125 us at M ~ 3.4k).  The
+// steps i >= s only ever CLEAR bits of the bitmap (a step keeps i iff it is the last hit on its
+// position j < s, i.e. the first in the reverse order), so they split into segments: segment g
+// (blocks [nbd g / G, nbd (g + 1) / G) of the nbd all-draw blocks) is replayed exactly once its
+// start bitmap is known -- the positions < s that no earlier segment hit.  So kSplitG waves per
+// workgroup (64 iterations, one wave per segment) first collect their segment's hit set H_g
+// (one LDS OR per draw, no return, no wait), then, after one barrier, replay their segment with
+// the bitmap avail & ~(H_0 | ... | H_{g-1}); a last wave replays the prefix / mixed blocks that
+// follow with avail & ~(H_0 | ... | H_{G-1}) -- exactly the state the serial replay reaches there.
+// Each wave first walks the glibc window back to its segment (31 subtractions per block, ~0.1 of
+// a draw).  The selection words are the serial kernel's, word for word.
+#ifndef ERP_SPLIT_G
+#define ERP_SPLIT_G 3
+#endif
+constexpr int kSplitG = ERP_SPLIT_G;  // draw segments (+ 1 prefix wave: 4 waves, one per SIMD)
+
+template <bool I24, int RS = 8>
+__device__ __forceinline__ void split_hits_block(uint32_t (&ring)[31], uint32_t* bm, int lane,
+                                                 int i0, int s, const uint64_t (&c)[31]) {
+    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
+    uint32_t jj[31];
+    lat_positions<I24, true>(ring, i0, c, jj);
+#pragma unroll
+    for (int u = 0; u < 31; u++) {
+        const uint32_t j = min(jj[u], (uint32_t)s);  // (bit s: allocated, cleared below)
+        asm volatile("ds_or_b32 %0, %1" : : "v"(lds_word_addr<RS>(bm_lane, j)), "v"(1u << (j & 31))
+                     : "memory");
+    }
+}
+
+// the window walked back over one block without draws
+__device__ __forceinline__ void ring_skip_block(uint32_t (&ring)[31]) {
+#pragma unroll
+    for (int u = 0; u < 31; u++) {
+        const int slot = 30 - u;
+        ring[slot] = ring[slot] - ring[(slot + 28) % 31];
+    }
+}
+
+// blocks [b0, b1) of the replay (block b: steps M-1-31b .. M-31-31b; those below step 1 ignored),
+// each block's divisor constants fetched one block ahead as in sampler_kernel<2/3>
+template <typename F>
+__device__ __forceinline__ void lat_blocks(int M, int s, int b0, int b1,
+                                           const double* __restrict__ rtab, F&& fn) {
+    uint64_t ca[31] = {}, cb[31] = {};
+    auto live = [&](int b) { return b < b1 && M - 1 - 31 * b >= 1; };
+    auto kind = [&](int b) { return live(b) ? lat_kind(M - 1 - 31 * b, s) : 4; };
+    int b = b0;
+    int ka = kind(b);
+    if (live(b) && ka < 4) lat_fetch(rtab, M - 1 - 31 * b, ka, ca);
+    while (live(b)) {
+        const int kb = kind(b + 1);
+        lat_ready(ca);
+        if (live(b + 1) && kb < 4) lat_fetch(rtab, M - 1 - 31 * (b + 1), kb, cb);
+        fn(b, ka, ca);
+        b++;
+        if (!live(b)) break;
+        ka = kind(b + 1);
+        lat_ready(cb);
+        if (live(b + 1) && ka < 4) lat_fetch(rtab, M - 1 - 31 * (b + 1), ka, ca);
+        fn(b, kb, cb);
+        b++;
+    }
+}
+
+__global__ __launch_bounds__(64 * (kSplitG + 1)) void sampler_split_kernel(
+    const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins, int nwaves, int nbw,
+    double sample_frac, const double* __restrict__ rtab, uint32_t* __restrict__ selw,
+    int32_t* __restrict__ flags, int nalloc) {
+    extern __shared__ uint32_t sm[];  // H[G][nalloc][64], then B[G + 1][nalloc][64]
+    __shared__ int esum[64];
+    const int p = blockIdx.y, w = blockIdx.x, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int M = counts[p];
+    const int s = (int)(M * sample_frac);
+    if (s < 1 || M < 2) return;  // (uniform over the workgroup)
+    asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\ts_nop 3" ::: "memory");
+    const size_t reg = (size_t)nalloc * 64;
+    uint32_t* H = sm + (size_t)wv * reg;                    // (segment waves)
+    uint32_t* Bm = sm + (size_t)(kSplitG + wv) * reg;        // this wave's replay bitmap
+    auto avail = [&](int k) -> uint32_t {
+        return k < (s >> 5) ? ~0u : k == (s >> 5) ? (1u << (s & 31)) - 1u : 0u;
+    };
+    if (wv < kSplitG)
+        for (int k = 0; k < nalloc; k++) H[k * 64 + lane] = 0u;
+    if (wv == 0) esum[lane] = 0;
+    const int nbd = M - 31 - s >= 0 ? (M - 31 - s) / 31 + 1 : 0;  // all-draw blocks
+    const int bb = wv < kSplitG ? nbd * wv / kSplitG : nbd;
+    const int be = wv < kSplitG ? nbd * (wv + 1) / kSplitG : 0x7fffffff;
+    uint32_t ring[31];
+    {
+        const uint32_t* wi = wins + ((size_t)p * nwaves + w) * 31 * 64 + lane;
+#pragma unroll
+        for (int t = 0; t < 31; t++) ring[t] = wi[t * 64];
+    }
+    for (int b = 0; b < bb; b++) ring_skip_block(ring);
+    __syncthreads();  // (H and esum cleared)
+    // pass 1 (segment waves): the segment's hit set (positions clamped to s like the replay's)
+    uint32_t ring0[31];
+#pragma unroll
+    for (int t = 0; t < 31; t++) ring0[t] = ring[t];
+    if (wv < kSplitG)
+        lat_blocks(M, s, bb, be, rtab, [&](int b, int kind, const uint64_t(&c)[31]) {
+            const int i0 = M - 1 - 31 * b;
+            if (kind == 0) split_hits_block<true>(ring, H, lane, i0, s, c);
+            else split_hits_block<false>(ring, H, lane, i0, s, c);
+        });
+    // (the asm ORs are not in the compiler's count: drain them before the barrier)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();  // (every segment's hits in H)
+    // this wave's start bitmap: avail minus the hits of the segments before it (all of them for
+    // the prefix wave); bit s and the words past it stay clear
+    const int lim = wv < kSplitG ? wv : kSplitG;
+    for (int k = 0; k < nalloc; k++) {
+        uint32_t e = 0u;
+        for (int x = 0; x < lim; x++) e |= sm[(size_t)x * reg + k * 64 + lane];
+        Bm[k * 64 + lane] = avail(k) & ~e;
+    }
+    // pass 2: the exact replay of this wave's blocks (the words are the serial kernel's)
+#pragma unroll
+    for (int t = 0; t < 31; t++) ring[t] = ring0[t];
+    uint32_t* out = selw + ((size_t)p * nwaves + w) * (size_t)nbw * 64 + lane;
+    const int b0 = (M - 1) / 31, u0 = (M - 1) % 31;  // slot of position 0 (a prefix-wave block)
+    int emitted = 0;
+    uint32_t lastw = 0;
+    lat_blocks(M, s, bb, be, rtab, [&](int b, int kind, const uint64_t(&c)[31]) {
+        const uint32_t word = replay_block_lat<true, 8>(ring, Bm, lane, M - 1 - 31 * b, s, kind, rtab, c);
+        emitted += __builtin_popcount(word);
+        if (b == b0) lastw = word;
+        else out[(size_t)b * 64] = word;
+    });
+    if (wv == kSplitG) {
+        if (Bm[lane] & 1u) {  // position 0 still unresolved: its value 0 stays in the prefix
+            lastw |= 1u << u0;
+            emitted++;
+        }
+        out[(size_t)b0 * 64] = lastw;
+    }
+    atomicAdd(&esum[lane], emitted);
+    __syncthreads();
+    if (wv == kSplitG && esum[lane] != s) atomicOr(&flags[p], 2);  // internal consistency check
+}
+
 // the estimate of one iteration from its selected vector e (rank-2 fix, decomposition, Euler
 // angles, validity) into its hypothesis record
 // ---- counter-based sampler (ERP_SAMPLER_PHILOX) ------------------------------------------
@@ -4787,6 +4930,22 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
 #define ERP_SAMPLER_LAUNCH(M)                                                                  \
     ERP_LAUNCH(sampler_kernel<M>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts, wins, \
                nwaves, sh.sel_words, sample_frac, rtab, selw, flags, nwords)
+        // the split replay (sampler_split_kernel) where the launch has <= 256 workgroups of
+        // 64 iterations (one pair at <= 16k iterations) and its 7 bitmaps fit the CU's LDS;
+        // ERP_SAMPLER_SPLIT = 0 / 1 forces it off / on (when the LDS fits)
+        static const int split_env = getenv("ERP_SAMPLER_SPLIT") ? atoi(getenv("ERP_SAMPLER_SPLIT")) : -1;
+        const size_t split_lds = (size_t)(2 * kSplitG + 1) * nwords * 64 * sizeof(uint32_t);
+        const bool split = !ilp && split_env != 0 && split_lds <= 150 * 1024 &&
+                           (split_env > 0 || (long)nwaves * sh.n_pairs <= 256);
+        if (split) {
+            static std::atomic<size_t> split_set{0};
+            const hipError_t se = ensure_dyn_lds((const void*)sampler_split_kernel, split_lds, split_set);
+            if (se != hipSuccess) return se;
+            ERP_LAUNCH(sampler_split_kernel, dim3(nwaves, sh.n_pairs), dim3(64 * (kSplitG + 1)),
+                       split_lds, st, counts, wins, nwaves, sh.sel_words, sample_frac, rtab, selw,
+                       flags, nwords);
+            return hipGetLastError();
+        }
         switch (mode) {
             case 1: ERP_SAMPLER_LAUNCH(1); break;
             case 2: ERP_SAMPLER_LAUNCH(2); break;

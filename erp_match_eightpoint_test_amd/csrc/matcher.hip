@@ -411,6 +411,7 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
     };
     auto tile_mma = [&](const char* sb, int u) __attribute__((always_inline)) -> Acc2 {
         (void)tile_mma_f;
+        (void)tile_frags;
         bf16x8 ah[4];
 #pragma unroll
         for (int c = 0; c < 4; c++)
