@@ -330,6 +330,20 @@ typedef double StepDiv;
 __device__ __forceinline__ StepDiv step_div(const double* rtab, int d) { return rtab[d]; }
 __device__ __forceinline__ uint32_t mod_i24(uint32_t x, StepDiv c, int d) { return mod_rup_i24(x, c, d); }
 #endif
+// the d < 256 steps (round 5): the same magic quotient (the table and its exactness check cover
+// every d >= 2, x < 2^31) with the remainder by a full 32-bit multiply (the quotient exceeds
+// mad_i24's 24 bits) -- 4 integer ops instead of the fp64 reciprocal's conversions, multiply,
+// truncation and residual FMA.  ERP_SAMPLER_MAGIC=0 keeps the fp64 path everywhere.
+__device__ __forceinline__ uint32_t mod_small(uint32_t x, uint64_t mt, double r, int d) {
+#if ERP_SAMPLER_MAGIC
+    (void)r;
+    const uint32_t q = __umulhi(x, (uint32_t)mt) >> (uint32_t)(mt >> 32);
+    return x - q * (uint32_t)d;
+#else
+    (void)mt;
+    return mod_rup(x, r, (double)d);
+#endif
+}
 
 // One block of 31 reverse steps i0, i0-1, ..., i0-30 of one lane's replay (ring = the 31-word
 // glibc window, advanced backwards in place).  Returns the block's selection word: bit u set
@@ -399,7 +413,7 @@ __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uin
     StepDiv mt[31];  // (I24: the d >= 256 divisor constants)
 #pragma unroll
     for (int u = 0; u < 31; u++) {
-        if (I24) mt[u] = step_div(rtab, i0 - u + 1);
+        if (I24 || ERP_SAMPLER_MAGIC) mt[u] = step_div(rtab, i0 - u + 1);
         else rt[u] = rtab[i0 - u + 1];
     }
     const uint32_t zero = 0;
@@ -413,7 +427,7 @@ __device__ __forceinline__ uint32_t replay_block_draws(uint32_t (&ring)[31], uin
             const uint32_t rv = ring[slot];
             ring[slot] = rv - ring[(slot + 28) % 31];
             uint32_t j = I24 ? mod_i24(rv >> 1, mt[u], ii + 1)
-                             : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
+                             : mod_small(rv >> 1, (uint64_t)mt[u], ERP_SAMPLER_MAGIC ? 0.0 : rt[u], ii + 1);
             if (ERP_SAMPLER_CLAMP) j = min(j, (uint32_t)s);  // (bit s: clear and allocated)
             olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), 1u << (j & 31), zero);
             pos[u] = j;
@@ -496,7 +510,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix_rd(uint32_t (&ring)[31],
         if (u == 0 || u == 16)  // the reciprocals in two halves (SGPR pressure)
 #pragma unroll
             for (int k = u; k < (u == 0 ? 16 : 31); k++) {
-                if (I24) mt[k] = step_div(rtab, i0 - k + 1);
+                if (I24 || ERP_SAMPLER_MAGIC) mt[k] = step_div(rtab, i0 - k + 1);
                 else rt[k] = rtab[i0 - k + 1];
             }
         uint32_t rd;
@@ -509,7 +523,7 @@ __device__ __forceinline__ uint32_t replay_block_prefix_rd(uint32_t (&ring)[31],
         const uint32_t rv = ring[slot];
         ring[slot] = rv - ring[(slot + 28) % 31];
         const uint32_t j = I24 ? mod_i24(rv >> 1, mt[u], ii + 1)
-                               : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
+                               : mod_small(rv >> 1, (uint64_t)mt[u], ERP_SAMPLER_MAGIC ? 0.0 : rt[u], ii + 1);
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(rd), "+v"(prev));
         if (u > 0) nw |= __builtin_amdgcn_ubfe(prev, ppos, 1) << (u - 1);
         const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)rd, ii & 31, 1);  // bm[i]
@@ -536,8 +550,11 @@ __device__ __forceinline__ uint32_t replay_block_mixed(uint32_t (&ring)[31], uin
         const uint32_t rv = ring[slot];
         ring[slot] = rv - ring[(slot + 28) % 31];
         if (ii < 1) continue;
-        const double r = rtab[ii + 1];
-        uint32_t j = mod_rup(rv >> 1, r, (double)(ii + 1));
+#if ERP_SAMPLER_MAGIC
+        uint32_t j = mod_small(rv >> 1, (uint64_t)step_div(rtab, ii + 1), 0.0, ii + 1);
+#else
+        uint32_t j = mod_rup(rv >> 1, rtab[ii + 1], (double)(ii + 1));
+#endif
         if (ERP_SAMPLER_CLAMP) j = min(j, (uint32_t)s);
         // bm[i] (read before the clear: j = i keeps the bit)
         const uint32_t bi = ii < s ? (bm[bm_index<RS>(ii >> 5, lane)] >> (ii & 31)) & 1u : 0u;
@@ -675,7 +692,7 @@ __device__ __forceinline__ uint32_t replay_block_ilp(uint32_t (&ring)[31], uint3
 template <bool I24>
 __device__ __forceinline__ uint32_t lat_mod(uint32_t x, uint64_t c, int d) {
     if (I24) return mod_i24(x, __builtin_bit_cast(StepDiv, c), d);
-    return mod_rup(x, __builtin_bit_cast(double, c), (double)d);
+    return mod_small(x, c, __builtin_bit_cast(double, c), d);
 }
 
 // block kinds: 0 draws (d >= 256), 1 draws, 2 prefix (d >= 256), 3 prefix, 4 mixed / ending
@@ -688,8 +705,8 @@ __device__ __forceinline__ int lat_kind(int i, int s) {
 // the constants of block i0 (kinds 0-3: every d = i0 - u + 1 >= 2) by vector loads
 __device__ __forceinline__ void lat_fetch(const double* __restrict__ rtab, int i0, int kind,
                                           uint64_t (&c)[31]) {
-    const uint64_t* t = reinterpret_cast<const uint64_t*>(rtab) +
-                        ((kind == 0 || kind == 2) && ERP_SAMPLER_MAGIC ? kRecipTable : 0);
+    const uint64_t* t = reinterpret_cast<const uint64_t*>(rtab) + (ERP_SAMPLER_MAGIC ? kRecipTable : 0);
+    (void)kind;
     int d0 = i0 + 1;
     asm volatile("" : "+v"(d0));  // a VGPR index: global (vmcnt) loads, not scalar ones
 #pragma unroll
