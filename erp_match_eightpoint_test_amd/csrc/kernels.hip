@@ -922,6 +922,9 @@ __global__ __launch_bounds__(64) void sampler_kernel(
 #ifndef ERP_SPLIT_G
 #define ERP_SPLIT_G 3
 #endif
+#ifndef ERP_SPLIT_STAMPS
+#define ERP_SPLIT_STAMPS 0
+#endif
 constexpr int kSplitG = ERP_SPLIT_G;  // draw segments (+ 1 prefix wave: 4 waves, one per SIMD)
 
 template <bool I24, int RS = 8>
@@ -984,6 +987,10 @@ __global__ __launch_bounds__(64 * (kSplitG + 1)) void sampler_split_kernel(
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;  // (uniform over the workgroup)
     asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\ts_nop 3" ::: "memory");
+#if ERP_SPLIT_STAMPS
+    uint64_t ts[8];
+    ts[0] = __builtin_amdgcn_s_memtime();
+#endif
     const size_t reg = (size_t)nalloc * 64;
     uint32_t* H = sm + (size_t)wv * reg;                    // (segment waves)
     uint32_t* Bm = sm + (size_t)(kSplitG + wv) * reg;        // this wave's replay bitmap
@@ -1003,6 +1010,9 @@ __global__ __launch_bounds__(64 * (kSplitG + 1)) void sampler_split_kernel(
         for (int t = 0; t < 31; t++) ring[t] = wi[t * 64];
     }
     for (int b = 0; b < bb; b++) ring_skip_block(ring);
+#if ERP_SPLIT_STAMPS
+    ts[1] = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();  // (H and esum cleared)
     // pass 1 (segment waves): the segment's hit set (positions clamped to s like the replay's)
     uint32_t ring0[31];
@@ -1016,15 +1026,35 @@ __global__ __launch_bounds__(64 * (kSplitG + 1)) void sampler_split_kernel(
         });
     // (the asm ORs are not in the compiler's count: drain them before the barrier)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#if ERP_SPLIT_STAMPS
+    ts[2] = __builtin_amdgcn_s_memtime();
+#endif
     __syncthreads();  // (every segment's hits in H)
+#if ERP_SPLIT_STAMPS
+    ts[3] = __builtin_amdgcn_s_memtime();
+#endif
     // this wave's start bitmap: avail minus the hits of the segments before it (all of them for
     // the prefix wave); bit s and the words past it stay clear
+    // (words 8 at a time, every region's read of them issued before the first use: one LDS
+    // round trip per 8 words instead of one per read -- 15-18k cycles -> a few thousand)
     const int lim = wv < kSplitG ? wv : kSplitG;
-    for (int k = 0; k < nalloc; k++) {
-        uint32_t e = 0u;
-        for (int x = 0; x < lim; x++) e |= sm[(size_t)x * reg + k * 64 + lane];
-        Bm[k * 64 + lane] = avail(k) & ~e;
+    for (int k0 = 0; k0 < nalloc; k0 += 8) {
+        uint32_t e[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int x = 0; x < kSplitG; x++) {
+            if (x < lim) {
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    if (k0 + q < nalloc) e[q] |= sm[(size_t)x * reg + (k0 + q) * 64 + lane];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++)
+            if (k0 + q < nalloc) Bm[(k0 + q) * 64 + lane] = avail(k0 + q) & ~e[q];
     }
+#if ERP_SPLIT_STAMPS
+    ts[4] = __builtin_amdgcn_s_memtime();
+#endif
     // pass 2: the exact replay of this wave's blocks (the words are the serial kernel's)
 #pragma unroll
     for (int t = 0; t < 31; t++) ring[t] = ring0[t];
@@ -1038,6 +1068,9 @@ __global__ __launch_bounds__(64 * (kSplitG + 1)) void sampler_split_kernel(
         if (b == b0) lastw = word;
         else out[(size_t)b * 64] = word;
     });
+#if ERP_SPLIT_STAMPS
+    ts[5] = __builtin_amdgcn_s_memtime();
+#endif
     if (wv == kSplitG) {
         if (Bm[lane] & 1u) {  // position 0 still unresolved: its value 0 stays in the prefix
             lastw |= 1u << u0;
@@ -1048,6 +1081,12 @@ __global__ __launch_bounds__(64 * (kSplitG + 1)) void sampler_split_kernel(
     atomicAdd(&esum[lane], emitted);
     __syncthreads();
     if (wv == kSplitG && esum[lane] != s) atomicOr(&flags[p], 2);  // internal consistency check
+#if ERP_SPLIT_STAMPS  // (diagnostic builds only: one workgroup's phase times, in shader cycles)
+    if (blockIdx.x == 0 && blockIdx.y == 0 && lane == 0)
+        printf("split wave %d: skip %d pass1 %d barrier %d init %d pass2 %d (blocks %d..%d, M %d s %d)\n",
+               wv, (int)(ts[1] - ts[0]), (int)(ts[2] - ts[1]), (int)(ts[3] - ts[2]),
+               (int)(ts[4] - ts[3]), (int)(ts[5] - ts[4]), bb, be, M, s);
+#endif
 }
 
 // the estimate of one iteration from its selected vector e (rank-2 fix, decomposition, Euler
