@@ -913,8 +913,11 @@ std::vector<uint8_t> graph_key(const erp_ctx* c, const erp_pair_batch* b, float 
     key_put(k, c->refine_hint);
     key_put(k, c->flat_refs);
     key_put(k, c->fuse_sampler);
-    const char* sb_env = getenv("ERP_SMALL_BATCH");  // (run_consensus's route)
-    key_put(k, sb_env ? atoi(sb_env) : -1);
+    // the knobs read at every call (run_consensus's route, launch_sampler's kernel choice)
+    for (const char* name : {"ERP_SMALL_BATCH", "ERP_SAMPLER_SPLIT", "ERP_SAMPLER_LAT", "ERP_SAMPLER_ILP"}) {
+        const char* v = getenv(name);
+        key_put(k, v ? atoi(v) : -1);
+    }
     const DevBuf* all[] = {&c->mblk, &c->zsel, &c->part, &c->part1, &c->pu, &c->ccount, &c->cand,
                            &c->bsel, &c->edges, &c->gfin, &c->matches, &c->counts, &c->flags,
                            &c->pts, &c->polyR, &c->polyQ, &c->idx, &c->gram, &c->hyps, &c->rv,

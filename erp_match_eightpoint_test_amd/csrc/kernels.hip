@@ -4973,8 +4973,9 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         // ERP_SAMPLER_ILP=1: the blocks with their 31 positions computed first (A/B knob).
         // The latency blocks (modes 2 / 3) where the launch leaves most SIMDs with at most one
         // wave (<= 1024 waves); ERP_SAMPLER_LAT = 0 / 1 / 2 forces mode 0 / 2 / 3
-        static const bool ilp = getenv("ERP_SAMPLER_ILP") && atoi(getenv("ERP_SAMPLER_ILP")) != 0;
-        static const int lat_env = getenv("ERP_SAMPLER_LAT") ? atoi(getenv("ERP_SAMPLER_LAT")) : -1;
+        // (read at every launch, like ERP_SMALL_BATCH: the GPU tests switch them within a process)
+        const bool ilp = getenv("ERP_SAMPLER_ILP") && atoi(getenv("ERP_SAMPLER_ILP")) != 0;
+        const int lat_env = getenv("ERP_SAMPLER_LAT") ? atoi(getenv("ERP_SAMPLER_LAT")) : -1;
         const int lat = lat_env >= 0 ? lat_env : (long)nwaves * sh.n_pairs <= 1024 ? kSamplerLatMode : 0;
         const int mode = ilp ? 1 : lat == 1 ? 2 : lat == 2 ? 3 : 0;
         // (s up to 16 383 at the 65 535-keypoint cap: 515 words x 256 B = 129 KB)
@@ -4989,7 +4990,7 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         // the split replay (sampler_split_kernel) where the launch has <= 256 workgroups of
         // 64 iterations (one pair at <= 16k iterations) and its 7 bitmaps fit the CU's LDS;
         // ERP_SAMPLER_SPLIT = 0 / 1 forces it off / on (when the LDS fits)
-        static const int split_env = getenv("ERP_SAMPLER_SPLIT") ? atoi(getenv("ERP_SAMPLER_SPLIT")) : -1;
+        const int split_env = getenv("ERP_SAMPLER_SPLIT") ? atoi(getenv("ERP_SAMPLER_SPLIT")) : -1;
         const size_t split_lds = (size_t)(2 * kSplitG + 1) * nwords * 64 * sizeof(uint32_t);
         const bool split = !ilp && split_env != 0 && split_lds <= 150 * 1024 &&
                            (split_env > 0 || (long)nwaves * sh.n_pairs <= 256);

@@ -472,6 +472,40 @@ def test_sampler_gram_fused_equals_standalone(gpu_lib, sizes, iters):
     assert np.all(results_to_numpy(o["results"])["status"] == 0)
 
 
+@pytest.mark.parametrize("sizes,iters", [([4096], 2000), ([512, 700, 300, 1024], 300),
+                                         ([9000], 200), ([60000], 70)])
+def test_sampler_kernels_identical(gpu_lib, monkeypatch, sizes, iters):
+    """every glibc-replay sampler kernel gives the same sample sets and records: the throughput
+    blocks (sampler_kernel<0>, ERP_SAMPLER_LAT=0), the latency blocks step by step (<2>) and
+    positions first (<3>), and the split replay (sampler_split_kernel: segments replayed from
+    their start bitmaps, ERP_SAMPLER_SPLIT=1 -- skipped by the launcher where its bitmaps do not
+    fit the LDS, M = 60000); ragged sizes, partial waves, the d < 256 blocks, the straddling and
+    last blocks"""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
+    pairs = [synth.make_pair(4300 + i, n_kpts=n) for i, n in enumerate(sizes)]
+    args = _batch(pairs)
+    outs = {}
+    for name, env in (("lat0", {"ERP_SAMPLER_LAT": "0", "ERP_SAMPLER_SPLIT": "0"}),
+                      ("lat1", {"ERP_SAMPLER_LAT": "1", "ERP_SAMPLER_SPLIT": "0"}),
+                      ("lat2", {"ERP_SAMPLER_LAT": "2", "ERP_SAMPLER_SPLIT": "0"}),
+                      ("split", {"ERP_SAMPLER_SPLIT": "1"})):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        o = PairBatchRunner(ctx=Context(0), iters=iters).run(*args, want=("samples",))
+        torch.cuda.synchronize()
+        r = results_to_numpy(o["results"])
+        assert np.all(r["status"] == 0), name
+        outs[name] = (r.view(np.uint8).copy(), o["samples"].cpu().numpy())
+        for k in env:
+            monkeypatch.delenv(k)
+    ra, sa = outs["lat0"]
+    for name in ("lat1", "lat2", "split"):
+        rb, sb = outs[name]
+        assert np.array_equal(sa, sb), name
+        assert np.array_equal(ra, rb), name
+
+
 def test_batch_full_size_properties(ctx, oracle):
     """configs[1] shape: 4096 x 4096 keypoints, 10k iterations.  Size-independent checks:
     matches bit-exact vs the oracle, sampled sets of a spread of iterations vs the oracle's
