@@ -133,8 +133,12 @@ struct erp_ctx {
     size_t snap_bytes = 0;
     uint64_t surf_key = 0;    // (W, H, params) of the SURF layer table in extra[1]
     uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
-    // consensus zoom levels (0-2; ERP_ZOOM_LEVELS, an A/B knob)
-    int zoom = getenv("ERP_ZOOM_LEVELS") ? atoi(getenv("ERP_ZOOM_LEVELS")) : 1;
+    // consensus zoom levels of the survivors (0-2; ERP_ZOOM_LEVELS, an A/B knob).  0 since r05:
+    // with the hinted refine windows (r04) the survivors' zoom no longer pays for itself --
+    // same-box A/B per 768-pair step (profiles/r05w_ab_zoom.txt): consensus 5.81 / 5.87 -> 5.67 /
+    // 5.67 ms, worst-case batch 16.2 / 16.1k -> 16.6 / 16.5k pairs/s.  (The second pre-pruning
+    // stage's fine pass uses the zoom kernel either way.)
+    int zoom = getenv("ERP_ZOOM_LEVELS") ? atoi(getenv("ERP_ZOOM_LEVELS")) : 0;
     // the matcher's ratio test decided by the bf16 bounds where they suffice (A/B knob)
     bool bound_ratio = getenv("ERP_NO_BOUND_RATIO") == nullptr;
     // zoomed central references before the pre-pruning (opt-in ERP_ZOOM_REFS=1: measured no

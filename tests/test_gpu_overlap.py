@@ -127,3 +127,26 @@ def test_small_batch_route_equals_pruning_route(overlap_setup, monkeypatch):
         if f not in ("binned_rows", "survivors"):
             assert np.array_equal(a[f], c[f]), f
     assert np.all(a["binned_rows"] == a["K"]) and np.all(c["binned_rows"] < c["K"])
+
+
+def test_survivor_zoom_equals_no_zoom(overlap_setup, monkeypatch):
+    """the survivors' zoom stage (ERP_ZOOM_LEVELS=1, the default until r05; 2 = a second level)
+    only tightens bounds before the refine: every result field equals the default route's (0),
+    only the work count `survivors` may differ -- on a 48-pair sub-batch through the pruning
+    route"""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
+    _, subs = overlap_setup
+    b = subs[2]["b"]
+    args = (b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"], b["off_r"], b["width"],
+            b["height"], b["max_nq"], b["max_nt"])
+    res = {}
+    for zl in ("0", "1", "2"):
+        monkeypatch.setenv("ERP_ZOOM_LEVELS", zl)  # (read at context creation)
+        out = PairBatchRunner(ctx=Context(0), iters=ITERS).run(*args)
+        torch.cuda.synchronize()
+        res[zl] = results_to_numpy(out["results"])
+    for zl in ("1", "2"):
+        for f in res["0"].dtype.names:
+            if f != "survivors":
+                assert np.array_equal(res["0"][f], res[zl][f]), (zl, f)
