@@ -396,7 +396,7 @@ bool ensure_matcher(erp_ctx* c, const erp::BatchShape& sh) {
     if (c->matcher == ERP_MATCHER_VALU_EXACT)
         return ensure(c->part, PQ * sh.xchunks * sizeof(erp::Top2)) && ensure(c->part1, fold);
     return ensure(c->part, PQ * sh.fchunks * sizeof(erp::Top2)) && ensure(c->part1, fold) &&
-           ensure(c->pu, PQ * sh.fchunks * sizeof(float2)) &&
+           ensure(c->pu, PQ * sh.fchunks * sizeof(float2) + PQ * sizeof(float)) &&  // + |q|^2
            ensure(c->ccount, PQ * sh.fchunks * 2 * 4) &&
            ensure(c->cand, erp::knn2_cand_bytes(sh)) &&
            ensure(c->tsplit, erp::knn2_split_bytes(sh)) &&

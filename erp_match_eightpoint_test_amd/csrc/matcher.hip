@@ -286,7 +286,8 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
                                                           bf16x8* __restrict__ cval,
                                                           const bf16x8* __restrict__ sent_hi,
                                                           const float* __restrict__ sent_tu,
-                                                          int tile_array) {
+                                                          int tile_array,
+                                                          float* __restrict__ qn) {
     __shared__ __align__(16) char sm[2 * kFStageB];
     // XCD-aware block order: workgroups are dealt to the 8 XCDs round-robin by linear id, so
     // XCD x gets the contiguous logical range [x NB/8, (x+1) NB/8) (query blocks fastest, then
@@ -326,6 +327,10 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
             qh[j][c] = round8(a, b, 1.f);
         }
         qq += __shfl_xor(qq, 32, 64);
+        // |q|^2 for knn2_rescore (its bound offsets; the f32 rounding of either summation order
+        // is far inside the 2.1e-4 S slack), so that it reads the query row only when an exact
+        // distance is needed (queries the bounds reject never do)
+        if (ch == 0 && h == 0 && qv[j]) qn[(size_t)p * max_nq + qi[j]] = qq;
         QB[j] = __builtin_fmaf(qq, kFEps, qq) + kFTiny;
         const float QL = __builtin_fmaf(qq, -kFEps, qq) - kFTiny;
         cq[j] = QB[j] - (QL - teM);       // thr = G + cq (rounded up below)
@@ -643,7 +648,8 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                                                            const bf16x8* __restrict__ cval,
                                                            Top2* __restrict__ part,
                                                            int32_t* __restrict__ ovf, int qblocks,
-                                                           float ratio, int tile_array) {
+                                                           float ratio, int tile_array,
+                                                           const float* __restrict__ qn) {
     __shared__ int32_t plist[kPassList * 256];
     __shared__ float plb[kPassList * 256];
     // XCD-aware block order as in knn2_filter (a pair's blocks on one XCD: its f32 train rows,
@@ -681,14 +687,17 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
             m1 = fminf(m1, v.x);
         }
         const float U2 = m2;
+        // the query row only once an exact distance is needed (since r05; |q|^2 from the filter)
         float4 qr[16];
+        bool have_q = false;
         const float4* qp = reinterpret_cast<const float4*>(dq + (qbase + q) * kDim);
-        float qq = 0.f;
+        auto load_q = [&]() {
+            if (have_q) return;
 #pragma unroll
-        for (int k = 0; k < 16; k++) {
-            qr[k] = qp[k];
-            qq += qr[k].x * qr[k].x + qr[k].y * qr[k].y + qr[k].z * qr[k].z + qr[k].w * qr[k].w;
-        }
+            for (int k = 0; k < 16; k++) qr[k] = qp[k];
+            have_q = true;
+        };
+        const float qq = qn[(size_t)p * max_nq + q];
         // l* = u' + lq <= the row's l (knn2_filter header; lq's rounding is inside the slack)
         const float teM = __uint_as_float(tmax[p]) * (2.f * kFEps) * (1.f + kFMargin) + kFTiny;
         const float lq = (__builtin_fmaf(qq, -kFEps, qq) - kFTiny) - teM;
@@ -755,6 +764,7 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
             }
             const float lother = r1 == ra ? l2 : l1;
             if (umin < lother) {
+                load_q();
                 const float e = exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + ra) * kDim));
                 const float lb2 = fmaxf(lother, 0.f);
                 if (__builtin_sqrtf(e) < ratio * __builtin_sqrtf(lb2)) {
@@ -779,6 +789,7 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                 plist[kb * 256 + threadIdx.x] = plist[k * 256 + threadIdx.x];
                 plb[kb * 256 + threadIdx.x] = plb[k * 256 + threadIdx.x];
             }
+            load_q();
             top2_consider(exact_l2(qr, reinterpret_cast<const float4*>(dt + (tbase + row) * kDim)),
                           row, b0, j0, b1);
         }
@@ -1194,10 +1205,11 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
     cand_split(sh, cand, &ctile, &cval);
     const int qblocks = (sh.max_nq + kFQ - 1) / kFQ;
     if ((size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 >= (1ull << 31)) return hipErrorInvalidValue;
+    float* qn = (float*)(pu + (size_t)sh.n_pairs * sh.max_nq * sh.fchunks);  // (after pu)
     ERP_LAUNCH(knn2_filter_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
                        st, desc_q, thi, tn, tmax, off_q, off_t, sh.fchunk_len, sh.fchunks,
                        sh.max_nq, sh.max_nt, qblocks, pu, ccount, ctile, cval,
-                       (const bf16x8*)sent, (const float*)(sent + 128), (int)cand_tile_array());
+                       (const bf16x8*)sent, (const float*)(sent + 128), (int)cand_tile_array(), qn);
     return hipGetLastError();
 }
 
@@ -1214,7 +1226,8 @@ hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const i
                        st, desc_q, desc_t, off_q, off_t, sh.max_nq, sh.fchunk_len, sh.fchunks,
                        split_tmax(sh, split), pu, ccount, ctile, cval, part, ovf, qblocks,
                        sh.fchunks == 1 ? ratio : -1.f,  // (bound decisions need one chunk)
-                       (int)cand_tile_array());
+                       (int)cand_tile_array(),
+                       (const float*)(pu + (size_t)sh.n_pairs * sh.max_nq * sh.fchunks));
     ERP_LAUNCH(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
                        sh.max_nq, sh.fchunk_len, sh.fchunks, ovf, part);
     return hipGetLastError();
