@@ -1289,7 +1289,11 @@ constexpr int kGramWords = 2;                                   // selection wor
 constexpr int kGramWordBytes = kGramN * 32;                     // one word's limb image (7 KB)
 constexpr int kGramSelOff = kGramWords * kGramWordBytes;        // selection words in a slot
 constexpr int kGramSlotBytes = kGramSelOff + kGramWords * kGramIters * 4;
-constexpr int kGramRing = 3;
+#ifndef ERP_GRAM_RING
+#define ERP_GRAM_RING 3
+#endif
+constexpr int kGramRing = ERP_GRAM_RING;  // slots: DMAs issued kGramRing - 1 steps ahead
+static_assert(kGramRing >= 3, "ring");
 constexpr int kGramPieces = kGramSelOff / 1024;                 // 1-KB limb pieces per step
 static_assert(kGramPieces == 14, "14 limb pieces of 1 KB per step");
 static_assert(kGramWaves % 2 == 0 && kGramWaves <= 14, "2 words x (kGramWaves / 2) chunks");
@@ -1371,10 +1375,10 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
     const int boff = r * 32 + (((hh ^ (r >> 3)) & 1) << 4);
     for (int st = 0; st < nsteps; st++) {
         // step st's DMAs retired: the kGramRing - 2 later steps may fly (pieces + 1 each)
-        static_assert(kGramRing == 3, "vmcnt counts");
         constexpr int kBase = kGramPieces / kGramWaves + 1;
-        if (extra) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBase + 1) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBase) : "memory");
+        static_assert((kBase + 1) * (kGramRing - 2) <= 63, "vmcnt range");
+        if (extra) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kBase + 1) * (kGramRing - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBase * (kGramRing - 2)) : "memory");
         __builtin_amdgcn_s_barrier();
         issue(st + kGramRing - 1);  // into the slot every wave finished reading in step st - 1
         const int8_t* slot = lds + (st % kGramRing) * kGramSlotBytes;
