@@ -918,7 +918,7 @@ std::vector<uint8_t> graph_key(const erp_ctx* c, const erp_pair_batch* b, float 
     key_put(k, c->flat_refs);
     key_put(k, c->fuse_sampler);
     // the knobs read at every call (run_consensus's route, launch_sampler's kernel choice)
-    for (const char* name : {"ERP_SMALL_BATCH", "ERP_SAMPLER_SPLIT", "ERP_SAMPLER_LAT", "ERP_SAMPLER_ILP"}) {
+    for (const char* name : {"ERP_SMALL_BATCH", "ERP_SAMPLER_SPLIT", "ERP_SAMPLER_LAT", "ERP_SAMPLER_ILP", "ERP_GRAM_WT"}) {
         const char* v = getenv(name);
         key_put(k, v ? atoi(v) : -1);
     }

@@ -1264,11 +1264,11 @@ __global__ __launch_bounds__(256) void gram_limbs_kernel(const int32_t* __restri
     for (int k = tid; k < kGramN * 32 / 16; k += 256) o[k] = reinterpret_cast<const uint4*>(tile)[k];
 }
 
-// Block = kGramWaves waves x 32 iterations (one MFMA row tile each); K loop over the pair's
-// selection words, two words (64 rows, 14 MFMAs per wave) per step.  Operands reach LDS only by
+// Block = kGramWaves waves x 32 WT iterations (WT MFMA row tiles each); K loop over the pair's
+// selection words, two words (64 rows, 14 WT MFMAs per wave) per step.  Operands reach LDS only by
 // LDS-DMA (global_load_lds: the 14 KB limb images of the step's two words and the block's
-// 2 x 32 kGramWaves selection words) into a ring of kGramRing slots, issued kGramRing - 1 steps
-// ahead: the selection words stream from HBM once, and their latency is covered by the ring, not
+// 2 x 32 WT kGramWaves selection words) into a ring of GramCfg::kRing slots, issued kRing - 1
+// steps ahead: the selection words stream from HBM once, and their latency is covered by the ring, not
 // by occupancy.  The limb images are read once per block and step, so the block's iteration
 // count sets the L2 -> LDS traffic per MFMA.  One raw
 // barrier per step after a counted vmcnt (never 0 in the loop); all LDS in one __shared__ array.
@@ -1284,19 +1284,35 @@ __global__ __launch_bounds__(256) void gram_limbs_kernel(const int32_t* __restri
 #define ERP_GRAM_SCHED 0
 #endif
 constexpr int kGramWaves = ERP_GRAM_WAVES;                      // waves per block
-constexpr int kGramIters = 32 * kGramWaves;                     // iterations per block
 constexpr int kGramWords = 2;                                   // selection words per K step
 constexpr int kGramWordBytes = kGramN * 32;                     // one word's limb image (7 KB)
 constexpr int kGramSelOff = kGramWords * kGramWordBytes;        // selection words in a slot
-constexpr int kGramSlotBytes = kGramSelOff + kGramWords * kGramIters * 4;
 #ifndef ERP_GRAM_RING
 #define ERP_GRAM_RING 3
 #endif
-constexpr int kGramRing = ERP_GRAM_RING;  // slots: DMAs issued kGramRing - 1 steps ahead
-static_assert(kGramRing >= 3, "ring");
+#ifndef ERP_GRAM_MINBLOCKS
+#define ERP_GRAM_MINBLOCKS 3
+#endif
 constexpr int kGramPieces = kGramSelOff / 1024;                 // 1-KB limb pieces per step
 static_assert(kGramPieces == 14, "14 limb pieces of 1 KB per step");
-static_assert(kGramWaves % 2 == 0 && kGramWaves <= 14, "2 words x (kGramWaves / 2) chunks");
+// WT = 32-iteration row tiles per wave (round 5).  WT = 2: every B fragment read from LDS feeds
+// two MFMAs (14 accumulator tiles, 256 registers, 2 waves per SIMD), 256 iterations per block, a
+// 5-slot ring (80 KB: the epilogue's 256 Grams fit) and 2 blocks per CU -- gram 5.12 -> 4.72 ms
+// per step (profiles/r05f_ab_gram_wt.txt).  WT = 1 (32 iterations per wave, 3 blocks per CU)
+// keeps small launches (one pair: 79 blocks of 128 iterations, not 40 of 256) spread over the
+// CUs.  ERP_GRAM_WT = 1 / 2 forces one (default 0: by launch size, launch_gram_mfma).
+template <int WT>
+struct GramCfg {
+    static constexpr int kIters = 32 * kGramWaves * WT;         // iterations per block
+    static constexpr int kChunks = kIters / 64;                 // 64-iteration sampler waves
+    static constexpr int kSelPW = kGramWords * kChunks / kGramWaves;  // selection-word DMAs per wave
+    static constexpr int kRing = WT == 1 ? ERP_GRAM_RING : 5;   // slots: DMAs kRing - 1 steps ahead
+    static constexpr int kSlotBytes = kGramSelOff + kGramWords * kIters * 4;
+    static constexpr int kMinBlocks = WT == 1 ? ERP_GRAM_MINBLOCKS : 2;
+    static_assert(kRing >= 3, "ring");
+    static_assert(kIters % 64 == 0 && kGramWords * kChunks % kGramWaves == 0 && kGramWaves <= 14,
+                  "whole selection-word DMAs per wave");
+};
 // limb pieces moved by wave w: the first (14 % W) waves move one more
 constexpr int gram_pieces_of(int w) {
     return kGramPieces / kGramWaves + (w < kGramPieces % kGramWaves ? 1 : 0);
@@ -1308,15 +1324,14 @@ constexpr int gram_piece0(int w) {
 typedef __attribute__((address_space(3))) void* lds_vptr;
 typedef const __attribute__((address_space(1))) void* glb_vptr;
 
-#ifndef ERP_GRAM_MINBLOCKS
-#define ERP_GRAM_MINBLOCKS 3
-#endif
-__global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma_kernel(
+template <int WT>
+__global__ __launch_bounds__(64 * kGramWaves, GramCfg<WT>::kMinBlocks) void gram_mfma_kernel(
     const int32_t* __restrict__ counts, const int8_t* __restrict__ limbs,
     const uint32_t* __restrict__ selw, int iters, int nwaves, int nbw, double sample_frac,
     double* __restrict__ gram, int nhb, double* __restrict__ evec,
     erp_hypothesis* __restrict__ hyps, double valid_abs) {
-    __shared__ __align__(16) int8_t lds[kGramRing * kGramSlotBytes];
+    using C = GramCfg<WT>;
+    __shared__ __align__(16) int8_t lds[C::kRing * C::kSlotBytes];
     // XCD-aware block order (1-D grid of nhb iteration blocks x pairs): workgroups go to the 8
     // XCDs round-robin by linear id, so XCD x takes the contiguous logical range
     // [x NB/8, (x+1) NB/8) -- all iteration blocks of a pair on one XCD, whose L2 then holds the
@@ -1328,17 +1343,16 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
     const int M = counts[p];
     const int s = (int)(M * sample_frac);
     if (s < 1 || M < 2) return;
-    const int hb = (lbk % nhb) * kGramIters;
+    const int hb = (lbk % nhb) * C::kIters;
     if (hb >= iters) return;  // uniform over the block
     const int nb = (M - 1) / 31 + 1;
     const int nsteps = (nb + kGramWords - 1) / kGramWords;  // words read: <= 2 nsteps - 1 <= nb < nbw
-    const int h0 = hb + wv * 32;
+    const int h0 = hb + wv * 32 * WT;
     const int r = lane & 31, hh = lane >> 5;
     const int8_t* lg = limbs + (size_t)p * nbw * kGramWordBytes + lane * 16;
     // wave wv moves limb pieces gram_piece0(wv) .. + gram_pieces_of(wv) - 1 and the selection
-    // word (wv / (W/2)) of 64-iteration chunk (wv % (W/2)) (chunks past the last iteration are
-    // clamped: their rows are never stored)
-    constexpr int kChunks = kGramWaves / 2;
+    // words d = wv C::kSelPW + e: word d / C::kChunks of 64-iteration chunk d % C::kChunks
+    // (chunks past the last iteration are clamped: their rows are never stored)
     const int lp0 = [&] {
         int v = 0;
 #pragma unroll
@@ -1346,12 +1360,18 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
         return v;
     }();
     const bool extra = wv < kGramPieces % kGramWaves;  // moves kGramPieces / W + 1 pieces
-    const int chunk = min((hb >> 6) + (wv % kChunks), nwaves - 1);
-    const uint32_t* sg = selw + ((size_t)p * nwaves + chunk) * (size_t)nbw * 64 + lane;
-    const int soff = kGramSelOff + wv * 256;
+    const uint32_t* sg[C::kSelPW];
+#pragma unroll
+    for (int e = 0; e < C::kSelPW; e++) {
+        const int d = wv * C::kSelPW + e;
+        const int chunk = min((hb >> 6) + d % C::kChunks, nwaves - 1);
+        sg[e] = selw + ((size_t)p * nwaves + chunk) * (size_t)nbw * 64 + lane +
+                (size_t)(d / C::kChunks) * 64;
+    }
+    const int soff = kGramSelOff + wv * C::kSelPW * 256;
     auto issue = [&](int step) {
         const int sx = min(step, nsteps - 1);  // past the end: a harmless reload, never read
-        int8_t* slot = lds + (step % kGramRing) * kGramSlotBytes;
+        int8_t* slot = lds + (step % C::kRing) * C::kSlotBytes;
         const int8_t* src = lg + (size_t)sx * kGramSelOff;
 #pragma unroll
         for (int k = 0; k < kGramPieces / kGramWaves; k++)
@@ -1361,27 +1381,30 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
             __builtin_amdgcn_global_load_lds(
                 (glb_vptr)(src + (lp0 + kGramPieces / kGramWaves) * 1024),
                 (lds_vptr)(slot + (lp0 + kGramPieces / kGramWaves) * 1024), 16, 0, 0);
-        __builtin_amdgcn_global_load_lds(
-            (glb_vptr)(sg + (size_t)(sx * kGramWords + wv / kChunks) * 64), (lds_vptr)(slot + soff),
-            4, 0, 0);
+#pragma unroll
+        for (int e = 0; e < C::kSelPW; e++)
+            __builtin_amdgcn_global_load_lds((glb_vptr)(sg[e] + (size_t)(sx * kGramWords) * 64),
+                                             (lds_vptr)(slot + soff + e * 256), 4, 0, 0);
     };
-    i32x16 acc[kGramTiles];
+    i32x16 acc[WT][kGramTiles];
 #pragma unroll
-    for (int t = 0; t < kGramTiles; t++)
+    for (int w = 0; w < WT; w++)
 #pragma unroll
-        for (int k = 0; k < 16; k++) acc[t][k] = 0;
+        for (int t = 0; t < kGramTiles; t++)
 #pragma unroll
-    for (int k = 0; k < kGramRing - 1; k++) issue(k);
+            for (int k = 0; k < 16; k++) acc[w][t][k] = 0;
+#pragma unroll
+    for (int k = 0; k < C::kRing - 1; k++) issue(k);
     const int boff = r * 32 + (((hh ^ (r >> 3)) & 1) << 4);
     for (int st = 0; st < nsteps; st++) {
-        // step st's DMAs retired: the kGramRing - 2 later steps may fly (pieces + 1 each)
-        constexpr int kBase = kGramPieces / kGramWaves + 1;
-        static_assert((kBase + 1) * (kGramRing - 2) <= 63, "vmcnt range");
-        if (extra) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kBase + 1) * (kGramRing - 2)) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBase * (kGramRing - 2)) : "memory");
+        // step st's DMAs retired: the C::kRing - 2 later steps may fly (pieces + 1 each)
+        constexpr int kBase = kGramPieces / kGramWaves + C::kSelPW;
+        static_assert((kBase + 1) * (C::kRing - 2) <= 63, "vmcnt range");
+        if (extra) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kBase + 1) * (C::kRing - 2)) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kBase * (C::kRing - 2)) : "memory");
         __builtin_amdgcn_s_barrier();
-        issue(st + kGramRing - 1);  // into the slot every wave finished reading in step st - 1
-        const int8_t* slot = lds + (st % kGramRing) * kGramSlotBytes;
+        issue(st + C::kRing - 1);  // into the slot every wave finished reading in step st - 1
+        const int8_t* slot = lds + (st % C::kRing) * C::kSlotBytes;
         // every B fragment of the step in flight at once (the MFMAs then wait on counted
         // lgkmcnts): the step's LDS latency is exposed once, not once per fragment pair
         i32x4 bf[kGramWords][kGramTiles];
@@ -1391,19 +1414,24 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
             for (int t = 0; t < kGramTiles; t++)
                 bf[i][t] = *reinterpret_cast<const i32x4*>(slot + i * kGramWordBytes +
                                                            t * 32 * 32 + boff);
-        uint32_t wsel[kGramWords];  // read after the fragments: one wait covers the step
+        uint32_t wsel[WT][kGramWords];  // read after the fragments: one wait covers the step
 #pragma unroll
-        for (int i = 0; i < kGramWords; i++)
-            wsel[i] = reinterpret_cast<const uint32_t*>(slot + kGramSelOff)[i * kGramIters + wv * 32 + r];
-        i32x4 a[kGramWords];
+        for (int w = 0; w < WT; w++)
 #pragma unroll
-        for (int i = 0; i < kGramWords; i++) {
-            const uint32_t wm = (st * kGramWords + i < nb) ? 0xffffu : 0u;  // words past nb
-            const uint32_t bits = (wsel[i] >> (16 * hh)) & wm;
+            for (int i = 0; i < kGramWords; i++)
+                wsel[w][i] = reinterpret_cast<const uint32_t*>(slot + kGramSelOff)[
+                    i * C::kIters + (wv * WT + w) * 32 + r];
+        i32x4 a[WT][kGramWords];
 #pragma unroll
-            for (int v = 0; v < 4; v++)
-                a[i][v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
-        }
+        for (int w = 0; w < WT; w++)
+#pragma unroll
+            for (int i = 0; i < kGramWords; i++) {
+                const uint32_t wm = (st * kGramWords + i < nb) ? 0xffffu : 0u;  // words past nb
+                const uint32_t bits = (wsel[w][i] >> (16 * hh)) & wm;
+#pragma unroll
+                for (int v = 0; v < 4; v++)
+                    a[w][i][v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
+            }
 #if ERP_GRAM_SCHED
         __builtin_amdgcn_sched_group_barrier(0x100, kGramWords * (kGramTiles + 1), 0);  // LDS reads
         __builtin_amdgcn_sched_group_barrier(0x002, 4 * kGramWords * 4, 0);            // VALU
@@ -1413,7 +1441,9 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
         for (int i = 0; i < kGramWords; i++)
 #pragma unroll
             for (int t = 0; t < kGramTiles; t++)
-                acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], bf[i][t], acc[t], 0, 0, 0);
+#pragma unroll
+                for (int w = 0; w < WT; w++)
+                    acc[w][t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[w][i], bf[i][t], acc[w][t], 0, 0, 0);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the ring's tail DMAs
     // recombine: row = (k & 3) + 8 (k >> 2) + 4 hh; entry r from tiles 0..5 of this lane,
@@ -1425,18 +1455,20 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
         // on one iteration per lane.  Only the lanes that do not settle write their Gram to HBM
         // (for eigen_fallback_kernel, which finds them by the NaN in evec).  hyps != NULL: the
         // settled lanes also run the estimate (estimate_kernel's work) here.
-        constexpr int kStg = kGramIters + 1;  // [36][kStg] doubles: odd stride, no bank conflicts
-        static_assert(36 * kStg * 8 <= kGramRing * kGramSlotBytes, "Gram stage fits the ring");
+        constexpr int kStg = C::kIters + 1;  // [36][kStg] doubles: odd stride, no bank conflicts
+        static_assert(36 * kStg * 8 <= C::kRing * C::kSlotBytes, "Gram stage fits the ring");
         double* stg = reinterpret_cast<double*>(lds);
         __syncthreads();  // every wave's last fragment reads have returned
 #pragma unroll
+        for (int w = 0; w < WT; w++)
+#pragma unroll
         for (int k = 0; k < 16; k++) {
-            const int row = wv * 32 + (k & 3) + 8 * (k >> 2) + 4 * hh;
+            const int row = (wv * WT + w) * 32 + (k & 3) + 8 * (k >> 2) + 4 * hh;
             long long v = 0;
 #pragma unroll
-            for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[t][k] << (8 * t);
+            for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[w][t][k] << (8 * t);
             long long v2 = 0;
-            const int x = acc[kGramLimbs][k];
+            const int x = acc[w][kGramLimbs][k];
 #pragma unroll
             for (int t = 0; t < kGramLimbs; t++)
                 v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
@@ -1444,7 +1476,7 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
             if (r < 4) stg[(32 + r) * kStg + row] = (double)v2 * (1.0 / kGramScale);
         }
         __syncthreads();
-        if (wv >= kGramIters / 64) return;
+        if (wv >= C::kIters / 64) return;
         const int hl = wv * 64 + lane, h = hb + hl;
         double e[9];
         const bool ok = gram_min_eigvec9_inv(stg, kStg, hl, e);
@@ -1464,13 +1496,15 @@ __global__ __launch_bounds__(64 * kGramWaves, ERP_GRAM_MINBLOCKS) void gram_mfma
         return;
     }
 #pragma unroll
+    for (int w = 0; w < WT; w++)
+#pragma unroll
     for (int k = 0; k < 16; k++) {
-        const int row = (k & 3) + 8 * (k >> 2) + 4 * hh;
+        const int row = w * 32 + (k & 3) + 8 * (k >> 2) + 4 * hh;
         long long v = 0;
 #pragma unroll
-        for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[t][k] << (8 * t);
+        for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[w][t][k] << (8 * t);
         long long v2 = 0;
-        const int x = acc[kGramLimbs][k];
+        const int x = acc[w][kGramLimbs][k];
 #pragma unroll
         for (int t = 0; t < kGramLimbs; t++)
             v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
@@ -5081,10 +5115,21 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
     const int nwaves = (sh.iters + 63) / 64;
     ERP_LAUNCH(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
                        pts, sh.max_nq, sh.sel_words, limbs);
-    const int nhb = (sh.iters + kGramIters - 1) / kGramIters;
-    ERP_LAUNCH(gram_mfma_kernel, dim3(nhb * sh.n_pairs), dim3(64 * kGramWaves), 0, st, counts, limbs,
-                       selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb, evec, hyps,
-                       valid_abs);
+    // row tiles per wave: 2 once the wide blocks give every CU two of them (GramCfg)
+    const char* wt_env = getenv("ERP_GRAM_WT");
+    const int wt_force = wt_env ? atoi(wt_env) : 0;
+    const int nhb2 = (sh.iters + GramCfg<2>::kIters - 1) / GramCfg<2>::kIters;
+    const bool wide = wt_force == 2 || (wt_force != 1 && (long long)nhb2 * sh.n_pairs >= 2 * 256);
+    if (wide) {
+        ERP_LAUNCH(gram_mfma_kernel<2>, dim3(nhb2 * sh.n_pairs), dim3(64 * kGramWaves), 0, st, counts,
+                   limbs, selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb2, evec, hyps,
+                   valid_abs);
+    } else {
+        const int nhb = (sh.iters + GramCfg<1>::kIters - 1) / GramCfg<1>::kIters;
+        ERP_LAUNCH(gram_mfma_kernel<1>, dim3(nhb * sh.n_pairs), dim3(64 * kGramWaves), 0, st, counts,
+                   limbs, selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb, evec, hyps,
+                   valid_abs);
+    }
     if (samples)
         ERP_LAUNCH(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
                            sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);
