@@ -32,7 +32,7 @@ STAGE_KERNEL = {
     "knn2_filter": "knn2_filter_kernel",
     "knn2_rescore": "knn2_rescore_kernel", "knn2_merge": "knn2_merge_kernel",
     "jump_prep": "jump_prep_kernel",
-    "windows": "sampler_window_kernel", "sampler": "sampler_kernel<0>", "gram": "gram_mfma_kernel",
+    "windows": "sampler_window_kernel", "sampler": "sampler_kernel<0>", "gram": "gram_mfma_kernel<2>",
     "eigen": "estimate_lite_kernel<false>", "valid_compact": "valid_place_kernel",
     "consensus_bounds": "consensus_bounds_kernel", "consensus_select": "consensus_select_kernel",
     "consensus_refine": "consensus_refine_kernel", "consensus_rows": "consensus_rows_kernel",
