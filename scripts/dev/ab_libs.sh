@@ -17,5 +17,5 @@ for r in $(seq 1 $ROUNDS); do for v in $LIBS; do
   ERP_LIB_PATH=scripts/dev/libs/$v/liberp_match.so timeout -k 10 400 python bench.py --no-cpu-baseline --steps 5 \
     --warmup 2 --hard-steps 0 --worst-steps 0 > gpurun_out/ab_$v$r.json 2> gpurun_out/ab_$v$r.err \
     || { tail -20 gpurun_out/ab_$v$r.err; exit 1; }
-  echo "$v$r $(python -c "import json;d=json.load(open('gpurun_out/ab_$v$r.json'));s=d['stages_ms_serial_step'];print(round(d['value']), round(d['ms_per_step'],2), '$STAGE', round(s['$STAGE'],3))")"
+  echo "$v$r $(python -c "import json;d=json.load(open('gpurun_out/ab_$v$r.json'));s=d['stages_ms_serial_step'];print(round(d['value']), round(d['ms_per_step'],2), '$STAGE', round(s['$STAGE'],3), 'rescore', round(s['knn2_rescore'],3))")"
 done; done
