@@ -84,6 +84,15 @@ def parse():
                     help="exact k=2 method: bf16-MFMA filter + rescoring, or the packed-FP32 sweep")
     ap.add_argument("--no-shard-consensus", action="store_true",
                     help="manual workload: replicate the consensus on every rank")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="N > 1: the process group's backend.  nccl (= RCCL) is the product path, "
+                         "one rank per GPU; gloo (collectives on host copies) with "
+                         "--ranks-on-device lets several ranks share one GPU, to rehearse the "
+                         "multi-rank launcher, gather and checks on a 1-GPU box (not a scaling "
+                         "number)")
+    ap.add_argument("--ranks-on-device", type=int, default=-1,
+                    help="N > 1, development: every rank uses this HIP device instead of "
+                         "LOCAL_RANK's (with --dist-backend gloo: RCCL refuses two ranks on one GPU)")
     ap.add_argument("--workload", choices=["pairs", "dense", "manual", "remap", "e2e"],
                     default="pairs",
                     help="pairs: configs[1] (the metric; configs[2] with --kpts 2048); dense: "
@@ -332,9 +341,9 @@ def run_dense(args):
         ctx.set_profiling(False)
         outs[name] = out.cpu().numpy()
         if name == "mfma":
-            kern = st.get("knn2_filter", 0) + st.get("knn2_candidates", 0)
-            work = 2 * 2.0 * n * n * 64  # two bf16 MFMA passes, 2 N T 64 flops each
-            roof = {"bound": "mfma", "kernels": "knn2_filter + knn2_candidates", "peak": PEAK_BF16_MFMA,
+            kern = st.get("knn2_filter", 0)
+            work = 2.0 * n * n * 64  # ONE bf16 MFMA pass: 2 N T 64 flops
+            roof = {"bound": "mfma", "kernels": "knn2_filter", "peak": PEAK_BF16_MFMA,
                     "unit": "TFLOP/s", "achieved": work / (kern / 1e3) / 1e12}
         else:
             kern = st.get("knn2_exact", 0)
@@ -614,7 +623,11 @@ def main():
     if args.gpus > 1 and args.workload in ("dense", "remap", "e2e"):
         raise SystemExit(f"bench.py: workload {args.workload} is single-GPU (--gpus 1)")
     import torch
-    if torch.cuda.device_count() < args.gpus:
+    if args.ranks_on_device >= 0 and args.dist_backend != "gloo":
+        raise SystemExit("bench.py: --ranks-on-device needs --dist-backend gloo (RCCL refuses "
+                         "two ranks on one GPU)")
+    need = args.ranks_on_device + 1 if args.ranks_on_device >= 0 else args.gpus
+    if torch.cuda.device_count() < need:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but only {torch.cuda.device_count()} "
                          "HIP device(s) visible")
     if args.workload == "dense":
@@ -628,12 +641,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.ranks_on_device >= 0:
+        local = args.ranks_on_device
     dist = None
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-        world = dist.get_world_size()  # the RCCL world actually formed
+        dist.init_process_group(args.dist_backend)
+        world = dist.get_world_size()  # the world actually formed
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 
@@ -654,6 +669,11 @@ def main():
         runner.reserve(len(part), b["max_nq"], b["max_nt"])
         subs.append(dict(b=b, ctx=ctx, runner=runner, stream=torch.cuda.Stream(dev),
                          res=torch.empty((len(part), 64), dtype=torch.uint8, device=dev)))
+
+    coll_dev = torch.device("cpu") if args.dist_backend == "gloo" else dev
+
+    def gather(o):  # the records' all-gather (host copies under gloo)
+        return D.gather_records(o.to(coll_dev))
 
     def call(batch=None):
         for i, sb in enumerate(subs):
@@ -684,7 +704,7 @@ def main():
             continue
         out = call()
         if dist is not None:
-            gathered = D.gather_records(out)
+            gathered = gather(out)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -694,7 +714,7 @@ def main():
     for _ in range(args.steps):
         out = call()
         if dist is not None:
-            gathered = D.gather_records(out)
+            gathered = gather(out)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -731,10 +751,22 @@ def main():
             if f not in ("binned_rows", "survivors"):
                 bad |= np.any((a[f] != c[f]).reshape(len(a), -1), axis=1)
         timed_result_diff = np.nonzero(bad)[0].tolist()
+    ranks_timed = None
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        # every rank's timed-vs-serial comparison, not only rank 0's: [ranks whose timed
+        # records differ from their serial pass, ranks whose RESULT fields differ, total pairs
+        # whose result fields differ]
+        flags = torch.tensor([0 if timed_identical is not False else 1,
+                              1 if timed_result_diff else 0,
+                              len(timed_result_diff or [])], dtype=torch.int64, device=coll_dev)
+        dist.all_reduce(flags, op=dist.ReduceOp.SUM)
+        f = [int(x) for x in flags.tolist()]
+        ranks_timed = {"ranks": world, "ranks_records_differ": f[0],
+                       "ranks_result_fields_differ": f[1], "pairs_result_fields_differ": f[2],
+                       "timed_records_identical": f[0] == 0}
     res = results_to_numpy(out)
     ok = bool(np.all(res["status"] == 0))
     err_deg = [float(np.degrees(np.abs(r["R"] - p["euler_gt"])).mean()) for r, p in zip(res, pairs)]
@@ -938,7 +970,12 @@ def main():
                                                             multi["oracle_all_equal"]),
                   "fields": "first pair of every rank's block: gathered record byte-identical "
                             "to a rank-0 recomputation; status, M, K, min_idx equal and R, T "
-                            "within 2e-6 of the oracle"}
+                            "within 2e-6 of the oracle",
+                  # every rank's timed step == its own serial pass, all-reduced (all pairs)
+                  "timed_records_identical": ranks_timed["timed_records_identical"],
+                  "timed_all_ranks": ranks_timed}
+        multi["dist_backend"] = args.dist_backend
+        multi["ranks_on_device"] = args.ranks_on_device if args.ranks_on_device >= 0 else None
     if world == 1 and not args.no_cpu_baseline:
         # the oracle's pairs: the first pair of every sub-batch, then the second of every
         # sub-batch, ... (every stream of the timed step is checked, not just sub-batch 0)
@@ -999,7 +1036,9 @@ def main():
                    "streams": S, "matcher": args.matcher,
                    "parallelism": f"pair-sharded x{world}", "sampler": ("glibc replay (seed 1)" if SAMPLER == 0
                                else "Philox4x32-10 + Floyd (seed 1; no reference counterpart)"),
-                   "rccl_world": world if dist is not None else None,
+                   "rccl_world": world if dist is not None and args.dist_backend == "nccl" else None,
+                   "dist_backend": args.dist_backend if dist is not None else None,
+                   "ranks_on_device": args.ranks_on_device if args.ranks_on_device >= 0 else None,
                    "profile_tag": args.profile_tag,
                    "inlier_frac": args.inlier_frac, "sigma": args.sigma},
         "roofline": roof,
