@@ -93,6 +93,9 @@ def parse():
     ap.add_argument("--ranks-on-device", type=int, default=-1,
                     help="N > 1, development: every rank uses this HIP device instead of "
                          "LOCAL_RANK's (with --dist-backend gloo: RCCL refuses two ranks on one GPU)")
+    ap.add_argument("--ctx-option", action="append", default=[], metavar="NAME=VALUE",
+                    help="erp_ctx_set_option on every context the bench makes (route options, "
+                         "capi.OPTIONS: same results, for A/B runs; e.g. lip2=0)")
     ap.add_argument("--workload", choices=["pairs", "dense", "manual", "remap", "e2e"],
                     default="pairs",
                     help="pairs: configs[1] (the metric; configs[2] with --kpts 2048); dense: "
@@ -159,13 +162,6 @@ def stage_work(stage, B, kpts, iters, res):
         flops = float(np.sum(nb * K * 8.0))  # 3 sub, 3 mul, 2 add per squared distance
         return flops, "TFLOP/s", PEAK_FP32_VALU_UNFUSED, "valu", \
             "8 fp32 ops per binned squared distance (binned_rows x K)"
-    if stage == "sampler_gram":
-        # the fused kernel: bound by the replay's VALU issue; its int8 MFMA work is reported
-        # beside (roofline["mfma_frac"])
-        ops = float(np.sum((M - 1) * iters * 4.0))
-        return ops, "Top/s", PEAK_VALU_OPS, "valu", \
-            "4 int/fp64 lane-ops per rand() draw (floor) of the fused sampler+Gram kernel; " \
-            "peak = wave64 2-cycle VALU issue"
     if stage == "sampler" and SAMPLER == 1:
         s = np.floor(M * 0.25)
         ops = float(np.sum(s * iters * 27.0))
@@ -213,6 +209,16 @@ def host_cpu_share():
 
 
 SAMPLER = 0  # erp_ransac_cfg.sampler of every run (--sampler): 0 glibc replay, 1 Philox
+CTX_OPTIONS: dict = {}  # --ctx-option: applied to every context by make_ctx
+
+
+def make_ctx(device: int, **extra):
+    """a Context with the --ctx-option route options (and `extra`) applied"""
+    from erp_match_eightpoint_test_amd import Context
+    ctx = Context(device)
+    for k, v in {**CTX_OPTIONS, **extra}.items():
+        ctx.set_option(k, v)
+    return ctx
 
 
 def oracle_pair(p, iters, nthreads):
@@ -325,7 +331,7 @@ def run_dense(args):
     methods = {}
     outs = {}
     for name, m in (("mfma", capi.MATCHER_MFMA_FILTER), ("valu", capi.MATCHER_VALU_EXACT)):
-        ctx = Context(0)
+        ctx = make_ctx(0)
         fm = feature_matcher(ctx=ctx, method=m)
         for _ in range(args.warmup):
             out = fm._match_device(q, t, 0.3)
@@ -388,7 +394,7 @@ def run_manual(args):
     c = synth.make_correspondences(args.seed, m=100, outlier_frac=0.6)
     kl = torch.from_numpy(c["kp_l"]).to(dev)
     kr = torch.from_numpy(c["kp_r"]).to(dev)
-    ctx = Context(local)
+    ctx = make_ctx(local)
 
     def step():
         return D.find_hypothesis_sharded_dev(ctx, c["W"], c["H"], kl, kr, 100, iters,
@@ -436,7 +442,7 @@ def run_manual(args):
     if rank == 0:
         # the unsharded find() on this GPU must give the same winner (outside the timed region)
         from erp_match_eightpoint_test_amd import eight_point
-        ep = eight_point(ctx=Context(local), iters=iters)
+        ep = eight_point(ctx=make_ctx(local), iters=iters)
         R1, T1 = ep.find(c["W"], c["H"], c["kp_l"], c["kp_r"])
         line = {"metric": f"find() calls/sec, {iters // 1000}k-iteration RANSAC on 100 manual-pickup "
                           "correspondences (60% outliers), hypothesis blocks sharded (configs[4])",
@@ -470,7 +476,7 @@ def run_remap(args):
     H, W, B = 2688, 5376, 16
     g = torch.Generator(device="cpu").manual_seed(args.seed)
     ims = torch.randint(0, 256, (B, H, W, 3), dtype=torch.uint8, generator=g).to(dev)
-    ctx = Context(0)
+    ctx = make_ctx(0)
     ss, er = spherical_surf(ctx=ctx), erp_rotation(ctx=ctx)
     bands = torch.zeros((B, 4, H // 4, W, 3), dtype=torch.uint8, device=dev)
     L = ctx.L
@@ -530,7 +536,7 @@ def run_e2e(args):
     dev = torch.device("cuda:0")
     H, W, B = 2688, 5376, 4
     rng = np.random.default_rng(args.seed)
-    ctx = Context(0)
+    ctx = make_ctx(0)
     ss, er, fm = spherical_surf(ctx=ctx), erp_rotation(ctx=ctx), feature_matcher(ctx=ctx)
     ep = eight_point(ctx=ctx, iters=args.iters)
     lefts, rights = [], []
@@ -617,6 +623,9 @@ def main():
     args = parse()
     global SAMPLER
     SAMPLER = 1 if args.sampler == "philox" else 0
+    for kv in args.ctx_option:
+        k, v = kv.split("=", 1)
+        CTX_OPTIONS[k] = int(v)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(_launch_ranks(args))
     check_world(args)
@@ -663,7 +672,7 @@ def main():
     subs = []
     for part in parts:  # one context (scratch) and one HIP stream per sub-batch
         b = to_device(part, dev)
-        ctx = Context(local)
+        ctx = make_ctx(local)
         ctx.set_matcher(0 if args.matcher == "mfma" else 1)
         runner = PairBatchRunner(ctx=ctx, iters=args.iters, sampler=SAMPLER)
         runner.reserve(len(part), b["max_nq"], b["max_nt"])
@@ -796,12 +805,6 @@ def main():
             roof["traffic_missing"] = f"profiles/{args.profile_tag}_pmc_{dom}.json"
         if peak == PEAK_VALU_OPS:
             roof["frac_vs_4cycle_issue"] = achieved / PEAK_VALU_OPS_4CYC
-        if dom == "sampler_gram":  # the MFMA half of the fused kernel against its own roof
-            g = stage_work("gram", args.pairs, args.kpts, args.iters, res)
-            gops = g[0] / stages[dom][1]
-            roof["mfma_achieved"] = gops / avg_s / 1e12
-            roof["mfma_peak"] = PEAK_I8_MFMA
-            roof["mfma_frac"] = roof["mfma_achieved"] / PEAK_I8_MFMA
     stage_roofs = {}
     for k in stages:
         w = stage_work(k, args.pairs, args.kpts, args.iters, res)
@@ -820,7 +823,7 @@ def main():
         b1 = to_device(pairs[:1], dev)
 
         def lat_run(graphs: bool) -> tuple:
-            ctx1 = Context(local)
+            ctx1 = make_ctx(local)
             ctx1.set_matcher(0 if args.matcher == "mfma" else 1)
             ctx1.set_graphs(graphs)  # erp_ctx_set_graphs: replay the captured launch sequence
             run1 = PairBatchRunner(ctx=ctx1, iters=args.iters, sampler=SAMPLER,
@@ -947,7 +950,9 @@ def main():
                 b1cache[r] = make_batch(r, 1, args.kpts, args.seed, args.inlier_frac, args.sigma)[0]
             return b1cache[r]
 
-        ctx_c = Context(local)
+        # (the pruning route, as the gathered batch took: the small-batch route would change the
+        # work counts binned_rows / survivors of the record, not its result fields)
+        ctx_c = make_ctx(local, small_batch=0)
         ctx_c.set_matcher(0 if args.matcher == "mfma" else 1)
         run_c = PairBatchRunner(ctx=ctx_c, iters=args.iters, sampler=SAMPLER)
 
@@ -1038,6 +1043,7 @@ def main():
                                else "Philox4x32-10 + Floyd (seed 1; no reference counterpart)"),
                    "rccl_world": world if dist is not None and args.dist_backend == "nccl" else None,
                    "dist_backend": args.dist_backend if dist is not None else None,
+                   "ctx_options": CTX_OPTIONS or None,
                    "ranks_on_device": args.ranks_on_device if args.ranks_on_device >= 0 else None,
                    "profile_tag": args.profile_tag,
                    "inlier_frac": args.inlier_frac, "sigma": args.sigma},

@@ -94,11 +94,16 @@ EXPORTED = ["erp_ctx_create", "erp_ctx_destroy", "erp_status_string", "erp_ransa
             "erp_consensus_hyps_finish_dev", "erp_surf_params_default",
             "erp_surf_detect_compute_dev", "erp_epipolar_draw_dev", "erp_draw_match_dev",
             "erp_random_shuffle_prefix", "erp_ctx_set_graphs", "erp_debug_check_pads", "erp_debug_lip_counters",
-            "erp_debug_snapshot"]
+            "erp_debug_snapshot", "erp_ctx_set_option", "erp_ctx_get_option",
+            "erp_debug_set_alloc_pad"]
 STAGES = ["knn2_filter", "knn2_merge", "bearings", "jump_prep", "sampler", "eigen",
           "valid_compact", "consensus_rows", "consensus_final", "consensus_bounds",
           "consensus_select", "windows", "gram", "knn2_candidates", "knn2_rescore",
           "consensus_refine", "knn2_exact", "sampler_gram", "inliers"]
+# erp_ctx_option (include/erp_match.h): route options, results identical on every setting
+OPTIONS = {"small_batch": 0, "sampler_lat": 1, "sampler_split": 2, "gram_tiles": 3,
+           "zoom_levels": 4, "small_zoom": 5, "lip2": 6, "lipg": 7, "refine_hint": 8,
+           "flat_refs": 9, "bound_ratio": 10, "debug_stages": 11, "debug_snap": 12}
 MATCHER_MFMA_FILTER = 0  # erp_matcher_method
 MATCHER_VALU_EXACT = 1
 
@@ -164,6 +169,10 @@ def load(build_if_missing: bool = False):
     L.erp_ctx_set_profiling.argtypes = [P, C.c_int32]
     L.erp_ctx_set_matcher.argtypes = [P, C.c_int32]
     L.erp_ctx_set_graphs.argtypes = [P, C.c_int32]
+    L.erp_ctx_set_option.argtypes = [P, C.c_int32, C.c_int32]
+    L.erp_ctx_get_option.argtypes = [P, C.c_int32, C.POINTER(C.c_int32)]
+    L.erp_debug_set_alloc_pad.argtypes = [C.c_size_t]
+    L.erp_debug_set_alloc_pad.restype = None
     L.erp_debug_check_pads.restype = C.c_int
     L.erp_debug_check_pads.argtypes = []
     L.erp_debug_lip_counters.restype = C.c_int
@@ -238,6 +247,16 @@ class Context:
     def set_matcher(self, method: int):
         """erp_ctx_set_matcher: MATCHER_MFMA_FILTER (default) or MATCHER_VALU_EXACT."""
         check(self.L.erp_ctx_set_matcher(self.h, int(method)), "set_matcher")
+
+    def set_option(self, name: str, value: int):
+        """erp_ctx_set_option: a route option by name (OPTIONS; include/erp_match.h documents
+        each).  Every setting gives the same results; the defaults are the measured fastest."""
+        check(self.L.erp_ctx_set_option(self.h, OPTIONS[name], int(value)), f"set_option({name})")
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int32()
+        check(self.L.erp_ctx_get_option(self.h, OPTIONS[name], C.byref(v)), f"get_option({name})")
+        return int(v.value)
 
     def stage_times(self) -> dict:
         """{stage: (total_ms, launches)} since the last call (syncs on the recorded events)."""

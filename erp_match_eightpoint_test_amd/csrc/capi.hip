@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -35,12 +36,10 @@ struct DevBuf {
     size_t n = 0;
 };
 
-// Debug: ERP_ALLOC_PAD = N gives every buffer N canary bytes (0xA5) past its end;
-// erp_debug_check_pads() reports buffers whose canary a kernel overwrote.
-size_t alloc_pad() {
-    static const size_t pad = getenv("ERP_ALLOC_PAD") ? (size_t)atoll(getenv("ERP_ALLOC_PAD")) : 0;
-    return pad;
-}
+// Debug: erp_debug_set_alloc_pad(N) gives every buffer allocated afterwards N canary bytes
+// (0xA5) past its end; erp_debug_check_pads() reports buffers whose canary a kernel overwrote.
+std::atomic<size_t> g_alloc_pad{0};
+size_t alloc_pad() { return g_alloc_pad.load(std::memory_order_relaxed); }
 std::mutex g_pad_mu;
 std::vector<std::pair<void*, size_t>> g_padded;
 
@@ -126,54 +125,33 @@ struct erp_ctx {
         sortbuf, w0, off, wh, results, in_a, in_b, in_c, in_d, dscale, lb, ub, surv, nsurv, wins,
         rtab, limbs, tsplit, ovf, remap_scr, vchunk, lipref, inl, hlite;
     DevBuf extra[13];         // erp_ctx_scratch_internal slots (1-11 SURF, 12 viz)
-    // debug (ERP_DEBUG_SNAP=1): lb, ub and the first-stage list counts right after the bounds
+    // route options (erp_ctx_set_option; include/erp_match.h documents each, defaults below)
+    int32_t opt[ERP_OPT_COUNT] = {
+        -1,  // SMALL_BATCH: auto
+        -1,  // SAMPLER_LAT: auto
+        -1,  // SAMPLER_SPLIT: auto
+        0,   // GRAM_TILES: auto
+        // ZOOM_LEVELS: 0 since r05 -- with the hinted refine windows (r04) the survivors' zoom
+        // no longer pays for itself; same-box A/B per 768-pair step (profiles/r05w_ab_zoom.txt):
+        // consensus 5.81 / 5.87 -> 5.67 / 5.67 ms, worst-case batch 16.2 / 16.1k -> 16.6 /
+        // 16.5k pairs/s.  (The second pre-pruning stage's fine pass uses the zoom kernel either way.)
+        0,
+        0,   // SMALL_ZOOM: the small-batch route skips the zoom (single pair 0.487 -> 0.437 ms)
+        1,   // LIP2: the second pre-pruning stage (kernels.hip consensus_lipschitz2_kernel)
+        1,   // LIPG: the central references' distance gradient (consensus_grad_kernel)
+        1,   // REFINE_HINT: sub-bins on each row's Lipschitz interval (consensus_hint_kernel)
+        25,  // FLAT_REFS: pairs whose first stage kept > 25 % of the rows take the flat route
+        1,   // BOUND_RATIO: the matcher's ratio test from the bf16 bounds where they suffice
+        -1,  // DEBUG_STAGES: every stage group
+        0};  // DEBUG_SNAP
+    // debug (ERP_OPT_DEBUG_SNAP): lb, ub and the first-stage list counts right after the bounds
     // pass, fetched with erp_debug_snapshot
-    bool snap_on = getenv("ERP_DEBUG_SNAP") && atoi(getenv("ERP_DEBUG_SNAP")) != 0;
     DevBuf snap;
     size_t snap_bytes = 0;
     uint64_t surf_key = 0;    // (W, H, params) of the SURF layer table in extra[1]
     uint32_t viz_epoch = 0;   // stamp epoch of the draw_match line buffer (extra[12])
-    // consensus zoom levels of the survivors (0-2; ERP_ZOOM_LEVELS, an A/B knob).  0 since r05:
-    // with the hinted refine windows (r04) the survivors' zoom no longer pays for itself --
-    // same-box A/B per 768-pair step (profiles/r05w_ab_zoom.txt): consensus 5.81 / 5.87 -> 5.67 /
-    // 5.67 ms, worst-case batch 16.2 / 16.1k -> 16.6 / 16.5k pairs/s.  (The second pre-pruning
-    // stage's fine pass uses the zoom kernel either way.)
-    int zoom = getenv("ERP_ZOOM_LEVELS") ? atoi(getenv("ERP_ZOOM_LEVELS")) : 0;
-    // the matcher's ratio test decided by the bf16 bounds where they suffice (A/B knob)
-    bool bound_ratio = getenv("ERP_NO_BOUND_RATIO") == nullptr;
-    // zoomed central references before the pre-pruning (opt-in ERP_ZOOM_REFS=1: measured no
-    // fewer binned rows)
-    int zoom_refs = getenv("ERP_ZOOM_REFS") ? atoi(getenv("ERP_ZOOM_REFS")) : 0;  // 2: all refs
-    // second pre-pruning stage: every 4th first-stage survivor on the fine grid as a reference
-    // for the others (kernels.hip consensus_lipschitz2_kernel; ERP_LIP2=0 for A/B)
-    int lip2 = getenv("ERP_LIP2") ? atoi(getenv("ERP_LIP2")) : 1;
-    // convexity-augmented pruning: the central first-stage references' distance gradient G
-    // (kernels.hip consensus_grad_kernel; ERP_LIPG=0 for A/B), for references with
-    // UB <= U * ERP_LIPG_FAC
-    int lipg = getenv("ERP_LIPG") ? atoi(getenv("ERP_LIPG")) : 1;
-    float lipg_fac = getenv("ERP_LIPG_FAC") ? (float)atof(getenv("ERP_LIPG_FAC")) : 1.1f;
-    // the refine pass's sub-bins placed on each row's Lipschitz interval around one survivor's
-    // exact rank keys (kernels.hip consensus_hint_kernel / refine_windows; ERP_REFINE_HINT=0
-    // for A/B: the boundary bins' fixed sub-bins)
-    int refine_hint = getenv("ERP_REFINE_HINT") ? atoi(getenv("ERP_REFINE_HINT")) : 1;
-    // flat pairs (the first-stage pruning kept more than this % of the rows): their first-stage
-    // references refined and the first stage re-run against them (kernels.hip
-    // consensus_flat_gate_kernel; ERP_FLAT_REFS=0 for A/B)
-    int flat_refs = getenv("ERP_FLAT_REFS") ? atoi(getenv("ERP_FLAT_REFS")) : 25;
-    // the sampler and the Gram as one kernel (sampler_gram_kernel, opt-in ERP_FUSE_SAMPLER=1):
-    // measured 1.6x SLOWER than the two standalone kernels (the Gram's int32
-    // accumulators leave room for one sampler wave per SIMD, and one wave alone issues VALU at
-    // about a third of the rate four waves reach), so the default is the standalone pair
-    bool fuse_sampler = getenv("ERP_FUSE_SAMPLER") && atoi(getenv("ERP_FUSE_SAMPLER")) != 0;
     // HIP-graph replay of erp_pair_batch_run (erp_ctx_set_graphs): key bytes -> executable graph
-    bool use_graphs = getenv("ERP_GRAPHS") && atoi(getenv("ERP_GRAPHS")) != 0;
-    // debug (ERP_DEBUG_STAGES, a bit mask; default every stage): which stage groups
-    // erp_pair_batch_run enqueues -- 1 matcher + gather, 2 jump polynomials + windows, 4 sampler,
-    // 8 Gram (with the fused eigen), 32 eigen fallback + estimate, 16 consensus.  A skipped stage leaves the previous call's
-    // scratch in place, so after one full call the later stages still read valid inputs (the
-    // LDS-interference probe, scripts/dev/lds_guard_probe.py, runs one stage group at a time)
-    // (read at every erp_pair_batch_run)
-    int dbg_stages = -1;
+    bool use_graphs = false;
     struct Graph {
         std::vector<uint8_t> key;
         hipGraphExec_t exec = nullptr;
@@ -449,7 +427,7 @@ erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int
         StageTimer _t(ctx, ERP_STAGE_KNN2_RESCORE, st);
         ERP_CK(erp::launch_knn2_rescore(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand,
                                         (erp::Top2*)ctx->part.p, (int32_t*)ctx->ovf.p,
-                                        ctx->bound_ratio ? ratio : -1.f, st));
+                                        ctx->opt[ERP_OPT_BOUND_RATIO] ? ratio : -1.f, st));
     }
     return fold_and_merge(ctx, oq, ot, sh, sh.fchunk_len, sh.fchunks, ratio, matches, counts,
                           flags, st, bo);
@@ -554,19 +532,23 @@ int32_t* lite_wsum(erp_ctx* c, const erp::BatchShape& sh) {
 }
 
 // estimator stages after counts/pts are in place (lite: the estimates in the lite layout)
-erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac_cfg* cfg,
+erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh_in, const erp_ransac_cfg* cfg,
                           const erp_batch_outputs* out, hipStream_t st, bool lite = false) {
     erp_ctx* ctx = c;
+    erp::BatchShape sh = sh_in;  // + the sampler / Gram route options
+    sh.sampler_lat = c->opt[ERP_OPT_SAMPLER_LAT];
+    sh.sampler_split = c->opt[ERP_OPT_SAMPLER_SPLIT];
+    sh.gram_tiles = c->opt[ERP_OPT_GRAM_TILES];
     auto* counts = (int32_t*)c->counts.p;
     auto* flags = (int32_t*)c->flags.p;
     auto* hyps = (out && out->hyps) ? out->hyps : (erp_hypothesis*)c->hyps.p;
     if (cfg->sampler == ERP_SAMPLER_PHILOX) {  // counter-based: no jump polynomials / windows
-        if (c->dbg_stages & 4) {
+        if (c->opt[ERP_OPT_DEBUG_STAGES] & 4) {
             StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
             ERP_CK(erp::launch_philox_sampler(counts, sh, cfg->sample_frac, cfg->seed, cfg->offset,
                                               sh.max_nq, (uint32_t*)c->idx.p, flags, st));
         }
-        if (c->dbg_stages & 8) {
+        if (c->opt[ERP_OPT_DEBUG_STAGES] & 8) {
             StageTimer _t(ctx, ERP_STAGE_GRAM, st);
             ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
                                          cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
@@ -574,7 +556,7 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
                                          ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr,
                                          ERP_FUSE_EIGEN == 2 ? hyps : nullptr, cfg->valid_abs, st));
         }
-        if (c->dbg_stages & 32) {
+        if (c->opt[ERP_OPT_DEBUG_STAGES] & 32) {
             StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
             ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
                                      cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
@@ -583,45 +565,31 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh, const erp_ransa
         }
         return run_inliers(c, sh, cfg, hyps, st);
     }
-    if (c->dbg_stages & 2) {
+    if (c->opt[ERP_OPT_DEBUG_STAGES] & 2) {
         StageTimer _t(ctx, ERP_STAGE_JUMP_PREP, st);
         ERP_CK(erp::launch_jump_prep(counts, sh, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p, st));
     }
-    if (c->dbg_stages & 2) {
+    if (c->opt[ERP_OPT_DEBUG_STAGES] & 2) {
         StageTimer _t(ctx, ERP_STAGE_WINDOWS, st);
         ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
                                    (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
                                    (uint32_t*)c->wins.p, (uint32_t*)c->idx.p, flags, st, 0));
     }
-    if (c->fuse_sampler && ERP_FUSE_EIGEN != 2 && erp::sampler_gram_fits(sh)) {
-        {
-            StageTimer _t(ctx, ERP_STAGE_GRAM, st);
-            ERP_CK(erp::launch_gram_limbs(counts, (double*)c->pts.p, sh, (int8_t*)c->limbs.p, st));
-        }
-        {
-            StageTimer _t(ctx, ERP_STAGE_SAMPLER_GRAM, st);
-            ERP_CK(erp::launch_sampler_gram(
-                counts, (uint32_t*)c->wins.p, (int8_t*)c->limbs.p, (double*)c->rtab.p, sh,
-                cfg->sample_frac, flags, (uint32_t*)c->idx.p, out ? out->samples : nullptr,
-                (double*)c->gram.p, ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr, st));
-        }
-    } else {
-        if (c->dbg_stages & 4) {
-            StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
-            ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
-                                       (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
-                                       (uint32_t*)c->wins.p, (uint32_t*)c->idx.p, flags, st, 1));
-        }
-        if (c->dbg_stages & 8) {
-            StageTimer _t(ctx, ERP_STAGE_GRAM, st);
-            ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
-                                         cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
-                                         out ? out->samples : nullptr,
-                                         ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr,
-                                         ERP_FUSE_EIGEN == 2 ? hyps : nullptr, cfg->valid_abs, st));
-        }
+    if (c->opt[ERP_OPT_DEBUG_STAGES] & 4) {
+        StageTimer _t(ctx, ERP_STAGE_SAMPLER, st);
+        ERP_CK(erp::launch_sampler(counts, (uint32_t*)c->polyR.p, (uint32_t*)c->polyQ.p,
+                                   (uint32_t*)c->w0.p, sh, cfg->sample_frac, (double*)c->rtab.p,
+                                   (uint32_t*)c->wins.p, (uint32_t*)c->idx.p, flags, st, 1));
     }
-    if (c->dbg_stages & 32) {
+    if (c->opt[ERP_OPT_DEBUG_STAGES] & 8) {
+        StageTimer _t(ctx, ERP_STAGE_GRAM, st);
+        ERP_CK(erp::launch_gram_mfma(counts, (double*)c->pts.p, (uint32_t*)c->idx.p, sh,
+                                     cfg->sample_frac, (int8_t*)c->limbs.p, (double*)c->gram.p,
+                                     out ? out->samples : nullptr,
+                                     ERP_FUSE_EIGEN ? (double*)c->gfin.p : nullptr,
+                                     ERP_FUSE_EIGEN == 2 ? hyps : nullptr, cfg->valid_abs, st));
+    }
+    if (c->opt[ERP_OPT_DEBUG_STAGES] & 32) {
         StageTimer _t(ctx, ERP_STAGE_EIGEN, st);
         ERP_CK(erp::launch_eigen(counts, (double*)c->gram.p, sh, cfg->sample_frac,
                                  cfg->valid_abs, (double*)c->gfin.p, hyps, st, ERP_FUSE_EIGEN,
@@ -669,12 +637,12 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     // launches (~0.2 ms) of the pruning stages, which only pay when many pairs share the chip
     // or K is large: the route is taken when n_pairs (2 iters)^2 <= 2e9 (one pair up to ~22k
     // iterations, five at 10k; configs[4]'s 100k-iteration find keeps the pruning), and never
-    // for the row-sharded phases.  ERP_SMALL_BATCH = n overrides: batches of <= n pairs take it
-    // (0 = never; read at every call)
-    const char* sb_env = getenv("ERP_SMALL_BATCH");
+    // for the row-sharded phases.  ERP_OPT_SMALL_BATCH = n >= 0 overrides: batches of <= n pairs
+    // take it (0 = never)
+    const int sb = c->opt[ERP_OPT_SMALL_BATCH];
     const double kk = 2.0 * sh.iters;
     const bool small = phase == 0 && nshards == 1 &&
-                       (sb_env ? sh.n_pairs <= atoi(sb_env) : sh.n_pairs * kk * kk <= 2e9);
+                       (sb >= 0 ? sh.n_pairs <= sb : sh.n_pairs * kk * kk <= 2e9);
     const bool prune = !small;
     if (phase != 2) {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
@@ -683,12 +651,13 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             cfg->trim_lo, cfg->trim_hi, lbp, ubp, bselp, shard,
                                             nshards, prune ? (int32_t*)c->surv.p : nullptr,
                                             prune ? (int32_t*)c->nsurv.p + sh.n_pairs : nullptr,
-                                            (int32_t*)c->zsel.p, c->zoom_refs, c->lip2,
-                                            (int32_t*)c->sortbuf.p, c->lipref.p, c->lipg,
-                                            c->lipg_fac, c->flat_refs, c->refine_hint, st,
+                                            (int32_t*)c->zsel.p, c->opt[ERP_OPT_LIP2],
+                                            (int32_t*)c->sortbuf.p,
+                                            c->lipref.p, c->opt[ERP_OPT_LIPG],
+                                            c->opt[ERP_OPT_FLAT_REFS], c->opt[ERP_OPT_REFINE_HINT], st,
                                             from_hyps && lite));  // (valid_place wrote the edges)
     }
-    if (c->snap_on && phase == 0) {
+    if (c->opt[ERP_OPT_DEBUG_SNAP] && phase == 0) {
         const size_t nrow = (size_t)sh.n_pairs * 2 * sh.iters;
         // (kernels.hip lipref_cap at the default second-stage step 4)
         const size_t lrb = (size_t)sh.n_pairs * (2 * sh.iters / 4 + 64) * 16 + (size_t)sh.n_pairs * 12;
@@ -696,8 +665,11 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
         if (!ensure(c->snap, c->snap_bytes)) return ERP_OUT_OF_MEMORY;
         ERP_CK(hipMemcpyAsync(c->snap.p, lbp, nrow * 8, hipMemcpyDeviceToDevice, st));
         ERP_CK(hipMemcpyAsync((char*)c->snap.p + nrow * 8, ubp, nrow * 8, hipMemcpyDeviceToDevice, st));
-        ERP_CK(hipMemcpyAsync((char*)c->snap.p + nrow * 16, (int32_t*)c->nsurv.p + sh.n_pairs,
-                              (size_t)sh.n_pairs * 4, hipMemcpyDeviceToDevice, st));
+        if (prune)
+            ERP_CK(hipMemcpyAsync((char*)c->snap.p + nrow * 16, (int32_t*)c->nsurv.p + sh.n_pairs,
+                                  (size_t)sh.n_pairs * 4, hipMemcpyDeviceToDevice, st));
+        else  // (the small-batch route lists nothing: -1 = every row binned)
+            ERP_CK(hipMemsetAsync((char*)c->snap.p + nrow * 16, 0xFF, (size_t)sh.n_pairs * 4, st));
         // + the first-stage references (float4 [P][cap]), their U [P] f64 and counts [P] i32
         ERP_CK(hipMemcpyAsync((char*)c->snap.p + nrow * 16 + (size_t)sh.n_pairs * 4, c->lipref.p, lrb,
                               hipMemcpyDeviceToDevice, st));
@@ -714,9 +686,8 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     }
     // small batches skip the zoom too: the exact pass takes the first selection's survivors
     // (~150 for a typical pair, one grid-wide launch); single pair 0.487 -> 0.437 ms
-    // (profiles/r05g_latency_ab.txt; ERP_SMALL_ZOOM=1 keeps it)
-    const char* sz_env = getenv("ERP_SMALL_ZOOM");
-    const int zoom_levels = prune || (sz_env && atoi(sz_env) != 0) ? c->zoom : 0;
+    // (profiles/r05g_latency_ab.txt; ERP_OPT_SMALL_ZOOM = 1 keeps it)
+    const int zoom_levels = prune || c->opt[ERP_OPT_SMALL_ZOOM] ? c->opt[ERP_OPT_ZOOM_LEVELS] : 0;
     for (int level = 1; level <= zoom_levels; level++) {
         {
             StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
@@ -741,7 +712,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
                                             bselp, lbp,
                                             ubp, (int32_t*)c->sortbuf.p, c->lipref.p,
-                                            c->refine_hint, st));
+                                            c->opt[ERP_OPT_REFINE_HINT], st));
     }
     if (prune) {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
@@ -765,7 +736,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                            cfg->sample_frac, cfg->trim_lo, cfg->trim_hi,
                                            (float*)c->sortbuf.p, results, st));
     }
-    if (c->snap_on && phase == 0 && c->snap_bytes) {
+    if (c->opt[ERP_OPT_DEBUG_SNAP] && phase == 0 && c->snap_bytes) {
         // + the consensus's rotation vectors (SoA [P][3][2 iters] f32) as they are at its end
         const size_t rvb = (size_t)sh.n_pairs * 6 * sh.iters * 4;
         const size_t head = c->snap_bytes;
@@ -789,7 +760,7 @@ erp_status run_estimator(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     const bool lite = use_lite(cfg, out);
     erp_status es = run_hypotheses(c, sh, cfg, out, st, lite);
     if (es != ERP_OK) return es;
-    if (!(c->dbg_stages & 16)) return ERP_OK;
+    if (!(c->opt[ERP_OPT_DEBUG_STAGES] & 16)) return ERP_OK;
     return run_consensus(c, sh, cfg, out, results, st, true, 0, 0, 1, nullptr, nullptr, nullptr,
                          lite);
 }
@@ -863,11 +834,7 @@ namespace {
 erp_status batch_enqueue(erp_ctx* ctx, const erp_pair_batch* b, float ratio,
                          const erp_ransac_cfg* cfg, const erp_batch_outputs* out,
                          const erp::BatchShape& sh, erp_dmatch* matches, hipStream_t st) {
-    {
-        const char* m = getenv("ERP_DEBUG_STAGES");
-        ctx->dbg_stages = m ? (int)strtol(m, nullptr, 0) : -1;
-    }
-    if (!(ctx->dbg_stages & 1)) return run_estimator(ctx, sh, cfg, out, out->results, st);
+    if (!(ctx->opt[ERP_OPT_DEBUG_STAGES] & 1)) return run_estimator(ctx, sh, cfg, out, out->results, st);
     // the optional outputs read zero past each pair's M / K / s, call after call (a HIP-graph
     // replay or a reused buffer would otherwise keep an earlier call's entries there)
     const size_t P = (size_t)sh.n_pairs, I = (size_t)sh.iters, Q = (size_t)b->max_nq;
@@ -899,7 +866,7 @@ void key_put(std::vector<uint8_t>& k, const T& v) {
 }
 
 // everything a captured pipeline bakes in: the call's structs and the context's scratch pointers
-// and knobs
+// and route options
 std::vector<uint8_t> graph_key(const erp_ctx* c, const erp_pair_batch* b, float ratio,
                                const erp_ransac_cfg* cfg, const erp_batch_outputs* out) {
     std::vector<uint8_t> k;
@@ -908,20 +875,7 @@ std::vector<uint8_t> graph_key(const erp_ctx* c, const erp_pair_batch* b, float 
     key_put(k, *out);
     key_put(k, ratio);
     key_put(k, c->matcher);
-    key_put(k, c->zoom);
-    key_put(k, c->bound_ratio);
-    key_put(k, c->zoom_refs);
-    key_put(k, c->lip2);
-    key_put(k, c->lipg);
-    key_put(k, c->lipg_fac);
-    key_put(k, c->refine_hint);
-    key_put(k, c->flat_refs);
-    key_put(k, c->fuse_sampler);
-    // the knobs read at every call (run_consensus's route, launch_sampler's kernel choice)
-    for (const char* name : {"ERP_SMALL_BATCH", "ERP_SAMPLER_SPLIT", "ERP_SAMPLER_LAT", "ERP_SAMPLER_ILP", "ERP_GRAM_WT"}) {
-        const char* v = getenv(name);
-        key_put(k, v ? atoi(v) : -1);
-    }
+    key_put(k, c->opt);
     const DevBuf* all[] = {&c->mblk, &c->zsel, &c->part, &c->part1, &c->pu, &c->ccount, &c->cand,
                            &c->bsel, &c->edges, &c->gfin, &c->matches, &c->counts, &c->flags,
                            &c->pts, &c->polyR, &c->polyQ, &c->idx, &c->gram, &c->hyps, &c->rv,
@@ -943,6 +897,35 @@ erp_status erp_ctx_set_graphs(erp_ctx* ctx, int32_t enable) {
     ctx->use_graphs = enable != 0;
     return ERP_OK;
 }
+
+erp_status erp_ctx_set_option(erp_ctx* ctx, int32_t option, int32_t value) {
+    if (!ctx || option < 0 || option >= ERP_OPT_COUNT) return ERP_INVALID_ARG;
+    int lo = 0, hi = 1;  // the on / off options
+    switch (option) {
+        case ERP_OPT_SMALL_BATCH: lo = -1; hi = INT32_MAX; break;
+        case ERP_OPT_SAMPLER_LAT: lo = -1; hi = 2; break;
+        case ERP_OPT_SAMPLER_SPLIT: lo = -1; hi = 1; break;
+        case ERP_OPT_GRAM_TILES: lo = 0; hi = 2; break;
+        case ERP_OPT_ZOOM_LEVELS: lo = 0; hi = 2; break;
+        case ERP_OPT_FLAT_REFS: lo = 0; hi = 100; break;
+        case ERP_OPT_LIPG: lo = 0; hi = 3; break;  // bit 0: first stage, bit 1: second stage
+        case ERP_OPT_DEBUG_STAGES: lo = -1; hi = 63; break;
+        default: break;
+    }
+    if (value < lo || value > hi) return ERP_INVALID_ARG;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    ctx->opt[option] = value;
+    return ERP_OK;
+}
+
+erp_status erp_ctx_get_option(erp_ctx* ctx, int32_t option, int32_t* value) {
+    if (!ctx || !value || option < 0 || option >= ERP_OPT_COUNT) return ERP_INVALID_ARG;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    *value = ctx->opt[option];
+    return ERP_OK;
+}
+
+void erp_debug_set_alloc_pad(size_t bytes) { g_alloc_pad.store(bytes, std::memory_order_relaxed); }
 
 erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* b, float ratio,
                               const erp_ransac_cfg* cfg, const erp_batch_outputs* out,
@@ -975,7 +958,7 @@ erp_status erp_pair_batch_run(erp_ctx* ctx, const erp_pair_batch* b, float ratio
     // then becomes part of the caller's graph)
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     if (st != nullptr) ERP_CK(hipStreamIsCapturing(st, &cap));
-    if (!ctx->use_graphs || ctx->profiling || st == nullptr || ctx->snap_on ||
+    if (!ctx->use_graphs || ctx->profiling || st == nullptr || ctx->opt[ERP_OPT_DEBUG_SNAP] ||
         cap != hipStreamCaptureStatusNone)
         return batch_enqueue(ctx, b, ratio, cfg, out, sh, matches, st);
     // graph replay: the same call (structs, buffers, scratch) as a captured one -> one launch

@@ -62,6 +62,9 @@ struct BatchShape {
     int max_s;                    // (int)(max_nq * sample_frac)
     int idx_stride;               // entries of one hypothesis in the debug samples output
     int sel_words;                // 31-step selection words per hypothesis (>= (M-1)/31 + 1)
+    // route options (erp_ctx_set_option; -1 / 0 = automatic): the sampler's block kind and split
+    // replay, the Gram kernel's row tiles per wave
+    int sampler_lat = -1, sampler_split = -1, gram_tiles = 0;
 };
 
 hipError_t launch_set_i32(int32_t* p, int32_t v, hipStream_t st);  // (values via kernel args:
@@ -138,18 +141,6 @@ int debug_lip_counters(uint32_t* out64);
 // launch_eigen with fused = 1.  hyps != NULL as well: the settled lanes' estimates too (fused = 2:
 // the fallback and thin eigen kernels then write their own lanes' records, no estimate_kernel)
 size_t gram_limbs_bytes(const BatchShape& sh);
-// the sampler and the Gram fused into one kernel (sampler_gram_kernel: the replay's selection
-// words stay in LDS); usable when the batch's bitmaps fit beside the LDS rings (max_s below
-// ~4000).  Runs gram_limbs first, then the fused kernel; selw (may be NULL) receives the
-// selection words too (only the debug `samples` output reads them).  Same outputs as
-// launch_sampler(part 1) + launch_gram_mfma with hyps == NULL (evec: the fused eigen stage).
-bool sampler_gram_fits(const BatchShape& sh);
-hipError_t launch_gram_limbs(const int32_t* counts, const double* pts, const BatchShape& sh,
-                             int8_t* limbs, hipStream_t st);
-hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* wins, const int8_t* limbs,
-                               const double* rtab, const BatchShape& sh, double sample_frac,
-                               int32_t* flags, uint32_t* selw, int32_t* samples, double* gram,
-                               double* evec, hipStream_t st);
 hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint32_t* selw,
                             const BatchShape& sh, double sample_frac, int8_t* limbs,
                             double* gram, int32_t* samples, double* evec,
@@ -200,9 +191,8 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
-                                   int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
-                                   void* lipref, int lipg, float gfac, int flat_pct,
-                                   int use_hint, hipStream_t st,
+                                   int32_t* zsel, int lip2, int32_t* list2, void* lipref,
+                                   int lipg, int flat_pct, int use_hint, hipStream_t st,
                                    bool edges_ready = false);
 size_t lipref_bytes(int n_pairs, int stride);
 // survivors = rows with LB <= min UB (again = 1: only pairs the refine pass touched)

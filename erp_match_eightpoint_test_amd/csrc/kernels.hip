@@ -587,99 +587,6 @@ constexpr int kIlpLag = 15;
 // the latency blocks' default (1: step by step, 2: positions first; ERP_SAMPLER_LAT overrides)
 constexpr int kSamplerLatMode = 2;
 
-// ---- the same blocks with the 31 draw positions computed FIRST (ILP variants) ---------------
-// A block's 31 positions depend only on the ring words the previous block left (the backwards
-// recurrence writes values for the NEXT block), so they are 31 independent modulo chains: with
-// them ahead of the LDS ops the scheduler interleaves the chains instead of running each draw's
-// dependent fp64 sequence behind the previous draw's volatile LDS op.  This is what a wave that
-// is alone on its SIMD needs (the fused sampler_gram_kernel: one sampler wave per SIMD); the
-// standalone sampler hides the same latency with four waves per SIMD.
-template <bool I24>
-__device__ __forceinline__ void block_positions(uint32_t (&ring)[31], int i0,
-                                                const double* __restrict__ rtab,
-                                                uint32_t (&jj)[31]) {
-    double rt[31];
-#pragma unroll
-    for (int u = 0; u < 31; u++) rt[u] = rtab[i0 - u + 1];
-#pragma unroll
-    for (int u = 0; u < 31; u++) {
-        const int ii = i0 - u;
-        const int slot = 30 - u;
-        const uint32_t rv = ring[slot];
-        ring[slot] = rv - ring[(slot + 28) % 31];
-        jj[u] = I24 ? mod_rup_i24(rv >> 1, rt[u], ii + 1) : mod_rup(rv >> 1, rt[u], (double)(ii + 1));
-    }
-}
-
-template <bool I24, int RS>
-__device__ __forceinline__ uint32_t replay_block_draws_ilp(uint32_t (&ring)[31], uint32_t* bm,
-                                                           int lane, int i0, int s,
-                                                           const double* __restrict__ rtab) {
-    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
-    uint32_t jj[31];
-    block_positions<I24>(ring, i0, rtab, jj);
-    if (ERP_SAMPLER_CLAMP)
-#pragma unroll
-        for (int u = 0; u < 31; u++) jj[u] = min(jj[u], (uint32_t)s);  // (bit s: clear, allocated)
-    const uint32_t zero = 0;
-    uint32_t olds[31];
-    uint32_t nw[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int u = 0; u < 31 + kIlpLag; u++) {
-        if (u < 31)
-            olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, jj[u]), 1u << (jj[u] & 31), zero);
-        const int v = u - kIlpLag;
-        if (v >= 0) {
-            lds_wait_n(olds[v], 30 - v < kIlpLag ? 30 - v : kIlpLag);
-            nw[v & 3] |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
-        }
-    }
-    return (nw[0] | nw[1]) | (nw[2] | nw[3]);  // four partial words: no serial OR chain
-}
-
-template <bool I24, int RS>
-__device__ __forceinline__ uint32_t replay_block_prefix_ilp(uint32_t (&ring)[31], uint32_t* bm,
-                                                            int lane, int i0,
-                                                            const double* __restrict__ rtab) {
-    const uint32_t bm_lane = (uint32_t)(size_t)(lds_u32*)bm + 4u * (uint32_t)lane;
-    uint32_t jj[31];
-    block_positions<I24>(ring, i0, rtab, jj);
-    const int base = i0 - 30;  // >= 1
-    const int wA = i0 >> 5, wB = base >> 5;
-    const uint32_t hi = bm[bm_index<RS>(wA, lane)], lo = bm[bm_index<RS>(wB, lane)];
-    uint32_t win = wA == wB ? (lo >> (base & 31)) : __builtin_amdgcn_alignbit(hi, lo, base & 31);
-    uint32_t olds[31];
-    uint32_t nw[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int u = 0; u < 31 + kIlpLag; u++) {
-        if (u < 31) {
-            const uint32_t j = jj[u];
-            const uint32_t bsp = (uint32_t)__builtin_amdgcn_sbfe((int)win, 30 - u, 1);  // bm[i]
-            const uint32_t bit = 1u << (j & 31);
-            olds[u] = lds_mskor_rtn(lds_word_addr<RS>(bm_lane, j), bit, bsp & bit);
-            const uint32_t t = min(j - (uint32_t)base, 31u);
-            const uint32_t m = 1u << t;
-            win = (win & ~m) | (bsp & m);
-        }
-        const int v = u - kIlpLag;
-        if (v >= 0) {
-            lds_wait_n(olds[v], 30 - v < kIlpLag ? 30 - v : kIlpLag);
-            nw[v & 3] |= __builtin_amdgcn_ubfe(olds[v], jj[v], 1) << v;
-        }
-    }
-    return (nw[0] | nw[1]) | (nw[2] | nw[3]);  // four partial words: no serial OR chain
-}
-
-template <int RS>
-__device__ __forceinline__ uint32_t replay_block_ilp(uint32_t (&ring)[31], uint32_t* bm, int lane,
-                                                     int i, int s, const double* __restrict__ rtab) {
-    if (i - 30 >= s && i - 30 >= 255) return replay_block_draws_ilp<true, RS>(ring, bm, lane, i, s, rtab);
-    if (i - 30 >= s) return replay_block_draws_ilp<false, RS>(ring, bm, lane, i, s, rtab);
-    if (i < s && i - 30 >= 255) return replay_block_prefix_ilp<true, RS>(ring, bm, lane, i, rtab);
-    if (i < s && i - 30 >= 1) return replay_block_prefix_ilp<false, RS>(ring, bm, lane, i, rtab);
-    return replay_block_mixed<RS>(ring, bm, lane, i, s, rtab);
-}
-
 // ---- latency variant (sampler_kernel<2>: waves alone on their SIMDs) -----------------------
 // SQ counters of the single-pair path (profiles/r05n_sq_latency.txt): the standalone sampler's
 // lone waves sat at s_waitcnt ~40 % of their cycles.  Each block's 31 divisor constants come
@@ -840,9 +747,9 @@ __device__ __forceinline__ uint32_t replay_block(uint32_t (&ring)[31], uint32_t*
 
 // One lane = one iteration; writes the iteration's selection bitmap in block space:
 // sel[p][w][b][lane] bit u <-> index i = M-1-31b-u (b = 0 .. (M-1)/31), exactly s bits set.
-// MODE 0: the throughput blocks; 1: the ILP blocks (A/B knob); 2: the latency blocks (constants
-// prefetched one block ahead by vector loads, two blocks per loop trip so that the two constant
-// sets alternate without register copies)
+// MODE 0: the throughput blocks; 2 / 3: the latency blocks, step by step / positions first
+// (constants prefetched one block ahead by vector loads, two blocks per loop trip so that the two
+// constant sets alternate without register copies)
 template <int MODE>
 __global__ __launch_bounds__(64) void sampler_kernel(
     const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins, int nwaves, int nbw,
@@ -895,9 +802,7 @@ __global__ __launch_bounds__(64) void sampler_kernel(
             emit(replay_block_lat<MODE == 3, 8>(ring, bm, lane, i, s, kb, rtab, cb));
         }
     } else {
-        while (i >= 1)
-            emit(MODE == 1 ? replay_block_ilp<8>(ring, bm, lane, i, s, rtab)
-                           : replay_block<8>(ring, bm, lane, i, s, rtab));
+        while (i >= 1) emit(replay_block<8>(ring, bm, lane, i, s, rtab));
     }
     if (bm[lane] & 1u) {  // position 0 still unresolved: its value 0 stays in the prefix
         lastw |= 1u << u0;
@@ -1505,231 +1410,6 @@ __global__ __launch_bounds__(64 * kGramWaves, GramCfg<WT>::kMinBlocks) void gram
         for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[w][t][k] << (8 * t);
         long long v2 = 0;
         const int x = acc[w][kGramLimbs][k];
-#pragma unroll
-        for (int t = 0; t < kGramLimbs; t++)
-            v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
-        if (h0 + row < iters) {
-            go[(size_t)r * iters + h0 + row] = (double)v * (1.0 / kGramScale);
-            if (r < 4) go[(size_t)(32 + r) * iters + h0 + row] = (double)v2 * (1.0 / kGramScale);
-        }
-    }
-}
-
-// ---- sampler -> Gram fusion ----------------------------------------------------------------
-// One workgroup = kFSw sampler waves (one iteration per lane, the replay of sampler_kernel) +
-// kFMw MFMA waves (32 iterations each, the K loop of gram_mfma_kernel), kFIters = 256
-// iterations of one pair.  The sampler waves emit selection words b = 2t, 2t+1 of step t into an
-// LDS ring while the MFMA waves consume step t-1's words with its limb images (LDS-DMA, issued
-// one step ahead), one barrier per step -- the K order both kernels already share
-// (src/eight_point.cpp:99-116: the sampled rows of each iteration's A^T A).  The selection words
-// never go to HBM (the standalone pair writes them and reads them back), and the VALU-bound
-// replay co-issues with the MFMA waves on every SIMD (MI355X_MICROARCH.md "Wave scheduling": an
-// MFMA-only and a VALU-only wave on one CU run concurrently).  12 waves per workgroup, one
-// workgroup per CU: each SIMD holds one sampler wave and two MFMA waves (<= 168 VGPRs).
-// LDS: [limb ring: 2 x 14 KB][selection ring: 2 x 2 KB] ... [bitmaps: rows x kFSw x 64 words]
-// with the bitmaps at the TOP of the allocation; draw positions j >= s are clamped to s (row
-// s / 32 is allocated, bit s clear: sampler_kernel's rule); rows between s and the allocated
-// count are cleared by the prologue.  The
-// Gram epilogue (fused eigen) reuses the whole allocation as the [36][257] double stage.
-constexpr int kFSw = 4;
-constexpr int kFMw = 8;
-constexpr int kFIters = 64 * kFSw;
-constexpr int kFThreads = 64 * (kFSw + kFMw);
-constexpr int kFRowBytes = 64 * 4 * kFSw;                 // one bitmap word of every wave
-constexpr int kFRS = 10;                                  // log2(kFRowBytes)
-static_assert((1 << kFRS) == kFRowBytes, "row shift");
-constexpr int kFLimbSlot = kGramSelOff;                   // the step's two limb images (14 KB)
-constexpr int kFRing = 3;                                 // limb slots: DMAs 2 steps ahead
-constexpr int kFSelSlot = kGramWords * kFIters * 4;       // the step's selection words (2 KB)
-constexpr int kFSelOff = kFRing * kFLimbSlot;
-constexpr int kFRingBytes = kFRing * kFLimbSlot + 2 * kFSelSlot;
-constexpr int kFStg = kFIters + 1;                        // odd stride: conflict-free
-constexpr int kFStgBytes = 36 * kFStg * 8;
-constexpr int kFMaxLds = 160 * 1024;
-static_assert(kGramWords == 2, "two words per step");
-
-// limb pieces (1 KB each, 14 per step) moved by MFMA wave k: the first 14 % 8 move one more
-__device__ __forceinline__ int fused_piece0(int k) {
-    return k * (kGramPieces / kFMw) + min(k, kGramPieces % kFMw);
-}
-__device__ __forceinline__ int fused_pieces(int k) {
-    return kGramPieces / kFMw + (k < kGramPieces % kFMw ? 1 : 0);
-}
-
-__global__ __launch_bounds__(kFThreads, 1) void sampler_gram_kernel(
-    const int32_t* __restrict__ counts, const uint32_t* __restrict__ wins,
-    const int8_t* __restrict__ limbs, const double* __restrict__ rtab, int iters, int nwaves,
-    int nbw, double sample_frac, int rows, int bm_base, int32_t* __restrict__ flags,
-    uint32_t* __restrict__ selw, double* __restrict__ gram, int nhb, double* __restrict__ evec,
-    int diag) {
-    extern __shared__ __align__(16) int8_t lds[];
-    // XCD-aware block order (gram_mfma_kernel): a pair's blocks on one XCD, whose L2 then
-    // serves the pair's limb images to all of them
-    const int NB = gridDim.x;
-    const int lbk = (NB & 7) ? (int)blockIdx.x : (int)((blockIdx.x & 7) * (NB >> 3) + (blockIdx.x >> 3));
-    const int p = lbk / nhb, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int M = counts[p];
-    const int s = (int)(M * sample_frac);
-    if (s < 1 || M < 2) return;  // uniform over the block
-    const int hb = (lbk % nhb) * kFIters;
-    if (hb >= iters) return;
-    const int b0 = (M - 1) / 31, u0 = (M - 1) % 31;  // word and bit of position 0
-    const int nb = b0 + 1;
-    const int nsteps = (nb + kGramWords - 1) / kGramWords;
-    uint32_t* selr = reinterpret_cast<uint32_t*>(lds + kFSelOff);  // [2][2][kFIters]
-    if (wv < kFSw) {
-        // ------------------------------------------------ sampler wave: 64 iterations
-        const int w = hb / 64 + wv;  // the standalone sampler's wave index (windows layout)
-        const bool live = w < nwaves;
-        asm volatile("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 3\n\ts_nop 3" ::: "memory");
-        uint32_t* bm = reinterpret_cast<uint32_t*>(lds + bm_base) + wv * 64;  // this wave's column
-        for (int k = 0; k < rows; k++)  // (every row of the allocation; none past it)
-            bm[bm_index<kFRS>(k, lane)] =
-                k < (s >> 5) ? ~0u : k == (s >> 5) ? (1u << (s & 31)) - 1u : 0u;
-        uint32_t ring[31];
-        if (live) {
-            const uint32_t* wi = wins + ((size_t)p * nwaves + w) * 31 * 64 + lane;
-#pragma unroll
-            for (int t = 0; t < 31; t++) ring[t] = wi[t * 64];
-        }
-        uint32_t* out = selw ? selw + ((size_t)p * nwaves + w) * (size_t)nbw * 64 + lane : nullptr;
-        int i = M - 1, emitted = 0;
-        for (int t = 0; t <= nsteps; t++) {
-            if (t < nsteps) {
-#pragma unroll 1
-                for (int q = 0; q < kGramWords; q++) {
-                    const int b = kGramWords * t + q;
-                    uint32_t word = 0;
-                    if (live && b < nb && !(diag & 2)) {
-                        if (i >= 1) {
-                            word = replay_block_ilp<kFRS>(ring, bm, lane, i, s, rtab);
-                            i -= 31;
-                        }
-                        if (b == b0 && (bm[lane] & 1u))  // position 0 still unresolved
-                            word |= 1u << u0;
-                        emitted += __builtin_popcount(word);
-                        if (out) out[(size_t)b * 64] = word;
-                    }
-                    selr[((t & 1) * kGramWords + q) * kFIters + wv * 64 + lane] = word;
-                }
-            }
-            __syncthreads();
-        }
-        if (live && emitted != s) atomicOr(&flags[p], 2);  // internal consistency check
-        if (evec && s >= 9) __syncthreads();  // the epilogue's staging barrier
-        return;
-    }
-    // ---------------------------------------------------- MFMA wave: 32 iterations
-    const int k = wv - kFSw;
-    i32x16 acc[kGramTiles];
-    {
-        const int r = lane & 31, hh = lane >> 5;
-        const int8_t* lg = limbs + (size_t)p * nbw * kGramWordBytes + lane * 16;
-        const int np = fused_pieces(k), pc0 = fused_piece0(k);
-        auto issue = [&](int step) {
-            int8_t* slot = lds + (step % kFRing) * kFLimbSlot;
-            const int8_t* src = lg + (size_t)step * kGramSelOff;
-            for (int q = 0; q < np; q++)
-                __builtin_amdgcn_global_load_lds((glb_vptr)(src + (pc0 + q) * 1024),
-                                                 (lds_vptr)(slot + (pc0 + q) * 1024), 16, 0, 0);
-        };
-#pragma unroll
-        for (int t = 0; t < kGramTiles; t++)
-#pragma unroll
-            for (int e = 0; e < 16; e++) acc[t][e] = 0;
-        const int boff = r * 32 + (((hh ^ (r >> 3)) & 1) << 4);
-        // step st's limbs are DMA'd at iteration st + 2 - kFRing (two steps ahead), into the slot
-        // the MFMA waves last read at iteration st + 1 - kFRing (finished before that barrier);
-        // iteration t waits for the DMA it issued kFRing - 2 iterations earlier
-        static_assert(kFRing == 3, "lookahead");
-        if (!(diag & 1)) issue(0);
-        for (int t = 0; t <= nsteps; t++) {
-            if (t + 1 < nsteps && !(diag & 1)) issue(t + 1);
-            if (t >= 1 && !(diag & 1)) {
-                const int st = t - 1;
-                const int8_t* slot = lds + (st % kFRing) * kFLimbSlot;
-                i32x4 bf[kGramWords][kGramTiles];
-#pragma unroll
-                for (int q = 0; q < kGramWords; q++)
-#pragma unroll
-                    for (int tt = 0; tt < kGramTiles; tt++)
-                        bf[q][tt] = *reinterpret_cast<const i32x4*>(slot + q * kGramWordBytes +
-                                                                    tt * 32 * 32 + boff);
-                uint32_t wsel[kGramWords];
-#pragma unroll
-                for (int q = 0; q < kGramWords; q++)
-                    wsel[q] = selr[((st & 1) * kGramWords + q) * kFIters + k * 32 + r];
-                i32x4 a[kGramWords];
-#pragma unroll
-                for (int q = 0; q < kGramWords; q++) {
-                    const uint32_t bits = (wsel[q] >> (16 * hh)) & 0xffffu;
-#pragma unroll
-                    for (int v = 0; v < 4; v++)
-                        a[q][v] = (int)((((bits >> (4 * v)) & 0xfu) * 0x00204081u) & 0x01010101u);
-                }
-#pragma unroll
-                for (int q = 0; q < kGramWords; q++)
-#pragma unroll
-                    for (int tt = 0; tt < kGramTiles; tt++)
-                        acc[tt] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[q], bf[q][tt], acc[tt], 0, 0, 0);
-            }
-            // step t's DMAs (issued in the previous iteration) have landed; step t + 1's may fly
-            if (t + 1 < nsteps && !(diag & 1)) {
-                if (np == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            __syncthreads();
-        }
-    }
-    // ---------------------------------------------------- epilogue (MFMA waves hold the sums)
-    double* go = gram + (size_t)p * 36 * iters;
-    if (evec && s >= 9) {  // uniform over the block
-        double* stg = reinterpret_cast<double*>(lds);
-        {
-            const int r = lane & 31, hh = lane >> 5;
-#pragma unroll
-            for (int e = 0; e < 16; e++) {
-                const int row = k * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
-                long long v = 0;
-#pragma unroll
-                for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[t][e] << (8 * t);
-                long long v2 = 0;
-                const int x = acc[kGramLimbs][e];
-#pragma unroll
-                for (int t = 0; t < kGramLimbs; t++)
-                    v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
-                stg[r * kFStg + row] = (double)v * (1.0 / kGramScale);
-                if (r < 4) stg[(32 + r) * kFStg + row] = (double)v2 * (1.0 / kGramScale);
-            }
-        }
-        __syncthreads();
-        if (k >= kFIters / 64) return;
-        const int hl = k * 64 + lane, h = hb + hl;
-        double e[9];
-        const bool ok = gram_min_eigvec9_inv(stg, kFStg, hl, e);
-        if (h >= iters) return;
-        if (!ok) {
-            e[0] = __builtin_nan("");
-#pragma unroll 4
-            for (int c = 0; c < 36; c++) go[(size_t)c * iters + h] = stg[c * kFStg + hl];
-        }
-        double* eo = evec + (size_t)p * 9 * iters + h;
-#pragma unroll
-        for (int c = 0; c < 9; c++) eo[(size_t)c * iters] = e[c];
-        return;
-    }
-    const int r = lane & 31, hh = lane >> 5;
-    const int h0 = hb + k * 32;
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-        const int row = (e & 3) + 8 * (e >> 2) + 4 * hh;
-        long long v = 0;
-#pragma unroll
-        for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[t][e] << (8 * t);
-        long long v2 = 0;
-        const int x = acc[kGramLimbs][e];
 #pragma unroll
         for (int t = 0; t < kGramLimbs; t++)
             v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
@@ -2911,6 +2591,9 @@ static_assert(kLipStep % 4 == 0, "a reference row is never a second-stage refere
 #endif
 constexpr int kRefStep = ERP_REF_STEP;  // every 16th survivor is refined first (refine pass)
 constexpr int kLipMinK = 1024;  // smaller sets: no pre-pruning (every non-reference row listed)
+// the convexity-augmented pruning's central references: UB_c <= U kLipGFac (consensus_grad_select;
+// r04 A/B, profiles/r04c_ab_consensus_knobs.txt: 1.03 cost +0.2 ms of consensus per step)
+constexpr float kLipGFac = 1.1f;
 #ifndef ERP_LIP2_STEP
 #define ERP_LIP2_STEP 4
 #endif
@@ -4197,41 +3880,7 @@ __global__ __launch_bounds__(256) void consensus_zoom_kernel(
                               bsel_out);
 }
 
-// Before the Lipschitz pre-pruning: the reference rows whose first-pass UB is within 3 % of the
-// smallest (<= kBoundRows of them: one zoom unit per pair) are listed for a zoom pass, so that
-// U = min UB over the references -- the bound every pruning test subtracts -- is ~4x tighter.
-__global__ __launch_bounds__(256) void consensus_pick_central_kernel(
-    const int32_t* __restrict__ kcount, const double* __restrict__ ub, int stride, int shard,
-    int nshards, int32_t* __restrict__ list, int32_t* __restrict__ count, int all) {
-    __shared__ double red[4];
-    __shared__ int n_s;
-    const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
-    const int K = kcount[p];
-    const int ra = (int)((int64_t)K * shard / nshards), rb = (int)((int64_t)K * (shard + 1) / nshards);
-    const int nref = rb > ra ? (rb - ra + kLipStep - 1) / kLipStep : 0;
-    const double* U = ub + (size_t)p * stride;
-    double m = __builtin_huge_val();
-    for (int c = tid; c < nref; c += 256) m = fmin(m, U[ra + c * kLipStep]);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = fmin(m, __shfl_xor(m, o, 64));
-    if (lane == 0) red[tid >> 6] = m;
-    if (tid == 0) n_s = 0;
-    __syncthreads();
-    m = fmin(fmin(red[0], red[1]), fmin(red[2], red[3]));
-    const double lim = all ? __builtin_huge_val() : m * 1.03;
-    const int cap = all ? stride : kBoundRows;
-    for (int c = tid; c < nref && m < __builtin_huge_val(); c += 256) {
-        const int row = ra + c * kLipStep;
-        if (U[row] <= lim) {
-            const int k = atomicAdd(&n_s, 1);
-            if (k < cap) list[(size_t)p * stride + k] = row;
-        }
-    }
-    __syncthreads();
-    if (tid == 0) count[p] = min(n_s, cap);
-}
-
-// ---- flat pairs (round 4, ERP_FLAT_REFS) -------------------------------------------------
+// ---- flat pairs (round 4, ERP_OPT_FLAT_REFS) -------------------------------------------------
 // A pair whose first-stage pruning kept more than flat_pct % of its rows is flat: every
 // trimmed mean lies within the coarse bounds' 2^-5 of the minimum (the two-cluster sets of R1
 // and R2 both valid in every iteration: K = 2 iters, every T within ~1e-3 of min T), so the
@@ -4972,18 +4621,11 @@ static int q_needed(int iters) {
 }
 
 // dynamic LDS above 64 KB is requested from the runtime first (hipFuncAttribute-
-// MaxDynamicSharedMemorySize); the largest size set per kernel is remembered, so the call is
-// made only when a launch needs more than any earlier one
-static hipError_t ensure_dyn_lds(const void* fn, size_t bytes, std::atomic<size_t>& done) {
-    if (bytes <= 64 * 1024 || bytes <= done.load(std::memory_order_relaxed)) return hipSuccess;
-    const hipError_t e =
-        hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
-    if (e == hipSuccess) {
-        size_t cur = done.load();
-        while (cur < bytes && !done.compare_exchange_weak(cur, bytes)) {
-        }
-    }
-    return e;
+// MaxDynamicSharedMemorySize) -- at every such launch: the attribute is per device, contexts may
+// live on any device of the process, and the call is cheap next to these launches
+static hipError_t ensure_dyn_lds(const void* fn, size_t bytes) {
+    if (bytes <= 64 * 1024) return hipSuccess;
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
 }
 
 hipError_t launch_jump_prep(const int32_t* counts, const BatchShape& sh, uint32_t* polyR,
@@ -5008,33 +4650,28 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
         // gfx950, scripts/dev/lds_oob.hip) so that no word of the allocation goes uncleared
         const int nwords = (sh.max_s / 32 + 1 + 4) / 5 * 5;
         const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
-        // ERP_SAMPLER_ILP=1: the blocks with their 31 positions computed first (A/B knob).
         // The latency blocks (modes 2 / 3) where the launch leaves most SIMDs with at most one
-        // wave (<= 1024 waves); ERP_SAMPLER_LAT = 0 / 1 / 2 forces mode 0 / 2 / 3
-        // (read at every launch, like ERP_SMALL_BATCH: the GPU tests switch them within a process)
-        const bool ilp = getenv("ERP_SAMPLER_ILP") && atoi(getenv("ERP_SAMPLER_ILP")) != 0;
-        const int lat_env = getenv("ERP_SAMPLER_LAT") ? atoi(getenv("ERP_SAMPLER_LAT")) : -1;
-        const int lat = lat_env >= 0 ? lat_env : (long)nwaves * sh.n_pairs <= 1024 ? kSamplerLatMode : 0;
-        const int mode = ilp ? 1 : lat == 1 ? 2 : lat == 2 ? 3 : 0;
+        // wave (<= 1024 waves); sh.sampler_lat (ERP_OPT_SAMPLER_LAT) = 0 / 1 / 2 forces mode
+        // 0 / 2 / 3
+        const int lat = sh.sampler_lat >= 0 ? sh.sampler_lat
+                                            : (long)nwaves * sh.n_pairs <= 1024 ? kSamplerLatMode : 0;
+        const int mode = lat == 1 ? 2 : lat == 2 ? 3 : 0;
         // (s up to 16 383 at the 65 535-keypoint cap: 515 words x 256 B = 129 KB)
-        static std::atomic<size_t> lds_set[4];
-        const void* fns[4] = {(const void*)sampler_kernel<0>, (const void*)sampler_kernel<1>,
+        const void* fns[4] = {(const void*)sampler_kernel<0>, nullptr,
                               (const void*)sampler_kernel<2>, (const void*)sampler_kernel<3>};
-        const hipError_t le = ensure_dyn_lds(fns[mode], shmem, lds_set[mode]);
+        const hipError_t le = ensure_dyn_lds(fns[mode], shmem);
         if (le != hipSuccess) return le;
 #define ERP_SAMPLER_LAUNCH(M)                                                                  \
     ERP_LAUNCH(sampler_kernel<M>, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts, wins, \
                nwaves, sh.sel_words, sample_frac, rtab, selw, flags, nwords)
         // the split replay (sampler_split_kernel) where the launch has <= 256 workgroups of
         // 64 iterations (one pair at <= 16k iterations) and its 7 bitmaps fit the CU's LDS;
-        // ERP_SAMPLER_SPLIT = 0 / 1 forces it off / on (when the LDS fits)
-        const int split_env = getenv("ERP_SAMPLER_SPLIT") ? atoi(getenv("ERP_SAMPLER_SPLIT")) : -1;
+        // sh.sampler_split (ERP_OPT_SAMPLER_SPLIT) = 0 / 1 forces it off / on (when the LDS fits)
         const size_t split_lds = (size_t)(2 * kSplitG + 1) * nwords * 64 * sizeof(uint32_t);
-        const bool split = !ilp && split_env != 0 && split_lds <= 150 * 1024 &&
-                           (split_env > 0 || (long)nwaves * sh.n_pairs <= 256);
+        const bool split = sh.sampler_split != 0 && split_lds <= 150 * 1024 &&
+                           (sh.sampler_split > 0 || (long)nwaves * sh.n_pairs <= 256);
         if (split) {
-            static std::atomic<size_t> split_set{0};
-            const hipError_t se = ensure_dyn_lds((const void*)sampler_split_kernel, split_lds, split_set);
+            const hipError_t se = ensure_dyn_lds((const void*)sampler_split_kernel, split_lds);
             if (se != hipSuccess) return se;
             ERP_LAUNCH(sampler_split_kernel, dim3(nwaves, sh.n_pairs), dim3(64 * (kSplitG + 1)),
                        split_lds, st, counts, wins, nwaves, sh.sel_words, sample_frac, rtab, selw,
@@ -5042,7 +4679,6 @@ hipError_t launch_sampler(const int32_t* counts, const uint32_t* polyR, const ui
             return hipGetLastError();
         }
         switch (mode) {
-            case 1: ERP_SAMPLER_LAUNCH(1); break;
             case 2: ERP_SAMPLER_LAUNCH(2); break;
             case 3: ERP_SAMPLER_LAUNCH(3); break;
             default: ERP_SAMPLER_LAUNCH(0); break;
@@ -5060,8 +4696,7 @@ hipError_t launch_philox_sampler(const int32_t* counts, const BatchShape& sh, do
     // one CU's LDS: 640 words = M <= 20 480; a pair with more matches gets ERP_INVALID_ARG
     const int nwords = std::min((max_m + 31) / 32, 640);
     const size_t shmem = (size_t)nwords * 64 * sizeof(uint32_t);
-    static std::atomic<size_t> lds_set{0};
-    const hipError_t le = ensure_dyn_lds((const void*)philox_sampler_kernel, shmem, lds_set);
+    const hipError_t le = ensure_dyn_lds((const void*)philox_sampler_kernel, shmem);
     if (le != hipSuccess) return le;
     ERP_LAUNCH(philox_sampler_kernel, dim3(nwaves, sh.n_pairs), dim3(64), shmem, st, counts,
                        sh.iters, nwaves, sh.sel_words, sample_frac, seed, offset, nwords, selw,
@@ -5086,12 +4721,13 @@ bool build_magic_table(uint64_t* mtab, int n) {
     return ok;
 }
 
-// debug counters of ERP_LIP_VERIFY builds (0 = copied and reset; -1 = not a verify build)
+// debug counters of ERP_LIP_VERIFY builds (0 = copied and reset; -1 = not a verify build;
+// -2 = the copy failed)
 int debug_lip_counters(uint32_t* out64) {
 #if ERP_LIP_VERIFY
-    if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_lip_dbg), 64 * 4) != hipSuccess) return 1;
+    if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(g_lip_dbg), 64 * 4) != hipSuccess) return -2;
     static const uint32_t zero[64] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lip_dbg), zero, 64 * 4) != hipSuccess) return 1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_lip_dbg), zero, 64 * 4) != hipSuccess) return -2;
     return 0;
 #else
     (void)out64;
@@ -5115,9 +4751,9 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
     const int nwaves = (sh.iters + 63) / 64;
     ERP_LAUNCH(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
                        pts, sh.max_nq, sh.sel_words, limbs);
-    // row tiles per wave: 2 once the wide blocks give every CU two of them (GramCfg)
-    const char* wt_env = getenv("ERP_GRAM_WT");
-    const int wt_force = wt_env ? atoi(wt_env) : 0;
+    // row tiles per wave: 2 once the wide blocks give every CU two of them (GramCfg);
+    // sh.gram_tiles (ERP_OPT_GRAM_TILES) = 1 / 2 forces one
+    const int wt_force = sh.gram_tiles;
     const int nhb2 = (sh.iters + GramCfg<2>::kIters - 1) / GramCfg<2>::kIters;
     const bool wide = wt_force == 2 || (wt_force != 1 && (long long)nhb2 * sh.n_pairs >= 2 * 256);
     if (wide) {
@@ -5130,62 +4766,6 @@ hipError_t launch_gram_mfma(const int32_t* counts, const double* pts, const uint
                    limbs, selw, sh.iters, nwaves, sh.sel_words, sample_frac, gram, nhb, evec, hyps,
                    valid_abs);
     }
-    if (samples)
-        ERP_LAUNCH(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
-                           sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);
-    return hipGetLastError();
-}
-
-hipError_t launch_gram_limbs(const int32_t* counts, const double* pts, const BatchShape& sh,
-                             int8_t* limbs, hipStream_t st) {
-    ERP_LAUNCH(gram_limbs_kernel, dim3(sh.sel_words, sh.n_pairs), dim3(256), 0, st, counts,
-                       pts, sh.max_nq, sh.sel_words, limbs);
-    return hipGetLastError();
-}
-
-// bitmap rows (one 32-position word of each sampler wave per row) and the allocation: rows cover
-// positions 0 .. max_s (sampler_kernel's rule), the total is a multiple of 5120 B (whole 1-KB
-// rows and whole 1280-B allocation granules) with the bitmaps at its top
-static void sampler_gram_lds(const BatchShape& sh, int* rows, int* bm_base, size_t* bytes) {
-    *rows = sh.max_s / 32 + 1;
-    size_t need = std::max<size_t>((size_t)kFRingBytes + (size_t)*rows * kFRowBytes,
-                                   (size_t)kFStgBytes);
-    need = (need + 5119) / 5120 * 5120;
-    *bytes = need;
-    *bm_base = (int)(need - (size_t)*rows * kFRowBytes);
-}
-
-// ERP_FUSED_DIAG (development): bit 0 = the MFMA waves skip their DMAs and MFMAs, bit 1 = the
-// sampler waves skip the replay (results are then wrong: timing decomposition only)
-static int fused_diag() {
-    static const int d = getenv("ERP_FUSED_DIAG") ? atoi(getenv("ERP_FUSED_DIAG")) : 0;
-    return d;
-}
-
-bool sampler_gram_fits(const BatchShape& sh) {
-    int rows, base;
-    size_t bytes;
-    sampler_gram_lds(sh, &rows, &base, &bytes);
-    return bytes <= (size_t)kFMaxLds;
-}
-
-hipError_t launch_sampler_gram(const int32_t* counts, const uint32_t* wins, const int8_t* limbs,
-                               const double* rtab, const BatchShape& sh, double sample_frac,
-                               int32_t* flags, uint32_t* selw, int32_t* samples, double* gram,
-                               double* evec, hipStream_t st) {
-    int rows, bm_base;
-    size_t bytes;
-    sampler_gram_lds(sh, &rows, &bm_base, &bytes);
-    if (bytes > (size_t)kFMaxLds) return hipErrorInvalidValue;
-    static std::atomic<size_t> lds_set{0};
-    const hipError_t le = ensure_dyn_lds((const void*)sampler_gram_kernel, bytes, lds_set);
-    if (le != hipSuccess) return le;
-    const int nwaves = (sh.iters + 63) / 64;
-    const int nhb = (sh.iters + kFIters - 1) / kFIters;
-    uint32_t* sw = samples ? selw : nullptr;
-    ERP_LAUNCH(sampler_gram_kernel, dim3(nhb * sh.n_pairs), dim3(kFThreads), bytes, st,
-                       counts, wins, limbs, rtab, sh.iters, nwaves, sh.sel_words, sample_frac,
-                       rows, bm_base, flags, sw, gram, nhb, evec, fused_diag());
     if (samples)
         ERP_LAUNCH(samples_kernel, dim3(nwaves, sh.n_pairs), dim3(64), 0, st, counts, selw,
                            sh.iters, nwaves, sh.sel_words, sh.idx_stride, sample_frac, samples);
@@ -5391,9 +4971,10 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                    float* edges, const BatchShape& sh, double trim_lo,
                                    double trim_hi, double* lb, double* ub, int32_t* bsel,
                                    int shard, int nshards, int32_t* rlist, int32_t* rcount,
-                                   int32_t* zsel, int zoom_refs, int lip2, int32_t* list2,
-                                   void* lipref, int lipg, float gfac, int flat_pct,
-                                   int use_hint, hipStream_t st, bool edges_ready) {
+                                   int32_t* zsel, int lip2, int32_t* list2, void* lipref,
+                                   int lipg, int flat_pct, int use_hint, hipStream_t st,
+                                   bool edges_ready) {
+    const float gfac = kLipGFac;
     if (!edges_ready)
         ERP_LAUNCH(consensus_edges_kernel, dim3(sh.n_pairs), dim3(256), 0, st, dscale, edges);
     const int stride = 2 * sh.iters;
@@ -5415,15 +4996,6 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
     dim3 g1((nref + kBoundRows - 1) / kBoundRows, sh.n_pairs);
     ERP_LAUNCH(consensus_bounds_kernel, g1, dim3(256), 0, st, kcount, rv, dscale, edges,
                        stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, kLipStep);
-    if (zoom_refs) {  // the central references on the zoom grid: a tighter U for the pruning
-        int32_t* cnt = rcount - sh.n_pairs;  // (nsurv[0 .. P): free until the first select)
-        ERP_LAUNCH(consensus_pick_central_kernel, dim3(sh.n_pairs), dim3(256), 0, st,
-                           kcount, (const double*)ub, stride, shard, nshards, rlist, cnt,
-                           zoom_refs > 1 ? 1 : 0);
-        const hipError_t ze = launch_consensus_zoom(kcount, rv, dscale, edges, sh, trim_lo,
-                                                    trim_hi, lb, ub, bsel, rlist, cnt, zsel, 1, st);
-        if (ze != hipSuccess) return ze;
-    }
     const int P = sh.n_pairs;
     const LipRefViews lr = lipref_views(lipref, P, stride);
     const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * P, st);

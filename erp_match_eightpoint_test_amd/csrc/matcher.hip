@@ -261,6 +261,12 @@ __device__ __forceinline__ int cand_tile(bf16x8 v0, bf16x8 v1) {
 // filter 2.96 -> 2.89 ms per step, but lanes that stop extracting leave holes in their lines --
 // filter writes 124 -> 194 MB and rescore reads 200 -> 217 MB per 128-pair launch
 // (profiles/r05q_ab_slots.txt), so the contiguous lists stay.
+// ERP_CAND_TILE_ARRAY=1 (development build only): the tile index of a candidate slot in its own
+// int32 array (the layout before round 3; the inline index won the A/B)
+#ifndef ERP_CAND_TILE_ARRAY
+#define ERP_CAND_TILE_ARRAY 0
+#endif
+constexpr int kCandTileArray = ERP_CAND_TILE_ARRAY;
 #ifndef ERP_CAND_INTERLEAVE
 #define ERP_CAND_INTERLEAVE 0
 #endif
@@ -286,8 +292,8 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
                                                           bf16x8* __restrict__ cval,
                                                           const bf16x8* __restrict__ sent_hi,
                                                           const float* __restrict__ sent_tu,
-                                                          int tile_array,
                                                           float* __restrict__ qn) {
+    constexpr int tile_array = kCandTileArray;
     __shared__ __align__(16) char sm[2 * kFStageB];
     // XCD-aware block order: workgroups are dealt to the 8 XCDs round-robin by linear id, so
     // XCD x gets the contiguous logical range [x NB/8, (x+1) NB/8) (query blocks fastest, then
@@ -648,8 +654,9 @@ __global__ __launch_bounds__(256) void knn2_rescore_kernel(const float* __restri
                                                            const bf16x8* __restrict__ cval,
                                                            Top2* __restrict__ part,
                                                            int32_t* __restrict__ ovf, int qblocks,
-                                                           float ratio, int tile_array,
+                                                           float ratio,
                                                            const float* __restrict__ qn) {
+    constexpr int tile_array = kCandTileArray;
     __shared__ int32_t plist[kPassList * 256];
     __shared__ float plb[kPassList * 256];
     // XCD-aware block order as in knn2_filter (a pair's blocks on one XCD: its f32 train rows,
@@ -1154,13 +1161,6 @@ __global__ __launch_bounds__(kMergeBlock) void knn2_merge_kernel(
 }  // namespace
 
 // ====================================================================== launchers =======
-// ERP_CAND_TILE_ARRAY=1: the tile index of a candidate slot in its own int32 array (the
-// layout before round 3, an A/B knob); default: inside the slot's bf16 bounds
-static bool cand_tile_array() {
-    static const bool v = getenv("ERP_CAND_TILE_ARRAY") && atoi(getenv("ERP_CAND_TILE_ARRAY")) != 0;
-    return v;
-}
-
 size_t knn2_cand_bytes(const BatchShape& sh) {
     return (size_t)sh.n_pairs * ((sh.max_nq + 31) / 32 * 32) * sh.fchunks * 2 * kCandSlots *
            (2 * sizeof(bf16x8) + 4);
@@ -1209,7 +1209,7 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
     ERP_LAUNCH(knn2_filter_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
                        st, desc_q, thi, tn, tmax, off_q, off_t, sh.fchunk_len, sh.fchunks,
                        sh.max_nq, sh.max_nt, qblocks, pu, ccount, ctile, cval,
-                       (const bf16x8*)sent, (const float*)(sent + 128), (int)cand_tile_array(), qn);
+                       (const bf16x8*)sent, (const float*)(sent + 128), qn);
     return hipGetLastError();
 }
 
@@ -1226,7 +1226,6 @@ hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const i
                        st, desc_q, desc_t, off_q, off_t, sh.max_nq, sh.fchunk_len, sh.fchunks,
                        split_tmax(sh, split), pu, ccount, ctile, cval, part, ovf, qblocks,
                        sh.fchunks == 1 ? ratio : -1.f,  // (bound decisions need one chunk)
-                       (int)cand_tile_array(),
                        (const float*)(pu + (size_t)sh.n_pairs * sh.max_nq * sh.fchunks));
     ERP_LAUNCH(knn2_sweep_kernel, dim3(256), dim3(256), 0, st, desc_q, desc_t, off_q, off_t,
                        sh.max_nq, sh.fchunk_len, sh.fchunks, ovf, part);

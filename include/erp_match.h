@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define ERP_MATCH_ABI_VERSION 1
+#define ERP_MATCH_ABI_VERSION 2  /* 2: erp_ctx_set_option replaced the environment knobs (r06) */
 
 typedef enum erp_status {
     ERP_OK = 0,
@@ -204,7 +204,7 @@ typedef enum erp_stage {
     ERP_STAGE_KNN2_RESCORE = 14,    /* exact flann::L2 distances of the candidates */
     ERP_STAGE_CONSENSUS_REFINE = 15, /* tighter bounds for the survivors (sub-bins) */
     ERP_STAGE_KNN2_EXACT = 16,      /* exact sweep on packed FP32 VALU (ERP_MATCHER_VALU_EXACT) */
-    ERP_STAGE_SAMPLER_GRAM = 17,    /* the sampler replay and the Gram MFMAs in one kernel */
+    ERP_STAGE_SAMPLER_GRAM = 17,    /* unused since r06 (the fused sampler + Gram kernel, slower, was removed) */
     ERP_STAGE_INLIERS = 18,         /* opt-in per-iteration inlier count (cfg.inlier_thr > 0) */
     ERP_STAGE_COUNT = 19
 } erp_stage;
@@ -231,19 +231,67 @@ erp_status erp_ctx_set_matcher(erp_ctx* ctx, int32_t method);
    captures anew (up to 8 graphs per context, least recently used dropped).  Not used while
    stage timing is on or on the NULL stream.  Default off. */
 erp_status erp_ctx_set_graphs(erp_ctx* ctx, int32_t enable);
-/* debugging hooks (no reference counterpart), inert unless their environment variable is set
-   when the buffers / context are created:
-   ERP_ALLOC_PAD = N: every device buffer gets N canary bytes past its end;
-   erp_debug_check_pads() returns how many canaries a kernel overwrote (reported on stderr).
-   ERP_DEBUG_SNAP = 1: erp_pair_batch_run keeps a device copy of lb, ub ([P][2 iters] f64 each),
-   the first-stage list counts ([P] i32) and the first-stage Lipschitz references right after
-   the bounds pass; erp_debug_snapshot copies it to host (returns its size; host NULL: size
-   only). */
+/* Route options of a context (no reference counterpart).  Each selects between code paths whose
+   results are identical -- by construction, and checked by the GPU tests that set it -- and
+   whose default is the measured fastest; none changes what is computed.  The library reads no
+   environment variable: these setters are the only way to steer a route.  Options are part of
+   a captured HIP graph's key (erp_ctx_set_graphs).  -1 = automatic where noted.
+   ERP_OPT_SMALL_BATCH    consensus route: -1 auto (n_pairs (2 iters)^2 <= 2e9); n >= 0: batches
+                          of <= n pairs bin every row in one pass (0 = never)
+   ERP_OPT_SAMPLER_LAT    glibc replay blocks: -1 auto (latency blocks for launches of <= 1024
+                          waves); 0 throughput blocks, 1 latency step by step, 2 latency with
+                          the block's positions first
+   ERP_OPT_SAMPLER_SPLIT  split replay: -1 auto (<= 256 workgroups); 0 off; 1 on (where its
+                          bitmaps fit the LDS)
+   ERP_OPT_GRAM_TILES     32-iteration row tiles per Gram MFMA wave: 0 auto (2 once the launch
+                          has >= 512 wide blocks), 1, 2
+   ERP_OPT_ZOOM_LEVELS    the survivors' zoom levels 0 (default) .. 2
+   ERP_OPT_SMALL_ZOOM     1: the small-batch route keeps the zoom levels (default 0)
+   ERP_OPT_LIP2           second pre-pruning stage 1 (default) / 0
+   ERP_OPT_LIPG           convexity-augmented pre-pruning: bit 0 first stage (default 1), bit 1
+                          second stage too (3), 0 off
+   ERP_OPT_REFINE_HINT    hinted refine windows 1 (default) / 0
+   ERP_OPT_FLAT_REFS      flat-pair route above this % of rows listed: 25 (default); 0 off
+   ERP_OPT_BOUND_RATIO    the matcher's ratio test decided from the bf16 bounds where they
+                          suffice 1 (default) / 0
+   ERP_OPT_DEBUG_STAGES   debug: bit mask of the stage groups erp_pair_batch_run enqueues (1
+                          matcher + gather, 2 jump polynomials + windows, 4 sampler, 8 Gram, 32
+                          eigen + estimate, 16 consensus); -1 (default) all.  A skipped group
+                          leaves the previous call's scratch in place.
+   ERP_OPT_DEBUG_SNAP     debug: 1 keeps a device copy of lb, ub ([P][2 iters] f64 each), the
+                          first-stage list counts ([P] i32) and the first-stage Lipschitz
+                          references right after the bounds pass, for erp_debug_snapshot */
+typedef enum erp_ctx_option {
+    ERP_OPT_SMALL_BATCH = 0,
+    ERP_OPT_SAMPLER_LAT = 1,
+    ERP_OPT_SAMPLER_SPLIT = 2,
+    ERP_OPT_GRAM_TILES = 3,
+    ERP_OPT_ZOOM_LEVELS = 4,
+    ERP_OPT_SMALL_ZOOM = 5,
+    ERP_OPT_LIP2 = 6,
+    ERP_OPT_LIPG = 7,
+    ERP_OPT_REFINE_HINT = 8,
+    ERP_OPT_FLAT_REFS = 9,
+    ERP_OPT_BOUND_RATIO = 10,
+    ERP_OPT_DEBUG_STAGES = 11,
+    ERP_OPT_DEBUG_SNAP = 12,
+    ERP_OPT_COUNT = 13
+} erp_ctx_option;
+/* ERP_INVALID_ARG for an unknown option or a value outside its range */
+erp_status erp_ctx_set_option(erp_ctx* ctx, int32_t option, int32_t value);
+erp_status erp_ctx_get_option(erp_ctx* ctx, int32_t option, int32_t* value);
+/* debugging hooks (no reference counterpart):
+   erp_debug_set_alloc_pad(N): device buffers allocated from then on get N canary bytes (0xA5)
+   past their end (process-wide; 0 = off, the default); erp_debug_check_pads() returns how
+   many canaries a kernel overwrote (reported on stderr).
+   erp_debug_snapshot (ERP_OPT_DEBUG_SNAP) copies the snapshot to host (returns its size; host
+   NULL: size only). */
+void erp_debug_set_alloc_pad(size_t bytes);
 int erp_debug_check_pads(void);
 long long erp_debug_snapshot(erp_ctx* ctx, void* host, size_t bytes);
 /* debug counters of a library built with -DERP_LIP_VERIFY=1 (the Lipschitz pruning pass
    re-checks its LDS operands against their global sources): copies 64 words into out64 and
-   resets them; returns 0, or -1 for a library built without the check. */
+   resets them; returns 0, -1 for a library built without the check, -2 when the copy failed. */
 int erp_debug_lip_counters(uint32_t* out64);
 
 /* device pointers; writes up to nq matches in ascending queryIdx order and *d_count. */

@@ -1,7 +1,7 @@
 """Probe (round 5): which pipeline stage perturbs kernels running beside it on other streams?
 
 Part 1 (GUARD=1): the LDS guard kernel (scripts/dev/lds_guard.hip) on a stream of its own while
-one stage group of the pipeline (ERP_DEBUG_STAGES mask) runs on S sub-batch streams: every LDS
+one stage group of the pipeline (ERP_OPT_DEBUG_STAGES mask) runs on S sub-batch streams: every LDS
 word of a guard workgroup that changes under it was written by another workgroup.
 
 Part 2 (PAIRS=1): the victim = sub-batch 0's consensus alone (mask 16), the aggressors = the other
@@ -37,7 +37,7 @@ for i in range(S):
 
 
 def run_one(sb, mask):
-    os.environ["ERP_DEBUG_STAGES"] = str(mask)
+    sb["run"].ctx.set_option("debug_stages", mask)  # (ERP_OPT_DEBUG_STAGES)
     b = sb["b"]
     with torch.cuda.stream(sb["st"]):
         o = sb["run"].run(b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"], b["off_r"],
@@ -50,7 +50,8 @@ def run_one(sb, mask):
 for sb in subs:
     run_one(sb, -1)
     torch.cuda.synchronize()
-os.environ["ERP_DEBUG_STAGES"] = "-1"
+for _sb in subs:
+    _sb["run"].ctx.set_option("debug_stages", -1)
 print("sampler", SAMPLER, "sub-batches", S, "lib", os.environ.get("ERP_LIB_PATH", "in-tree"), flush=True)
 
 if os.environ.get("GUARD", "1") == "1":
@@ -106,7 +107,8 @@ if os.environ.get("GUARD", "1") == "1":
             print(f"   blk {blk} word {idx} got {got:#010x} expected {exp:#010x} "
                   f"(cleared {exp & ~got:#010x}, set {got & ~exp:#010x}) hw_id {hw:#x} xcc {xcc:#x} "
                   f"t+{dt / 100:.0f} us", flush=True)
-    os.environ["ERP_DEBUG_STAGES"] = "-1"
+    for _sb in subs:
+        _sb["run"].ctx.set_option("debug_stages", -1)
 
 if os.environ.get("PK", "0") == "1":
     # the packed-f32 pruning test against scalar f32 (scripts/dev/lds_guard.hip pk_probe_kernel)
@@ -143,7 +145,8 @@ if os.environ.get("PK", "0") == "1":
             blk, tid, q, d0, t0s, d1, t1s, dt = (int(x) for x in r)
             print(f"   blk {blk} tid {tid} ref {q}: lo {d0:#010x} vs {t0s:#010x}, hi {d1:#010x} vs {t1s:#010x}, t+{dt / 100:.0f} us",
                   flush=True)
-    os.environ["ERP_DEBUG_STAGES"] = "-1"
+    for _sb in subs:
+        _sb["run"].ctx.set_option("debug_stages", -1)
 
 if os.environ.get("PAIRS", "1") == "1":
     vic = subs[0]

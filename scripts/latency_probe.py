@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def probe(runs: int, kpts: int, iters: int, seed: int, graphs: bool = False) -> dict:
+def probe(runs: int, kpts: int, iters: int, seed: int, graphs: bool = False, opts=None) -> dict:
     import torch
 
     from erp_match_eightpoint_test_amd import Context, PairBatchRunner, synth
@@ -36,6 +36,9 @@ def probe(runs: int, kpts: int, iters: int, seed: int, graphs: bool = False) -> 
             t(np.array([0, kpts], np.int64)), t(np.array([0, kpts], np.int64)),
             t(np.array([p["W"]], np.int32)), t(np.array([p["H"]], np.int32)), kpts, kpts)
     ctx = Context(0)
+    for kv in opts or []:  # --ctx-option name=value (erp_ctx_set_option)
+        k, v = kv.split("=")
+        ctx.set_option(k, int(v))
     ctx.set_graphs(graphs)  # erp_ctx_set_graphs: replay the captured launch sequence
     run = PairBatchRunner(ctx=ctx, iters=iters, reuse_outputs=True)
     st = torch.cuda.Stream(dev)  # (graphs need a capturable, non-NULL stream)
@@ -99,6 +102,8 @@ def main():
     ap.add_argument("--iters", type=int, default=10000)
     ap.add_argument("--seed", type=int, default=20200423)
     ap.add_argument("--graph", action="store_true", help="erp_ctx_set_graphs: HIP-graph replay")
+    ap.add_argument("--ctx-option", action="append", default=[],
+                    help="name=value: erp_ctx_set_option on the context (e.g. sampler_lat=1)")
     ap.add_argument("--report", default=None, help="rocprofv3 run_kernel_trace.csv to split")
     ap.add_argument("--host-json", default=None, help="merge this probe() record into --report")
     a = ap.parse_args()
@@ -108,7 +113,7 @@ def main():
             r["host"] = json.load(open(a.host_json))
         print(json.dumps(r, indent=1))
         return
-    print(json.dumps(probe(a.runs, a.kpts, a.iters, a.seed, a.graph)))
+    print(json.dumps(probe(a.runs, a.kpts, a.iters, a.seed, a.graph, a.ctx_option)))
 
 
 if __name__ == "__main__":

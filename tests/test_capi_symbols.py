@@ -35,7 +35,7 @@ def test_every_declared_symbol_exported(lib):
 
 def test_non_compute_entry_points(lib):
     from erp_match_eightpoint_test_amd import capi
-    assert lib.erp_abi_version() == 1
+    assert lib.erp_abi_version() == 2
     cfg = capi.RansacCfg()
     lib.erp_ransac_cfg_default(C.byref(cfg))
     assert (cfg.iters, cfg.sample_frac, cfg.trim_lo, cfg.trim_hi, cfg.valid_abs, cfg.seed) == \
@@ -46,6 +46,27 @@ def test_non_compute_entry_points(lib):
 def test_null_ctx_rejected(lib):
     assert lib.erp_ctx_destroy(None) == 1
     assert lib.erp_match_two_image(None, None, 0, None, 0, 64, None, None) == 1
+    assert lib.erp_ctx_set_option(None, 0, 0) == 1
+    v = C.c_int32()
+    assert lib.erp_ctx_get_option(None, 0, C.byref(v)) == 1
+
+
+def test_release_library_reads_no_environment():
+    """route choices are context options (erp_ctx_set_option), not environment variables: the
+    release library imports no getenv / secure_getenv at all (VERDICT r05 "next" 6)"""
+    from erp_match_eightpoint_test_amd import _build
+    out = os.popen(f"nm -D --undefined-only {_build.LIB_PATH}").read()
+    assert "getenv" not in out, [ln for ln in out.splitlines() if "getenv" in ln]
+
+
+def test_option_names_match_header():
+    """capi.OPTIONS mirrors the erp_ctx_option enum of include/erp_match.h"""
+    from erp_match_eightpoint_test_amd import capi
+    src = open(os.path.join(ROOT, "include", "erp_match.h")).read()
+    enum = dict((m.group(1).lower(), int(m.group(2)))
+                for m in re.finditer(r"ERP_OPT_([A-Z0-9_]+) = (\d+),", src))
+    enum.pop("count", None)
+    assert enum == capi.OPTIONS
 
 
 def test_cpp_class_api_symbols():

@@ -106,8 +106,45 @@ def test_lite_estimates_equal_records(overlap_setup):
         assert np.array_equal(lite[k].view(np.uint8), rec[k].view(np.uint8)), k
 
 
-def test_small_batch_route_equals_pruning_route(overlap_setup, monkeypatch):
-    """a batch of <= ERP_SMALL_BATCH pairs bins every row (no pre-pruning: the single-pair
+def test_lite_estimates_equal_records_one_pair(overlap_setup):
+    """the one-pair launch takes estimate_lite_kernel<true> (the eigen leftovers inlined: launches
+    of <= 1024 waves) -- against the record path on the same pair, byte for byte"""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner
+    pairs, _ = overlap_setup
+    sb = dict(b=bench.to_device(pairs[:1], "cuda"),
+              run=PairBatchRunner(ctx=Context(0), iters=ITERS), st=torch.cuda.Stream())
+    lite = _run(sb, want=("rvec", "tvec"))
+    torch.cuda.synchronize()
+    lite = {k: v.cpu().numpy() for k, v in lite.items()}
+    rec = _run(sb, want=("rvec", "tvec", "hyps"))
+    torch.cuda.synchronize()
+    rec = {k: v.cpu().numpy() for k, v in rec.items()}
+    for k in ("results", "rvec", "tvec"):
+        assert np.array_equal(lite[k].view(np.uint8), rec[k].view(np.uint8)), k
+
+
+def test_gram_row_tiles_identical(overlap_setup):
+    """the Gram kernel with one or two 32-iteration row tiles per wave (ERP_OPT_GRAM_TILES 1 / 2;
+    the launcher picks 2 for launches of >= 512 wide blocks) on the same 48-pair sub-batch: the
+    hypothesis records (E included), the sample sets and the result records byte-identical"""
+    import torch
+    from erp_match_eightpoint_test_amd import Context, PairBatchRunner
+    _, subs = overlap_setup
+    outs = {}
+    for wt in (1, 2):
+        c = Context(0)
+        c.set_option("gram_tiles", wt)
+        sb = dict(b=subs[3]["b"], run=PairBatchRunner(ctx=c, iters=ITERS), st=torch.cuda.Stream())
+        o = _run(sb, want=("hyps", "samples"))
+        torch.cuda.synchronize()
+        outs[wt] = {k: v.cpu().numpy() for k, v in o.items()}
+    for k in ("results", "hyps", "samples"):
+        assert np.array_equal(outs[1][k].view(np.uint8), outs[2][k].view(np.uint8)), k
+
+
+def test_small_batch_route_equals_pruning_route(overlap_setup):
+    """a batch of <= ERP_OPT_SMALL_BATCH pairs bins every row (no pre-pruning: the single-pair
     latency route); the same pairs through the pruning route give every result field equal
     (only the work counts binned_rows / survivors may differ)"""
     import torch
@@ -117,9 +154,10 @@ def test_small_batch_route_equals_pruning_route(overlap_setup, monkeypatch):
     args = (b["desc_l"], b["desc_r"], b["kp_l"], b["kp_r"], b["off_l"], b["off_r"], b["width"],
             b["height"], b["max_nq"], b["max_nt"])
     res = {}
-    for route, limit in (("all_rows", "8"), ("prune", "0")):
-        monkeypatch.setenv("ERP_SMALL_BATCH", limit)
-        out = PairBatchRunner(ctx=Context(0), iters=ITERS).run(*args)
+    for route, limit in (("all_rows", 8), ("prune", 0)):
+        c = Context(0)
+        c.set_option("small_batch", limit)
+        out = PairBatchRunner(ctx=c, iters=ITERS).run(*args)
         torch.cuda.synchronize()
         res[route] = results_to_numpy(out["results"])
     a, c = res["all_rows"], res["prune"]
@@ -129,8 +167,8 @@ def test_small_batch_route_equals_pruning_route(overlap_setup, monkeypatch):
     assert np.all(a["binned_rows"] == a["K"]) and np.all(c["binned_rows"] < c["K"])
 
 
-def test_survivor_zoom_equals_no_zoom(overlap_setup, monkeypatch):
-    """the survivors' zoom stage (ERP_ZOOM_LEVELS=1, the default until r05; 2 = a second level)
+def test_survivor_zoom_equals_no_zoom(overlap_setup):
+    """the survivors' zoom stage (ERP_OPT_ZOOM_LEVELS = 1, the default until r05; 2 = a second level)
     only tightens bounds before the refine: every result field equals the default route's (0),
     only the work count `survivors` may differ -- on a 48-pair sub-batch through the pruning
     route"""
@@ -142,8 +180,9 @@ def test_survivor_zoom_equals_no_zoom(overlap_setup, monkeypatch):
             b["height"], b["max_nq"], b["max_nt"])
     res = {}
     for zl in ("0", "1", "2"):
-        monkeypatch.setenv("ERP_ZOOM_LEVELS", zl)  # (read at context creation)
-        out = PairBatchRunner(ctx=Context(0), iters=ITERS).run(*args)
+        c = Context(0)
+        c.set_option("zoom_levels", int(zl))
+        out = PairBatchRunner(ctx=c, iters=ITERS).run(*args)
         torch.cuda.synchronize()
         res[zl] = results_to_numpy(out["results"])
     for zl in ("1", "2"):

@@ -283,13 +283,18 @@ def test_eight_point_estimation_api(ctx, oracle):
 
 
 # ---------------------------------------------------------------------- batch pipeline
+SMALL_BATCH = {"prune": 0, "all_rows": 1000000}
+
+
 @pytest.fixture(params=["prune", "all_rows"])
-def consensus_path(request, monkeypatch):
+def consensus_path(request, ctx):
     """both consensus routes: the Lipschitz / gradient / second-stage pre-pruning that batches
-    of more than ERP_SMALL_BATCH pairs take, and the every-row bounds pass of small batches (the
-    single-pair call, capi.hip run_consensus)"""
-    monkeypatch.setenv("ERP_SMALL_BATCH", "0" if request.param == "prune" else "1000000")
-    return request.param
+    of more than ERP_OPT_SMALL_BATCH pairs take, and the every-row bounds pass of small batches
+    (the single-pair call, capi.hip run_consensus) -- set on the module's context (tests that
+    make their own contexts apply SMALL_BATCH[consensus_path] to them)"""
+    ctx.set_option("small_batch", SMALL_BATCH[request.param])
+    yield request.param
+    ctx.set_option("small_batch", -1)
 
 
 def _batch(pairs, device="cuda"):
@@ -440,65 +445,32 @@ def test_batch_pipeline_valu_matcher_equals_mfma(gpu_lib):
         assert M > 0 and np.array_equal(ma[i, :M], mb[i, :M])
 
 
-@pytest.mark.parametrize("sizes,iters", [([512, 700, 300, 1024], 300), ([4096, 2048], 1000),
-                                         ([9000], 300)])
-def test_sampler_gram_fused_equals_standalone(gpu_lib, sizes, iters):
-    """the fused sampler->Gram kernel (opt-in ERP_FUSE_SAMPLER=1) and the standalone sampler +
-    Gram kernels (default) give byte-identical records, hypotheses and sample sets: ragged pair
-    sizes, partial 256-iteration blocks, M = 9000 (s = 2250: 71 bitmap rows, the fused LDS
-    near its largest)"""
-    import os as _os
-
-    import torch
-    from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
-    pairs = [synth.make_pair(4100 + i, n_kpts=n) for i, n in enumerate(sizes)]
-    args = _batch(pairs)
-    outs = {}
-    for fuse in ("1", "0"):
-        _os.environ["ERP_FUSE_SAMPLER"] = fuse
-        try:
-            c = Context(0)
-        finally:
-            del _os.environ["ERP_FUSE_SAMPLER"]
-        o = PairBatchRunner(ctx=c, iters=iters).run(*args, want=("hyps", "samples"))
-        torch.cuda.synchronize()
-        outs[fuse] = (results_to_numpy(o["results"]).view(np.uint8).copy(),
-                      o["hyps"].cpu().numpy(), o["samples"].cpu().numpy())
-    ra, ha, sa = outs["1"]
-    rb, hb, sb = outs["0"]
-    assert np.array_equal(ra, rb)
-    assert np.array_equal(ha, hb)
-    assert np.array_equal(sa, sb)
-    assert np.all(results_to_numpy(o["results"])["status"] == 0)
-
-
 @pytest.mark.parametrize("sizes,iters", [([4096], 2000), ([512, 700, 300, 1024], 300),
                                          ([9000], 200), ([60000], 70)])
-def test_sampler_kernels_identical(gpu_lib, monkeypatch, sizes, iters):
+def test_sampler_kernels_identical(gpu_lib, sizes, iters):
     """every glibc-replay sampler kernel gives the same sample sets and records: the throughput
-    blocks (sampler_kernel<0>, ERP_SAMPLER_LAT=0), the latency blocks step by step (<2>) and
-    positions first (<3>), and the split replay (sampler_split_kernel: segments replayed from
-    their start bitmaps, ERP_SAMPLER_SPLIT=1 -- skipped by the launcher where its bitmaps do not
-    fit the LDS, M = 60000); ragged sizes, partial waves, the d < 256 blocks, the straddling and
-    last blocks"""
+    blocks (sampler_kernel<0>, ERP_OPT_SAMPLER_LAT = 0), the latency blocks step by step (<2>)
+    and positions first (<3>), and the split replay (sampler_split_kernel: segments replayed from
+    their start bitmaps, ERP_OPT_SAMPLER_SPLIT = 1 -- skipped by the launcher where its bitmaps
+    do not fit the LDS, M = 60000); ragged sizes, partial waves, the d < 256 blocks, the
+    straddling and last blocks"""
     import torch
     from erp_match_eightpoint_test_amd import Context, PairBatchRunner, results_to_numpy
     pairs = [synth.make_pair(4300 + i, n_kpts=n) for i, n in enumerate(sizes)]
     args = _batch(pairs)
     outs = {}
-    for name, env in (("lat0", {"ERP_SAMPLER_LAT": "0", "ERP_SAMPLER_SPLIT": "0"}),
-                      ("lat1", {"ERP_SAMPLER_LAT": "1", "ERP_SAMPLER_SPLIT": "0"}),
-                      ("lat2", {"ERP_SAMPLER_LAT": "2", "ERP_SAMPLER_SPLIT": "0"}),
-                      ("split", {"ERP_SAMPLER_SPLIT": "1"})):
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        o = PairBatchRunner(ctx=Context(0), iters=iters).run(*args, want=("samples",))
+    for name, opts in (("lat0", {"sampler_lat": 0, "sampler_split": 0}),
+                       ("lat1", {"sampler_lat": 1, "sampler_split": 0}),
+                       ("lat2", {"sampler_lat": 2, "sampler_split": 0}),
+                       ("split", {"sampler_split": 1})):
+        c = Context(0)
+        for k, v in opts.items():
+            c.set_option(k, v)
+        o = PairBatchRunner(ctx=c, iters=iters).run(*args, want=("samples",))
         torch.cuda.synchronize()
         r = results_to_numpy(o["results"])
         assert np.all(r["status"] == 0), name
         outs[name] = (r.view(np.uint8).copy(), o["samples"].cpu().numpy())
-        for k in env:
-            monkeypatch.delenv(k)
     ra, sa = outs["lat0"]
     for name in ("lat1", "lat2", "split"):
         rb, sb = outs[name]
@@ -955,8 +927,8 @@ def test_consensus_lipschitz_prepruning(ctx, oracle, case, consensus_path):
 
 @pytest.mark.parametrize("case", ["cluster", "cluster_outliers", "shell", "two_clusters",
                                   "bench_pairs"])
-def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case, consensus_path):
-    """the convexity-augmented pruning (central references' distance gradient G, ERP_LIPG) keeps
+def test_consensus_grad_pruning_exact(gpu_lib, oracle, case, consensus_path):
+    """the convexity-augmented pruning (central references' distance gradient G, ERP_OPT_LIPG) keeps
     every result field the Lipschitz-only run gives (status, K, min_idx, R, T, min_dist,
     near_ties), is deterministic run to run (every byte, binned_rows included), and bins no more
     rows than Lipschitz alone -- on synthetic clouds against the oracle and on configs[1]-shaped
@@ -966,8 +938,10 @@ def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case, consen
     from erp_match_eightpoint_test_amd import dist as D
 
     def ctx_with(v):
-        monkeypatch.setenv("ERP_LIPG", v)
-        return Context(0)
+        c = Context(0)
+        c.set_option("lipg", int(v))
+        c.set_option("small_batch", SMALL_BATCH[consensus_path])
+        return c
 
     if case == "bench_pairs":
         pairs = [synth.make_pair(20200423 + i, n_kpts=2048) for i in range(6)]
@@ -986,7 +960,7 @@ def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case, consen
             # (a second-stage reference the gradient prunes no longer prunes for stage 2: a few
             # rows may move to the coarse list, so the bound is on the total, not per row)
             assert b["binned_rows"].sum() <= a["binned_rows"].sum(), v
-            print(f"binned rows lipschitz {a['binned_rows'].tolist()} -> ERP_LIPG={v} "
+            print(f"binned rows lipschitz {a['binned_rows'].tolist()} -> lipg={v} "
                   f"{b['binned_rows'].tolist()}")
         return
     rng = np.random.default_rng({"cluster": 21, "cluster_outliers": 22, "shell": 23,
@@ -1022,9 +996,9 @@ def test_consensus_grad_pruning_exact(gpu_lib, oracle, monkeypatch, case, consen
 
 
 @pytest.mark.parametrize("case", ["two_clusters", "twin_pairs", "bench_pairs"])
-def test_consensus_refine_hint_and_flat_exact(gpu_lib, oracle, monkeypatch, case, consensus_path):
-    """the refine pass's hinted sub-bin windows (ERP_REFINE_HINT; kernels.hip
-    consensus_hint_kernel / refine_windows) and the flat-pair route (ERP_FLAT_REFS: the
+def test_consensus_refine_hint_and_flat_exact(gpu_lib, oracle, case, consensus_path):
+    """the refine pass's hinted sub-bin windows (ERP_OPT_REFINE_HINT; kernels.hip
+    consensus_hint_kernel / refine_windows) and the flat-pair route (ERP_OPT_FLAT_REFS: the
     first-stage references refined, the first stage re-run against them) keep every result
     field of the run without them, are deterministic run to run, and leave no more survivors
     for the exact pass -- on a synthetic two-cluster set against the oracle, on two-cluster
@@ -1037,9 +1011,11 @@ def test_consensus_refine_hint_and_flat_exact(gpu_lib, oracle, monkeypatch, case
     from erp_match_eightpoint_test_amd import dist as D
 
     def ctx_with(hint, flat):
-        monkeypatch.setenv("ERP_REFINE_HINT", hint)
-        monkeypatch.setenv("ERP_FLAT_REFS", flat)
-        return Context(0)
+        c = Context(0)
+        c.set_option("refine_hint", int(hint))
+        c.set_option("flat_refs", int(flat))
+        c.set_option("small_batch", SMALL_BATCH[consensus_path])
+        return c
 
     variants = (("0", "0"), ("1", "0"), ("1", "25"), ("1", "25"))
     fields = ("status", "M", "K", "min_idx", "R", "T", "min_dist", "near_ties")
