@@ -268,7 +268,7 @@ def check_gathered(gathered, per_rank: int, world: int, rerun_fn, oracle_fn=None
     that pair (dict with M, K, min_idx, R, T), the gathered record is also checked against the
     CPU restatement (src/eight_point.cpp:152-192: K equal, min_idx equal by min_idx_agrees --
     given the oracle's per-iteration validity flags o["hyp"] when present -- and R / T within
-    2e-6)."""
+    1e-6)."""
     from .capi import RESULT_DTYPE
     g = np.ascontiguousarray(np.asarray(gathered, np.uint8)).reshape(-1, RESULT_DTYPE.itemsize)
     bad_bytes, bad_oracle, swaps = [], [], []
@@ -287,8 +287,8 @@ def check_gathered(gathered, per_rank: int, world: int, rerun_fn, oracle_fn=None
                 swaps.append(r)
             ok = (int(x["status"]) == 0 and int(x["M"]) == int(o["M"]) and
                   int(x["K"]) == int(o["K"]) and agree and
-                  float(np.abs(x["R"] - o["R"]).max()) <= 2e-6 and
-                  float(np.abs(x["T"] - o["T"]).max()) <= 2e-6)
+                  float(np.abs(x["R"] - o["R"]).max()) <= 1e-6 and
+                  float(np.abs(x["T"] - o["T"]).max()) <= 1e-6)
             if not ok:
                 bad_oracle.append(r)
     out = {"ranks_checked": world, "records_identical": not bad_bytes,

@@ -1,12 +1,13 @@
 #!/bin/bash
 # GPU suite, then the default bench line, then (N > 1 rehearsal) the 2-rank bench on one device.
-#   TAG=r06c bash scripts/gpu_check.sh        (SKIP_TESTS=1 / SKIP_BENCH=1 / SKIP_RANKS=1)
+#   TAG=r06c bash scripts/gpu_check.sh    (SKIP_TESTS=1 / SKIP_BENCH=1 / SKIP_RANKS=1; TEST_K=<-k expr>)
+# ERP_PARITY_OUT: the tests' measured parity deviations -> gpurun_out/parity_$TAG.json
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; mkdir -p gpurun_out
 TAG=${TAG:-r06c}
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  echo "== gpu tests" && timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider \
-    --timeout 300 --timeout-method thread ${TEST_ARGS:-} > gpurun_out/pytest_gpu_${TAG}.log 2>&1 \
+  echo "== gpu tests" && ERP_PARITY_OUT=gpurun_out/parity_${TAG}.json timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu -p no:cacheprovider \
+    --timeout 300 --timeout-method thread ${TEST_K:+-k "$TEST_K"} > gpurun_out/pytest_gpu_${TAG}.log 2>&1 \
     || { tail -40 gpurun_out/pytest_gpu_${TAG}.log; exit 1; }
   tail -3 gpurun_out/pytest_gpu_${TAG}.log
 fi

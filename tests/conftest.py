@@ -17,6 +17,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running test")
 
 
+def pytest_sessionfinish(session, exitstatus):
+    """ERP_PARITY_OUT=<path>: the measured parity deviations of the run (tests/parity_log.py)"""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import parity_log
+    parity_log.dump()
+
+
 @pytest.fixture(scope="session")
 def oracle():
     import oracle as O

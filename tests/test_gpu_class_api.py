@@ -15,6 +15,7 @@ from erp_match_eightpoint_test_amd import synth
 from erp_match_eightpoint_test_amd.capi import RESULT_DTYPE
 
 pytestmark = pytest.mark.gpu
+TOL_RT = 1e-6  # R (rad) / T against the oracle (profiles/r06d_parity_deviations.json)
 
 
 @pytest.fixture(scope="module")
@@ -53,7 +54,7 @@ def test_class_api_driver_vs_oracle(driver, oracle, tmp_path, n, iters):
     res = raw[24:].view(RESULT_DTYPE)[0]
     assert res["status"] == 0 and res["M"] == len(ref)
     assert res["K"] == o["K"] and res["min_idx"] == o["min_idx"]
-    assert np.abs(R - o["R"]).max() <= 2e-6 and np.abs(T - o["T"]).max() <= 2e-6
+    assert np.abs(R - o["R"]).max() <= TOL_RT and np.abs(T - o["T"]).max() <= TOL_RT
     # eight_point_estimation on 200 bearings: {R1, R2} as a set, T, validity count
     e = oracle.eight_point_estimation(bl, br)
     est = np.fromfile(outd / "est.bin", np.uint8)
@@ -61,12 +62,12 @@ def test_class_api_driver_vs_oracle(driver, oracle, tmp_path, n, iters):
     v = est[36:].view(np.int32)
     same = max(np.abs(f9[0:3] - e["R1"]).max(), np.abs(f9[3:6] - e["R2"]).max())
     swap = max(np.abs(f9[0:3] - e["R2"]).max(), np.abs(f9[3:6] - e["R1"]).max())
-    assert min(same, swap) <= 2e-6
-    assert np.abs(f9[6:9] - e["T"]).max() <= 2e-6
+    assert min(same, swap) <= TOL_RT
+    assert np.abs(f9[6:9] - e["T"]).max() <= TOL_RT
     assert int(v.sum()) == int(e["R1_valid"]) + int(e["R2_valid"])
     # initial_guess on the same bearings (the driver's cfg.iters; glibc stream from offset 0)
     g = oracle.initial_guess(bl, br, oracle.make_cfg(iters=iters))
     raw = np.fromfile(outd / "guess.bin", np.uint8)
     res = raw[24:].view(RESULT_DTYPE)[0]
     assert res["K"] == g["K"] and res["min_idx"] == g["min_idx"]
-    assert np.abs(raw[:12].view(np.float32) - g["R"]).max() <= 2e-6
+    assert np.abs(raw[:12].view(np.float32) - g["R"]).max() <= TOL_RT

@@ -5,12 +5,14 @@ Bars (DESIGN.md "Parity"):
 * sampler: every iteration's sampled index set identical (glibc replay is integer work);
 * per-iteration E within 1e-6 (after sign alignment; north_star allows 1e-4; typical 1e-12,
   thin-SVD samples with a small s-th singular value reach ~2e-8), {R1,R2} equal as a set within
-  2e-6 rad, T within 2e-6;
-* final R, T: equal to the oracle's within 2e-6 (same consensus winner up to identical values).
+  TOL_RT rad, T within TOL_RT;
+* final R, T: equal to the oracle's within TOL_RT (same consensus winner up to identical values).
+The largest deviation each fixture shows is recorded (tests/parity_log.py, ERP_PARITY_OUT).
 """
 from __future__ import annotations
 
 import os
+import sys
 
 import numpy as np
 import pytest
@@ -19,6 +21,8 @@ from erp_match_eightpoint_test_amd import synth
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
+sys.path.insert(0, os.path.dirname(__file__))
+from parity_log import record  # noqa: E402  (the measured deviations, ERP_PARITY_OUT)
 
 
 @pytest.fixture(scope="module")
@@ -148,14 +152,20 @@ def test_match_device_path(mctx, oracle):
 
 
 # --------------------------------------------------------------------------- estimator
-def _check_hyps(gh, oh, tol=2e-6):
+TOL_RT = 1e-6  # R (rad) / T against the oracle (1e-6); measured: parity_log
+
+
+def _check_hyps(gh, oh, tol=TOL_RT, fixture=None):
     for a, b in zip(gh, oh):
         assert a["R1_valid"] + a["R2_valid"] == b["R1_valid"] + b["R2_valid"]
         same = max(np.abs(a["R1"] - b["R1"]).max(), np.abs(a["R2"] - b["R2"]).max())
         swap = max(np.abs(a["R1"] - b["R2"]).max(), np.abs(a["R2"] - b["R1"]).max())
+        e = min(np.abs(a["E"] - b["E"]).max(), np.abs(a["E"] + b["E"]).max())
+        if fixture:
+            record(fixture + ": every iteration", R=min(same, swap),
+                   T=np.abs(a["T"] - b["T"]).max(), E=e)
         assert min(same, swap) <= tol
         assert np.abs(a["T"] - b["T"]).max() <= tol
-        e = min(np.abs(a["E"] - b["E"]).max(), np.abs(a["E"] + b["E"]).max())
         assert e <= 1e-6
 
 
@@ -181,10 +191,11 @@ def test_find_golden_fixture(ctx):
     g = _npz("find_400_it80.npz")
     st, r, hyps = _run_find_dev(ctx, g["kl"], g["kr"], int(g["W"]), int(g["H"]), 80)
     assert st == 0 and r["status"] == 0
-    _check_hyps(hyps, g["hyp"])
+    _check_hyps(hyps, g["hyp"], fixture="find_400_it80")
     assert r["K"] == int(g["K"])
-    assert np.abs(r["R"] - g["R"]).max() <= 2e-6
-    assert np.abs(r["T"] - g["T"]).max() <= 2e-6
+    record("find_400_it80: result", R=np.abs(r["R"] - g["R"]).max(), T=np.abs(r["T"] - g["T"]).max())
+    assert np.abs(r["R"] - g["R"]).max() <= TOL_RT
+    assert np.abs(r["T"] - g["T"]).max() <= TOL_RT
     # KAT: the recovered rotation is the synthetic ground truth (two_synthesis_image_test)
     assert np.degrees(np.abs(r["R"] - g["euler_gt"])).mean() < 1.0
 
@@ -194,17 +205,19 @@ def test_find_host_api_matches_dev(ctx):
     g = _npz("find_400_it80.npz")
     ep = eight_point(ctx=ctx)
     R, T = ep.find(int(g["W"]), int(g["H"]), g["kl"], g["kr"], len(g["kl"]))
-    assert np.abs(R - g["R"]).max() <= 2e-6 and np.abs(T - g["T"]).max() <= 2e-6
+    assert np.abs(R - g["R"]).max() <= TOL_RT and np.abs(T - g["T"]).max() <= TOL_RT
 
 
 def test_find_manual_regime_fixture(ctx):
     g = _npz("find_manual_100_it500.npz")
     st, r, hyps = _run_find_dev(ctx, g["kl"], g["kr"], int(g["W"]), int(g["H"]), 500)
     assert st == 0 and r["status"] == 0
-    _check_hyps(hyps, g["hyp"])
+    _check_hyps(hyps, g["hyp"], fixture="find_manual_100_it500")
     assert r["K"] == int(g["K"])
-    assert np.abs(r["R"] - g["R"]).max() <= 2e-6
-    assert np.abs(r["T"] - g["T"]).max() <= 2e-6
+    record("find_manual_100_it500: result", R=np.abs(r["R"] - g["R"]).max(),
+           T=np.abs(r["T"] - g["T"]).max())
+    assert np.abs(r["R"] - g["R"]).max() <= TOL_RT
+    assert np.abs(r["T"] - g["T"]).max() <= TOL_RT
 
 
 @pytest.mark.parametrize("m", [4, 8, 20, 35, 36])
@@ -214,8 +227,9 @@ def test_find_thin_svd_edges(ctx, m):
     assert st == int(g[f"m{m}_status"]) == 0
     if m >= 8:  # sample_n = 1 (m = 4) is rank-1: the rank-2 fix / decomposition is
         # ill-posed there (documented), so only the sampled sets and E are compared
-        _check_hyps(hyps, g[f"m{m}_hyp"])
-        assert np.abs(r["R"] - g[f"m{m}_R"]).max() <= 2e-6
+        _check_hyps(hyps, g[f"m{m}_hyp"], fixture=f"find_edges m={m}")
+        record(f"find_edges m={m}: result", R=np.abs(r["R"] - g[f"m{m}_R"]).max())
+        assert np.abs(r["R"] - g[f"m{m}_R"]).max() <= TOL_RT
     else:
         for a, b in zip(hyps, g[f"m{m}_hyp"]):
             assert min(np.abs(a["E"] - b["E"]).max(), np.abs(a["E"] + b["E"]).max()) <= 1e-6
@@ -277,8 +291,8 @@ def test_eight_point_estimation_api(ctx, oracle):
     R1, R2, T, v1, v2, E = eight_point(ctx=ctx).eight_point_estimation(2048, 1024, bl, br)
     same = max(np.abs(R1 - ho["R1"]).max(), np.abs(R2 - ho["R2"]).max())
     swap = max(np.abs(R1 - ho["R2"]).max(), np.abs(R2 - ho["R1"]).max())
-    assert min(same, swap) <= 2e-6
-    assert np.abs(T - ho["T"]).max() <= 2e-6
+    assert min(same, swap) <= TOL_RT
+    assert np.abs(T - ho["T"]).max() <= TOL_RT
     assert min(np.abs(E - ho["E"]).max(), np.abs(E + ho["E"]).max()) <= 1e-8
 
 
@@ -336,8 +350,8 @@ def test_batch_pipeline_vs_oracle(ctx, oracle):
         assert np.array_equal(got_s, np.sort(o["samples"], axis=1))
         _check_hyps(hyps[i], o["hyp"])
         assert res[i]["K"] == o["K"]
-        assert np.abs(res[i]["R"] - o["R"]).max() <= 2e-6
-        assert np.abs(res[i]["T"] - o["T"]).max() <= 2e-6
+        assert np.abs(res[i]["R"] - o["R"]).max() <= TOL_RT
+        assert np.abs(res[i]["T"] - o["T"]).max() <= TOL_RT
         # consensus: the oracle's trimmed means on the GPU's own R list pick the same winner
         K = o["K"]
         rv = outs["rvec"][i, :K].cpu().numpy()
@@ -565,8 +579,8 @@ def test_philox_sampler_vs_oracle(gpu_lib, oracle, sizes, iters):
                         detail=True)
         _check_hyps(hyps[i], o["hyp"])
         assert res[i]["K"] == o["K"]
-        assert np.abs(res[i]["R"] - o["R"]).max() <= 2e-6
-        assert np.abs(res[i]["T"] - o["T"]).max() <= 2e-6
+        assert np.abs(res[i]["R"] - o["R"]).max() <= TOL_RT
+        assert np.abs(res[i]["T"] - o["T"]).max() <= TOL_RT
 
 
 def test_philox_hypothesis_blocks_by_offset(ctx, oracle):
@@ -695,7 +709,7 @@ def test_hypothesis_blocks_by_offset_match_full_run(ctx, oracle):
     rvec, tvec = D.valid_list(merged)
     res = D.gpu_consensus(ctx, "cuda")(rvec, tvec)
     assert res["status"] == 0 and res["K"] == int(g["K"])
-    assert np.abs(res["R"] - g["R"]).max() <= 2e-6 and np.abs(res["T"] - g["T"]).max() <= 2e-6
+    assert np.abs(res["R"] - g["R"]).max() <= TOL_RT and np.abs(res["T"] - g["T"]).max() <= TOL_RT
 
 
 @pytest.mark.parametrize("world", [1, 3, 8])

@@ -72,8 +72,8 @@ def test_gram_estimator_vs_oracle(oracle, harness, s):
         # vector inside decomposeEssentialMat), T equal
         same = max(np.abs(ho["R1"] - h["R1"]).max(), np.abs(ho["R2"] - h["R2"]).max())
         swap = max(np.abs(ho["R1"] - h["R2"]).max(), np.abs(ho["R2"] - h["R1"]).max())
-        assert min(same, swap) <= 2e-6, (s, trial)
-        assert np.abs(ho["T"] - h["T"]).max() <= 2e-6
+        assert min(same, swap) <= 1e-6, (s, trial)
+        assert np.abs(ho["T"] - h["T"]).max() <= 1e-6
     assert worst_e < 1e-8
 
 
