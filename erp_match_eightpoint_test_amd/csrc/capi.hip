@@ -137,10 +137,12 @@ struct erp_ctx {
         // 16.5k pairs/s.  (The second pre-pruning stage's fine pass uses the zoom kernel either way.)
         0,
         0,   // SMALL_ZOOM: the small-batch route skips the zoom (single pair 0.487 -> 0.437 ms)
-        1,   // LIP2: the second pre-pruning stage (kernels.hip consensus_lipschitz2_kernel)
-        1,   // LIPG: the central references' distance gradient (consensus_grad_kernel)
-        1,   // REFINE_HINT: sub-bins on each row's Lipschitz interval (consensus_hint_kernel)
-        25,  // FLAT_REFS: pairs whose first stage kept > 25 % of the rows take the flat route
+        // LIP2 / LIPG / REFINE_HINT / FLAT_REFS: -1 = automatic (pruning_opts): on for batches of
+        // >= kFewPairs pairs, off below
+        -1,  // LIP2: the second pre-pruning stage (kernels.hip consensus_lipschitz2_kernel)
+        -1,  // LIPG: the central references' distance gradient (consensus_grad_kernel)
+        -1,  // REFINE_HINT: sub-bins on each row's Lipschitz interval (consensus_hint_kernel)
+        -1,  // FLAT_REFS: pairs whose first stage kept > 25 % of the rows take the flat route
         1,   // BOUND_RATIO: the matcher's ratio test from the bf16 bounds where they suffice
         -1,  // DEBUG_STAGES: every stage group
         0};  // DEBUG_SNAP
@@ -599,6 +601,24 @@ erp_status run_hypotheses(erp_ctx* c, const erp::BatchShape& sh_in, const erp_ra
     return run_inliers(c, sh, cfg, hyps, st);
 }
 
+// The pruning refinements of rounds 3-4 (second stage, gradient references, flat route, hinted
+// refine windows) were tuned on 128-pair launches.  A launch of a few pairs with a large K
+// (configs[4]: one find of 100k iterations, K ~ 89k) runs their per-pair passes on a handful of
+// blocks each: there they cost more than they save -- bench.py --workload manual, one box
+// (profiles/r06h_manual_opts.txt): 2.11 ms per find with all four, 1.53 ms without.  So their
+// automatic setting (-1) is on for launches of >= kFewPairs pairs and off below; an explicit
+// option value always wins.  (Results are identical either way: tests/test_gpu_parity.py.)
+constexpr int kFewPairs = 8;
+struct PruningOpts {
+    int lip2, lipg, flat_pct, hint;
+};
+PruningOpts pruning_opts(const erp_ctx* c, const erp::BatchShape& sh) {
+    const bool few = sh.n_pairs < kFewPairs;
+    auto pick = [&](int v, int on) { return v >= 0 ? v : (few ? 0 : on); };
+    return PruningOpts{pick(c->opt[ERP_OPT_LIP2], 1), pick(c->opt[ERP_OPT_LIPG], 1),
+                       pick(c->opt[ERP_OPT_FLAT_REFS], 25), pick(c->opt[ERP_OPT_REFINE_HINT], 1)};
+}
+
 // consensus stages after the hypothesis records are in place (counts may be null when the
 // valid list is given directly: erp_consensus_dev)
 // phase: 0 = everything; 1 = compaction + bounds of rows shard / nshards only (into lb_/ub_/
@@ -644,6 +664,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
     const bool small = phase == 0 && nshards == 1 &&
                        (sb >= 0 ? sh.n_pairs <= sb : sh.n_pairs * kk * kk <= 2e9);
     const bool prune = !small;
+    const PruningOpts po = pruning_opts(c, sh);
     if (phase != 2) {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_BOUNDS, st);
         ERP_CK(erp::launch_consensus_bounds((int32_t*)c->kcount.p, (float*)c->rv.p,
@@ -651,10 +672,9 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             cfg->trim_lo, cfg->trim_hi, lbp, ubp, bselp, shard,
                                             nshards, prune ? (int32_t*)c->surv.p : nullptr,
                                             prune ? (int32_t*)c->nsurv.p + sh.n_pairs : nullptr,
-                                            (int32_t*)c->zsel.p, c->opt[ERP_OPT_LIP2],
-                                            (int32_t*)c->sortbuf.p,
-                                            c->lipref.p, c->opt[ERP_OPT_LIPG],
-                                            c->opt[ERP_OPT_FLAT_REFS], c->opt[ERP_OPT_REFINE_HINT], st,
+                                            (int32_t*)c->zsel.p, po.lip2,
+                                            (int32_t*)c->sortbuf.p, c->lipref.p, po.lipg,
+                                            po.flat_pct, po.hint, st,
                                             from_hyps && lite));  // (valid_place wrote the edges)
     }
     if (c->opt[ERP_OPT_DEBUG_SNAP] && phase == 0) {
@@ -712,7 +732,7 @@ erp_status run_consensus(erp_ctx* c, const erp::BatchShape& sh, const erp_ransac
                                             (int32_t*)c->surv.p, (int32_t*)c->nsurv.p,
                                             bselp, lbp,
                                             ubp, (int32_t*)c->sortbuf.p, c->lipref.p,
-                                            c->opt[ERP_OPT_REFINE_HINT], st));
+                                            po.hint, st));
     }
     if (prune) {
         StageTimer _t(ctx, ERP_STAGE_CONSENSUS_SELECT, st);
@@ -907,8 +927,10 @@ erp_status erp_ctx_set_option(erp_ctx* ctx, int32_t option, int32_t value) {
         case ERP_OPT_SAMPLER_SPLIT: lo = -1; hi = 1; break;
         case ERP_OPT_GRAM_TILES: lo = 0; hi = 2; break;
         case ERP_OPT_ZOOM_LEVELS: lo = 0; hi = 2; break;
-        case ERP_OPT_FLAT_REFS: lo = 0; hi = 100; break;
-        case ERP_OPT_LIPG: lo = 0; hi = 3; break;  // bit 0: first stage, bit 1: second stage
+        case ERP_OPT_FLAT_REFS: lo = -1; hi = 100; break;
+        case ERP_OPT_LIPG: lo = -1; hi = 3; break;  // bit 0: first stage, bit 1: second stage
+        case ERP_OPT_LIP2: lo = -1; hi = 1; break;
+        case ERP_OPT_REFINE_HINT: lo = -1; hi = 1; break;
         case ERP_OPT_DEBUG_STAGES: lo = -1; hi = 63; break;
         default: break;
     }

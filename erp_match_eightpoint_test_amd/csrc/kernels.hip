@@ -2594,6 +2594,7 @@ constexpr int kLipMinK = 1024;  // smaller sets: no pre-pruning (every non-refer
 // the convexity-augmented pruning's central references: UB_c <= U kLipGFac (consensus_grad_select;
 // r04 A/B, profiles/r04c_ab_consensus_knobs.txt: 1.03 cost +0.2 ms of consensus per step)
 constexpr float kLipGFac = 1.1f;
+constexpr int kGradBlocks = 2048;  // consensus_grad_kernel's grid (grid-stride over the references)
 #ifndef ERP_LIP2_STEP
 #define ERP_LIP2_STEP 4
 #endif
@@ -5016,7 +5017,9 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                            (const double*)lr.U, gfac, lr.gsel, lr.gcnt, lr.gcap);
         ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st, (const int32_t*)lr.gcnt,
                            P, 1, 0, lr.goff);
-        ERP_LAUNCH(consensus_grad_kernel, dim3(std::min(P * 64, 2048)), dim3(256), 0, st,
+        // (2048 blocks whatever the batch: one pair of configs[4] has ~1000 central references
+        // of K ~ 89k columns each; the former min(64 P, 2048) gave it 64 blocks)
+        ERP_LAUNCH(consensus_grad_kernel, dim3(kGradBlocks), dim3(256), 0, st,
                            kcount, rv, dscale, stride, trim_lo, trim_hi, (const double*)lb,
                            (const int32_t*)bsel, (const int32_t*)lr.gsel, (const int32_t*)lr.goff,
                            P, lr.gcap, lr.gref);
@@ -5093,7 +5096,7 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                                (const double*)lr.U, gfac, lr.gsel, lr.gcnt, lr.gcap);
             ERP_LAUNCH(list_prefix_kernel, dim3(1), dim3(1024), 0, st,
                                (const int32_t*)lr.gcnt, P, 1, 0, lr.goff);
-            ERP_LAUNCH(consensus_grad_kernel, dim3(std::min(P * 64, 2048)), dim3(256), 0,
+            ERP_LAUNCH(consensus_grad_kernel, dim3(kGradBlocks), dim3(256), 0,
                                st, kcount, rv, dscale, stride, trim_lo, trim_hi, (const double*)lb,
                                (const int32_t*)bsel, (const int32_t*)lr.gsel,
                                (const int32_t*)lr.goff, P, lr.gcap, lr.gref);

@@ -247,11 +247,14 @@ erp_status erp_ctx_set_graphs(erp_ctx* ctx, int32_t enable);
                           has >= 512 wide blocks), 1, 2
    ERP_OPT_ZOOM_LEVELS    the survivors' zoom levels 0 (default) .. 2
    ERP_OPT_SMALL_ZOOM     1: the small-batch route keeps the zoom levels (default 0)
-   ERP_OPT_LIP2           second pre-pruning stage 1 (default) / 0
-   ERP_OPT_LIPG           convexity-augmented pre-pruning: bit 0 first stage (default 1), bit 1
-                          second stage too (3), 0 off
-   ERP_OPT_REFINE_HINT    hinted refine windows 1 (default) / 0
-   ERP_OPT_FLAT_REFS      flat-pair route above this % of rows listed: 25 (default); 0 off
+   ERP_OPT_LIP2           second pre-pruning stage 1 / 0
+   ERP_OPT_LIPG           convexity-augmented pre-pruning: bit 0 first stage (1), bit 1 second
+                          stage too (3), 0 off
+   ERP_OPT_REFINE_HINT    hinted refine windows 1 / 0
+   ERP_OPT_FLAT_REFS      flat-pair route above this % of rows listed (25); 0 off
+                          (these four: -1, the default, = automatic: the values in brackets / 1
+                          for launches of >= 8 pairs, 0 below -- a few pairs with a large K, as
+                          configs[4]'s one 100k-iteration find, run faster without them)
    ERP_OPT_BOUND_RATIO    the matcher's ratio test decided from the bf16 bounds where they
                           suffice 1 (default) / 0
    ERP_OPT_DEBUG_STAGES   debug: bit mask of the stage groups erp_pair_batch_run enqueues (1
