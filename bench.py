@@ -44,7 +44,7 @@ PEAK_VALU_OPS = 256 * 4 * 32 * 2.4e9 / 1e12          # 78.6 T lane-ops/s
 PEAK_VALU_OPS_4CYC = PEAK_VALU_OPS / 2                # secondary: every op at 4 cycles (39.3)
 # profiles/<tag>_pmc_<stage>.json of the shipped step (768 pairs, 6 sub-batches = 128-pair
 # launches): the HBM bytes per launch that roofline.traffic reports
-PROFILE_TAG = "r05g"
+PROFILE_TAG = "r06j"
 
 
 def parse():
@@ -805,6 +805,19 @@ def main():
             roof["traffic_missing"] = f"profiles/{args.profile_tag}_pmc_{dom}.json"
         if peak == PEAK_VALU_OPS:
             roof["frac_vs_4cycle_issue"] = achieved / PEAK_VALU_OPS_4CYC
+        sol = os.path.join(ROOT, "profiles", "r06b_sampler_sol.json")
+        if dom == "sampler" and SAMPLER == 0 and os.path.exists(sol):
+            # the measured floor of the same replay (scripts/dev/sampler_sol.hip: the backwards
+            # ring + magic modulo alone, same launch shape), same-box run
+            with open(sol) as f:
+                so = json.load(f)
+            v = so["variants"]
+            roof["speed_of_light_probe"] = {
+                "source": os.path.relpath(sol, ROOT),
+                "generator_ms": v["V0"]["ms"], "generator_modulo_ms": v["V1"]["ms"],
+                "plus_bitmap_bookkeeping_ms": v["V2"]["ms"],
+                "sampler_kernel_ms_same_box": so["real_sampler_kernel_ms"],
+                "sampler_over_generator_modulo": so["real_over_floor_V1"]}
     stage_roofs = {}
     for k in stages:
         w = stage_work(k, args.pairs, args.kpts, args.iters, res)
