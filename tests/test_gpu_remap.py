@@ -144,3 +144,21 @@ def test_rectify_and_vertical(rctx, oracle):
     m = oracle.inv3(oracle.inv3(oracle.eular2rot([th, 0, 0])))
     _certify(v, oracle.vertical_rotate(rl, fill=2), lambda ix: (H - 1 - ix[:, 1], ix[:, 0]),
              m, W, H)
+
+
+def test_rotate_image_random_rotations(rctx, oracle):
+    """rotate_image under 10 random rotations (the seams, the poles and arbitrary boundary
+    crossings inside the view) against the oracle's literal double formula: byte-exact up to the
+    certified truncation-boundary pixels (the fp64 fast path and its correctly rounded deferral
+    band, remap.hip)"""
+    from erp_match_eightpoint_test_amd import erp_rotation
+    er = erp_rotation(ctx=rctx)
+    H, W = 672, 1344
+    im = _image(77, H, W)
+    rng = np.random.default_rng(2024)
+    for _ in range(10):
+        th = rng.uniform(-np.pi, np.pi, 3)
+        R = oracle.eular2rot(th)
+        got = er.rotate_image(_dev(im), R, fill=4).cpu().numpy()
+        _certify(got, oracle.rotate_image(im, R, fill=4), lambda ix: (ix[:, 0], ix[:, 1]),
+                 oracle.inv3(R), W, H)
