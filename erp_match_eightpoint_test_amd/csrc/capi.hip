@@ -423,7 +423,7 @@ erp_status run_matcher(erp_ctx* ctx, const float* dq, const float* dt, const int
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_FILTER, st);
         ERP_CK(erp::launch_knn2_filter(dq, dt, oq, ot, sh, ctx->tsplit.p, pu, cc, cand, st,
-                                       (int32_t*)ctx->ovf.p));
+                                       (int32_t*)ctx->ovf.p, flags));
     }
     {
         StageTimer _t(ctx, ERP_STAGE_KNN2_RESCORE, st);
@@ -868,7 +868,8 @@ erp_status batch_enqueue(erp_ctx* ctx, const erp_pair_batch* b, float ratio,
                {out->tvec, P * 2 * I * 12}, {out->dist, P * 2 * I * 8}};
     for (const auto& o : opt)
         if (o.p) ERP_CK(hipMemsetAsync(o.p, 0, o.bytes, st));
-    ERP_CK(hipMemsetAsync(ctx->flags.p, 0, (size_t)sh.n_pairs * 4, st));
+    if (ctx->matcher == ERP_MATCHER_VALU_EXACT)  // (knn2_split_kernel resets them on the MFMA path)
+        ERP_CK(hipMemsetAsync(ctx->flags.p, 0, (size_t)sh.n_pairs * 4, st));
     // the merge writes the gather + bearings as it places each match (src/spherical_surf.cpp:
     // 155-162, src/eight_point.cpp:163-186; bearings_from_matches_kernel's work)
     const erp::BearingOut bo{b->kp_l, b->kp_r, b->width, b->height, (double*)ctx->pts.p,

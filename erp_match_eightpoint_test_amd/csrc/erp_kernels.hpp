@@ -84,7 +84,7 @@ size_t knn2_cand_bytes(const BatchShape& sh);
 hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
                               const int64_t* off_t, const BatchShape& sh, void* split,
                               float2* pu, int32_t* ccount, void* cand, hipStream_t st,
-                              int32_t* ovf);
+                              int32_t* ovf, int32_t* flags);  // flags [n_pairs] zeroed (may be null)
 // ovf = scratch of 4 + 12 * n_pairs * max_nq * fchunks bytes: overflowed (pair, query, chunk)
 // for the exact sweep (counter zeroed by the launch_knn2_filter before it)
 hipError_t launch_knn2_rescore(const float* desc_q, const float* desc_t, const int64_t* off_q,

@@ -2636,10 +2636,16 @@ __global__ __launch_bounds__(256) void consensus_lip_refs_kernel(
     const int32_t* __restrict__ slist, const int32_t* __restrict__ scount, int lstep, int shard,
     int nshards, const int32_t* __restrict__ zb, float4* __restrict__ lref,
     double* __restrict__ lU, int32_t* __restrict__ lcnt, int cap,
-    const int32_t* __restrict__ gate = nullptr) {
+    const int32_t* __restrict__ gate = nullptr, int32_t* __restrict__ z0 = nullptr,
+    int32_t* __restrict__ z1 = nullptr) {
     __shared__ double red[4];
     __shared__ int nlive;
     const int p = blockIdx.x, tid = threadIdx.x, lane = wave_lane();
+    // z0 / z1: per-pair list counters the next kernel appends to, reset here (no memset launch)
+    if (tid == 0) {
+        if (z0) z0[p] = 0;
+        if (z1) z1[p] = 0;
+    }
     if (gate && gate[p] <= 0) return;  // (the flat-pair re-run: other pairs keep their refs)
     const int K = kcount[p];
     const int ra = slist ? 0 : (int)((int64_t)K * shard / nshards);
@@ -4999,17 +5005,13 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                        stride, trim_lo, trim_hi, lb, ub, bsel, shard, nshards, kLipStep);
     const int P = sh.n_pairs;
     const LipRefViews lr = lipref_views(lipref, P, stride);
-    const hipError_t me = hipMemsetAsync(rcount, 0, sizeof(int32_t) * P, st);
-    if (me != hipSuccess) return me;
     const bool two = lip2 && list2;  // second pre-pruning stage
-    if (two) {
-        const hipError_t m1 = hipMemsetAsync(lr.r2cnt, 0, sizeof(int32_t) * P, st);
-        if (m1 != hipSuccess) return m1;
-    }
+    // (the list counters rcount and r2cnt are reset by the references kernel)
     ERP_LAUNCH(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
                        trim_lo, trim_hi, (const double*)lb, (const double*)ub,
                        (const int32_t*)nullptr, (const int32_t*)nullptr, kLipStep, shard, nshards,
-                       (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap);
+                       (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap,
+                       (const int32_t*)nullptr, rcount, two ? lr.r2cnt : (int32_t*)nullptr);
     if (lipg & 1) {  // the central references' G (convexity-augmented pruning)
         ERP_LAUNCH(consensus_grad_select_kernel, dim3(P), dim3(256), 0, st, kcount, stride,
                            (const double*)lb, (const double*)ub, (const int32_t*)bsel, kLipStep,
@@ -5083,12 +5085,12 @@ hipError_t launch_consensus_bounds(const int32_t* kcount, const float* rv, const
                            (const float*)edz, (const int32_t*)zb, stride, trim_lo, trim_hi, lb, ub,
                            (const int32_t*)lr.r2list, (const int32_t*)lr.r2cnt,
                            (const int32_t*)uoff, P, zsel, 1, dscale, bsel);
-        const hipError_t m2 = hipMemsetAsync(n2, 0, sizeof(int32_t) * 2 * P, st);  // + nfb
-        if (m2 != hipSuccess) return m2;
+        // (n2 and nfb = n2 + P reset by the references kernel)
         ERP_LAUNCH(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv,
                            stride, trim_lo, trim_hi, (const double*)lb, (const double*)ub,
                            (const int32_t*)lr.r2list, (const int32_t*)lr.r2cnt, 1, shard,
-                           nshards, (const int32_t*)zb, lr.ref, lr.U, lr.cnt, lr.cap);
+                           nshards, (const int32_t*)zb, lr.ref, lr.U, lr.cnt, lr.cap,
+                           (const int32_t*)nullptr, n2, n2 + P);
         if (lipg & 2) {  // G of the central second-stage references (fine bounds)
             ERP_LAUNCH(consensus_grad_select_kernel, dim3(P), dim3(256), 0, st, kcount,
                                stride, (const double*)lb, (const double*)ub, (const int32_t*)bsel,
@@ -5162,11 +5164,11 @@ hipError_t launch_consensus_refine(const int32_t* kcount, const float* rv, const
                        stride, trim_lo, trim_hi, surv, nsurv, bsel, lb, ub, surv, stride,
                        (const int32_t*)nullptr, kRefStep, hint, (const int32_t*)uoff, P);
     // (B) Lipschitz pruning of the other survivors against the refined references
-    const hipError_t me = hipMemsetAsync(n2, 0, sizeof(int32_t) * P, st);
-    if (me != hipSuccess) return me;
+    // (n2 reset by the references kernel)
     ERP_LAUNCH(consensus_lip_refs_kernel, dim3(P), dim3(256), 0, st, kcount, rv, stride,
                        trim_lo, trim_hi, (const double*)lb, (const double*)ub, surv, nsurv,
-                       kRefStep, 0, 1, (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap);
+                       kRefStep, 0, 1, (const int32_t*)nullptr, lr.ref, lr.U, lr.cnt, lr.cap,
+                       (const int32_t*)nullptr, n2);
     ERP_LAUNCH(consensus_lipschitz_kernel, dim3((stride + 511) / 512, P), dim3(256), 0, st,
                        kcount, rv, stride, lb, ub, surv, nsurv, list2, l2stride, n2, 0, 1,
                        kRefStep, (const float4*)lr.ref, (const double*)lr.U,

@@ -160,18 +160,25 @@ __device__ __forceinline__ float sq8(const float4 a, const float4 b) {
 }
 
 // train rows -> thi [pair][max_nt][64] = bf16(-2 t) (round to nearest; exact scaling of
-// bf16(t)), tu [pair][max_nt] = |t|^2 (1 + eps) (the filter's C operand), tmax[pair] =
-// max |t|^2 (float bits; zeroed before); four threads per row (16 dims each)
+// bf16(t)), tu [pair][max_nt] = |t|^2 (1 + eps) (the filter's C operand), tmaxb[pair][block] =
+// the block's max |t|^2 (float bits; knn2_filter reduces a pair's blocks); four threads per row
+// (16 dims each).  Block (0, p) also resets the per-call state of pair p (flags) and block (0, 0)
+// the batch's (the rescore's overflow counter, the filter's sentinel row): the kernels that read
+// them run after this one on the stream -- no memset launches (single-pair latency)
 __global__ __launch_bounds__(256) void knn2_split_kernel(const float* __restrict__ dt,
                                                          const int64_t* __restrict__ off_t,
                                                          int max_nt, bf16x8* __restrict__ thi,
                                                          float* __restrict__ tn,
-                                                         uint32_t* __restrict__ tmax,
-                                                         int32_t* __restrict__ ovf) {
+                                                         uint32_t* __restrict__ tmaxb,
+                                                         int32_t* __restrict__ ovf,
+                                                         uint32_t* __restrict__ sent,
+                                                         int32_t* __restrict__ flags) {
     const int p = blockIdx.y, tid = threadIdx.x;
-    // the rescore's overflow-list counter starts at zero (knn2_rescore runs after this kernel;
-    // one launch fewer than a separate reset: single-pair latency)
-    if (ovf && blockIdx.x == 0 && p == 0 && tid == 0) ovf[0] = 0;
+    if (blockIdx.x == 0) {
+        if (flags && tid == 0) flags[p] = 0;
+        if (p == 0 && tid < 33) sent[tid] = tid < 32 ? 0u : 0x7f800000u;  // 64 bf16 zeros, tu = inf
+        if (ovf && p == 0 && tid == 0) ovf[0] = 0;
+    }
     const int j = blockIdx.x * 64 + (tid >> 2), part = tid & 3;
     const int64_t tbase = off_t[p];
     const int nt = (int)(off_t[p + 1] - tbase);
@@ -195,7 +202,20 @@ __global__ __launch_bounds__(256) void knn2_split_kernel(const float* __restrict
     if ((tid & 63) == 0) wmax[tid >> 6] = m;
     __syncthreads();
     if (tid == 0)  // |t|^2 >= 0: the float bits order like the values
-        atomicMax(&tmax[p], __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]))));
+        tmaxb[(size_t)p * gridDim.x + blockIdx.x] =
+            __float_as_uint(fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3])));
+}
+
+// max |t|^2 of pair p over its split blocks' maxima (every wave of the calling block; the
+// blocks past the pair's rows wrote nothing)
+__device__ __forceinline__ uint32_t pair_tmax(const uint32_t* __restrict__ tmaxb, int p, int nt,
+                                              int max_nt) {
+    const int nbx = (max_nt + 63) / 64, nb = (nt + 63) / 64, lane = threadIdx.x & 63;
+    uint32_t m = 0;
+    for (int b = lane; b < nb; b += 64) m = max(m, tmaxb[(size_t)p * nbx + b]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o, 64));
+    return m;
 }
 
 // min trees of the filter (v_min3_f32 / v_min_f32: the file is built with -fno-honor-nans, so
@@ -281,7 +301,8 @@ __device__ __forceinline__ size_t cand_slot(int p, int ch, int chunks, int nqb, 
 __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const float* __restrict__ dq,
                                                           const bf16x8* __restrict__ thi,
                                                           const float* __restrict__ tn,
-                                                          const uint32_t* __restrict__ tmax,
+                                                          const uint32_t* __restrict__ tmaxb,
+                                                          uint32_t* __restrict__ tmax,
                                                           const int64_t* __restrict__ off_q,
                                                           const int64_t* __restrict__ off_t,
                                                           int chunk_len, int chunks, int max_nq,
@@ -311,8 +332,11 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
     if (q0 >= nq || t0 >= nt) return;  // uniform over the block
     const int t1 = min(t0 + chunk_len, nt);
     const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, r = lane & 31;
-    // teM >= 2 eps |t|^2 for every row of the pair
-    const float teM = __uint_as_float(tmax[p]) * (2.f * kFEps) * (1.f + kFMargin) + kFTiny;
+    // teM >= 2 eps |t|^2 for every row of the pair (the pair's max for knn2_rescore from the
+    // pair's first block)
+    const uint32_t tmx = pair_tmax(tmaxb, p, nt, max_nt);
+    if (qb == 0 && ch == 0 && tid == 0) tmax[p] = tmx;
+    const float teM = __uint_as_float(tmx) * (2.f * kFEps) * (1.f + kFMargin) + kFTiny;
     // the wave's two 32-query column blocks: fragments dims 16c + 8h .. +7, rounded once
     bf16x8 qh[2][4];
     float QB[2], cq[2];
@@ -1166,9 +1190,10 @@ size_t knn2_cand_bytes(const BatchShape& sh) {
            (2 * sizeof(bf16x8) + 4);
 }
 
-size_t knn2_split_bytes(const BatchShape& sh) {  // rows, tu, tmax, sentinel row (+ align)
+size_t knn2_split_bytes(const BatchShape& sh) {  // rows, tu, tmax, sentinel row, block maxima
     return (size_t)sh.n_pairs * sh.max_nt * (kDim * sizeof(__bf16) + sizeof(float)) +
-           (size_t)sh.n_pairs * sizeof(uint32_t) + 16 + 128 + 16;
+           (size_t)sh.n_pairs * sizeof(uint32_t) + 16 + 128 + 16 +
+           (size_t)sh.n_pairs * ((sh.max_nt + 63) / 64) * sizeof(uint32_t);
 }
 
 static void cand_split(const BatchShape& sh, void* cand, int32_t** ctile, bf16x8** cval) {
@@ -1189,17 +1214,14 @@ static char* split_sentinel(const BatchShape& sh, void* split) {
 hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const int64_t* off_q,
                               const int64_t* off_t, const BatchShape& sh, void* split,
                               float2* pu, int32_t* ccount, void* cand, hipStream_t st,
-                              int32_t* ovf) {
+                              int32_t* ovf, int32_t* flags) {
     bf16x8* thi = (bf16x8*)split;
     float* tn = (float*)(thi + (size_t)sh.n_pairs * sh.max_nt * 8);
     uint32_t* tmax = split_tmax(sh, split);
     char* sent = split_sentinel(sh, split);
-    hipError_t e = hipMemsetAsync(tmax, 0, (size_t)sh.n_pairs * sizeof(uint32_t), st);
-    if (e == hipSuccess) e = hipMemsetAsync(sent, 0, 128, st);
-    if (e == hipSuccess) e = hipMemsetD32Async((hipDeviceptr_t)(sent + 128), 0x7f800000u, 1, st);
-    if (e != hipSuccess) return e;
+    uint32_t* tmaxb = (uint32_t*)(sent + 144);  // (after the sentinel row and its tu, 16-B aligned)
     ERP_LAUNCH(knn2_split_kernel, dim3((sh.max_nt + 63) / 64, sh.n_pairs), dim3(256), 0,
-                       st, desc_t, off_t, sh.max_nt, thi, tn, tmax, ovf);
+                       st, desc_t, off_t, sh.max_nt, thi, tn, tmaxb, ovf, (uint32_t*)sent, flags);
     int32_t* ctile;
     bf16x8* cval;
     cand_split(sh, cand, &ctile, &cval);
@@ -1207,7 +1229,8 @@ hipError_t launch_knn2_filter(const float* desc_q, const float* desc_t, const in
     if ((size_t)sh.n_pairs * sh.max_nq * sh.fchunks * 2 >= (1ull << 31)) return hipErrorInvalidValue;
     float* qn = (float*)(pu + (size_t)sh.n_pairs * sh.max_nq * sh.fchunks);  // (after pu)
     ERP_LAUNCH(knn2_filter_kernel, dim3(qblocks * sh.fchunks * sh.n_pairs), dim3(256), 0,
-                       st, desc_q, thi, tn, tmax, off_q, off_t, sh.fchunk_len, sh.fchunks,
+                       st, desc_q, thi, tn, (const uint32_t*)tmaxb, tmax, off_q, off_t,
+                       sh.fchunk_len, sh.fchunks,
                        sh.max_nq, sh.max_nt, qblocks, pu, ccount, ctile, cval,
                        (const bf16x8*)sent, (const float*)(sent + 128), qn);
     return hipGetLastError();

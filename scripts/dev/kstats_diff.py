@@ -17,8 +17,8 @@ def load(f):
 
 a, b = load(sys.argv[1]), load(sys.argv[2])
 subs = int(sys.argv[3]) if len(sys.argv) > 3 else 6
-na = a["sampler_kernel<false>"][1] / subs
-nb = b["sampler_kernel<false>"][1] / subs
+na = a[next(k for k in a if k.startswith("sampler_kernel"))][1] / subs
+nb = b[next(k for k in b if k.startswith("sampler_kernel"))][1] / subs
 ta = tb = 0.0
 for k in sorted(set(a) | set(b), key=lambda k: -b.get(k, (0, 0))[0]):
     x, y = a.get(k, (0, 0)), b.get(k, (0, 0))
