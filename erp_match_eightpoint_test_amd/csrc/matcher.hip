@@ -233,24 +233,34 @@ __device__ __forceinline__ float second4(float a0, float a1, float b0, float b1)
 }
 
 // A candidate slot is one 32-B record: the tile's 16 bounds as bf16, with the tile's index
-// (tile0 / 32 < 2048: rows < 65536, chunk lengths are multiples of 32) in the 16 mantissa LSBs
-// (bit 2 d of the index in dword d's low half, bit 2 d + 1 in its high half).  The knn2_rescore
-// side widens each value by 2^-6 |v| instead of 2^-8 |v| (round to nearest: 1/2 ulp, the
-// replaced LSB: 1 ulp, so |v - u'| <= 3 2^-8 |v|).  Before round 3 the tile index went to a
-// separate int32 array: a scattered 4-B store per slot that HBM wrote as a whole sector (the
-// filter's slot writes 0.72 GB per 192-pair launch against 0.35 GB of bounds;
+// (tile0 / 32 < 2048: rows < 65536, chunk lengths are multiples of 32) in the 16 mantissa LSBs:
+// bit d of the index in dword d's low half, bit d + 8 in its high half (d < 8).  The
+// knn2_rescore side widens each value by 2^-6 |v| instead of 2^-8 |v| (round to nearest: 1/2
+// ulp, the replaced LSB: 1 ulp, so |v - u'| <= 3 2^-8 |v|).  Before round 3 the tile index went
+// to a separate int32 array: a scattered 4-B store per slot that HBM wrote as a whole sector
+// (the filter's slot writes 0.72 GB per 192-pair launch against 0.35 GB of bounds;
 // ERP_CAND_TILE_ARRAY=1 keeps that layout for A/B; with the interleaved slots of
 // ERP_CAND_INTERLEAVE=1 its stores coalesce, profiles/r05q_ab_slots.txt).
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ bf16x8 cand_embed_tile(bf16x8 b, int g, int tile0) {
+// v_bfi_b32: (m & b) | (~m & w) with the mask in a VGPR and the wave-uniform bits in an SGPR
+// (one VALU op per dword; the compiler's AND + OR took two: a VOP3 on gfx950 reads one SGPR and
+// no literal).  w is a v_cvt_pk_bf16_f32 result, not an MFMA result: no MFMA read hazard.
+__device__ __forceinline__ uint32_t bfi_lsb(uint32_t m, uint32_t b, uint32_t w) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "s"(b), "v"(w));
+    return r;
+}
+// T = the tile index spread for the embedding: bits 0-7 at 0-7, bits 8-15 at 16-23, so that
+// dword d takes (T >> d) under the mask 0x00010001 (one scalar shift per dword)
+__device__ __forceinline__ uint32_t cand_spread(int tile0) {
     const uint32_t ti = (uint32_t)tile0 >> 5;
+    return (ti & 0xffu) | ((ti >> 8) << 16);
+}
+__device__ __forceinline__ bf16x8 cand_embed_tile(bf16x8 b, int g, uint32_t T) {
     u32x4 w = __builtin_bit_cast(u32x4, b);
+    const uint32_t m = 0x00010001u;
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int d = 4 * g + k;
-        const uint32_t bits = ((ti >> (2 * d)) & 1u) | (((ti >> (2 * d + 1)) & 1u) << 16);
-        w[k] = (w[k] & 0xfffefffeu) | bits;
-    }
+    for (int k = 0; k < 4; k++) w[k] = bfi_lsb(m, T >> (4 * g + k), w[k]);
     return __builtin_bit_cast(bf16x8, w);
 }
 __device__ __forceinline__ int cand_tile(bf16x8 v0, bf16x8 v1) {
@@ -259,7 +269,7 @@ __device__ __forceinline__ int cand_tile(bf16x8 v0, bf16x8 v1) {
 #pragma unroll
     for (int d = 0; d < 8; d++) {
         const uint32_t w = d < 4 ? a[d] : b[d - 4];
-        ti |= ((w & 1u) << (2 * d)) | (((w >> 16) & 1u) << (2 * d + 1));
+        ti |= ((w & 1u) << d) | (((w >> 16) & 1u) << (d + 8));
     }
     return (int)(ti << 5);
 }
@@ -369,9 +379,18 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
     float thr[2] = {-kInf, -kInf};
     int ncand[2] = {0, 0};
     uint32_t cl[2];  // (pair, query, chunk, lane half) list index (< 2^31: the launcher checks)
+    // the lists' first slot records, computed once (the 64-bit slot arithmetic inside the
+    // extraction branch cost ~20 VALU per taken branch)
+    bf16x8* clist[2];
+    int32_t* ctl[2];
+    constexpr int kSlotStride = ERP_CAND_INTERLEAVE ? 64 : 1;
 #pragma unroll
-    for (int j = 0; j < 2; j++)
+    for (int j = 0; j < 2; j++) {
         cl[j] = (((uint32_t)p * (uint32_t)max_nq + (uint32_t)qi[j]) * (uint32_t)chunks + ch) * 2u + h;
+        const size_t s0 = cand_slot(p, ch, chunks, (max_nq + 31) >> 5, qi[j], h, 0);
+        clist[j] = cval + s0 * 2;
+        ctl[j] = tile_array ? ctile + s0 : nullptr;
+    }
     // staging by LDS-DMA: wave w moves the stage's 1-KB pieces 4 w .. 4 w + 3 (8 rows each;
     // lane -> row 8 k + (lane >> 3), swizzled source piece) and, waves 0 and 1, 64 tu each;
     // rows past the chunk read the sentinel row (bf16 zeros, tu = +inf)
@@ -507,14 +526,14 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
         if (extract && min2f(ta, tb) <= thr[j]) {
             const int sl = ncand[j]++;
             if (sl < kCandSlots && !ERP_FILTER_ABLATE) {
-                const size_t slot = cand_slot(p, ch, chunks, (max_nq + 31) >> 5, qi[j], h, sl);
-                if (tile_array) ctile[slot] = tile0;
+                if (tile_array) ctl[j][sl * kSlotStride] = tile0;
 #pragma unroll
                 for (int g = 0; g < 2; g++) {
                     bf16x8 b;
 #pragma unroll
                     for (int i = 0; i < 8; i++) b[i] = (__bf16)e[8 * g + i];
-                    cval[slot * 2 + g] = tile_array ? b : cand_embed_tile(b, g, tile0);
+                    clist[j][sl * (2 * kSlotStride) + g] =
+                        tile_array ? b : cand_embed_tile(b, g, cand_spread(tile0));
                 }
             }
         }
