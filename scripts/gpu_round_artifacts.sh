@@ -4,9 +4,9 @@
 #   1. the GPU parity tests (SKIP_TESTS=1 skips them: the bench / profile passes alone), with the
 #      real-pair gaps against the reference's recovered (R, T) written to real_gaps_<TAG>.json;
 #   2. the default bench (with the CPU baseline and the oracle parity check);
-#   3. EXTRA_BENCH=1: the counter-based sampler line (--sampler philox), the worst-case batch
-#      as the timed batch (--main-batch worst, for its stage times), configs[2]'s shape
-#      (--kpts 2048 --pairs 1024) and the single-pair latency probe;
+#   3. EXTRA_BENCH=1: the worst-case batch as the timed batch (--main-batch worst: its stage
+#      times and its own oracle parity), configs[2]'s shape (--kpts 2048 --pairs 1024), the
+#      single-pair latency probe, and with PHILOX=1 the counter-based sampler line;
 #   4. a rocprofv3 kernel-trace --stats run and two PMC passes (FETCH_SIZE, WRITE_SIZE; separate
 #      passes, kernel trace only) of the bench workload with --steps 0 --warmup 2: bench.py then
 #      runs only its serial profile pass (the default step's sub-batches one after the other), so
@@ -30,12 +30,16 @@ echo "== bench (default, with cpu baseline)" && timeout -k 10 600 python bench.p
   > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err || { tail -20 gpurun_out/bench_${TAG}.err; exit 1; }
 tail -c 400 gpurun_out/bench_${TAG}.json
 if [ "${EXTRA_BENCH:-0}" = "1" ]; then
-  echo "== bench --sampler philox" && timeout -k 10 600 python bench.py --sampler philox --profile-tag ${TAG} \
-    --hard-steps 0 --worst-steps 0 > gpurun_out/bench_philox_${TAG}.json 2> gpurun_out/bench_philox_${TAG}.err \
-    || { tail -20 gpurun_out/bench_philox_${TAG}.err; exit 1; }
-  tail -c 300 gpurun_out/bench_philox_${TAG}.json
+  if [ "${PHILOX:-0}" = "1" ]; then  # (the counter-based sampler: an option, not measured every round)
+    echo "== bench --sampler philox" && timeout -k 10 600 python bench.py --sampler philox --profile-tag ${TAG} \
+      --hard-steps 0 --worst-steps 0 > gpurun_out/bench_philox_${TAG}.json 2> gpurun_out/bench_philox_${TAG}.err \
+      || { tail -20 gpurun_out/bench_philox_${TAG}.err; exit 1; }
+    tail -c 300 gpurun_out/bench_philox_${TAG}.json
+  fi
+  # the worst-case batch as the timed batch, with its own oracle check (a bounded CPU sample of
+  # the first pair of every sub-batch, then the second, ...) and timed-vs-serial comparison
   echo "== bench --main-batch worst" && timeout -k 10 600 python bench.py --main-batch worst --steps 3 \
-    --hard-steps 0 --worst-steps 0 --no-cpu-baseline --profile-tag ${TAG} > gpurun_out/bench_worst_${TAG}.json \
+    --hard-steps 0 --worst-steps 0 --cpu-seconds 8 --profile-tag ${TAG} > gpurun_out/bench_worst_${TAG}.json \
     2> gpurun_out/bench_worst_${TAG}.err || { tail -20 gpurun_out/bench_worst_${TAG}.err; exit 1; }
   tail -c 300 gpurun_out/bench_worst_${TAG}.json
   echo "== bench configs[2] shape (2048 x 2048 keypoints, 1024 pairs per step)" && timeout -k 10 600 \
