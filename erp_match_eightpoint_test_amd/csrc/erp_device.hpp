@@ -142,46 +142,59 @@ ERP_HD inline void svd3_opencv(const double* src, double* w_out, double* u, doub
         }
         W[i] = sqrt(sd);
     }
-    // selection sort descending, swapping rows of At and Vt
-    for (int i = 0; i < 2; i++) {
-        int j = i;
-        for (int k = i + 1; k < 3; k++)
-            if (W[j] < W[k]) j = k;
-        if (i != j) {
-            double t = W[i];
-            W[i] = W[j];
-            W[j] = t;
-            for (int k = 0; k < 3; k++) {
-                t = At[i * 3 + k];
-                At[i * 3 + k] = At[j * 3 + k];
-                At[j * 3 + k] = t;
-                t = V[i * 3 + k];
-                V[i * 3 + k] = V[j * 3 + k];
-                V[j * 3 + k] = t;
-            }
+    // selection sort descending, swapping rows of At and Vt: i = 0 swaps row 0 with the first
+    // maximum j, i = 1 rows 1 and 2 if W[1] < W[2].  Written as conditional swaps with fixed
+    // indices (the same moves: a per-lane row index j made every access a select chain over
+    // all 21 values, ~190 v_cndmask per decomposition)
+    auto cswap = [&](bool c, int a, int b) {
+        double t = W[a];
+        W[a] = c ? W[b] : t;
+        W[b] = c ? t : W[b];
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            t = At[a * 3 + k];
+            At[a * 3 + k] = c ? At[b * 3 + k] : t;
+            At[b * 3 + k] = c ? t : At[b * 3 + k];
+            t = V[a * 3 + k];
+            V[a * 3 + k] = c ? V[b * 3 + k] : t;
+            V[b * 3 + k] = c ? t : V[b * 3 + k];
         }
+    };
+    {
+        const bool j1 = W[0] < W[1];              // k = 1
+        const bool j2 = (j1 ? W[1] : W[0]) < W[2];  // k = 2 against W[j]
+        cswap(j1 && !j2, 0, 1);
+        cswap(j2, 0, 2);
+        cswap(W[1] < W[2], 1, 2);
     }
     uint64_t rng = 0x12345678;
+#pragma unroll
     for (int i = 0; i < 3; i++) {
         double sd = W[i];
         for (int ii = 0; ii < 100 && sd <= minval; ii++) {
             const double val0 = 1. / 3;
+#pragma unroll
             for (int k = 0; k < 3; k++) At[i * 3 + k] = (cv_rng_next(rng) & 256) != 0 ? val0 : -val0;
             for (int it2 = 0; it2 < 2; it2++) {
+#pragma unroll
                 for (int j = 0; j < i; j++) {
                     sd = 0;
+#pragma unroll
                     for (int k = 0; k < 3; k++) sd += At[i * 3 + k] * At[j * 3 + k];
                     double asum = 0;
+#pragma unroll
                     for (int k = 0; k < 3; k++) {
                         const double t = At[i * 3 + k] - sd * At[j * 3 + k];
                         At[i * 3 + k] = t;
                         asum += fabs(t);
                     }
                     asum = asum > eps * 100 ? 1 / asum : 0;
+#pragma unroll
                     for (int k = 0; k < 3; k++) At[i * 3 + k] *= asum;
                 }
             }
             sd = 0;
+#pragma unroll
             for (int k = 0; k < 3; k++) {
                 const double t = At[i * 3 + k];
                 sd += t * t;
@@ -749,9 +762,10 @@ ERP_HD inline void gram_min_eigvec9_jacobi(const double* g36, int stride, int h,
 }
 
 // L D L^T of B = G - mu I from the 36 Gram values, in place in S (L below the diagonal, stored
-// at ut9(j, i); D on the diagonal, clamped at floor_d)
+// at ut9(j, i); D on the diagonal, clamped at floor_d) and 1/D in dinv (the division the
+// factorisation makes anyway: the solves only multiply by it)
 ERP_HD ERP_INLINE void gram_ldlt9(const double* g36, int stride, int h, double mu, double floor_d,
-                                  double* S) {
+                                  double* S, double* dinv) {
     gram36_to_ut(g36, stride, h, S);
 #pragma unroll
     for (int i = 0; i < 9; i++) S[ut9(i, i)] -= mu;
@@ -763,6 +777,7 @@ ERP_HD ERP_INLINE void gram_ldlt9(const double* g36, int stride, int h, double m
         d = d > floor_d ? d : floor_d;
         S[ut9(j, j)] = d;
         const double inv = 1.0 / d;
+        dinv[j] = inv;
 #pragma unroll
         for (int i = j + 1; i < 9; i++) {
             double v = S[ut9(j, i)];
@@ -782,7 +797,7 @@ ERP_HD ERP_INLINE void gram_ldlt9(const double* g36, int stride, int h, double m
 // the Jacobi path (eigenvalue shift + inverse iteration, gram_min_eigvec9_jacobi).
 // The inverse-iteration part alone (the device kernel runs the Jacobi fallback in a second,
 // rarely busy kernel so that its registers do not size the common one): false = not settled.
-// D is kept as 1/D on the diagonal of S (the solves only multiply by it).
+// The solves multiply by 1/D (gram_ldlt9's dinv).
 ERP_HD ERP_INLINE bool gram_min_eigvec9_inv(const double* g36, int stride, int h, double* e) {
     constexpr int kInvIt = 10;
     double S[45];
@@ -790,9 +805,8 @@ ERP_HD ERP_INLINE bool gram_min_eigvec9_inv(const double* g36, int stride, int h
 #pragma unroll
     for (int i = 0; i < 9; i++) tr += g36[(6 * sym3(i / 3, i / 3) + sym3(i % 3, i % 3)) * stride + h];
     const double tiny = kDblEps * (tr > 0 ? tr : 1.0);
-    gram_ldlt9(g36, stride, h, -16 * tiny, tiny * 1e-3, S);
-#pragma unroll
-    for (int i = 0; i < 9; i++) S[ut9(i, i)] = 1.0 / S[ut9(i, i)];
+    double dinv[9];
+    gram_ldlt9(g36, stride, h, -16 * tiny, tiny * 1e-3, S, dinv);
     double x[9];
 #pragma unroll
     for (int i = 0; i < 9; i++) x[i] = 1.0 / 3.0;
@@ -807,7 +821,7 @@ ERP_HD ERP_INLINE bool gram_min_eigvec9_inv(const double* g36, int stride, int h
             y[i] = v;
         }
 #pragma unroll
-        for (int i = 0; i < 9; i++) y[i] *= S[ut9(i, i)];
+        for (int i = 0; i < 9; i++) y[i] *= dinv[i];
 #pragma unroll
         for (int i = 8; i >= 0; i--)  // L^T z = y
 #pragma unroll
@@ -841,10 +855,8 @@ ERP_HD inline void gram_min_eigvec9(const double* g36, int stride, int h, double
 #pragma unroll
     for (int i = 0; i < 9; i++) tr += g36[(6 * sym3(i / 3, i / 3) + sym3(i % 3, i % 3)) * stride + h];
     const double tiny = kDblEps * (tr > 0 ? tr : 1.0);
-    gram_ldlt9(g36, stride, h, -16 * tiny, tiny * 1e-3, S);
     double dinv[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) dinv[i] = 1.0 / S[ut9(i, i)];
+    gram_ldlt9(g36, stride, h, -16 * tiny, tiny * 1e-3, S, dinv);
     double x[9];
 #pragma unroll
     for (int i = 0; i < 9; i++) x[i] = 1.0 / 3.0;

@@ -1122,6 +1122,18 @@ constexpr double kGramScale = 0x1p44;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 
+// G 2^44 = sum_t a_t 256^t from the six limb sums, times 2^-44, in fp64 without the int64
+// recombination (|a_t| <= 65537 * 128 < 2^24): the partial sums of limbs 0-2 and 3-5 are
+// integers below 2^41 (exact in fp64, the power-of-two scalings too), and the last FMA rounds
+// their exact sum once -- the same correctly rounded value as (double)(int64 sum) * 2^-44, for
+// 6 conversions and 5 FMAs instead of the int64 shifts, adds and int64 -> fp64 conversions
+__device__ __forceinline__ double gram_join(int a0, int a1, int a2, int a3, int a4, int a5) {
+    const double lo = __builtin_fma((double)a2, 0x1p-28,
+                                    __builtin_fma((double)a1, 0x1p-36, (double)a0 * 0x1p-44));
+    const double hi = __builtin_fma((double)a5, 0x1p16, __builtin_fma((double)a4, 0x1p8, (double)a3));
+    return __builtin_fma(hi, 0x1p-20, lo);
+}
+
 __device__ __forceinline__ int gram_col(int limb, int c) {
     return c < 32 ? limb * 32 + c : 192 + limb * 4 + (c - 32);
 }
@@ -1369,16 +1381,14 @@ __global__ __launch_bounds__(64 * kGramWaves, GramCfg<WT>::kMinBlocks) void gram
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const int row = (wv * WT + w) * 32 + (k & 3) + 8 * (k >> 2) + 4 * hh;
-            long long v = 0;
-#pragma unroll
-            for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[w][t][k] << (8 * t);
-            long long v2 = 0;
+            static_assert(kGramLimbs == 6, "gram_join takes six limbs");
             const int x = acc[w][kGramLimbs][k];
+            int y[kGramLimbs];
 #pragma unroll
-            for (int t = 0; t < kGramLimbs; t++)
-                v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
-            stg[r * kStg + row] = (double)v * (1.0 / kGramScale);
-            if (r < 4) stg[(32 + r) * kStg + row] = (double)v2 * (1.0 / kGramScale);
+            for (int t = 0; t < kGramLimbs; t++) y[t] = __shfl(x, (lane & 32) + 4 * t + (r & 3), 64);
+            stg[r * kStg + row] = gram_join(acc[w][0][k], acc[w][1][k], acc[w][2][k], acc[w][3][k],
+                                            acc[w][4][k], acc[w][5][k]);
+            if (r < 4) stg[(32 + r) * kStg + row] = gram_join(y[0], y[1], y[2], y[3], y[4], y[5]);
         }
         __syncthreads();
         if (wv >= C::kIters / 64) return;
@@ -1405,17 +1415,15 @@ __global__ __launch_bounds__(64 * kGramWaves, GramCfg<WT>::kMinBlocks) void gram
 #pragma unroll
     for (int k = 0; k < 16; k++) {
         const int row = w * 32 + (k & 3) + 8 * (k >> 2) + 4 * hh;
-        long long v = 0;
-#pragma unroll
-        for (int t = 0; t < kGramLimbs; t++) v += (long long)acc[w][t][k] << (8 * t);
-        long long v2 = 0;
         const int x = acc[w][kGramLimbs][k];
+        int y[kGramLimbs];
 #pragma unroll
-        for (int t = 0; t < kGramLimbs; t++)
-            v2 += (long long)__shfl(x, (lane & 32) + 4 * t + (r & 3), 64) << (8 * t);
+        for (int t = 0; t < kGramLimbs; t++) y[t] = __shfl(x, (lane & 32) + 4 * t + (r & 3), 64);
         if (h0 + row < iters) {
-            go[(size_t)r * iters + h0 + row] = (double)v * (1.0 / kGramScale);
-            if (r < 4) go[(size_t)(32 + r) * iters + h0 + row] = (double)v2 * (1.0 / kGramScale);
+            go[(size_t)r * iters + h0 + row] = gram_join(acc[w][0][k], acc[w][1][k], acc[w][2][k],
+                                                         acc[w][3][k], acc[w][4][k], acc[w][5][k]);
+            if (r < 4)
+                go[(size_t)(32 + r) * iters + h0 + row] = gram_join(y[0], y[1], y[2], y[3], y[4], y[5]);
         }
     }
 }
