@@ -77,7 +77,7 @@ def parse():
                     help="pairs workload: timed steps of a second, harder batch (half the left "
                          "keypoints without a partner, descriptor noise 0.035, 30%% of the true "
                          "matches at wrong positions) reported beside the headline; 0 = off")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0)  # (~48 oracle pairs: the parity sample)
     ap.add_argument("--profile-tag", default=PROFILE_TAG,
                     help="profiles/<tag>_pmc_<stage>.json: HBM bytes per launch (roofline.traffic)")
     ap.add_argument("--matcher", choices=["mfma", "valu"], default="mfma",
