@@ -75,12 +75,12 @@ __device__ int block_exclusive_scan(int v, int* ws, int* total) {
 //     (each <= 2^-24 3 S) add < 2e-5 S, so |a - e| <= 0.0078444 S for the reference's exact
 //     f32 value e, against eps = 0x1.08p-7 = 0.0080566: u = a + eps S >= e + 2.1e-4 S and
 //     l = a - eps S <= e - 2.1e-4 S.  QB = |q|^2 (1 + eps) + tiny turns u' into u = u' + QB.
-//     Running bound: every lane keeps the two smallest of its (tile, 8-row group) minima of u'
-//     (a tile's elements 0-7 and 8-15 are disjoint train rows; since r05, before which the
-//     groups were fixed -- all tiles' elements 0-7, all 8-15 -- and looser whenever both
-//     smallest rows fell in one of them: rescore 1.21 -> 0.89 ms per step), two minima of
-//     disjoint row sets, so the second smallest of a query's four kept minima (both lane
-//     halves) G bounds the chunk's second smallest u' from above, and G + QB >= e_(2) (the
+//     Running bound: every lane keeps the two smallest of its tile minima of u' (the lane's
+//     16 rows of a tile; since r06w -- r05 kept (tile, 8-row group) minima, and before it the
+//     groups were fixed, all tiles' elements 0-7 and all 8-15, looser whenever both smallest
+//     rows fell in one of them: rescore 1.21 -> 0.89 ms per step), two minima of disjoint row
+//     sets, so the second smallest of a query's four kept minima (both lane halves) G bounds
+//     the chunk's second smallest u' from above, and G + QB >= e_(2) (the
 //     true second-neighbour distance).  A row t with e_t <= e_(2) (both neighbours and all
 //     their ties) has l_t <= e_(2) - 2.1e-4 S_t <= G + QB, i.e.
 //       u'_t <= G + (QB - QL) + 2 eps |t|^2 <= thr := G + (QB - QL) + teM,
@@ -136,11 +136,6 @@ constexpr int kFStageB = kFHiB + kFST * kFT * 4;  // + 512
 #define ERP_FILTER_WARM 8
 #endif
 constexpr int kFWarm = ERP_FILTER_WARM;
-// running bound from the two smallest (tile, group) minima per lane (round 5) instead of the
-// minima of two fixed row groups (ERP_FILTER_TOP2=0)
-#ifndef ERP_FILTER_TOP2
-#define ERP_FILTER_TOP2 1
-#endif
 // timing ablations only (wrong results): 1 = no candidate slot stores
 #ifndef ERP_FILTER_ABLATE
 #define ERP_FILTER_ABLATE 0
@@ -497,33 +492,26 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
     };
     // updc: std::integral_constant<bool, false> in the final recompute of the warm stages
     auto tile_epi = [&](int j, f32x16 e, int tile0, bool extract, auto updc) __attribute__((always_inline)) {
-        float ta = min3f(e[0], e[1], e[2]);
-        ta = min3f(ta, e[3], e[4]);
-        ta = min3f(ta, e[5], e[6]);
-        ta = min2f(ta, e[7]);
-        float tb = min3f(e[8], e[9], e[10]);
-        tb = min3f(tb, e[11], e[12]);
-        tb = min3f(tb, e[13], e[14]);
-        tb = min2f(tb, e[15]);
-#if ERP_FILTER_TOP2
-        // the lane's two smallest minima over all (tile, 8-row group)s seen: gm[j][0] <= gm[j][1],
-        // minima of two disjoint row sets, so 2 rows have u' <= gm[j][1]; tighter than a fixed
-        // split of the rows into two groups whenever both smallest rows fall in one group.  Not
-        // in the final recompute of the warm stages: a (tile, group) seen twice could fill both
-        // places with one row set (the fixed-group minima were idempotent)
+        // the running bound: the lane's two smallest TILE minima (16 rows each), minima of
+        // disjoint row sets, so 2 rows have u' <= gm[j][1].  Round 5's (tile, 8-row group)
+        // minima were tighter only when both smallest rows of the lane's ~2k share one tile
+        // (~1 %), for two trees of 8 and a 6-op update against one tree of 16 and 3 ops here
+        // (filter -3 %, rescore unchanged, profiles/r06w_ab_filter_top2.txt); before r05 the
+        // minima of two fixed row groups were looser still (rescore 1.21 -> 0.89 ms).  Not in the
+        // final recompute of the warm stages: a tile seen twice could fill both places
+        float t = min3f(e[0], e[1], e[2]);
+#pragma unroll
+        for (int k = 3; k < 15; k += 2) t = min3f(t, e[k], e[k + 1]);
+        t = min2f(t, e[15]);
         if (decltype(updc)::value) {
-            const float lo = min2f(ta, tb), hi = fmaxf(ta, tb);
-            gm[j][1] = min2f(fmaxf(gm[j][0], lo), min2f(gm[j][1], hi));
-            gm[j][0] = min2f(gm[j][0], lo);
+            gm[j][1] = min2f(fmaxf(gm[j][0], t), gm[j][1]);
+            gm[j][0] = min2f(gm[j][0], t);
         }
-#else
-        gm[j][0] = min2f(gm[j][0], ta);
-        gm[j][1] = min2f(gm[j][1], tb);
-#endif
+        const float tmin = t;
         // a lane whose 16 rows of the tile may hold a candidate stores them whole (16 bounds
         // as bf16 carrying the tile index: two 16-B stores); knn2_rescore picks the rows under
         // the final bound (widening each stored value by its bf16 rounding and the replaced LSB)
-        if (extract && min2f(ta, tb) <= thr[j]) {
+        if (extract && tmin <= thr[j]) {
             const int sl = ncand[j]++;
             if (sl < kCandSlots && !ERP_FILTER_ABLATE) {
                 if (tile_array) ctl[j][sl * kSlotStride] = tile0;
