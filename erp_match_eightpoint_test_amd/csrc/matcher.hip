@@ -136,7 +136,8 @@ constexpr int kFStageB = kFHiB + kFST * kFT * 4;  // + 512
 #define ERP_FILTER_WARM 8
 #endif
 constexpr int kFWarm = ERP_FILTER_WARM;
-// timing ablations only (wrong results): 1 = no candidate slot stores
+// timing ablations only (wrong results): 1 = no candidate slot stores, 2 = no staging DMAs after
+// the first stage (every stage reuses the first stage's rows)
 #ifndef ERP_FILTER_ABLATE
 #define ERP_FILTER_ABLATE 0
 #endif
@@ -513,7 +514,7 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
         // the final bound (widening each stored value by its bf16 rounding and the replaced LSB)
         if (extract && tmin <= thr[j]) {
             const int sl = ncand[j]++;
-            if (sl < kCandSlots && !ERP_FILTER_ABLATE) {
+            if (sl < kCandSlots && ERP_FILTER_ABLATE != 1) {
                 if (tile_array) ctl[j][sl * kSlotStride] = tile0;
 #pragma unroll
                 for (int g = 0; g < 2; g++) {
@@ -579,7 +580,7 @@ __global__ __launch_bounds__(256) ERP_FILTER_WAVES void knn2_filter_kernel(const
         const int st = it < nstages ? it : it - nstages;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (it < last) {
+        if (it < last && ERP_FILTER_ABLATE != 2) {
             const int nx = it + 1 < nstages ? it + 1 : it + 1 - nstages;
             dma(sm + (1 - BUF) * kFStageB, nx);
         }
