@@ -584,7 +584,8 @@ __device__ __forceinline__ void lds_wait_n(uint32_t& o, int n) {
 // a wave alone on its SIMD has nothing else to cover the masked-OR latency: the ILP variants keep
 // up to 15 in flight (the lgkmcnt limit) instead of kReplayLag
 constexpr int kIlpLag = 15;
-// the latency blocks' default (1: step by step, 2: positions first; ERP_SAMPLER_LAT overrides)
+// the latency blocks' default (1: step by step, 2: positions first; the context option
+// ERP_OPT_SAMPLER_LAT overrides)
 constexpr int kSamplerLatMode = 2;
 
 // ---- latency variant (sampler_kernel<2>: waves alone on their SIMDs) -----------------------
