@@ -1330,8 +1330,8 @@ extern "C" int erp_debug_check_pads(void) {
     return bad;
 }
 
-// debug (context option ERP_OPT_DEBUG_SNAP = 1): the last run's snapshot (lb [P][2 iters] f64, ub, first-stage
-// counts [P] i32) into host memory; returns the snapshot's size in bytes (0: none)
+// debug (context option ERP_OPT_DEBUG_SNAP = 1): the last run's snapshot (lb [P][2 iters] f64,
+// ub, first-stage counts [P] i32) into host memory; returns the snapshot's size in bytes (0: none)
 extern "C" long long erp_debug_snapshot(erp_ctx* ctx, void* host, size_t bytes) {
     if (!ctx || !ctx->snap_bytes) return 0;
     if (host && bytes >= ctx->snap_bytes) {
