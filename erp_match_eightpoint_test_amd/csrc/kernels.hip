@@ -334,18 +334,11 @@ __device__ __forceinline__ uint32_t mod_i24(uint32_t x, StepDiv c, int d) { retu
 // every d >= 2, x < 2^31) with the remainder by a full 32-bit multiply (the quotient exceeds
 // mad_i24's 24 bits) -- 4 integer ops instead of the fp64 reciprocal's conversions, multiply,
 // truncation and residual FMA.  ERP_SAMPLER_MAGIC=0 keeps the fp64 path everywhere.
-// q d as one v_mul_lo_u32 with the uniform d in an SGPR (x - q d written plainly becomes a
-// v_mad_u64_u32 -- the 64-bit multiply-add -- of which only the low half is used)
-__device__ __forceinline__ uint32_t mul_lo_uniform(uint32_t a, uint32_t d) {
-    uint32_t r;
-    asm("v_mul_lo_u32 %0, %1, %2" : "=v"(r) : "v"(a), "s"(d));
-    return r;
-}
 __device__ __forceinline__ uint32_t mod_small(uint32_t x, uint64_t mt, double r, int d) {
 #if ERP_SAMPLER_MAGIC
     (void)r;
     const uint32_t q = __umulhi(x, (uint32_t)mt) >> (uint32_t)(mt >> 32);
-    return x - mul_lo_uniform(q, (uint32_t)d);
+    return x - q * (uint32_t)d;
 #else
     (void)mt;
     return mod_rup(x, r, (double)d);
