@@ -963,9 +963,15 @@ def main():
                 b1cache[r] = make_batch(r, 1, args.kpts, args.seed, args.inlier_frac, args.sigma)[0]
             return b1cache[r]
 
-        # (the pruning route, as the gathered batch took: the small-batch route would change the
-        # work counts binned_rows / survivors of the record, not its result fields)
-        ctx_c = make_ctx(local, small_batch=0)
+        # (the pruning route, as the gathered batch took: the small-batch route -- and the
+        # automatic pruning options, which a launch of fewer than 8 pairs resolves to off
+        # (capi.hip pruning_opts) -- would change the work counts binned_rows / survivors of the
+        # record, not its result fields; so the sub-batch's own resolution is set explicitly)
+        few = len(parts[0]) < 8  # (each rank's first pair is in its sub-batch 0)
+        auto = {"lip2": 0 if few else 1, "lipg": 0 if few else 1, "flat_refs": 0 if few else 25,
+                "refine_hint": 0 if few else 1}
+        ctx_c = make_ctx(local, small_batch=0,
+                         **{k: v for k, v in auto.items() if k not in CTX_OPTIONS})
         ctx_c.set_matcher(0 if args.matcher == "mfma" else 1)
         run_c = PairBatchRunner(ctx=ctx_c, iters=args.iters, sampler=SAMPLER)
 
