@@ -2576,7 +2576,7 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(
 // Lipschitz pre-pruning (before the full bounds pass).  The trimmed mean T(x) of the distances
 // from x to the set is 1-Lipschitz in x (every distance is, so are the order statistics and
 // their mean): T(i) >= T(c) - d(i, c).  The bounds kernel first runs on the reference rows
-// c = 0, kLipStep, 2 kLipStep, ... (1/32 of the rows); with U = their smallest UB, a row i with
+// c = 0, kLipStep, 2 kLipStep, ... (1/48 of the rows); with U = their smallest UB, a row i with
 // d(i, c) < LB(c) - U for some reference c has T(i) > U >= the final min UB, so it cannot be the
 // argmin and skips the K-column histogram pass.  The test runs in squared f32 distances against
 // per-reference thresholds thr_c = (LB_c (1 - M) - U (1 + M))^2 (1 - M): the margins M (kLipM,
@@ -2586,12 +2586,15 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(
 // boundary bins (select drops them); the others are appended (any order) to the per-pair list
 // that the second bounds pass reads.  Synthetic configs[1] pairs (one cluster of ~1e4 valid
 // rotations): ~80 % of the rows are pruned for ~1/16 + ~1/20 of the full pass's distances.
-// every 32nd row is a reference row (16 until r04: with the 1e-6 margins of kLipM fewer
+// every 32nd row was a reference row from r04 to r06 (16 until r04: with the 1e-6 margins of kLipM fewer
 // references prune as much; same-box A/Bs per 768-pair step, profiles/r04c_ab_lip_step.txt:
 // consensus 6.60 / 6.62 ms at 16, 6.95 / 7.09 at 12, 6.00 / 6.04 at 24, 5.96 / 5.91 at 32,
-// 5.83 / 5.82 at 48, 6.08 / 6.07 at 64; pairs/s +3-4 % at 24-48)
+// 5.83 / 5.82 at 48, 6.08 / 6.07 at 64; pairs/s +3-4 % at 24-48).  Every 48th since r06aj:
+// re-measured at the round-6 tree (second stage, convexity pruning, refine hints), 48 took the
+// consensus 5.51-5.58 -> 5.35-5.45 ms per step and +1.5-2 % pairs/s on two boxes, worst case
+// unchanged; 40 and 64 were no better than 32 (profiles/r06aj_ab_lip_step.txt)
 #ifndef ERP_LIP_STEP
-#define ERP_LIP_STEP 32
+#define ERP_LIP_STEP 48
 #endif
 constexpr int kLipStep = ERP_LIP_STEP;
 static_assert(kLipStep % 4 == 0, "a reference row is never a second-stage reference (is_ref2)");
@@ -2912,7 +2915,7 @@ __device__ void lip_append(const LipShared& sh, int na, int32_t* __restrict__ li
 // Lipschitz pre-pruning (before the full bounds pass).  The trimmed mean T(x) of the distances
 // from x to the set is 1-Lipschitz in x (every distance is, so are the order statistics and
 // their mean): T(i) >= T(c) - d(i, c).  The bounds kernel first runs on the reference rows
-// c = 0, kLipStep, 2 kLipStep, ... (1/32 of the rows); with U = their smallest UB, a row i with
+// c = 0, kLipStep, 2 kLipStep, ... (1/48 of the rows); with U = their smallest UB, a row i with
 // d(i, c) < LB(c) - U for some reference c has T(i) > U >= the final min UB, so it cannot be the
 // argmin and skips the K-column histogram pass.  The test runs in squared f32 distances against
 // per-reference thresholds thr_c = (LB_c (1 - M) - U (1 + M))^2 (1 - M): the margins M (kLipM,

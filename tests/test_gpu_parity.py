@@ -934,7 +934,7 @@ def test_consensus_lipschitz_prepruning(ctx, oracle, case, consensus_path):
     assert res["min_idx"] == mi
     assert np.array_equal(res["R"], rv[mi]) and np.array_equal(res["T"], tv[mi])
     assert abs(res["min_dist"] - dref[mi]) <= 1e-12 * abs(dref[mi])
-    assert (K + 31) // 32 <= res["binned_rows"] <= K  # (the reference rows: every 32nd)
+    assert (K + 47) // 48 <= res["binned_rows"] <= K  # (the reference rows: every 48th)
     if case in ("cluster", "cluster_outliers", "uniform_cube") and consensus_path == "prune":
         assert res["binned_rows"] < K // 2, res["binned_rows"]
 
