@@ -2605,7 +2605,10 @@ constexpr int kRefStep = ERP_REF_STEP;  // every 16th survivor is refined first 
 constexpr int kLipMinK = 1024;  // smaller sets: no pre-pruning (every non-reference row listed)
 // the convexity-augmented pruning's central references: UB_c <= U kLipGFac (consensus_grad_select;
 // r04 A/B, profiles/r04c_ab_consensus_knobs.txt: 1.03 cost +0.2 ms of consensus per step)
-constexpr float kLipGFac = 1.1f;
+#ifndef ERP_LIP_GFAC
+#define ERP_LIP_GFAC 1.1f
+#endif
+constexpr float kLipGFac = ERP_LIP_GFAC;
 constexpr int kGradBlocks = 2048;  // consensus_grad_kernel's grid (grid-stride over the references)
 #ifndef ERP_LIP2_STEP
 #define ERP_LIP2_STEP 4
