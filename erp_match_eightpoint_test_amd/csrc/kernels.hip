@@ -2598,10 +2598,12 @@ __global__ __launch_bounds__(256) void consensus_bounds_kernel(
 #endif
 constexpr int kLipStep = ERP_LIP_STEP;
 static_assert(kLipStep % 4 == 0, "a reference row is never a second-stage reference (is_ref2)");
+// every 8th survivor is refined first (refine pass; 16th until r06am: the worst-case batch
+// 17.1 -> 18.2k pairs/s on two boxes, the headline unchanged, profiles/r06am_ab_ref_step.txt)
 #ifndef ERP_REF_STEP
-#define ERP_REF_STEP 16
+#define ERP_REF_STEP 8
 #endif
-constexpr int kRefStep = ERP_REF_STEP;  // every 16th survivor is refined first (refine pass)
+constexpr int kRefStep = ERP_REF_STEP;
 constexpr int kLipMinK = 1024;  // smaller sets: no pre-pruning (every non-reference row listed)
 // the convexity-augmented pruning's central references: UB_c <= U kLipGFac (consensus_grad_select;
 // r04 A/B, profiles/r04c_ab_consensus_knobs.txt: 1.03 cost +0.2 ms of consensus per step)
@@ -2933,7 +2935,7 @@ __device__ void lip_append(const LipShared& sh, int na, int32_t* __restrict__ li
 // row-sharded consensus: U is then the shard's smallest reference UB, still >= the global
 // minimum of T, so every pruning stays rigorous); else the per-pair survivor list
 // slist[p][0 .. scount[p]) after the first select (before the refine pass, whose reference
-// survivors, every 16th, are already refined).  The references: consensus_lip_refs_kernel.
+// survivors, every kRefStep-th, are already refined).  The references: consensus_lip_refs_kernel.
 __global__ __launch_bounds__(256) void consensus_lipschitz_kernel(
     const int32_t* __restrict__ kcount, const float* __restrict__ rv, int stride,
     double* __restrict__ lb, double* __restrict__ ub, const int32_t* __restrict__ slist,
@@ -4315,7 +4317,7 @@ __global__ __launch_bounds__(1024) void consensus_select_kernel(const int32_t* _
     __syncthreads();
     double minub = sm[0];
     for (int w = 1; w < 16; w++) minub = fmin(minub, sm[w]);
-    // compaction in row order: the refine pass takes every 16th survivor by list position as
+    // compaction in row order: the refine pass takes every kRefStep-th survivor by list position as
     // its references, so an arrival-order list (one LDS atomic per wave, until r04) made the
     // reference set -- and, once the refined references prune well, the survivor count --
     // differ run to run.  Wave w owns the rows [w C, (w + 1) C): pass 1 counts its survivors
