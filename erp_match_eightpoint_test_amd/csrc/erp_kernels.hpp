@@ -12,7 +12,10 @@ namespace erp {
 constexpr int kDim = 64;          // SURF descriptor length (extended=false)
 constexpr int kMaxQ = 24;         // jump polynomials x^(64(M-1)2^k): waves per pair < 2^24
 constexpr int kPolyWords = 31;    // glibc TYPE_3 degree
-constexpr int kCandSlots = 28;    // matcher: tiles with candidate rows kept per (query, train
+#ifndef ERP_CAND_SLOTS
+#define ERP_CAND_SLOTS 28
+#endif
+constexpr int kCandSlots = ERP_CAND_SLOTS;    // matcher: tiles with candidate rows kept per (query, train
                                   // chunk, lane half) (more: exact sweep of the chunk)
 
 // the batch pipeline's gather + bearings (bearings_from_matches_kernel's work), done by
