@@ -44,7 +44,7 @@ PEAK_VALU_OPS = 256 * 4 * 32 * 2.4e9 / 1e12          # 78.6 T lane-ops/s
 PEAK_VALU_OPS_4CYC = PEAK_VALU_OPS / 2                # secondary: every op at 4 cycles (39.3)
 # profiles/<tag>_pmc_<stage>.json of the shipped step (768 pairs, 6 sub-batches = 128-pair
 # launches): the HBM bytes per launch that roofline.traffic reports
-PROFILE_TAG = "r06z"
+PROFILE_TAG = "r06ap"
 
 
 def parse():
